@@ -1,0 +1,121 @@
+// pybind11 module `_hopsx_ops`: thin bindings of the C ABI in ops_api.h.
+// Device pointers and the hipStream_t arrive as Python ints (tensor.data_ptr(),
+// torch.cuda.current_stream().cuda_stream); shape/dtype validation lives in
+// hops_examples_amd/ops/_C.py so this layer stays a zero-cost trampoline.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <vector>
+
+#include "ops_api.h"
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+template <class T>
+static inline T* P(u p) {
+  return reinterpret_cast<T*>(p);
+}
+static inline hipStream_t S(u s) { return reinterpret_cast<hipStream_t>(s); }
+
+PYBIND11_MODULE(_hopsx_ops, m) {
+  m.doc() = "hopsx CDNA4 (gfx950) HIP kernel library";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("gemm", [](u A, long lda, int akc, u B, long ldb, int bkc, int M, int N, int K, int epi, u out, long ldo,
+                   u bias, float alpha, float beta, int act, u aux, long ldaux, u colsum, u st) {
+    return hopsx_gemm(P<void>(A), lda, akc, P<void>(B), ldb, bkc, M, N, K, epi, P<void>(out), ldo, P<float>(bias),
+                      alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), S(st));
+  });
+  m.def("conv2d_fwd", [](u x, u w, std::vector<int> g, int epi, u out, u bias, int act, u colsum, u st) {
+    return hopsx_conv2d_fwd(P<void>(x), P<void>(w), g.data(), epi, P<void>(out), P<float>(bias), act,
+                            P<float>(colsum), S(st));
+  });
+  m.def("conv2d_dgrad", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u st) {
+    return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
+                              S(st));
+  });
+  m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u st) {
+    return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), S(st));
+  });
+  m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
+                            int sw, int ph, int pw, u st) {
+    return hopsx_maxpool2d_fwd(P<void>(x), P<void>(y), P<unsigned char>(am), B, H, W, C, OH, OW, KH, KW, sh, sw, ph,
+                               pw, S(st));
+  });
+  m.def("maxpool2d_bwd", [](u dy, u am, u x, u dx, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
+                            int sw, int ph, int pw, int act, u colsum, u st) {
+    return hopsx_maxpool2d_bwd(P<void>(dy), P<unsigned char>(am), P<void>(x), P<void>(dx), B, H, W, C, OH, OW, KH, KW,
+                               sh, sw, ph, pw, act, P<float>(colsum), S(st));
+  });
+  m.def("avgpool_global_fwd", [](u x, u y, int B, int HW, int C, u st) {
+    return hopsx_avgpool_global_fwd(P<void>(x), P<void>(y), B, HW, C, S(st));
+  });
+  m.def("avgpool_global_bwd", [](u dy, u dx, int B, int HW, int C, u st) {
+    return hopsx_avgpool_global_bwd(P<void>(dy), P<void>(dx), B, HW, C, S(st));
+  });
+  m.def("loss_fwd_bwd", [](int kind, u logits, int lf32, u target, int B, int C, float gscale, u loss_sum, u correct,
+                           u dl, int df32, u st) {
+    return hopsx_loss_fwd_bwd(kind, P<void>(logits), lf32, P<void>(target), B, C, gscale, P<float>(loss_sum),
+                              P<int>(correct), P<void>(dl), df32, S(st));
+  });
+  m.def("optim_step", [](int kind, u p, u g, u s1, u s2, u s3, u shadow, long n, std::vector<float> hp, u step,
+                         int zero_grad, u st) {
+    return hopsx_optim_step(kind, P<float>(p), P<float>(g), P<float>(s1), P<float>(s2), P<float>(s3),
+                            P<void>(shadow), n, hp.data(), (int)hp.size(), P<float>(step), zero_grad, S(st));
+  });
+  m.def("dropout_fwd", [](u x, u y, long n, float p, u rng, unsigned salt, u st) {
+    return hopsx_dropout_fwd(P<void>(x), P<void>(y), n, p, P<unsigned long long>(rng), salt, S(st));
+  });
+  m.def("dropout_bwd", [](u dy, u dx, long n, float p, u rng, unsigned salt, u st) {
+    return hopsx_dropout_bwd(P<void>(dy), P<void>(dx), n, p, P<unsigned long long>(rng), salt, S(st));
+  });
+  m.def("rng_advance", [](u rng, u st) { return hopsx_rng_advance(P<unsigned long long>(rng), S(st)); });
+  m.def("cast_f32_bf16", [](u x, u y, long n, u st) { return hopsx_cast_f32_bf16(P<float>(x), P<void>(y), n, S(st)); });
+  m.def("cast_bf16_f32", [](u x, u y, long n, u st) { return hopsx_cast_bf16_f32(P<void>(x), P<float>(y), n, S(st)); });
+  m.def("u8_normalize", [](u x, u y, long n, float scale, float shift, u st) {
+    return hopsx_u8_normalize(P<unsigned char>(x), P<void>(y), n, scale, shift, S(st));
+  });
+  m.def("colsum_bf16", [](u x, u out, int M, int N, u st) {
+    return hopsx_colsum_bf16(P<void>(x), P<float>(out), M, N, S(st));
+  });
+  m.def("act_bwd", [](u dy, u y, u dx, long n, int act, u st) {
+    return hopsx_act_bwd(P<void>(dy), P<void>(y), P<void>(dx), n, act, S(st));
+  });
+  m.def("add_bf16", [](u a, u b, u o, long n, int act, u st) {
+    return hopsx_add_bf16(P<void>(a), P<void>(b), P<void>(o), n, act, S(st));
+  });
+  m.def("bn_fwd_train", [](u x, u y, u g, u b, u mean, u rstd, u rm, u rv, float mom, float eps, int M, int C, u res,
+                           int act, u st) {
+    return hopsx_bn_fwd_train(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(mean), P<float>(rstd),
+                              P<float>(rm), P<float>(rv), mom, eps, M, C, P<void>(res), act, S(st));
+  });
+  m.def("bn_fwd_infer", [](u x, u y, u g, u b, u rm, u rv, float eps, int M, int C, u res, int act, u st) {
+    return hopsx_bn_fwd_infer(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(rm), P<float>(rv), eps, M, C,
+                              P<void>(res), act, S(st));
+  });
+  m.def("bn_bwd", [](u dy, u x, u y, u g, u mean, u rstd, u dx, u dg, u db, u ws, int M, int C, int act, u dres,
+                     u st) {
+    return hopsx_bn_bwd(P<void>(dy), P<void>(x), P<void>(y), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
+                        P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), S(st));
+  });
+  m.def("embedding_bag_fwd", [](u table, u idx, u offs, int nbags, int dim, long nidx, int mode, u out, int of32,
+                                long ldo, u st) {
+    return hopsx_embedding_bag_fwd(P<float>(table), P<long>(idx), P<long>(offs), nbags, dim, nidx, mode, P<void>(out),
+                                   of32, ldo, S(st));
+  });
+  m.def("embedding_bag_bwd", [](u dout, int df32, long ldo, u idx, u offs, int nbags, int dim, long nidx, int mode,
+                                u dtable, u st) {
+    return hopsx_embedding_bag_bwd(P<void>(dout), df32, ldo, P<long>(idx), P<long>(offs), nbags, dim, nidx, mode,
+                                   P<float>(dtable), S(st));
+  });
+  m.def("column_stats", [](u x, int rows, int cols, u out, u st) {
+    return hopsx_column_stats(P<float>(x), rows, cols, P<float>(out), S(st));
+  });
+  m.def("column_hist", [](u x, int rows, int cols, u mins, u maxs, int bins, u hist, u st) {
+    return hopsx_column_hist(P<float>(x), rows, cols, P<float>(mins), P<float>(maxs), bins, P<unsigned>(hist), S(st));
+  });
+  m.def("gram", [](u x, u mean, int rows, int cols, u gram, u st) {
+    return hopsx_gram(P<float>(x), P<float>(mean), rows, cols, P<float>(gram), S(st));
+  });
+}

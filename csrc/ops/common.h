@@ -1,0 +1,80 @@
+// hopsx CDNA4 (gfx950) kernel library — shared device helpers.
+//
+// All kernels in csrc/ops are written for MI355X only: 64-lane waves, MFMA
+// bf16 16x16x32 tiles, 160 KiB LDS per CU, 8 XCDs with private L2s.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HOPSX_WAVE 64
+
+typedef uint16_t bf16_raw;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4* lds_v4_ptr;
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even fp32 -> bf16 (NaN preserved)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming T1):
+// consecutive logical tiles land on the same XCD so neighbouring tiles share L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg <= 8) return bid;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// Counter-based RNG (splitmix-style hash): stateless, so dropout masks are
+// regenerated in the backward pass from (seed, offset, index) instead of stored.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= (z >> 31);
+  return (uint32_t)(z >> 8);
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
+  return (hash_u32(seed, idx) & 0xFFFFFF) * (1.0f / 16777216.0f);
+}
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+// derivative of the activation expressed through its OUTPUT y
+__device__ __forceinline__ float act_grad_from_out(float y, int act) {
+  switch (act) {
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_SIGMOID: return y * (1.f - y);
+    case ACT_TANH: return 1.f - y * y;
+    default: return 1.f;
+  }
+}
+
+#define HOPSX_CHECK_LAUNCH() (void)hipGetLastError()

@@ -1,0 +1,136 @@
+// Memory-bound helpers: dropout (stateless counter RNG whose state lives on the
+// device so graph replays draw fresh masks), dtype casts, the uint8 image
+// "landing" normaliser, bias-gradient column sums and activation backward.
+// bf16 streams are moved 8 elements (16 B) per lane where the layout allows.
+#include "common.h"
+#include "ops_api.h"
+
+static inline int ew_grid(long n, int per_thread = 1) {
+  long g = (n / per_thread + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+__device__ __forceinline__ uint64_t drop_key(const unsigned long long* rng, unsigned salt) {
+  return (uint64_t)rng[0] ^ ((uint64_t)salt * 0xD1B54A32D192ED03ull) ^ ((uint64_t)rng[1] * 0x8CB92BA72F3D8DD7ull);
+}
+
+__global__ void dropout_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y, long n, float p,
+                          const unsigned long long* __restrict__ rng, unsigned salt) {
+  const uint64_t key = drop_key(rng, salt);
+  const float scale = 1.f / (1.f - p);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float keep = uniform01(key, i) >= p ? scale : 0.f;
+    y[i] = f2bf(bf2f(x[i]) * keep);
+  }
+}
+
+__global__ void rng_adv_k(unsigned long long* rng) { rng[1] += 1; }
+
+__global__ void cast_f32_bf16_k(const float* __restrict__ x, bf16_raw* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+__global__ void cast_bf16_f32_k(const bf16_raw* __restrict__ x, float* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = bf2f(x[i]);
+}
+
+// y = x * scale + shift, uint8 -> bf16, 8 elements per lane when aligned
+__global__ void u8_norm_k(const unsigned char* __restrict__ x, bf16_raw* __restrict__ y, long n, float scale,
+                          float shift, int vec) {
+  const long n8 = vec ? n / 8 : 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const uint2 v = ((const uint2*)x)[i];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (short)f2bf(((v.x >> (8 * j)) & 0xff) * scale + shift);
+      o[j + 4] = (short)f2bf(((v.y >> (8 * j)) & 0xff) * scale + shift);
+    }
+    ((bf16x8*)y)[i] = o;
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i] * scale + shift);
+}
+
+// out[n] += sum_m x[m][n]; one workgroup owns a column strip, rows split over gridDim.y
+__global__ __launch_bounds__(256) void colsum_k(const bf16_raw* __restrict__ x, float* __restrict__ out, int M,
+                                                int N, int rows_per_block) {
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float s = 0.f;
+  if (n < N)
+    for (int m = r0 + (threadIdx.x >> 6); m < r1; m += 4) s += bf2f(x[(long)m * N + n]);
+  __shared__ float red[4][64];
+  red[threadIdx.x >> 6][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && n < N) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(out + n, t);
+  }
+}
+
+__global__ void act_bwd_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ y, bf16_raw* __restrict__ dx,
+                          long n, int act) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dx[i] = f2bf(bf2f(dy[i]) * act_grad_from_out(bf2f(y[i]), act));
+}
+
+__global__ void add_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ b, bf16_raw* __restrict__ o,
+                      long n, int act) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    o[i] = f2bf(apply_act(bf2f(a[i]) + bf2f(b[i]), act));
+}
+
+extern "C" int hopsx_dropout_fwd(const void* x, void* y, long n, float p, const unsigned long long* rng,
+                                 unsigned salt, hipStream_t st) {
+  hipLaunchKernelGGL(dropout_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, n, p, rng,
+                     salt);
+  return (int)hipGetLastError();
+}
+// the backward of dropout is the same mask applied to dy
+extern "C" int hopsx_dropout_bwd(const void* dy, void* dx, long n, float p, const unsigned long long* rng,
+                                 unsigned salt, hipStream_t st) {
+  return hopsx_dropout_fwd(dy, dx, n, p, rng, salt, st);
+}
+extern "C" int hopsx_rng_advance(unsigned long long* rng, hipStream_t st) {
+  hipLaunchKernelGGL(rng_adv_k, dim3(1), dim3(1), 0, st, rng);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_cast_f32_bf16(const float* x, void* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16_k, dim3(ew_grid(n)), dim3(256), 0, st, x, (bf16_raw*)y, n);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_cast_bf16_f32(const void* x, float* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_f32_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)x, y, n);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_u8_normalize(const unsigned char* x, void* y, long n, float scale, float shift, hipStream_t st) {
+  const int vec = ((uintptr_t)x % 8 == 0) && ((uintptr_t)y % 16 == 0);
+  hipLaunchKernelGGL(u8_norm_k, dim3(ew_grid(n, vec ? 8 : 1)), dim3(256), 0, st, x, (bf16_raw*)y, n, scale, shift,
+                     vec);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_colsum_bf16(const void* x, float* out, int M, int N, hipStream_t st) {
+  const int gx = (N + 63) / 64;
+  int gy = (M + 255) / 256;
+  const int max_gy = (1024 + gx - 1) / gx;
+  if (gy > max_gy) gy = max_gy;
+  if (gy < 1) gy = 1;
+  const int rpb = (M + gy - 1) / gy;
+  hipLaunchKernelGGL(colsum_k, dim3(gx, gy), dim3(256), 0, st, (const bf16_raw*)x, out, M, N, rpb);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_act_bwd(const void* dy, const void* y, void* dx, long n, int act, hipStream_t st) {
+  hipLaunchKernelGGL(act_bwd_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)y,
+                     (bf16_raw*)dx, n, act);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_add_bf16(const void* a, const void* b, void* out, long n, int act, hipStream_t st) {
+  hipLaunchKernelGGL(add_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)a, (const bf16_raw*)b,
+                     (bf16_raw*)out, n, act);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,474 @@
+// hopsx MFMA GEMM engine for gfx950 (MI355X).
+//
+// One templated main loop serves every matmul-shaped op in the framework:
+// dense GEMM (Linear fwd / dgrad / wgrad), implicit-GEMM conv2d fwd / dgrad /
+// wgrad and the wide&deep / MLP towers.  The operand *loaders* are functors
+// that return 8 consecutive bf16 values along the operand's contiguous axis,
+// so im2col / transposed-conv gathers happen on the fly while a tile is
+// staged into LDS — nothing is materialised in HBM.
+//
+// Design (see /opt/skills/guides/cdna_hip_programming.md §3, §5):
+//  * v_mfma_f32_16x16x32_bf16, fp32 accumulate, 4 waves (256 threads) per
+//    workgroup, BK = 64.
+//  * Two LDS images per operand:
+//      KC  ("K contiguous")  [rows][64 k]   read with ds_read_b128,
+//                                            16-B chunk XOR-swizzled c^(row&7)
+//                                            -> conflict-free (4 LDS cycles).
+//      RC  ("row contiguous") [64 k][rows]  read with ds_read_b64_tr_b16 (T10)
+//                                            hardware transpose, chunk XOR
+//                                            swizzle keyed on k.
+//    So a transposed operand (dgrad's W, wgrad's dY and X) never needs a
+//    transposed copy in HBM.
+//  * Register-staged double buffer (T14): tile t+1's global loads are issued
+//    before tile t's MFMAs and written to the other LDS buffer afterwards.
+//  * XCD-aware bijective workgroup remap (T1) and split-K over gridDim.y with
+//    fp32 atomics for reduction-heavy shapes (wgrad with K = batch*pixels).
+//  * Fused epilogues: bias + activation, bf16/fp32 store, fp32 atomic
+//    accumulate (gradient buffers), activation-derivative mask, and an
+//    optional per-column sum (bias gradient) reduced in-wave + one atomic per
+//    column per wave.
+#pragma once
+#include "common.h"
+
+namespace hopsx {
+
+constexpr int GEMM_BK = 64;
+
+__device__ __forceinline__ int rc_swz(int k, int cpr) {
+  return (2 * ((k & 3) | (((k >> 3) & 1) << 2))) & (cpr - 1);
+}
+
+// ----------------------------------------------------------------------------
+// Loaders: bf16x8 load(outer, inner, outer_lim, inner_lim) returns elements
+// (outer, inner .. inner+7) — 8 consecutive along the contiguous axis, zero
+// outside [0, lim).  inner is always a multiple of 8.
+// ----------------------------------------------------------------------------
+struct DenseLoader {
+  const bf16_raw* p;
+  long ld;
+  int vec;  // ld % 8 == 0 and base 16-B aligned
+  __device__ __forceinline__ bf16x8 load(int o, int i, int olim, int ilim) const {
+    bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (o >= olim) return r;
+    const bf16_raw* q = p + (long)o * ld + i;
+    if (vec && i + 8 <= ilim) return *(const bf16x8*)q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (i + j < ilim) ? (short)q[j] : (short)0;
+    return r;
+  }
+};
+
+struct ConvGeom {
+  int B, H, W, C;      // input NHWC
+  int OH, OW, CO;      // output NHWC
+  int KH, KW, sh, sw, ph, pw, dh, dw;
+};
+
+// im2col view of X: (outer = output pixel m, inner = k = (kh, kw, ci))
+struct Im2colLoader {
+  const bf16_raw* x;
+  ConvGeom g;
+  int vec;  // C % 8 == 0 and aligned
+  __device__ __forceinline__ short at(int b, int oh, int ow, int k) const {
+    const int ci = k % g.C;
+    const int t = k / g.C;
+    const int kw = t % g.KW, kh = t / g.KW;
+    const int ih = oh * g.sh - g.ph + kh * g.dh;
+    const int iw = ow * g.sw - g.pw + kw * g.dw;
+    if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return 0;
+    return (short)x[(((long)b * g.H + ih) * g.W + iw) * g.C + ci];
+  }
+  __device__ __forceinline__ bf16x8 load(int m, int k, int olim, int ilim) const {
+    bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (m >= olim) return r;
+    const int ohw = g.OH * g.OW;
+    const int b = m / ohw, rem = m - b * ohw;
+    const int oh = rem / g.OW, ow = rem - oh * g.OW;
+    if (vec && k + 8 <= ilim) {
+      const int ci = k % g.C;
+      const int t = k / g.C;
+      const int kw = t % g.KW, kh = t / g.KW;
+      const int ih = oh * g.sh - g.ph + kh * g.dh;
+      const int iw = ow * g.sw - g.pw + kw * g.dw;
+      if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return r;
+      return *(const bf16x8*)(x + (((long)b * g.H + ih) * g.W + iw) * g.C + ci);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (k + j < ilim) ? at(b, oh, ow, k + j) : (short)0;
+    return r;
+  }
+};
+
+// dgrad A operand: (outer = input pixel (b, ih, iw), inner = k = (kh, kw, co))
+// value = dY[b, oh, ow, co] with oh*sh = ih + ph - kh*dh (zero if not integral)
+struct ConvDgradALoader {
+  const bf16_raw* dy;
+  ConvGeom g;
+  int vec;  // CO % 8 == 0 and aligned
+  __device__ __forceinline__ short at(int b, int ih, int iw, int k) const {
+    const int co = k % g.CO;
+    const int t = k / g.CO;
+    const int kw = t % g.KW, kh = t / g.KW;
+    const int hn = ih + g.ph - kh * g.dh, wn = iw + g.pw - kw * g.dw;
+    if (hn < 0 || wn < 0) return 0;
+    const int oh = hn / g.sh, ow = wn / g.sw;
+    if (oh * g.sh != hn || ow * g.sw != wn || oh >= g.OH || ow >= g.OW) return 0;
+    return (short)dy[(((long)b * g.OH + oh) * g.OW + ow) * g.CO + co];
+  }
+  __device__ __forceinline__ bf16x8 load(int m, int k, int olim, int ilim) const {
+    bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (m >= olim) return r;
+    const int hw = g.H * g.W;
+    const int b = m / hw, rem = m - b * hw;
+    const int ih = rem / g.W, iw = rem - ih * g.W;
+    if (vec && k + 8 <= ilim) {
+      const int co = k % g.CO;
+      const int t = k / g.CO;
+      const int kw = t % g.KW, kh = t / g.KW;
+      const int hn = ih + g.ph - kh * g.dh, wn = iw + g.pw - kw * g.dw;
+      if (hn < 0 || wn < 0) return r;
+      const int oh = hn / g.sh, ow = wn / g.sw;
+      if (oh * g.sh != hn || ow * g.sw != wn || oh >= g.OH || ow >= g.OW) return r;
+      return *(const bf16x8*)(dy + (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (k + j < ilim) ? at(b, ih, iw, k + j) : (short)0;
+    return r;
+  }
+};
+
+// dgrad B operand: W[co][kh][kw][ci] viewed as (outer = k = (kh, kw, co), inner = ci)
+struct ConvWeightTLoader {
+  const bf16_raw* w;
+  ConvGeom g;
+  int vec;  // C % 8 == 0 and aligned
+  __device__ __forceinline__ bf16x8 load(int k, int ci, int olim, int ilim) const {
+    bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (k >= olim) return r;
+    const int co = k % g.CO;
+    const int t = k / g.CO;
+    const int kw = t % g.KW, kh = t / g.KW;
+    const bf16_raw* q = w + (((long)co * g.KH + kh) * g.KW + kw) * g.C + ci;
+    if (vec && ci + 8 <= ilim) return *(const bf16x8*)q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (ci + j < ilim) ? (short)q[j] : (short)0;
+    return r;
+  }
+};
+
+// ----------------------------------------------------------------------------
+// Epilogues.  operator()(m, n, v) handles one output element and returns the
+// value that should enter the optional column sum.
+// ----------------------------------------------------------------------------
+struct EpiStoreBF16 {  // out = act(alpha*acc + bias[n])
+  bf16_raw* out;
+  long ldo;
+  const float* bias;
+  float alpha;
+  int act;
+  float* colsum;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    v = v * alpha + (bias ? bias[n] : 0.f);
+    v = apply_act(v, act);
+    out[(long)m * ldo + n] = f2bf(v);
+    return v;
+  }
+};
+
+struct EpiStoreF32 {  // out = act(alpha*acc + bias[n]) + beta*out
+  float* out;
+  long ldo;
+  const float* bias;
+  float alpha, beta;
+  int act;
+  float* colsum;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    v = v * alpha + (bias ? bias[n] : 0.f);
+    v = apply_act(v, act);
+    float* o = out + (long)m * ldo + n;
+    if (beta != 0.f) v += beta * *o;
+    *o = v;
+    return v;
+  }
+};
+
+struct EpiAtomicF32 {  // out += alpha*acc (split-K safe)
+  float* out;
+  long ldo;
+  float alpha;
+  float* colsum;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    v *= alpha;
+    atomicAdd(out + (long)m * ldo + n, v);
+    return v;
+  }
+};
+
+// out = acc * act'(y[m,n])  (backprop through the activation whose OUTPUT is y)
+struct EpiDActBF16 {
+  bf16_raw* out;
+  long ldo;
+  const bf16_raw* y;
+  long ldy;
+  int act;
+  float* colsum;  // optional: bias gradient of the layer that produced y
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    if (y) v *= act_grad_from_out(bf2f(y[(long)m * ldy + n]), act);
+    out[(long)m * ldo + n] = f2bf(v);
+    return v;
+  }
+};
+
+// ----------------------------------------------------------------------------
+// Main loop
+// ----------------------------------------------------------------------------
+template <int BM, int BN, int WAVES_M, bool A_KC, bool B_KC, class AL, class BL, class EP>
+__global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl, const EP ep, int M, int N,
+                                                       int K, int kps) {
+  constexpr int BK = GEMM_BK;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave tile must hold a 16x16 fragment");
+  constexpr int A_CH = BM * BK / 8, B_CH = BN * BK / 8;  // 16-B chunks per tile
+  constexpr int A_PT = (A_CH + 255) / 256, B_PT = (B_CH + 255) / 256;
+  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
+
+  __shared__ __attribute__((aligned(16))) bf16_raw smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+
+  const int ntn = (N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * kps;
+  const int kend = min(K, kbeg + kps);
+  if (kbeg >= kend) return;
+  const int nt = (kend - kbeg + BK - 1) / BK;
+
+  bf16x8 ra[A_PT], rb[B_PT];
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < A_CH) {
+        if (A_KC) {
+          const int r = idx >> 3, c = idx & 7;
+          ra[i] = al.load(m0 + r, k0 + 8 * c, M, kend);
+        } else {
+          const int cpr = BM / 8;
+          const int kr = idx / cpr, c = idx - kr * cpr;
+          ra[i] = al.load(k0 + kr, m0 + 8 * c, kend, M);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < B_CH) {
+        if (B_KC) {
+          const int r = idx >> 3, c = idx & 7;
+          rb[i] = bl.load(n0 + r, k0 + 8 * c, N, kend);
+        } else {
+          const int cpr = BN / 8;
+          const int kr = idx / cpr, c = idx - kr * cpr;
+          rb[i] = bl.load(k0 + kr, n0 + 8 * c, kend, N);
+        }
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    bf16_raw* sa = smem + buf * (A_ELEMS + B_ELEMS);
+    bf16_raw* sb = sa + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < A_CH) {
+        int off;
+        if (A_KC) {
+          const int r = idx >> 3, c = idx & 7;
+          off = r * BK + 8 * (c ^ (r & 7));
+        } else {
+          const int cpr = BM / 8;
+          const int kr = idx / cpr, c = idx - kr * cpr;
+          off = kr * BM + 8 * (c ^ rc_swz(kr, cpr));
+        }
+        *(bf16x8*)(sa + off) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < B_CH) {
+        int off;
+        if (B_KC) {
+          const int r = idx >> 3, c = idx & 7;
+          off = r * BK + 8 * (c ^ (r & 7));
+        } else {
+          const int cpr = BN / 8;
+          const int kr = idx / cpr, c = idx - kr * cpr;
+          off = kr * BN + 8 * (c ^ rc_swz(kr, cpr));
+        }
+        *(bf16x8*)(sb + off) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // tr-read lane roles (T10): lane 4q+p of a 16-lane group addresses row q, cols 4p..4p+3
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+
+  auto frag_kc = [&](const bf16_raw* s, int row, int kk) -> bf16x8 {
+    const int chunk = kk * 4 + fq;
+    return *(const bf16x8*)(s + row * BK + 8 * (chunk ^ (row & 7)));
+  };
+  auto frag_rc = [&](const bf16_raw* s, int col0, int kk, int ROWS) -> bf16x8 {
+    // rows of the LDS image are k, columns are m (or n); ROWS = BM or BN
+    const int cpr = ROWS / 8;
+    const int col = col0 + 4 * tp;
+    const int k1 = kk * 32 + 8 * fq + tq;
+    const int k2 = k1 + 4;
+    const bf16_raw* p1 = s + k1 * ROWS + 8 * ((col >> 3) ^ rc_swz(k1, cpr)) + (col & 7);
+    const bf16_raw* p2 = s + k2 * ROWS + 8 * ((col >> 3) ^ rc_swz(k2, cpr)) + (col & 7);
+    bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_ptr)(p1));
+    bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_ptr)(p2));
+    return (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  };
+
+  gload(kbeg);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) gload(kbeg + (t + 1) * BK);
+    const bf16_raw* sa = smem + cur * (A_ELEMS + B_ELEMS);
+    const bf16_raw* sb = sa + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int rbase = wm * WTM + i * 16;
+        af[i] = A_KC ? frag_kc(sa, rbase + fr, kk) : frag_rc(sa, rbase, kk, BM);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int cbase = wn * WTN + j * 16;
+        bfr[j] = B_KC ? frag_kc(sb, cbase + fr, kk) : frag_rc(sb, cbase, kk, BN);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nt) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + reg
+  float cs[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) cs[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WTN + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+        if (m < M && n < N) cs[j] += ep(m, n, acc[i][j][r]);
+      }
+    }
+  }
+  if (ep.colsum) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v = cs[j];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int n = n0 + wn * WTN + j * 16 + fr;
+      if (fq == 0 && n < N) atomicAdd(ep.colsum + n, v);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Host-side config selection + launch
+// ----------------------------------------------------------------------------
+struct GemmPlan {
+  int cfg;    // 0: 128x128, 1: 64x64, 2: 32x32
+  int split;  // split-K factor (only honoured for atomic epilogues)
+  int kps;    // K per split (multiple of BK)
+};
+
+inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu = 256) {
+  GemmPlan p;
+  const long t128 = ((M + 127) / 128) * ((N + 127) / 128);
+  const long t64 = ((M + 63) / 64) * ((N + 63) / 64);
+  if (M >= 128 && N >= 128 && t128 >= num_cu) p.cfg = 0;
+  else if (M >= 48 && N >= 48 && t64 >= num_cu / 2) p.cfg = 1;
+  else if (M > 32 && N > 32 && t64 >= 32) p.cfg = 1;
+  else p.cfg = 2;
+  const int bm = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
+  const long tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm);
+  p.split = 1;
+  if (allow_split) {
+    const long target = 2L * num_cu;
+    if (tiles < target) {
+      long s = (target + tiles - 1) / tiles;
+      const long maxs = (K + 4 * GEMM_BK - 1) / (4 * GEMM_BK);  // >= 4 k-tiles per split
+      if (s > maxs) s = maxs;
+      if (s < 1) s = 1;
+      p.split = (int)s;
+    }
+  }
+  long kps = (K + p.split - 1) / p.split;
+  kps = ((kps + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
+  p.kps = (int)(kps > 0 ? kps : GEMM_BK);
+  p.split = (int)((K + p.kps - 1) / p.kps);
+  if (p.split < 1) p.split = 1;
+  return p;
+}
+
+template <bool A_KC, bool B_KC, class AL, class BL, class EP>
+inline void launch_gemm(const AL& al, const BL& bl, const EP& ep, int M, int N, int K, bool allow_split,
+                        hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  if (K <= 0) K = 1;  // degenerate: zero-length reduction still runs the epilogue
+  GemmPlan p = plan_gemm(M, N, K, allow_split);
+  const int bm = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bm - 1) / bm);
+  dim3 grid((unsigned)tiles, (unsigned)p.split);
+  switch (p.cfg) {
+    case 0:
+      hipLaunchKernelGGL((mfma_gemm_kernel<128, 128, 2, A_KC, B_KC, AL, BL, EP>), grid, dim3(256), 0, st, al, bl,
+                         ep, M, N, K, p.kps);
+      break;
+    case 1:
+      hipLaunchKernelGGL((mfma_gemm_kernel<64, 64, 2, A_KC, B_KC, AL, BL, EP>), grid, dim3(256), 0, st, al, bl, ep,
+                         M, N, K, p.kps);
+      break;
+    default:
+      hipLaunchKernelGGL((mfma_gemm_kernel<32, 32, 2, A_KC, B_KC, AL, BL, EP>), grid, dim3(256), 0, st, al, bl, ep,
+                         M, N, K, p.kps);
+      break;
+  }
+}
+
+inline int is_vec_ok(const void* p, long ld) { return (ld % 8 == 0) && ((uintptr_t)p % 16 == 0); }
+
+}  // namespace hopsx

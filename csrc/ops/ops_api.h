@@ -1,0 +1,79 @@
+// C ABI of the hopsx CDNA4 kernel library.  Every entry point takes raw device
+// pointers plus the hipStream_t to launch on (PyTorch's current stream), never
+// allocates, never synchronises — so whole training steps that call them can
+// be captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+
+enum GemmEpi : int { EPI_STORE_BF16 = 0, EPI_STORE_F32 = 1, EPI_ATOMIC_F32 = 2, EPI_DACT_BF16 = 3 };
+
+extern "C" {
+// ---- GEMM / conv (gemm.hip, conv.hip) ----
+int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K, int epi,
+               void* out, long ldo, const float* bias, float alpha, float beta, int act, const void* aux, long ldaux,
+               float* colsum, hipStream_t st);
+int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out, const float* bias, int act,
+                     float* colsum, hipStream_t st);
+int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act,
+                       float* colsum, hipStream_t st);
+int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias, hipStream_t st);
+
+// ---- pooling (pool.hip) ----
+int hopsx_maxpool2d_fwd(const void* x, void* y, unsigned char* argmax, int B, int H, int W, int C, int OH, int OW,
+                        int KH, int KW, int sh, int sw, int ph, int pw, hipStream_t st);
+int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, const void* x, void* dx, int B, int H, int W,
+                        int C, int OH, int OW, int KH, int KW, int sh, int sw, int ph, int pw, int act,
+                        float* colsum, hipStream_t st);
+int hopsx_avgpool_global_fwd(const void* x, void* y, int B, int HW, int C, hipStream_t st);
+int hopsx_avgpool_global_bwd(const void* dy, void* dx, int B, int HW, int C, hipStream_t st);
+
+// ---- losses (loss.hip) ----
+// kind: 0 softmax cross-entropy (int labels), 1 softmax CE (dense/one-hot targets),
+//       2 sigmoid BCE from logits, 3 MSE, 4 BCE on probabilities
+int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
+                       float grad_scale, float* loss_sum, int* correct, void* dlogits, int dlogits_f32,
+                       hipStream_t st);
+
+// ---- optimizers (optim.hip) ----
+// kind: 0 SGD(momentum/nesterov), 1 Adam, 2 AdamW, 3 Adadelta, 4 RMSprop, 5 Adagrad, 6 FTRL
+int hopsx_optim_step(int kind, float* param, float* grad, float* s1, float* s2, float* s3, void* shadow_bf16,
+                     long n, const float* hp, int nhp, float* step_dev, int zero_grad, hipStream_t st);
+
+// ---- dropout / RNG (elementwise.hip) ----
+int hopsx_dropout_fwd(const void* x, void* y, long n, float p, const unsigned long long* rng, unsigned salt,
+                      hipStream_t st);
+int hopsx_dropout_bwd(const void* dy, void* dx, long n, float p, const unsigned long long* rng, unsigned salt,
+                      hipStream_t st);
+int hopsx_rng_advance(unsigned long long* rng, hipStream_t st);
+
+// ---- elementwise / reductions (elementwise.hip) ----
+int hopsx_cast_f32_bf16(const float* x, void* y, long n, hipStream_t st);
+int hopsx_cast_bf16_f32(const void* x, float* y, long n, hipStream_t st);
+int hopsx_u8_normalize(const unsigned char* x, void* y, long n, float scale, float shift, hipStream_t st);
+int hopsx_colsum_bf16(const void* x, float* out, int M, int N, hipStream_t st);
+int hopsx_act_bwd(const void* dy, const void* y, void* dx, long n, int act, hipStream_t st);
+int hopsx_add_bf16(const void* a, const void* b, void* out, long n, int act, hipStream_t st);
+
+// ---- batch norm (norm.hip), NHWC, per-channel over M = B*H*W rows ----
+int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
+                       float* rstd_out, float* running_mean, float* running_var, float momentum, float eps, int M,
+                       int C, const void* residual, int act, hipStream_t st);
+int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, const float* beta, const float* running_mean,
+                       const float* running_var, float eps, int M, int C, const void* residual, int act,
+                       hipStream_t st);
+int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
+                 const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
+                 void* dresidual, hipStream_t st);
+
+// ---- embedding bag (embedding.hip) ----
+int hopsx_embedding_bag_fwd(const float* table, const long* idx, const long* offsets, int nbags, int dim,
+                            long nidx, int mode, void* out, int out_f32, long ldo, hipStream_t st);
+int hopsx_embedding_bag_bwd(const void* dout, int dout_f32, long ldo, const long* idx, const long* offsets,
+                            int nbags, int dim, long nidx, int mode, float* dtable, hipStream_t st);
+
+// ---- column statistics for the feature store (stats.hip) ----
+int hopsx_column_stats(const float* x, int rows, int cols, float* out_stats, hipStream_t st);
+int hopsx_column_hist(const float* x, int rows, int cols, const float* mins, const float* maxs, int bins,
+                      unsigned* hist, hipStream_t st);
+int hopsx_gram(const float* x, const float* mean, int rows, int cols, float* gram, hipStream_t st);
+}

@@ -1,0 +1,83 @@
+"""Framework configuration: kwargs first, then ``HOPSX_*`` environment overrides.
+
+Mirrors the knobs the reference passes through Spark job configs
+(``jobs-client/spark/job_config.json:1-23``: executor gpus, ``spark.tensorflow.num.ps``)
+and the implicit Hopsworks project context (project name / user / root).
+
+Environment:
+  HOPSX_PROJECT_ROOT   local directory that plays the role of the HopsFS project
+                       (default ``~/.hopsx/projects/<name>``)
+  HOPSX_PROJECT_NAME   project name (default ``demo``)
+  HOPSX_USER           project user (default ``$USER``)
+  HOPSX_GPUS_PER_WORKER, HOPSX_NUM_PS, HOPSX_BUCKET_MB, HOPSX_DTYPE (bf16|fp32),
+  HOPSX_GRAPH (1 = capture steady-state train steps into hipGraphs)
+"""
+from __future__ import annotations
+
+import dataclasses
+import getpass
+import os
+from pathlib import Path
+
+
+@dataclasses.dataclass
+class Config:
+    project_name: str = "demo"
+    project_root: Path = Path.home() / ".hopsx" / "projects" / "demo"
+    user: str = "hopsx"
+    gpus_per_worker: int = 1
+    num_ps: int = 1
+    bucket_mb: float = 25.0
+    dtype: str = "bf16"
+    graph: bool = True
+    app_id: str = ""
+
+    @property
+    def hdfs_prefix(self) -> str:
+        return "hopsfs://"
+
+
+_cfg: Config | None = None
+
+
+def _user() -> str:
+    try:
+        return getpass.getuser()
+    except Exception:  # pragma: no cover
+        return "hopsx"
+
+
+def get() -> Config:
+    global _cfg
+    if _cfg is None:
+        name = os.environ.get("HOPSX_PROJECT_NAME", "demo")
+        root = os.environ.get("HOPSX_PROJECT_ROOT")
+        c = Config(
+            project_name=name,
+            project_root=Path(root) if root else Path.home() / ".hopsx" / "projects" / name,
+            user=os.environ.get("HOPSX_USER", _user()),
+            gpus_per_worker=int(os.environ.get("HOPSX_GPUS_PER_WORKER", "1")),
+            num_ps=int(os.environ.get("HOPSX_NUM_PS", "1")),
+            bucket_mb=float(os.environ.get("HOPSX_BUCKET_MB", "25")),
+            dtype=os.environ.get("HOPSX_DTYPE", "bf16"),
+            graph=os.environ.get("HOPSX_GRAPH", "1") == "1",
+        )
+        c.project_root.mkdir(parents=True, exist_ok=True)
+        _cfg = c
+    return _cfg
+
+
+def reset() -> None:
+    global _cfg
+    _cfg = None
+
+
+def set(**kw) -> Config:  # noqa: A001 - mirrors a config setter
+    c = get()
+    for k, v in kw.items():
+        if not hasattr(c, k):
+            raise AttributeError(k)
+        setattr(c, k, Path(v) if k == "project_root" else v)
+    if "project_root" in kw:
+        c.project_root.mkdir(parents=True, exist_ok=True)
+    return c

@@ -1,0 +1,399 @@
+"""Autograd-integrated ops backed by the gfx950 kernels.
+
+GPU path (tensors on ``cuda``): bf16 NHWC activations, MFMA kernels, weight
+gradients accumulated straight into the ParamArena grad buffer (the Function
+returns ``None`` for arena-managed weights and notifies the data-parallel
+engine that the gradient is ready, so bucketed all-reduce can start while the
+rest of the backward runs).
+
+CPU path: plain fp32 PyTorch with the same NHWC semantics — used by the CPU
+test-suite and the ``experiment.launch`` CPU config (BASELINE.json config 1).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..runtime import arena as _arena
+from ..runtime import hooks
+from . import kernels as K
+from ._C import ACT, LOSS
+
+BF16 = torch.bfloat16
+
+
+def _cpu_act(y, act):
+    a = ACT[act] if not isinstance(act, int) else act
+    if a == 1:
+        return F.relu(y)
+    if a == 2:
+        return torch.sigmoid(y)
+    if a == 3:
+        return torch.tanh(y)
+    return y
+
+
+def _wgrad_buf(p):
+    g = _arena.grad_target(p)
+    if g is None:
+        g = torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+    return g
+
+
+def _ret_grad(p, buf):
+    """Return value for a weight's gradient: None when it went into the arena."""
+    if p is None or not p.requires_grad:
+        return None
+    hooks.grad_ready(p)
+    return None if _arena.grad_target(p) is buf else buf
+
+
+def to_compute(x: torch.Tensor) -> torch.Tensor:
+    """Move an activation to the compute dtype of its device (bf16 on GPU)."""
+    if x.is_cuda and x.dtype != BF16:
+        if x.dtype == torch.uint8:
+            return K.u8_normalize(x.contiguous(), 1.0, 0.0)
+        return x.to(BF16)
+    return x.contiguous()
+
+
+# ===================================================================== Linear
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act, out_f32):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        wb = _arena.weight_bf16(w)
+        y = K.linear_fwd(x2, wb, b, act=act, out_f32=out_f32)
+        ctx.save_for_backward(x2, y)
+        ctx.w, ctx.b, ctx.act, ctx.xshape = w, b, act, x.shape
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, y = ctx.saved_tensors
+        w, b, act = ctx.w, ctx.b, ctx.act
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != BF16:
+            dy2 = dy2.to(BF16)
+        dy2 = dy2.contiguous()
+        if ACT.get(act, act) not in (0, None) and y.dtype == BF16:
+            dy2 = K.act_bwd(dy2, y, act)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.linear_dgrad(dy2, _arena.weight_bf16(w)).view(ctx.xshape)
+        gw = _wgrad_buf(w)
+        K.linear_wgrad(dy2, x2, gw)
+        gb = None
+        if b is not None:
+            gb = _wgrad_buf(b)
+            K.colsum(dy2, gb)
+        return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None
+
+
+def linear(x, w, b=None, act=None, out_f32=False):
+    """y = act(x @ w.T + b); w is [out, in] (fp32 master; bf16 shadow used on GPU)."""
+    if not x.is_cuda:
+        return _cpu_act(F.linear(x.float(), w, b), act)
+    return _LinearFn.apply(to_compute(x), w, b, ACT[act] if not isinstance(act, int) else act, out_f32)
+
+
+# ===================================================================== Conv2d
+def _pad_same(k, d=1):
+    tot = d * (k - 1)
+    return tot // 2
+
+
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, dilation, act):
+        x = x.contiguous()
+        wb = _arena.weight_bf16(w)
+        g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
+        y = K.conv2d_fwd(x, wb, g, bias=b, act=act)
+        ctx.save_for_backward(x, y)
+        ctx.w, ctx.b, ctx.g, ctx.act = w, b, g, act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
+        dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
+        if act:
+            dy = K.act_bwd(dy, y, act)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g)
+        gw = _wgrad_buf(w)
+        K.conv2d_wgrad(dy, x, g, gw)
+        gb = None
+        if b is not None:
+            gb = _wgrad_buf(b)
+            K.colsum(dy.view(-1, dy.shape[-1]), gb)
+        return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None
+
+
+def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None):
+    """NHWC conv. x [B,H,W,C], w [CO,KH,KW,C]. padding: int, tuple, 'valid' or 'same' (stride 1)."""
+    st = (stride, stride) if isinstance(stride, int) else tuple(stride)
+    dl = (dilation, dilation) if isinstance(dilation, int) else tuple(dilation)
+    if padding == "valid":
+        pd = (0, 0)
+    elif padding == "same":
+        pd = (_pad_same(w.shape[1], dl[0]), _pad_same(w.shape[2], dl[1]))
+    else:
+        pd = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    a = ACT[act] if not isinstance(act, int) else act
+    if not x.is_cuda:
+        xr = x.float().permute(0, 3, 1, 2)
+        if padding == "same" and (w.shape[1] % 2 == 0 or w.shape[2] % 2 == 0):
+            # TF 'same' pads the extra row/col at the end for even kernels
+            th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
+            xr = F.pad(xr, (tw // 2, tw - tw // 2, th // 2, th - th // 2))
+            pd = (0, 0)
+        y = F.conv2d(xr, w.permute(0, 3, 1, 2), b, st, pd, dl)
+        return _cpu_act(y, a).permute(0, 2, 3, 1).contiguous()
+    if padding == "same" and (w.shape[1] % 2 == 0 or w.shape[2] % 2 == 0):
+        th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
+        x = F.pad(to_compute(x), (0, 0, tw // 2, tw - tw // 2, th // 2, th - th // 2))
+        pd = (0, 0)
+    return _Conv2dFn.apply(to_compute(x), w, b, st, pd, dl, a)
+
+
+# ==================================================================== pooling
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        x = x.contiguous()
+        y, am = K.maxpool2d_fwd(x, k, s, p)
+        ctx.save_for_backward(am)
+        ctx.cfg = (x.shape, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        shape, k, s, p = ctx.cfg
+        dy = dy.to(BF16).contiguous()
+        return K.maxpool2d_bwd(dy, am, shape, k, s, p), None, None, None
+
+
+def max_pool2d(x, kernel, stride=None, padding=0):
+    k = (kernel, kernel) if isinstance(kernel, int) else tuple(kernel)
+    s = k if stride is None else ((stride, stride) if isinstance(stride, int) else tuple(stride))
+    p = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    if not x.is_cuda:
+        return F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous()
+    return _MaxPoolFn.apply(to_compute(x), k, s, p)
+
+
+class _GapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return K.gap_fwd(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K.gap_bwd(dy.to(BF16).contiguous(), ctx.shape)
+
+
+def global_avg_pool(x):
+    if not x.is_cuda:
+        return x.mean(dim=(1, 2))
+    return _GapFn.apply(to_compute(x))
+
+
+# ==================================================================== dropout
+_RNG: dict = {}
+
+
+def rng_state(device) -> torch.Tensor:
+    """Per-device (seed, counter) int64 pair; advanced once per train step."""
+    key = str(device)
+    if key not in _RNG:
+        seed = int(torch.randint(0, 2**62, (1,)).item())
+        _RNG[key] = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+    return _RNG[key]
+
+
+def seed_device_rng(seed: int, device) -> None:
+    rng_state(device).copy_(torch.tensor([seed, 0], dtype=torch.int64))
+
+
+def advance_rng(device) -> None:
+    if torch.device(device).type == "cuda":
+        K.rng_advance(rng_state(device))
+    else:
+        rng_state(device)[1] += 1
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, salt):
+        rng = rng_state(x.device)
+        ctx.cfg = (p, salt, rng)
+        return K.dropout(x.contiguous(), p, rng, salt)
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, salt, rng = ctx.cfg
+        return K.dropout(dy.to(BF16).contiguous(), p, rng, salt), None, None
+
+
+def dropout(x, p: float, training: bool = True, salt: int = 0):
+    if not training or p <= 0:
+        return x
+    if not x.is_cuda:
+        return F.dropout(x, p, True)
+    return _DropoutFn.apply(to_compute(x), float(p), salt)
+
+
+# ================================================================== batchnorm
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act):
+        C = x.shape[-1]
+        x2 = x.contiguous().view(-1, C)
+        mean = torch.empty(C, device=x.device)
+        rstd = torch.empty(C, device=x.device)
+        r2 = residual.contiguous().view(-1, C) if residual is not None else None
+        y = K.bn_fwd_train(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
+        ctx.save_for_backward(x2, y, mean, rstd)
+        ctx.p = (gamma, beta, act, x.shape, residual is not None)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, y, mean, rstd = ctx.saved_tensors
+        gamma, beta, act, shape, has_res = ctx.p
+        C = shape[-1]
+        dy2 = dy.to(BF16).contiguous().view(-1, C)
+        gg, gb = _wgrad_buf(gamma), _wgrad_buf(beta)
+        ws = torch.empty(2 * C, device=dy.device)
+        dres = torch.empty_like(dy2) if has_res else None
+        dx = K.bn_bwd(dy2, x2, y, gamma, mean, rstd, gg, gb, ws, act=act, dresidual=dres)
+        return (dx.view(shape), _ret_grad(gamma, gg), _ret_grad(beta, gb), None, None, None, None,
+                dres.view(shape) if has_res else None, None)
+
+
+def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentum=0.1, eps=1e-5, residual=None,
+               act=None):
+    """NHWC batch norm with fused residual add + activation: act(bn(x) + residual)."""
+    a = ACT[act] if not isinstance(act, int) else act
+    C = x.shape[-1]
+    if not x.is_cuda:
+        y = F.batch_norm(x.reshape(-1, C).float(), running_mean, running_var, gamma, beta, training, momentum, eps)
+        y = y.view(x.shape)
+        if residual is not None:
+            y = y + residual
+        return _cpu_act(y, a)
+    x = to_compute(x)
+    residual = to_compute(residual) if residual is not None else None
+    if training:
+        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a)
+    y = K.bn_fwd_infer(x.contiguous().view(-1, C), gamma, beta, running_mean, running_var, eps,
+                       residual=None if residual is None else residual.contiguous().view(-1, C), act=a)
+    return y.view(x.shape)
+
+
+# ============================================================== embedding bag
+class _EmbagFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, offsets, table, mode, nbags):
+        out = torch.empty(nbags, table.shape[1], device=table.device, dtype=torch.float32)
+        K.embedding_bag_fwd(table.detach(), idx, offsets, mode, out)
+        ctx.save_for_backward(idx, offsets if offsets is not None else torch.empty(0, device=idx.device))
+        ctx.p = (table, mode, nbags, offsets is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        idx, offs = ctx.saved_tensors
+        table, mode, nbags, has_offs = ctx.p
+        g = _wgrad_buf(table)
+        K.embedding_bag_bwd(dout.float().contiguous(), idx, offs if has_offs else None, mode, g, nbags)
+        return None, None, _ret_grad(table, g), None, None
+
+
+def embedding_bag(idx, table, offsets=None, mode="sum"):
+    """idx: 1-D int64 (with offsets) or [B] (one index per bag). Returns fp32 [bags, dim]."""
+    m = {"sum": 0, "mean": 1}[mode]
+    if not table.is_cuda:
+        if offsets is None:
+            return F.embedding(idx, table)
+        return F.embedding_bag(idx, table, offsets, mode=mode)
+    idx = idx.long().contiguous()
+    nb = idx.numel() if offsets is None else offsets.numel()
+    return _EmbagFn.apply(idx, None if offsets is None else offsets.long().contiguous(), table, m, nb)
+
+
+# ===================================================================== losses
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, kind, stats):
+        B, C = logits.shape
+        loss_sum = torch.zeros(1, device=logits.device)
+        correct = torch.zeros(1, device=logits.device, dtype=torch.int32)
+        dl = torch.empty(B, C, device=logits.device, dtype=torch.float32)
+        K.loss_fwd_bwd(kind, logits.contiguous(), target.contiguous(), 1.0 / (B * (C if kind in (2, 3, 4) else 1)),
+                       loss_sum, correct, dl)
+        if stats is not None:
+            stats["correct"] = correct
+            stats["count"] = B * (C if kind in (2, 4) else 1)
+        ctx.save_for_backward(dl)
+        ctx.dtype = logits.dtype
+        return (loss_sum / (B * (C if kind in (2, 3, 4) else 1))).squeeze(0)
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return (dl * g).to(ctx.dtype), None, None, None
+
+
+def _cpu_loss(kind, logits, target, stats):
+    logits = logits.float()
+    if kind == 0:
+        loss = F.cross_entropy(logits, target.long())
+        corr = (logits.argmax(1) == target.long()).sum()
+        cnt = logits.shape[0]
+    elif kind == 1:
+        loss = -(target * F.log_softmax(logits, 1)).sum(1).mean()
+        corr = (logits.argmax(1) == target.argmax(1)).sum()
+        cnt = logits.shape[0]
+    elif kind == 2:
+        loss = F.binary_cross_entropy_with_logits(logits, target.float())
+        corr = ((logits > 0) == (target > 0.5)).sum()
+        cnt = target.numel()
+    elif kind == 3:
+        loss = F.mse_loss(logits, target.float())
+        corr, cnt = torch.zeros(()), 1
+    else:
+        p = logits.clamp(1e-7, 1 - 1e-7)
+        loss = F.binary_cross_entropy(p, target.float())
+        corr = ((logits > 0.5) == (target > 0.5)).sum()
+        cnt = target.numel()
+    if stats is not None:
+        stats["correct"] = corr
+        stats["count"] = cnt
+    return loss
+
+
+def loss(logits, target, kind: str = "sparse_ce", stats: dict | None = None):
+    """Fused loss (+ gradient + correct-count in the same kernel).
+
+    kind: sparse_ce (int labels), ce (one-hot/soft targets), bce_logits, bce (probabilities), mse.
+    ``stats`` (optional dict) receives a device tensor ``correct`` and ``count``.
+    """
+    k = LOSS[kind]
+    if logits.dim() == 1:
+        logits = logits.unsqueeze(1)
+    if k in (2, 3, 4) and target.dim() == 1:
+        target = target.unsqueeze(1)
+    if not logits.is_cuda:
+        return _cpu_loss(k, logits, target, stats)
+    if k == 0:
+        target = target.long()
+    else:
+        target = target.float()
+    return _LossFn.apply(logits, target, k, stats)

@@ -1,0 +1,298 @@
+"""Typed, validated launchers for the gfx950 kernels (no autograd here).
+
+Conventions: activations are bf16 row-major (NHWC for images), weights used by
+the MFMA kernels are the bf16 *shadow* of the fp32 master parameters, gradient
+buffers are fp32 and are ACCUMULATED into (atomics) so they must be zeroed by
+the caller (the fused optimizers zero them after consuming them).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _C
+from ._C import ACT, EPI_ATOMIC_F32, EPI_DACT_BF16, EPI_STORE_BF16, EPI_STORE_F32, check, ptr, stream
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _req(t: torch.Tensor, dtype, name: str, contiguous=True):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a GPU tensor")
+    if contiguous and not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+
+
+def act_id(act) -> int:
+    return act if isinstance(act, int) else ACT[act]
+
+
+# ---------------------------------------------------------------- dense GEMM
+def gemm_raw(a, lda, a_kc, b, ldb, b_kc, M, N, K, epi, out, ldo, bias=None, alpha=1.0, beta=0.0, act=0, aux=None,
+             ldaux=0, colsum=None):
+    rc = _C.ext().gemm(ptr(a), lda, int(a_kc), ptr(b), ldb, int(b_kc), M, N, K, epi, ptr(out), ldo, ptr(bias),
+                       float(alpha), float(beta), act_id(act), ptr(aux), ldaux, ptr(colsum), stream())
+    check(rc, "gemm")
+
+
+def linear_fwd(x, w, bias=None, act=0, out=None, out_f32=False, colsum=None):
+    """y[M,N] = act(x[M,K] @ w[N,K]^T + bias)."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K, (x.shape, w.shape)
+    _req(x, BF16, "x")
+    _req(w, BF16, "w")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=F32 if out_f32 else BF16)
+    epi = EPI_STORE_F32 if out.dtype == F32 else EPI_STORE_BF16
+    gemm_raw(x, K, True, w, K, True, M, N, K, epi, out, N, bias=bias, act=act, colsum=colsum)
+    return out
+
+
+def linear_dgrad(dy, w, yprev=None, act_prev=0, out=None, colsum=None):
+    """dx[M,K] = (dy[M,N] @ w[N,K]) * act'(yprev)  (+ column sum -> previous layer's bias grad)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    _req(dy, BF16, "dy")
+    _req(w, BF16, "w")
+    if out is None:
+        out = torch.empty(M, K, device=dy.device, dtype=BF16)
+    gemm_raw(dy, N, True, w, K, False, M, K, N, EPI_DACT_BF16, out, K, act=act_prev if yprev is not None else 0,
+             aux=yprev, ldaux=K, colsum=colsum)
+    return out
+
+
+def linear_wgrad(dy, x, dw, alpha=1.0):
+    """dw[N,K] += dy[M,N]^T @ x[M,K]  (fp32 atomics, split-K over the batch)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    _req(dy, BF16, "dy")
+    _req(x, BF16, "x")
+    _req(dw, F32, "dw")
+    gemm_raw(dy, N, False, x, K, False, N, K, M, EPI_ATOMIC_F32, dw, K, alpha=alpha)
+    return dw
+
+
+def colsum(x, out):
+    """out[N] += sum_m x[M,N]."""
+    _req(x, BF16, "x")
+    M, N = x.reshape(-1, x.shape[-1]).shape
+    check(_C.ext().colsum_bf16(ptr(x), ptr(out), M, N, stream()), "colsum")
+    return out
+
+
+# -------------------------------------------------------------- conv2d NHWC
+def conv_geom(x_shape, w_shape, stride, padding, dilation):
+    B, H, W, C = x_shape
+    CO, KH, KW, CI = w_shape
+    assert CI == C, (x_shape, w_shape)
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+    OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+    return [B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw, dh, dw]
+
+
+def conv2d_fwd(x, w, geom, bias=None, act=0, out=None, colsum=None):
+    _req(x, BF16, "x")
+    _req(w, BF16, "w")
+    B, OH, OW, CO = geom[0], geom[4], geom[5], geom[6]
+    if out is None:
+        out = torch.empty(B, OH, OW, CO, device=x.device, dtype=BF16)
+    epi = EPI_STORE_F32 if out.dtype == F32 else EPI_STORE_BF16
+    check(_C.ext().conv2d_fwd(ptr(x), ptr(w), geom, epi, ptr(out), ptr(bias), act_id(act), ptr(colsum), stream()),
+          "conv2d_fwd")
+    return out
+
+
+def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None):
+    _req(dy, BF16, "dy")
+    B, H, W, C = geom[:4]
+    if out is None:
+        out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+    check(_C.ext().conv2d_dgrad(ptr(dy), ptr(w), geom, ptr(out), ptr(yprev), act_id(act_prev) if yprev is not None
+                                else 0, ptr(colsum), stream()), "conv2d_dgrad")
+    return out
+
+
+def conv2d_wgrad(dy, x, geom, dw):
+    _req(dy, BF16, "dy")
+    _req(x, BF16, "x")
+    _req(dw, F32, "dw")
+    check(_C.ext().conv2d_wgrad(ptr(dy), ptr(x), geom, ptr(dw), 0, stream()), "conv2d_wgrad")
+    return dw
+
+
+# ------------------------------------------------------------------ pooling
+def pool_out(H, W, k, s, p):
+    return (H + 2 * p[0] - k[0]) // s[0] + 1, (W + 2 * p[1] - k[1]) // s[1] + 1
+
+
+def maxpool2d_fwd(x, k, s, p, out=None, argmax=None):
+    B, H, W, C = x.shape
+    OH, OW = pool_out(H, W, k, s, p)
+    if out is None:
+        out = torch.empty(B, OH, OW, C, device=x.device, dtype=BF16)
+    if argmax is None:
+        argmax = torch.empty(B, OH, OW, C, device=x.device, dtype=torch.uint8)
+    check(_C.ext().maxpool2d_fwd(ptr(x), ptr(out), ptr(argmax), B, H, W, C, OH, OW, k[0], k[1], s[0], s[1], p[0],
+                                 p[1], stream()), "maxpool_fwd")
+    return out, argmax
+
+
+def maxpool2d_bwd(dy, argmax, x_shape, k, s, p, x=None, act=0, out=None, colsum=None):
+    B, H, W, C = x_shape
+    OH, OW = dy.shape[1], dy.shape[2]
+    if out is None:
+        out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+    check(_C.ext().maxpool2d_bwd(ptr(dy), ptr(argmax), ptr(x), ptr(out), B, H, W, C, OH, OW, k[0], k[1], s[0], s[1],
+                                 p[0], p[1], act_id(act), ptr(colsum), stream()), "maxpool_bwd")
+    return out
+
+
+def gap_fwd(x, out=None):
+    B, H, W, C = x.shape
+    if out is None:
+        out = torch.empty(B, C, device=x.device, dtype=BF16)
+    check(_C.ext().avgpool_global_fwd(ptr(x), ptr(out), B, H * W, C, stream()), "gap_fwd")
+    return out
+
+
+def gap_bwd(dy, x_shape, out=None):
+    B, H, W, C = x_shape
+    if out is None:
+        out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+    check(_C.ext().avgpool_global_bwd(ptr(dy), ptr(out), B, H * W, C, stream()), "gap_bwd")
+    return out
+
+
+# ------------------------------------------------------------------- losses
+def loss_fwd_bwd(kind: int, logits, target, grad_scale, loss_sum, correct, dlogits=None):
+    B, C = logits.shape
+    check(_C.ext().loss_fwd_bwd(kind, ptr(logits), int(logits.dtype == F32), ptr(target), B, C, float(grad_scale),
+                                ptr(loss_sum), ptr(correct), ptr(dlogits),
+                                int(dlogits is not None and dlogits.dtype == F32), stream()), "loss")
+    return dlogits
+
+
+# --------------------------------------------------------------- optimizers
+def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True):
+    n = param.numel()
+    check(_C.ext().optim_step(kind, ptr(param), ptr(grad), ptr(s1), ptr(s2), ptr(s3), ptr(shadow), n,
+                              [float(v) for v in hp], ptr(step_dev), int(zero_grad), stream()), "optim")
+
+
+# ------------------------------------------------------------- misc / RNG
+def dropout(x, p, rng, salt, out=None):
+    if out is None:
+        out = torch.empty_like(x)
+    check(_C.ext().dropout_fwd(ptr(x), ptr(out), x.numel(), float(p), ptr(rng), int(salt) & 0xFFFFFFFF, stream()),
+          "dropout")
+    return out
+
+
+def rng_advance(rng):
+    check(_C.ext().rng_advance(ptr(rng), stream()), "rng_advance")
+
+
+def cast_f32_bf16(x, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=BF16)
+    check(_C.ext().cast_f32_bf16(ptr(x), ptr(out), x.numel(), stream()), "cast")
+    return out
+
+
+def u8_normalize(x, scale, shift, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=BF16)
+    check(_C.ext().u8_normalize(ptr(x), ptr(out), x.numel(), float(scale), float(shift), stream()), "u8_normalize")
+    return out
+
+
+def act_bwd(dy, y, act, out=None):
+    if out is None:
+        out = torch.empty_like(dy)
+    check(_C.ext().act_bwd(ptr(dy), ptr(y), ptr(out), dy.numel(), act_id(act), stream()), "act_bwd")
+    return out
+
+
+def add(a, b, act=0, out=None):
+    if out is None:
+        out = torch.empty_like(a)
+    check(_C.ext().add_bf16(ptr(a), ptr(b), ptr(out), a.numel(), act_id(act), stream()), "add")
+    return out
+
+
+# ---------------------------------------------------------------- batchnorm
+def bn_fwd_train(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, residual=None, act=0, out=None):
+    M, C = x2d.shape
+    if out is None:
+        out = torch.empty_like(x2d)
+    check(_C.ext().bn_fwd_train(ptr(x2d), ptr(out), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), ptr(rmean),
+                                ptr(rvar), float(momentum), float(eps), M, C, ptr(residual), act_id(act), stream()),
+          "bn_fwd_train")
+    return out
+
+
+def bn_fwd_infer(x2d, gamma, beta, rmean, rvar, eps, residual=None, act=0, out=None):
+    M, C = x2d.shape
+    if out is None:
+        out = torch.empty_like(x2d)
+    check(_C.ext().bn_fwd_infer(ptr(x2d), ptr(out), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), float(eps), M, C,
+                                ptr(residual), act_id(act), stream()), "bn_fwd_infer")
+    return out
+
+
+def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None, out=None):
+    M, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    check(_C.ext().bn_bwd(ptr(dy), ptr(x), ptr(y), ptr(gamma), ptr(mean), ptr(rstd), ptr(out), ptr(dgamma),
+                          ptr(dbeta), ptr(ws), M, C, act_id(act), ptr(dresidual), stream()), "bn_bwd")
+    return out
+
+
+# ------------------------------------------------------------ embedding bag
+def embedding_bag_fwd(table, idx, offsets, mode, out, ldo=None):
+    nb = out.shape[0] if offsets is None else offsets.numel()
+    dim = table.shape[1]
+    check(_C.ext().embedding_bag_fwd(ptr(table), ptr(idx), ptr(offsets), nb, dim, idx.numel(), mode, ptr(out),
+                                     int(out.dtype == F32), ldo if ldo is not None else out.stride(0), stream()),
+          "embedding_bag_fwd")
+    return out
+
+
+def embedding_bag_bwd(dout, idx, offsets, mode, dtable, nbags, ldo=None):
+    dim = dtable.shape[1]
+    check(_C.ext().embedding_bag_bwd(ptr(dout), int(dout.dtype == F32), ldo if ldo is not None else dout.stride(0),
+                                     ptr(idx), ptr(offsets), nbags, dim, idx.numel(), mode, ptr(dtable), stream()),
+          "embedding_bag_bwd")
+    return dtable
+
+
+# --------------------------------------------------------- column statistics
+def column_stats(x):
+    """x [rows, cols] f32 on GPU -> [cols, 5] = count, sum, sumsq, min, max (NaN = missing)."""
+    rows, cols = x.shape
+    out = torch.zeros(cols, 5, device=x.device, dtype=F32)
+    out[:, 3] = float("inf")
+    out[:, 4] = float("-inf")
+    check(_C.ext().column_stats(ptr(x), rows, cols, ptr(out), stream()), "column_stats")
+    return out
+
+
+def column_hist(x, mins, maxs, bins):
+    rows, cols = x.shape
+    hist = torch.zeros(cols, bins, device=x.device, dtype=torch.int32)
+    check(_C.ext().column_hist(ptr(x), rows, cols, ptr(mins), ptr(maxs), bins, ptr(hist), stream()), "column_hist")
+    return hist
+
+
+def gram(x, mean):
+    rows, cols = x.shape
+    g = torch.zeros(cols, cols, device=x.device, dtype=F32)
+    check(_C.ext().gram(ptr(x), ptr(mean), rows, cols, ptr(g), stream()), "gram")
+    return g
