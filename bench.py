@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST CNN (experiment.mirrored model) training throughput.
+
+BASELINE.json metric "images/sec MNIST CNN + steps/sec Chicago-taxi DNN at 1/2/4/8 MI355X",
+config 2 "MNIST CNN experiment.mirrored bf16 on 8xMI355X (RCCL gradient all-reduce)".
+
+Model   : the MirroredStrategy MNIST CNN of the reference
+          (notebooks/ml/Distributed_Training/mirrored_strategy/mirroredstrategy_mnist_example.ipynb:189-207;
+          Conv32 k2 -> Conv64 k2 -> MaxPool2 -> Dropout .01 -> Dense128 -> Dense10, 1,394,282 params,
+          Adadelta(1.0), categorical cross-entropy), random init.
+Data    : synthetic uint8 28x28 images + labels resident in HBM (no dataset download possible).
+Scaling : weak — per-GPU batch fixed (reference: 32 x num_replicas_in_sync, :128-131).
+Step    : full training step inside the timed region — forward, fused loss, backward,
+          RCCL gradient all-reduce (world > 1), fused Adadelta update.  hipGraph replay.
+
+Also measures the Chicago-taxi wide&deep trainer (steps/sec) unless --no-taxi.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("HOPSX_BENCH_BATCH", "32")))
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-taxi", action="store_true")
+    ap.add_argument("--taxi-batch", type=int, default=512)
+    return ap.parse_args()
+
+
+def timed(step_fn, n, sync_dev):
+    from hops_examples_amd.parallel import dist as hdist
+
+    hdist.barrier()
+    torch.cuda.synchronize(sync_dev)
+    t0 = time.perf_counter()
+    for i in range(n):
+        step_fn(i)
+    torch.cuda.synchronize(sync_dev)
+    hdist.barrier()
+    el = time.perf_counter() - t0
+    return hdist.all_reduce_scalar(el, "max")
+
+
+def main():
+    a = parse()
+    from hops_examples_amd.parallel import dist as hdist
+
+    rank, local_rank, world = hdist.init()
+    if world != a.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = hdist.device()
+    torch.manual_seed(1234 + rank)
+
+    from hops_examples_amd import optim
+    from hops_examples_amd.models.mnist import MirroredMnistCNN, param_count
+    from hops_examples_amd.parallel.dp import DataParallel
+    from hops_examples_amd.runtime.arena import ParamArena
+    from hops_examples_amd.runtime.step import TrainStep
+
+    B = a.batch_per_gpu
+    model = MirroredMnistCNN().to(dev)
+    nparams = param_count(model)
+    ParamArena.from_module(model, dev)
+    opt = optim.Adadelta(model, lr=1.0)
+    dp = DataParallel(model) if world > 1 else None
+    step = TrainStep(model, opt, "sparse_ce", dp=dp, graph=not a.no_graph)
+
+    nb = 8
+    xs = torch.randint(0, 256, (nb, B, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (nb, B), dtype=torch.int64, device=dev)
+    out = {}
+
+    def run(i):
+        out["r"] = step(xs[i % nb], ys[i % nb])
+
+    for i in range(a.warmup):
+        run(i)
+    el = timed(run, a.steps, dev)
+    loss = float(out["r"]["loss"].item())
+    ms = el / a.steps * 1e3
+    ips = B * world * a.steps / el
+
+    taxi = None
+    if not a.no_taxi:
+        try:
+            from hops_examples_amd.models.widedeep import bench_taxi
+
+            taxi = bench_taxi(dev, a.taxi_batch, max(20, a.steps // 2), max(5, a.warmup // 2), timed, world,
+                              graph=not a.no_graph)
+        except Exception as e:  # keep the headline metric even if the secondary one fails
+            taxi = {"error": repr(e)[:300]}
+
+    if rank == 0:
+        rec = {
+            "metric": "images/sec MNIST CNN + steps/sec Chicago-taxi DNN at 1/2/4/8 MI355X",
+            "value": round(ips, 1),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uint8 28x28 images + labels in HBM), random-init weights",
+            "config": {
+                "model": f"MNIST CNN (experiment.mirrored model, {nparams} params), Adadelta(1.0)",
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "hipgraph": not a.no_graph,
+            },
+            "final_loss": round(loss, 4),
+            "chicago_taxi": taxi,
+        }
+        print(json.dumps(rec), flush=True)
+    hdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -23,9 +23,9 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   m.attr("ARCH") = "gfx950";
 
   m.def("gemm", [](u A, long lda, int akc, u B, long ldb, int bkc, int M, int N, int K, int epi, u out, long ldo,
-                   u bias, float alpha, float beta, int act, u aux, long ldaux, u colsum, u st) {
+                   u bias, float alpha, float beta, int act, u aux, long ldaux, u colsum, u ws, long ws_elems, u st) {
     return hopsx_gemm(P<void>(A), lda, akc, P<void>(B), ldb, bkc, M, N, K, epi, P<void>(out), ldo, P<float>(bias),
-                      alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), S(st));
+                      alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), P<float>(ws), ws_elems, S(st));
   });
   m.def("conv2d_fwd", [](u x, u w, std::vector<int> g, int epi, u out, u bias, int act, u colsum, u st) {
     return hopsx_conv2d_fwd(P<void>(x), P<void>(w), g.data(), epi, P<void>(out), P<float>(bias), act,
@@ -39,14 +39,14 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), S(st));
   });
   m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
-                            int sw, int ph, int pw, u st) {
+                            int sw, int ph, int pw, float p, u rng, unsigned salt, u st) {
     return hopsx_maxpool2d_fwd(P<void>(x), P<void>(y), P<unsigned char>(am), B, H, W, C, OH, OW, KH, KW, sh, sw, ph,
-                               pw, S(st));
+                               pw, p, P<unsigned long long>(rng), salt, S(st));
   });
   m.def("maxpool2d_bwd", [](u dy, u am, u x, u dx, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
-                            int sw, int ph, int pw, int act, u colsum, u st) {
+                            int sw, int ph, int pw, int act, u colsum, float p, u rng, unsigned salt, u st) {
     return hopsx_maxpool2d_bwd(P<void>(dy), P<unsigned char>(am), P<void>(x), P<void>(dx), B, H, W, C, OH, OW, KH, KW,
-                               sh, sw, ph, pw, act, P<float>(colsum), S(st));
+                               sh, sw, ph, pw, act, P<float>(colsum), p, P<unsigned long long>(rng), salt, S(st));
   });
   m.def("avgpool_global_fwd", [](u x, u y, int B, int HW, int C, u st) {
     return hopsx_avgpool_global_fwd(P<void>(x), P<void>(y), B, HW, C, S(st));
@@ -60,9 +60,10 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                               P<int>(correct), P<void>(dl), df32, S(st));
   });
   m.def("optim_step", [](int kind, u p, u g, u s1, u s2, u s3, u shadow, long n, std::vector<float> hp, u step,
-                         int zero_grad, u st) {
+                         u arrive, u rng, int zero_grad, u st) {
     return hopsx_optim_step(kind, P<float>(p), P<float>(g), P<float>(s1), P<float>(s2), P<float>(s3),
-                            P<void>(shadow), n, hp.data(), (int)hp.size(), P<float>(step), zero_grad, S(st));
+                            P<void>(shadow), n, hp.data(), (int)hp.size(), P<float>(step), P<unsigned>(arrive),
+                            P<unsigned long long>(rng), zero_grad, S(st));
   });
   m.def("dropout_fwd", [](u x, u y, long n, float p, u rng, unsigned salt, u st) {
     return hopsx_dropout_fwd(P<void>(x), P<void>(y), n, p, P<unsigned long long>(rng), salt, S(st));
@@ -81,6 +82,9 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   });
   m.def("act_bwd", [](u dy, u y, u dx, long n, int act, u st) {
     return hopsx_act_bwd(P<void>(dy), P<void>(y), P<void>(dx), n, act, S(st));
+  });
+  m.def("act_bwd_colsum", [](u dy, u y, u dx, int M, int N, int act, u colsum, u st) {
+    return hopsx_act_bwd_colsum(P<void>(dy), P<void>(y), P<void>(dx), M, N, act, P<float>(colsum), S(st));
   });
   m.def("add_bf16", [](u a, u b, u o, long n, int act, u st) {
     return hopsx_add_bf16(P<void>(a), P<void>(b), P<void>(o), n, act, S(st));

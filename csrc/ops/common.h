@@ -57,6 +57,11 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
   return (hash_u32(seed, idx) & 0xFFFFFF) * (1.0f / 16777216.0f);
 }
 
+// dropout key for (device RNG state, per-layer salt); state = {seed, step counter}
+__device__ __forceinline__ uint64_t drop_key(const unsigned long long* rng, unsigned salt) {
+  return (uint64_t)rng[0] ^ ((uint64_t)salt * 0xD1B54A32D192ED03ull) ^ ((uint64_t)rng[1] * 0x8CB92BA72F3D8DD7ull);
+}
+
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
 
 __device__ __forceinline__ float apply_act(float v, int act) {

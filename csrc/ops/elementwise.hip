@@ -12,9 +12,6 @@ static inline int ew_grid(long n, int per_thread = 1) {
   return (int)g;
 }
 
-__device__ __forceinline__ uint64_t drop_key(const unsigned long long* rng, unsigned salt) {
-  return (uint64_t)rng[0] ^ ((uint64_t)salt * 0xD1B54A32D192ED03ull) ^ ((uint64_t)rng[1] * 0x8CB92BA72F3D8DD7ull);
-}
 
 __global__ void dropout_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y, long n, float p,
                           const unsigned long long* __restrict__ rng, unsigned salt) {
@@ -79,6 +76,30 @@ __global__ void act_bwd_k(const bf16_raw* __restrict__ dy, const bf16_raw* __res
     dx[i] = f2bf(bf2f(dy[i]) * act_grad_from_out(bf2f(y[i]), act));
 }
 
+// dx = dy * act'(y) and colsum[n] += sum_m dx[m][n] in one pass (bias gradient of
+// the layer whose activation output is y); one workgroup per (64-column strip, row slab)
+__global__ __launch_bounds__(256) void act_bwd_colsum_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ y,
+                                                        bf16_raw* __restrict__ dx, int M, int N, int act,
+                                                        float* __restrict__ colsum, int rpb) {
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+  float s = 0.f;
+  if (n < N)
+    for (int m = r0 + (threadIdx.x >> 6); m < r1; m += 4) {
+      const long i = (long)m * N + n;
+      float v = bf2f(dy[i]);
+      if (y) v *= act_grad_from_out(bf2f(y[i]), act);
+      dx[i] = f2bf(v);
+      s += v;
+    }
+  if (!colsum) return;
+  __shared__ float red[4][64];
+  red[threadIdx.x >> 6][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && n < N)
+    atomicAdd(colsum + n, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
 __global__ void add_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ b, bf16_raw* __restrict__ o,
                       long n, int act) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -114,7 +135,7 @@ extern "C" int hopsx_u8_normalize(const unsigned char* x, void* y, long n, float
                      vec);
   return (int)hipGetLastError();
 }
-extern "C" int hopsx_colsum_bf16(const void* x, float* out, int M, int N, hipStream_t st) {
+extern "C" int hopsx_colsum_bf16_scalar(const void* x, float* out, int M, int N, hipStream_t st) {
   const int gx = (N + 63) / 64;
   int gy = (M + 255) / 256;
   const int max_gy = (1024 + gx - 1) / gx;
@@ -127,6 +148,18 @@ extern "C" int hopsx_colsum_bf16(const void* x, float* out, int M, int N, hipStr
 extern "C" int hopsx_act_bwd(const void* dy, const void* y, void* dx, long n, int act, hipStream_t st) {
   hipLaunchKernelGGL(act_bwd_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)y,
                      (bf16_raw*)dx, n, act);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_act_bwd_colsum_scalar(const void* dy, const void* y, void* dx, int M, int N, int act, float* colsum,
+                                    hipStream_t st) {
+  const int gx = (N + 63) / 64;
+  int gy = (M + 255) / 256;
+  const int max_gy = (2048 + gx - 1) / gx;
+  if (gy > max_gy) gy = max_gy;
+  if (gy < 1) gy = 1;
+  const int rpb = (M + gy - 1) / gy;
+  hipLaunchKernelGGL(act_bwd_colsum_k, dim3(gx, gy), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)y,
+                     (bf16_raw*)dx, M, N, act, colsum, rpb);
   return (int)hipGetLastError();
 }
 extern "C" int hopsx_add_bf16(const void* a, const void* b, void* out, long n, int act, hipStream_t st) {

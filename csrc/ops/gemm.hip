@@ -4,6 +4,49 @@
 
 using namespace hopsx;
 
+// Finishing pass of a split-K GEMM whose partial sums were atomically
+// accumulated into the fp32 workspace: bias + activation (or activation
+// derivative) + dtype cast + optional bias-gradient column sum, one thread per
+// output column so the column sum needs a single atomic per column.
+__global__ __launch_bounds__(256) void splitk_finish_k(const float* __restrict__ ws, int M, int N, int epi,
+                                                       void* __restrict__ out, long ldo, const float* __restrict__ bias,
+                                                       float alpha, float beta, int act,
+                                                       const bf16_raw* __restrict__ aux, long ldaux,
+                                                       float* __restrict__ colsum, int rows_per_block) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int m0 = blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  const float b = bias ? bias[n] : 0.f;
+  float cs = 0.f;
+  for (int m = m0; m < m1; ++m) {
+    float v = ws[(long)m * N + n];
+    if (epi == EPI_DACT_BF16) {
+      if (aux) v *= act_grad_from_out(bf2f(aux[(long)m * ldaux + n]), act);
+      ((bf16_raw*)out)[(long)m * ldo + n] = f2bf(v);
+    } else {
+      v = apply_act(v * alpha + b, act);
+      if (epi == EPI_STORE_BF16) {
+        ((bf16_raw*)out)[(long)m * ldo + n] = f2bf(v);
+      } else {
+        float* o = (float*)out + (long)m * ldo + n;
+        if (beta != 0.f) v += beta * *o;
+        *o = v;
+      }
+    }
+    cs += v;
+  }
+  if (colsum) atomicAdd(colsum + n, cs);
+}
+
+// Small-M / long-K GEMMs (e.g. the MNIST Dense(128) over 10816 features at batch
+// 32: 4 output tiles) cannot fill 256 CUs without splitting K.  Non-atomic
+// epilogues then go through an fp32 workspace: memset node + atomic split-K
+// GEMM + finishing pass (all graph-capturable).
+static bool want_splitk(int M, int N, int K) {
+  GemmPlan p = plan_gemm(M, N, K, true);
+  return p.split >= 4;
+}
+
 template <bool AK, bool BK_>
 static int dispatch_epi(const DenseLoader& al, const DenseLoader& bl, int M, int N, int K, int epi, void* out,
                         long ldo, const float* bias, float alpha, float beta, int act, const void* aux, long ldaux,
@@ -37,9 +80,22 @@ static int dispatch_epi(const DenseLoader& al, const DenseLoader& bl, int M, int
 
 extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K,
                           int epi, void* out, long ldo, const float* bias, float alpha, float beta, int act,
-                          const void* aux, long ldaux, float* colsum, hipStream_t st) {
+                          const void* aux, long ldaux, float* colsum, float* ws, long ws_elems, hipStream_t st) {
   DenseLoader al{(const bf16_raw*)A, lda, is_vec_ok(A, lda)};
   DenseLoader bl{(const bf16_raw*)B, ldb, is_vec_ok(B, ldb)};
+  if (ws && epi != EPI_ATOMIC_F32 && (long)M * N <= ws_elems && want_splitk(M, N, K)) {
+    hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), st);
+    int rc = hopsx_gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, EPI_ATOMIC_F32, ws, N, nullptr, 1.f, 0.f, 0, nullptr, 0,
+                        nullptr, nullptr, 0, st);
+    if (rc) return rc;
+    const int gx = (N + 255) / 256;
+    int gy = (M + 63) / 64;
+    if (gy < 1) gy = 1;
+    const int rpb = (M + gy - 1) / gy;
+    hipLaunchKernelGGL(splitk_finish_k, dim3(gx, gy), dim3(256), 0, st, ws, M, N, epi, out, ldo, bias, alpha, beta,
+                       act, (const bf16_raw*)aux, ldaux, colsum, rpb);
+    return (int)hipGetLastError();
+  }
   if (a_kc && b_kc)
     return dispatch_epi<true, true>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st);
   if (a_kc && !b_kc)

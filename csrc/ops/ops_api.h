@@ -11,7 +11,7 @@ extern "C" {
 // ---- GEMM / conv (gemm.hip, conv.hip) ----
 int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K, int epi,
                void* out, long ldo, const float* bias, float alpha, float beta, int act, const void* aux, long ldaux,
-               float* colsum, hipStream_t st);
+               float* colsum, float* ws, long ws_elems, hipStream_t st);
 int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out, const float* bias, int act,
                      float* colsum, hipStream_t st);
 int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act,
@@ -19,11 +19,13 @@ int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx,
 int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias, hipStream_t st);
 
 // ---- pooling (pool.hip) ----
+// optional fused dropout on the pooled output (p > 0, rng/salt as hopsx_dropout_fwd)
 int hopsx_maxpool2d_fwd(const void* x, void* y, unsigned char* argmax, int B, int H, int W, int C, int OH, int OW,
-                        int KH, int KW, int sh, int sw, int ph, int pw, hipStream_t st);
+                        int KH, int KW, int sh, int sw, int ph, int pw, float p, const unsigned long long* rng,
+                        unsigned salt, hipStream_t st);
 int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, const void* x, void* dx, int B, int H, int W,
                         int C, int OH, int OW, int KH, int KW, int sh, int sw, int ph, int pw, int act,
-                        float* colsum, hipStream_t st);
+                        float* colsum, float p, const unsigned long long* rng, unsigned salt, hipStream_t st);
 int hopsx_avgpool_global_fwd(const void* x, void* y, int B, int HW, int C, hipStream_t st);
 int hopsx_avgpool_global_bwd(const void* dy, void* dx, int B, int HW, int C, hipStream_t st);
 
@@ -37,7 +39,8 @@ int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void*
 // ---- optimizers (optim.hip) ----
 // kind: 0 SGD(momentum/nesterov), 1 Adam, 2 AdamW, 3 Adadelta, 4 RMSprop, 5 Adagrad, 6 FTRL
 int hopsx_optim_step(int kind, float* param, float* grad, float* s1, float* s2, float* s3, void* shadow_bf16,
-                     long n, const float* hp, int nhp, float* step_dev, int zero_grad, hipStream_t st);
+                     long n, const float* hp, int nhp, float* step_dev, unsigned* arrive, unsigned long long* rng,
+                     int zero_grad, hipStream_t st);
 
 // ---- dropout / RNG (elementwise.hip) ----
 int hopsx_dropout_fwd(const void* x, void* y, long n, float p, const unsigned long long* rng, unsigned salt,
@@ -52,6 +55,8 @@ int hopsx_cast_bf16_f32(const void* x, float* y, long n, hipStream_t st);
 int hopsx_u8_normalize(const unsigned char* x, void* y, long n, float scale, float shift, hipStream_t st);
 int hopsx_colsum_bf16(const void* x, float* out, int M, int N, hipStream_t st);
 int hopsx_act_bwd(const void* dy, const void* y, void* dx, long n, int act, hipStream_t st);
+int hopsx_act_bwd_colsum(const void* dy, const void* y, void* dx, int M, int N, int act, float* colsum,
+                         hipStream_t st);
 int hopsx_add_bf16(const void* a, const void* b, void* out, long n, int act, hipStream_t st);
 
 // ---- batch norm (norm.hip), NHWC, per-channel over M = B*H*W rows ----

@@ -4,8 +4,11 @@
 // gradient all-reduce of the same flat buffer), which also:
 //   * scales the gradient (1/world_size for a mean all-reduce, loss scaling),
 //   * refreshes the bf16 shadow copy the MFMA kernels read,
-//   * zeroes the gradient in place for the next step's atomic accumulation.
-// The step counter lives on the device so the whole step is hipGraph-capturable.
+//   * zeroes the gradient in place for the next step's atomic accumulation,
+//   * bumps the device step counter and the dropout RNG counter (last-arriving
+//     workgroup), so a captured step needs no extra bookkeeping launches.
+// Streams are moved as float4 (16 B/lane); the grid is capped at 2 workgroups
+// per CU so the single arrival counter sees only ~512 atomics.
 #include "common.h"
 #include "ops_api.h"
 
@@ -13,100 +16,157 @@ struct OptHP {
   float lr, gscale, wd, a, b, c, d, e;
 };
 
-__global__ void step_inc_k(float* step) { step[0] += 1.f; }
+template <int KIND>
+__device__ __forceinline__ float upd(float w, float gr, float& s1, float& s2, float& s3, const OptHP& h, float bc1,
+                                     float bc2) {
+  if (KIND == 0) {  // SGD + momentum (+ nesterov), L2 weight decay
+    gr += h.wd * w;
+    if (h.a != 0.f) {
+      const float buf = h.a * s1 + (1.f - h.b) * gr;
+      s1 = buf;
+      gr = (h.c != 0.f) ? gr + h.a * buf : buf;
+    }
+    w -= h.lr * gr;
+  } else if (KIND == 1 || KIND == 2) {  // Adam / AdamW
+    if (KIND == 1) gr += h.wd * w;
+    else w -= h.lr * h.wd * w;
+    s1 = h.a * s1 + (1.f - h.a) * gr;
+    s2 = h.b * s2 + (1.f - h.b) * gr * gr;
+    w -= h.lr * (s1 / bc1) / (sqrtf(s2 / bc2) + h.c);
+  } else if (KIND == 3) {  // Adadelta
+    gr += h.wd * w;
+    s1 = h.a * s1 + (1.f - h.a) * gr * gr;
+    const float delta = sqrtf(s2 + h.b) / sqrtf(s1 + h.b) * gr;
+    s2 = h.a * s2 + (1.f - h.a) * delta * delta;
+    w -= h.lr * delta;
+  } else if (KIND == 4) {  // RMSprop (optionally centered, momentum)
+    gr += h.wd * w;
+    s1 = h.a * s1 + (1.f - h.a) * gr * gr;
+    float avg;
+    if (h.d != 0.f) {
+      s3 = h.a * s3 + (1.f - h.a) * gr;
+      avg = sqrtf(fmaxf(s1 - s3 * s3, 0.f)) + h.b;
+    } else {
+      avg = sqrtf(s1) + h.b;
+    }
+    if (h.c != 0.f) {
+      s2 = h.c * s2 + gr / avg;
+      w -= h.lr * s2;
+    } else {
+      w -= h.lr * gr / avg;
+    }
+  } else if (KIND == 5) {  // Adagrad
+    gr += h.wd * w;
+    s1 += gr * gr;
+    w -= h.lr * gr / (sqrtf(s1) + h.a);
+  } else if (KIND == 6) {  // FTRL-proximal (lr_power = -0.5), s1 = z, s2 = n
+    const float nn = s2 + gr * gr;
+    const float sigma = (sqrtf(nn) - sqrtf(s2)) / h.lr;
+    s1 += gr - sigma * w;
+    s2 = nn;
+    w = (fabsf(s1) <= h.a) ? 0.f : -(s1 - copysignf(h.a, s1)) / ((h.c + sqrtf(nn)) / h.lr + 2.f * h.b);
+  }
+  return w;
+}
+
+template <int KIND>
+constexpr int nstate() {
+  return KIND == 0 ? 1 : (KIND == 4 ? 3 : (KIND == 5 ? 1 : 2));
+}
 
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __restrict__ g, float* __restrict__ s1,
                                                float* __restrict__ s2, float* __restrict__ s3,
                                                bf16_raw* __restrict__ shadow, long n, OptHP h,
-                                               const float* __restrict__ step_dev, int zero_grad) {
-  const float t = step_dev ? step_dev[0] : 1.f;
+                                               float* __restrict__ step_dev, unsigned* __restrict__ arrive,
+                                               unsigned long long* __restrict__ rng, int zero_grad, int vec) {
+  // step_dev holds the number of COMPLETED steps; this step is t = step + 1.
+  // Every workgroup reads it before its final barrier; the last workgroup to
+  // finish bumps it (and the dropout RNG counter).
+  const float t = (step_dev ? step_dev[0] : 0.f) + 1.f;
   float bc1 = 1.f, bc2 = 1.f;
   if (KIND == 1 || KIND == 2) {
     bc1 = 1.f - __powf(h.a, t);
     bc2 = 1.f - __powf(h.b, t);
   }
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float w = p[i];
-    float gr = g[i] * h.gscale;
-    if (zero_grad) g[i] = 0.f;
-    if (KIND == 0) {  // SGD + momentum (+ nesterov), L2 weight decay
-      gr += h.wd * w;
-      if (h.a != 0.f) {
-        float buf = h.a * s1[i] + (1.f - h.b) * gr;
-        s1[i] = buf;
-        gr = (h.c != 0.f) ? gr + h.a * buf : buf;
-      }
-      w -= h.lr * gr;
-    } else if (KIND == 1 || KIND == 2) {  // Adam / AdamW
-      if (KIND == 1) gr += h.wd * w;
-      else w -= h.lr * h.wd * w;
-      const float m = h.a * s1[i] + (1.f - h.a) * gr;
-      const float v = h.b * s2[i] + (1.f - h.b) * gr * gr;
-      s1[i] = m;
-      s2[i] = v;
-      w -= h.lr * (m / bc1) / (sqrtf(v / bc2) + h.c);
-    } else if (KIND == 3) {  // Adadelta
-      gr += h.wd * w;
-      const float ag = h.a * s1[i] + (1.f - h.a) * gr * gr;
-      const float delta = sqrtf(s2[i] + h.b) / sqrtf(ag + h.b) * gr;
-      s1[i] = ag;
-      s2[i] = h.a * s2[i] + (1.f - h.a) * delta * delta;
-      w -= h.lr * delta;
-    } else if (KIND == 4) {  // RMSprop (optionally centered, momentum)
-      gr += h.wd * w;
-      const float v = h.a * s1[i] + (1.f - h.a) * gr * gr;
-      s1[i] = v;
-      float avg;
-      if (h.d != 0.f) {
-        const float ga = h.a * s3[i] + (1.f - h.a) * gr;
-        s3[i] = ga;
-        avg = sqrtf(fmaxf(v - ga * ga, 0.f)) + h.b;
-      } else {
-        avg = sqrtf(v) + h.b;
-      }
-      if (h.c != 0.f) {
-        const float buf = h.c * s2[i] + gr / avg;
-        s2[i] = buf;
-        w -= h.lr * buf;
-      } else {
-        w -= h.lr * gr / avg;
-      }
-    } else if (KIND == 5) {  // Adagrad
-      gr += h.wd * w;
-      const float s = s1[i] + gr * gr;
-      s1[i] = s;
-      w -= h.lr * gr / (sqrtf(s) + h.a);
-    } else if (KIND == 6) {  // FTRL-proximal (lr_power = -0.5), s1 = z, s2 = n
-      const float nn = s2[i] + gr * gr;
-      const float sigma = (sqrtf(nn) - sqrtf(s2[i])) / h.lr;
-      const float z = s1[i] + gr - sigma * w;
-      s1[i] = z;
-      s2[i] = nn;
-      w = (fabsf(z) <= h.a) ? 0.f : -(z - copysignf(h.a, z)) / ((h.c + sqrtf(nn)) / h.lr + 2.f * h.b);
+  constexpr int NS = nstate<KIND>();
+  const long n4 = vec ? (n >> 2) : 0;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 w = ((float4*)p)[i];
+    float4 gr = ((float4*)g)[i];
+    if (zero_grad) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 a = NS >= 1 ? ((float4*)s1)[i] : make_float4(0, 0, 0, 0);
+    float4 b = NS >= 2 ? ((float4*)s2)[i] : make_float4(0, 0, 0, 0);
+    float4 c = NS >= 3 ? ((float4*)s3)[i] : make_float4(0, 0, 0, 0);
+    w.x = upd<KIND>(w.x, gr.x * h.gscale, a.x, b.x, c.x, h, bc1, bc2);
+    w.y = upd<KIND>(w.y, gr.y * h.gscale, a.y, b.y, c.y, h, bc1, bc2);
+    w.z = upd<KIND>(w.z, gr.z * h.gscale, a.z, b.z, c.z, h, bc1, bc2);
+    w.w = upd<KIND>(w.w, gr.w * h.gscale, a.w, b.w, c.w, h, bc1, bc2);
+    ((float4*)p)[i] = w;
+    if (NS >= 1) ((float4*)s1)[i] = a;
+    if (NS >= 2) ((float4*)s2)[i] = b;
+    if (NS >= 3) ((float4*)s3)[i] = c;
+    if (shadow) {
+      const uint32_t lo = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
+      const uint32_t hi = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
+      ((uint2*)shadow)[i] = make_uint2(lo, hi);
     }
+  }
+  for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float a = NS >= 1 ? s1[i] : 0.f, b = NS >= 2 ? s2[i] : 0.f, c = NS >= 3 ? s3[i] : 0.f;
+    const float gr = g[i] * h.gscale;
+    if (zero_grad) g[i] = 0.f;
+    const float w = upd<KIND>(p[i], gr, a, b, c, h, bc1, bc2);
     p[i] = w;
+    if (NS >= 1) s1[i] = a;
+    if (NS >= 2) s2[i] = b;
+    if (NS >= 3) s3[i] = c;
     if (shadow) shadow[i] = f2bf(w);
+  }
+  if (arrive) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = atomicAdd(arrive, 1u);
+      if (prev == gridDim.x - 1) {
+        if (step_dev) step_dev[0] = t;
+        if (rng) rng[1] += 1ull;
+        atomicExch(arrive, 0u);
+      }
+    }
   }
 }
 
+__global__ void bump_k(float* step_dev, unsigned long long* rng) {
+  if (step_dev) step_dev[0] += 1.f;
+  if (rng) rng[1] += 1ull;
+}
+
 extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, float* s2, float* s3,
-                                void* shadow_bf16, long n, const float* hp, int nhp, float* step_dev, int zero_grad,
-                                hipStream_t st) {
+                                void* shadow_bf16, long n, const float* hp, int nhp, float* step_dev,
+                                unsigned* arrive, unsigned long long* rng, int zero_grad, hipStream_t st) {
   OptHP h{0, 1, 0, 0, 0, 0, 0, 0};
   float* hv = &h.lr;
   for (int i = 0; i < nhp && i < 8; ++i) hv[i] = hp[i];
-  if (step_dev) hipLaunchKernelGGL(step_inc_k, dim3(1), dim3(1), 0, st, step_dev);
-  long g = (n + 255) / 256;
-  if (g > 4096) g = 4096;
+  // 16-B vector path needs 16-B aligned streams
+  const bool aligned = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)s3) % 16 == 0 &&
+                       ((uintptr_t)shadow_bf16 % 8 == 0);
+  long g = ((aligned ? n / 4 : n) + 255) / 256;
+  if (g > 512) g = 512;
   if (g < 1) g = 1;
   bf16_raw* sh = (bf16_raw*)shadow_bf16;
-#define OPT_CASE(K) \
-  case K: hipLaunchKernelGGL(optim_k<K>, dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, zero_grad); break;
+  // without an arrival counter the bookkeeping needs its own tiny launch
+  unsigned* arr = (step_dev || rng) ? arrive : nullptr;
+#define OPT_CASE(K)                                                                                                   \
+  case K:                                                                                                             \
+    hipLaunchKernelGGL(optim_k<K>, dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, arr, rng, \
+                       zero_grad, (int)aligned);                                                                      \
+    break;
   switch (kind) {
     OPT_CASE(0) OPT_CASE(1) OPT_CASE(2) OPT_CASE(3) OPT_CASE(4) OPT_CASE(5) OPT_CASE(6)
     default: return -2;
   }
 #undef OPT_CASE
+  if ((step_dev || rng) && !arrive) hipLaunchKernelGGL(bump_k, dim3(1), dim3(1), 0, st, step_dev, rng);
   return (int)hipGetLastError();
 }

@@ -15,8 +15,11 @@ static inline int grid_for(long n, int block = 256) {
 __global__ __launch_bounds__(256) void maxpool_fwd_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y,
                                                      unsigned char* __restrict__ am, int B, int H, int W, int C,
                                                      int OH, int OW, int KH, int KW, int sh, int sw, int ph,
-                                                     int pw) {
+                                                     int pw, float p, const unsigned long long* __restrict__ rng,
+                                                     unsigned salt) {
   const long total = (long)B * OH * OW * C;
+  const uint64_t key = p > 0.f ? drop_key(rng, salt) : 0;
+  const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = i % C;
     long t = i / C;
@@ -36,6 +39,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const bf16_raw* __restrict_
         if (v > best) { best = v; bi = kh * KW + kw; }
       }
     }
+    if (p > 0.f) best = uniform01(key, i) >= p ? best * dscale : 0.f;
     y[i] = f2bf(best);
     if (am) am[i] = (unsigned char)bi;
   }
@@ -45,8 +49,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const bf16_raw* __restrict_
 __global__ __launch_bounds__(256) void maxpool_bwd_k(const bf16_raw* __restrict__ dy, const unsigned char* __restrict__ am,
                                                      const bf16_raw* __restrict__ x, bf16_raw* __restrict__ dx, int B,
                                                      int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
-                                                     int sw, int ph, int pw, int act, float* __restrict__ colsum) {
-  extern __shared__ float scs[];  // per-block channel partial sums (C floats)
+                                                     int sw, int ph, int pw, int act, float* __restrict__ colsum,
+                                                     float p, const unsigned long long* __restrict__ rng,
+                                                     unsigned salt) {
+  extern __shared__ float scs[];
+  const uint64_t key = p > 0.f ? drop_key(rng, salt) : 0;
+  const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;  // per-block channel partial sums (C floats)
   const long total = (long)B * H * W * C;
   if (colsum) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) scs[c] = 0.f;
@@ -70,7 +78,11 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k(const bf16_raw* __restrict_
         const int kw = iw - (ow * sw - pw);
         if (kw < 0 || kw >= KW) continue;
         const long o = (((long)b * OH + oh) * OW + ow) * C + c;
-        if (am[o] == kh * KW + kw) g += bf2f(dy[o]);
+        if (am[o] == kh * KW + kw) {
+          float d = bf2f(dy[o]);
+          if (p > 0.f) d = uniform01(key, o) >= p ? d * dscale : 0.f;
+          g += d;
+        }
       }
     }
     if (act != ACT_NONE && x) g *= act_grad_from_out(bf2f(x[i]), act);
@@ -102,21 +114,166 @@ __global__ void gap_bwd_k(const bf16_raw* __restrict__ dy, bf16_raw* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fast path: non-overlapping windows (stride == kernel, no padding — every
+// reference CNN), C % 8 == 0.  One thread per (output pixel, 8 channels): 16-B
+// loads/stores, argmax packed as 8 bytes.  The backward writes each window
+// exactly once (value at the argmax, zero elsewhere, plus the floor-mode
+// remainder rows/cols), so it needs no gather and no zero-fill pass; bias-grad
+// partials stay in registers (channel group is fixed per thread because the
+// grid stride is a multiple of C/8) and hit LDS/global atomics once per thread.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void maxpool_fwd8_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y,
+                                                      unsigned char* __restrict__ am, int B, int H, int W, int C,
+                                                      int OH, int OW, int KH, int KW, float p,
+                                                      const unsigned long long* __restrict__ rng, unsigned salt) {
+  const int G = C >> 3;
+  const long total = (long)B * OH * OW * G;
+  const uint64_t key = p > 0.f ? drop_key(rng, salt) : 0;
+  const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = t % G;
+    const long pix = t / G;
+    const int ow = pix % OW;
+    const long r = pix / OW;
+    const int oh = r % OH;
+    const int b = r / OH;
+    float best[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int kh = 0; kh < KH; ++kh)
+      for (int kw = 0; kw < KW; ++kw) {
+        const bf16x8 v = *(const bf16x8*)(x + (((long)b * H + oh * KH + kh) * W + ow * KW + kw) * C + cg * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f((uint16_t)v[j]);
+          if (f > best[j]) { best[j] = f; bi[j] = (unsigned char)(kh * KW + kw); }
+        }
+      }
+    const long o = pix * C + cg * 8;
+    bf16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = best[j];
+      if (p > 0.f) f = uniform01(key, o + j) >= p ? f * dscale : 0.f;
+      out[j] = (short)f2bf(f);
+    }
+    *(bf16x8*)(y + o) = out;
+    if (am) {
+      uint2 packed;
+      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((unsigned)bi[7] << 24);
+      *(uint2*)(am + o) = packed;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd8_k(const bf16_raw* __restrict__ dy, const unsigned char* __restrict__ am,
+                                                      const bf16_raw* __restrict__ x, bf16_raw* __restrict__ dx, int B,
+                                                      int H, int W, int C, int OH, int OW, int KH, int KW, int act,
+                                                      float* __restrict__ colsum, float p,
+                                                      const unsigned long long* __restrict__ rng, unsigned salt) {
+  extern __shared__ float scs[];
+  const int G = C >> 3;
+  const long total = (long)B * OH * OW * G;
+  const uint64_t key = p > 0.f ? drop_key(rng, salt) : 0;
+  const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (colsum) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) scs[c] = 0.f;
+    __syncthreads();
+  }
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int my_cg = -1;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = t % G;
+    my_cg = cg;
+    const long pix = t / G;
+    const int ow = pix % OW;
+    const long r = pix / OW;
+    const int oh = r % OH;
+    const int b = r / OH;
+    const long o = pix * C + cg * 8;
+    const bf16x8 dv = *(const bf16x8*)(dy + o);
+    const uint2 pk = *(const uint2*)(am + o);
+    float d[8];
+    int a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = bf2f((uint16_t)dv[j]);
+      if (p > 0.f) f = uniform01(key, o + j) >= p ? f * dscale : 0.f;
+      d[j] = f;
+      a[j] = ((j < 4 ? pk.x : pk.y) >> (8 * (j & 3))) & 0xff;
+    }
+    const int h1 = (oh == OH - 1) ? H : oh * KH + KH;
+    const int w1 = (ow == OW - 1) ? W : ow * KW + KW;
+    for (int ih = oh * KH; ih < h1; ++ih)
+      for (int iw = ow * KW; iw < w1; ++iw) {
+        const int kh = ih - oh * KH, kw = iw - ow * KW;
+        const bool inwin = kh < KH && kw < KW;
+        const int pos = kh * KW + kw;
+        const long xi = (((long)b * H + ih) * W + iw) * C + cg * 8;
+        bf16x8 xv = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (inwin && act != ACT_NONE && x) xv = *(const bf16x8*)(x + xi);
+        bf16x8 outv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float g = (inwin && a[j] == pos) ? d[j] : 0.f;
+          if (act != ACT_NONE && x && g != 0.f) g *= act_grad_from_out(bf2f((uint16_t)xv[j]), act);
+          outv[j] = (short)f2bf(g);
+          cs[j] += g;
+        }
+        *(bf16x8*)(dx + xi) = outv;
+      }
+  }
+  if (colsum) {
+    if (my_cg >= 0)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (cs[j] != 0.f) atomicAdd(&scs[my_cg * 8 + j], cs[j]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x)
+      if (scs[c] != 0.f) atomicAdd(colsum + c, scs[c]);
+  }
+}
+
+static bool pool_fast(int C, int KH, int KW, int sh, int sw, int ph, int pw, const void* a, const void* b,
+                      const void* c, const void* d) {
+  return C % 8 == 0 && (256 % (C / 8) == 0) && sh == KH && sw == KW && ph == 0 && pw == 0 && KH * KW <= 255 &&
+         (((uintptr_t)a | (uintptr_t)b | (uintptr_t)d) % 16 == 0) && ((uintptr_t)c % 8 == 0);
+}
+
 extern "C" int hopsx_maxpool2d_fwd(const void* x, void* y, unsigned char* argmax, int B, int H, int W, int C, int OH,
-                                   int OW, int KH, int KW, int sh, int sw, int ph, int pw, hipStream_t st) {
+                                   int OW, int KH, int KW, int sh, int sw, int ph, int pw, float p,
+                                   const unsigned long long* rng, unsigned salt, hipStream_t st) {
+  if (argmax && pool_fast(C, KH, KW, sh, sw, ph, pw, x, y, argmax, nullptr)) {
+    const long n8 = (long)B * OH * OW * (C / 8);
+    hipLaunchKernelGGL(maxpool_fwd8_k, dim3(grid_for(n8)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, argmax,
+                       B, H, W, C, OH, OW, KH, KW, p, rng, salt);
+    return (int)hipGetLastError();
+  }
   const long n = (long)B * OH * OW * C;
   hipLaunchKernelGGL(maxpool_fwd_k, dim3(grid_for(n)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, argmax, B,
-                     H, W, C, OH, OW, KH, KW, sh, sw, ph, pw);
+                     H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, p, rng, salt);
   return (int)hipGetLastError();
 }
 
 extern "C" int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, const void* x, void* dx, int B, int H,
                                    int W, int C, int OH, int OW, int KH, int KW, int sh, int sw, int ph, int pw,
-                                   int act, float* colsum, hipStream_t st) {
-  const long n = (long)B * H * W * C;
+                                   int act, float* colsum, float p, const unsigned long long* rng, unsigned salt,
+                                   hipStream_t st) {
   const size_t shm = colsum ? (size_t)C * sizeof(float) : 0;
+  if (pool_fast(C, KH, KW, sh, sw, ph, pw, dy, dx, argmax, x)) {
+    const long n8 = (long)B * OH * OW * (C / 8);
+    int g = grid_for(n8);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(maxpool_bwd8_k, dim3(g), dim3(256), shm, st, (const bf16_raw*)dy, argmax, (const bf16_raw*)x,
+                       (bf16_raw*)dx, B, H, W, C, OH, OW, KH, KW, act, colsum, p, rng, salt);
+    return (int)hipGetLastError();
+  }
+  const long n = (long)B * H * W * C;
   hipLaunchKernelGGL(maxpool_bwd_k, dim3(grid_for(n, 256) > 1024 ? 1024 : grid_for(n, 256)), dim3(256), shm, st, (const bf16_raw*)dy, argmax,
-                     (const bf16_raw*)x, (bf16_raw*)dx, B, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, act, colsum);
+                     (const bf16_raw*)x, (bf16_raw*)dx, B, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, act, colsum, p, rng, salt);
   return (int)hipGetLastError();
 }
 

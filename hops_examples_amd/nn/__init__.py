@@ -1,0 +1,184 @@
+"""Keras-flavoured layer set on top of the gfx950 kernels (NHWC images).
+
+Layers mirror what the reference notebooks build with ``tf.keras.layers``
+(Conv2D / MaxPooling2D / Dropout / Flatten / Dense with fused activations,
+e.g. notebooks/ml/Experiment/Tensorflow/mnist.ipynb:154-164) and with
+``torch.nn`` (notebooks/ml/Experiment/PyTorch/mnist.ipynb:118-134), but run on
+hand-written MFMA kernels: the activation is fused into the producing GEMM's
+epilogue and the weights are read from the ParamArena's bf16 shadow.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from ..ops import functional as HF
+
+__all__ = [
+    "Linear", "Dense", "Conv2d", "Conv2D", "MaxPool2d", "MaxPooling2D", "Dropout", "Flatten", "BatchNorm2d",
+    "GlobalAvgPool2d", "EmbeddingBag", "Activation", "Sequential", "functional",
+]
+
+functional = HF
+Sequential = nn.Sequential
+
+
+def _glorot(shape, fan_in, fan_out):
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return torch.empty(shape).uniform_(-lim, lim)
+
+
+class Linear(nn.Module):
+    """y = act(x W^T + b); W: [out, in]. ``activation`` in {None, 'relu', 'sigmoid', 'tanh'}."""
+
+    def __init__(self, in_features, out_features, bias=True, activation=None, init="glorot", out_f32=False):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.activation = activation
+        self.out_f32 = out_f32
+        if init == "glorot":
+            w = _glorot((out_features, in_features), in_features, out_features)
+        else:  # torch default (kaiming-uniform a=sqrt(5))
+            w = torch.empty(out_features, in_features)
+            nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        self.weight = nn.Parameter(w)
+        if bias:
+            if init == "glorot":
+                b = torch.zeros(out_features)
+            else:
+                bound = 1 / math.sqrt(in_features)
+                b = torch.empty(out_features).uniform_(-bound, bound)
+            self.bias = nn.Parameter(b)
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        return HF.linear(x, self.weight, self.bias, self.activation, self.out_f32)
+
+    def extra_repr(self):
+        return f"{self.in_features}, {self.out_features}, act={self.activation}"
+
+
+Dense = Linear
+
+
+class Conv2d(nn.Module):
+    """NHWC conv; weight [out, kh, kw, in]. padding: int | 'valid' | 'same'."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, bias=True,
+                 activation=None, init="glorot"):
+        super().__init__()
+        kh, kw = (kernel_size, kernel_size) if isinstance(kernel_size, int) else kernel_size
+        self.cfg = dict(stride=stride, padding=padding, dilation=dilation)
+        self.activation = activation
+        self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, (kh, kw)
+        fan_in, fan_out = in_channels * kh * kw, out_channels * kh * kw
+        if init == "glorot":
+            w = _glorot((out_channels, kh, kw, in_channels), fan_in, fan_out)
+        elif init == "he":
+            w = torch.randn(out_channels, kh, kw, in_channels) * math.sqrt(2.0 / fan_in)
+        else:
+            bound = 1 / math.sqrt(fan_in)
+            w = torch.empty(out_channels, kh, kw, in_channels).uniform_(-bound, bound)
+        self.weight = nn.Parameter(w)
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(out_channels) if init != "torch" else
+                                     torch.empty(out_channels).uniform_(-1 / math.sqrt(fan_in), 1 / math.sqrt(fan_in)))
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        return HF.conv2d(x, self.weight, self.bias, act=self.activation, **self.cfg)
+
+    def extra_repr(self):
+        return f"{self.in_channels}, {self.out_channels}, k={self.kernel_size}, {self.cfg}, act={self.activation}"
+
+
+Conv2D = Conv2d
+
+
+class MaxPool2d(nn.Module):
+    """NHWC max-pool; ``dropout`` > 0 fuses the Dropout that follows it in the
+    reference models into the same kernel (mask regenerated in backward)."""
+
+    def __init__(self, kernel_size, stride=None, padding=0, dropout=0.0):
+        super().__init__()
+        self.k, self.s, self.p = kernel_size, stride, padding
+        self.dropout = float(dropout)
+        _salt_counter[0] += 1
+        self.salt = _salt_counter[0] * 7919
+
+    def forward(self, x):
+        return HF.max_pool2d(x, self.k, self.s, self.p, self.dropout, self.training, self.salt)
+
+
+MaxPooling2D = MaxPool2d
+
+
+class GlobalAvgPool2d(nn.Module):
+    def forward(self, x):
+        return HF.global_avg_pool(x)
+
+
+_salt_counter = [0]
+
+
+class Dropout(nn.Module):
+    """Counter-RNG dropout; the mask is regenerated (not stored) in backward."""
+
+    def __init__(self, p=0.5):
+        super().__init__()
+        self.p = float(p)
+        _salt_counter[0] += 1
+        self.salt = _salt_counter[0] * 7919
+
+    def forward(self, x):
+        return HF.dropout(x, self.p, self.training, self.salt)
+
+
+class Flatten(nn.Module):
+    def forward(self, x):
+        return x.reshape(x.shape[0], -1)
+
+
+class Activation(nn.Module):
+    def __init__(self, act):
+        super().__init__()
+        self.act = act
+
+    def forward(self, x):
+        if self.act in (None, "linear"):
+            return x
+        if x.is_cuda:
+            x = HF.to_compute(x)
+            return {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}[self.act](x)
+        return HF._cpu_act(x, self.act)
+
+
+class BatchNorm2d(nn.Module):
+    """NHWC batch norm; ``forward(x, residual=None)`` computes act(bn(x) + residual)."""
+
+    def __init__(self, num_features, momentum=0.1, eps=1e-5, activation=None, zero_init=False):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(num_features) if zero_init else torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.momentum, self.eps, self.activation = momentum, eps, activation
+
+    def forward(self, x, residual=None):
+        return HF.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
+                             self.momentum, self.eps, residual, self.activation)
+
+
+class EmbeddingBag(nn.Module):
+    def __init__(self, num_embeddings, embedding_dim, mode="sum", init_std=None):
+        super().__init__()
+        std = init_std if init_std is not None else 1.0 / math.sqrt(embedding_dim)
+        self.weight = nn.Parameter(torch.randn(num_embeddings, embedding_dim) * std)
+        self.mode = mode
+
+    def forward(self, idx, offsets=None):
+        return HF.embedding_bag(idx, self.weight, offsets, self.mode)

@@ -76,17 +76,17 @@ class _LinearFn(torch.autograd.Function):
         if dy2.dtype != BF16:
             dy2 = dy2.to(BF16)
         dy2 = dy2.contiguous()
-        if ACT.get(act, act) not in (0, None) and y.dtype == BF16:
-            dy2 = K.act_bwd(dy2, y, act)
+        gb = _wgrad_buf(b) if b is not None else None
+        if act and y.dtype == BF16:
+            # activation backward + bias gradient in one pass
+            dy2 = K.act_bwd_colsum(dy2, y, act, gb)
+        elif gb is not None:
+            K.colsum(dy2, gb)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.linear_dgrad(dy2, _arena.weight_bf16(w)).view(ctx.xshape)
         gw = _wgrad_buf(w)
         K.linear_wgrad(dy2, x2, gw)
-        gb = None
-        if b is not None:
-            gb = _wgrad_buf(b)
-            K.colsum(dy2, gb)
         return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None
 
 
@@ -119,17 +119,16 @@ class _Conv2dFn(torch.autograd.Function):
         x, y = ctx.saved_tensors
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
+        gb = _wgrad_buf(b) if b is not None else None
         if act:
-            dy = K.act_bwd(dy, y, act)
+            dy = K.act_bwd_colsum(dy, y, act, gb)
+        elif gb is not None:
+            K.colsum(dy.view(-1, dy.shape[-1]), gb)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g)
         gw = _wgrad_buf(w)
         K.conv2d_wgrad(dy, x, g, gw)
-        gb = None
-        if b is not None:
-            gb = _wgrad_buf(b)
-            K.colsum(dy.view(-1, dy.shape[-1]), gb)
         return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None
 
 
@@ -163,28 +162,32 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None):
 # ==================================================================== pooling
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p):
+    def forward(ctx, x, k, s, p, drop_p, salt):
         x = x.contiguous()
-        y, am = K.maxpool2d_fwd(x, k, s, p)
+        rng = rng_state(x.device) if drop_p > 0 else None
+        y, am = K.maxpool2d_fwd(x, k, s, p, drop_p=drop_p, rng=rng, salt=salt)
         ctx.save_for_backward(am)
-        ctx.cfg = (x.shape, k, s, p)
+        ctx.cfg = (x.shape, k, s, p, drop_p, rng, salt)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (am,) = ctx.saved_tensors
-        shape, k, s, p = ctx.cfg
+        shape, k, s, p, drop_p, rng, salt = ctx.cfg
         dy = dy.to(BF16).contiguous()
-        return K.maxpool2d_bwd(dy, am, shape, k, s, p), None, None, None
+        return K.maxpool2d_bwd(dy, am, shape, k, s, p, drop_p=drop_p, rng=rng, salt=salt), None, None, None, None, None
 
 
-def max_pool2d(x, kernel, stride=None, padding=0):
+def max_pool2d(x, kernel, stride=None, padding=0, dropout_p: float = 0.0, training: bool = True, salt: int = 0):
+    """NHWC max-pool; ``dropout_p`` > 0 fuses a following Dropout into the same kernel (fwd and bwd)."""
     k = (kernel, kernel) if isinstance(kernel, int) else tuple(kernel)
     s = k if stride is None else ((stride, stride) if isinstance(stride, int) else tuple(stride))
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    dp = float(dropout_p) if training else 0.0
     if not x.is_cuda:
-        return F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous()
-    return _MaxPoolFn.apply(to_compute(x), k, s, p)
+        y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous()
+        return F.dropout(y, dp, True) if dp > 0 else y
+    return _MaxPoolFn.apply(to_compute(x), k, s, p, dp, salt)
 
 
 class _GapFn(torch.autograd.Function):
@@ -333,8 +336,8 @@ class _LossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, kind, stats):
         B, C = logits.shape
-        loss_sum = torch.zeros(1, device=logits.device)
-        correct = torch.zeros(1, device=logits.device, dtype=torch.int32)
+        loss_sum = torch.empty(1, device=logits.device)  # the kernel overwrites / zero-fills itself
+        correct = torch.empty(1, device=logits.device, dtype=torch.int32)
         dl = torch.empty(B, C, device=logits.device, dtype=torch.float32)
         K.loss_fwd_bwd(kind, logits.contiguous(), target.contiguous(), 1.0 / (B * (C if kind in (2, 3, 4) else 1)),
                        loss_sum, correct, dl)
@@ -343,7 +346,7 @@ class _LossFn(torch.autograd.Function):
             stats["count"] = B * (C if kind in (2, 4) else 1)
         ctx.save_for_backward(dl)
         ctx.dtype = logits.dtype
-        return (loss_sum / (B * (C if kind in (2, 3, 4) else 1))).squeeze(0)
+        return loss_sum.squeeze(0)
 
     @staticmethod
     def backward(ctx, g):
@@ -377,6 +380,32 @@ def _cpu_loss(kind, logits, target, stats):
         stats["correct"] = corr
         stats["count"] = cnt
     return loss
+
+
+def loss_and_grad(logits, target, kind: str = "sparse_ce"):
+    """Non-autograd fused loss for training loops that seed backward themselves:
+    returns (mean loss [1], correct [1] int32, count, dlogits in the logits' dtype).
+    ``logits.backward(dlogits)`` then runs the model backward with no extra
+    elementwise kernels (the 1/count mean scaling is folded into the loss kernel)."""
+    k = LOSS[kind]
+    if logits.dim() == 1:
+        logits = logits.unsqueeze(1)
+    B, C = logits.shape
+    cnt = B * (C if k in (2, 3, 4) else 1)
+    if k in (2, 3, 4) and target.dim() == 1:
+        target = target.unsqueeze(1)
+    if not logits.is_cuda:
+        lg = logits.detach().float().requires_grad_(True)
+        st: dict = {}
+        l = _cpu_loss(k, lg, target, st)
+        (g,) = torch.autograd.grad(l, (lg,))
+        return l.detach().view(1), torch.as_tensor(st["correct"]).view(1), st["count"], g.to(logits.dtype)
+    target = target.long() if k == 0 else target.float()
+    loss_sum = torch.empty(1, device=logits.device)
+    correct = torch.empty(1, device=logits.device, dtype=torch.int32)
+    dl = torch.empty(B, C, device=logits.device, dtype=logits.dtype)
+    K.loss_fwd_bwd(k, logits.detach().contiguous(), target.contiguous(), 1.0 / cnt, loss_sum, correct, dl)
+    return loss_sum, correct, (B if k in (0, 1) else cnt), dl
 
 
 def loss(logits, target, kind: str = "sparse_ce", stats: dict | None = None):

@@ -31,10 +31,19 @@ def act_id(act) -> int:
 
 # ---------------------------------------------------------------- dense GEMM
 def gemm_raw(a, lda, a_kc, b, ldb, b_kc, M, N, K, epi, out, ldo, bias=None, alpha=1.0, beta=0.0, act=0, aux=None,
-             ldaux=0, colsum=None):
+             ldaux=0, colsum=None, ws=None):
+    """ws: optional fp32 workspace (>= M*N) enabling split-K for small-M/long-K store epilogues."""
     rc = _C.ext().gemm(ptr(a), lda, int(a_kc), ptr(b), ldb, int(b_kc), M, N, K, epi, ptr(out), ldo, ptr(bias),
-                       float(alpha), float(beta), act_id(act), ptr(aux), ldaux, ptr(colsum), stream())
+                       float(alpha), float(beta), act_id(act), ptr(aux), ldaux, ptr(colsum), ptr(ws),
+                       0 if ws is None else ws.numel(), stream())
     check(rc, "gemm")
+
+
+def _splitk_ws(M, N, K, device):
+    # split-K pays when the output has few tiles but the reduction is long
+    if M * N <= (1 << 22) and K >= 1024 and (M <= 128 or N <= 128):
+        return torch.empty(M * N, device=device, dtype=F32)
+    return None
 
 
 def linear_fwd(x, w, bias=None, act=0, out=None, out_f32=False, colsum=None):
@@ -47,7 +56,8 @@ def linear_fwd(x, w, bias=None, act=0, out=None, out_f32=False, colsum=None):
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=F32 if out_f32 else BF16)
     epi = EPI_STORE_F32 if out.dtype == F32 else EPI_STORE_BF16
-    gemm_raw(x, K, True, w, K, True, M, N, K, epi, out, N, bias=bias, act=act, colsum=colsum)
+    gemm_raw(x, K, True, w, K, True, M, N, K, epi, out, N, bias=bias, act=act, colsum=colsum,
+             ws=_splitk_ws(M, N, K, x.device))
     return out
 
 
@@ -60,7 +70,7 @@ def linear_dgrad(dy, w, yprev=None, act_prev=0, out=None, colsum=None):
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=BF16)
     gemm_raw(dy, N, True, w, K, False, M, K, N, EPI_DACT_BF16, out, K, act=act_prev if yprev is not None else 0,
-             aux=yprev, ldaux=K, colsum=colsum)
+             aux=yprev, ldaux=K, colsum=colsum, ws=_splitk_ws(M, K, N, dy.device))
     return out
 
 
@@ -131,7 +141,8 @@ def pool_out(H, W, k, s, p):
     return (H + 2 * p[0] - k[0]) // s[0] + 1, (W + 2 * p[1] - k[1]) // s[1] + 1
 
 
-def maxpool2d_fwd(x, k, s, p, out=None, argmax=None):
+def maxpool2d_fwd(x, k, s, p, out=None, argmax=None, drop_p=0.0, rng=None, salt=0):
+    """Max-pool (NHWC) with an optional fused dropout on the pooled output."""
     B, H, W, C = x.shape
     OH, OW = pool_out(H, W, k, s, p)
     if out is None:
@@ -139,17 +150,20 @@ def maxpool2d_fwd(x, k, s, p, out=None, argmax=None):
     if argmax is None:
         argmax = torch.empty(B, OH, OW, C, device=x.device, dtype=torch.uint8)
     check(_C.ext().maxpool2d_fwd(ptr(x), ptr(out), ptr(argmax), B, H, W, C, OH, OW, k[0], k[1], s[0], s[1], p[0],
-                                 p[1], stream()), "maxpool_fwd")
+                                 p[1], float(drop_p), ptr(rng), int(salt) & 0xFFFFFFFF, stream()), "maxpool_fwd")
     return out, argmax
 
 
-def maxpool2d_bwd(dy, argmax, x_shape, k, s, p, x=None, act=0, out=None, colsum=None):
+def maxpool2d_bwd(dy, argmax, x_shape, k, s, p, x=None, act=0, out=None, colsum=None, drop_p=0.0, rng=None, salt=0):
+    """Gather backward of max-pool; optionally re-applies the fused dropout mask, multiplies by
+    act'(x) (x = pool input = previous activation output) and emits that layer's bias gradient."""
     B, H, W, C = x_shape
     OH, OW = dy.shape[1], dy.shape[2]
     if out is None:
         out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
     check(_C.ext().maxpool2d_bwd(ptr(dy), ptr(argmax), ptr(x), ptr(out), B, H, W, C, OH, OW, k[0], k[1], s[0], s[1],
-                                 p[0], p[1], act_id(act), ptr(colsum), stream()), "maxpool_bwd")
+                                 p[0], p[1], act_id(act), ptr(colsum), float(drop_p), ptr(rng),
+                                 int(salt) & 0xFFFFFFFF, stream()), "maxpool_bwd")
     return out
 
 
@@ -179,10 +193,16 @@ def loss_fwd_bwd(kind: int, logits, target, grad_scale, loss_sum, correct, dlogi
 
 
 # --------------------------------------------------------------- optimizers
-def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True):
+def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True, arrive=None, rng=None):
+    """One fused update over flat buffers.  ``step_dev`` (f32[1]) counts completed steps and,
+    with ``arrive`` (int32[1], zero-initialised), is bumped in-kernel by the last workgroup,
+    together with the dropout RNG counter ``rng[1]`` when given."""
     n = param.numel()
+    if step_dev is not None and arrive is None:
+        arrive = torch.zeros(1, device=param.device, dtype=torch.int32)
     check(_C.ext().optim_step(kind, ptr(param), ptr(grad), ptr(s1), ptr(s2), ptr(s3), ptr(shadow), n,
-                              [float(v) for v in hp], ptr(step_dev), int(zero_grad), stream()), "optim")
+                              [float(v) for v in hp], ptr(step_dev), ptr(arrive), ptr(rng), int(zero_grad), stream()),
+          "optim")
 
 
 # ------------------------------------------------------------- misc / RNG
@@ -216,6 +236,17 @@ def act_bwd(dy, y, act, out=None):
     if out is None:
         out = torch.empty_like(dy)
     check(_C.ext().act_bwd(ptr(dy), ptr(y), ptr(out), dy.numel(), act_id(act), stream()), "act_bwd")
+    return out
+
+
+def act_bwd_colsum(dy, y, act, colsum, out=None):
+    """dx = dy * act'(y) (y may be None = identity) and colsum += sum over rows of dx."""
+    if out is None:
+        out = torch.empty_like(dy)
+    N = dy.shape[-1]
+    M = dy.numel() // N
+    check(_C.ext().act_bwd_colsum(ptr(dy), ptr(y), ptr(out), M, N, act_id(act), ptr(colsum), stream()),
+          "act_bwd_colsum")
     return out
 
 

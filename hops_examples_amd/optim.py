@@ -1,0 +1,240 @@
+"""Fused optimizers over a ParamArena: ONE kernel launch per step for the
+whole model (update + bf16 shadow refresh + gradient zeroing), with the step
+counter on the device so the step can be captured into a hipGraph.
+
+Defaults follow the frameworks the reference notebooks use:
+Keras ``Adadelta(1.0)`` (rho 0.95, eps 1e-7; notebooks/ml/Experiment/Tensorflow/mnist.ipynb:176),
+``torch.optim.SGD(lr=0.01, momentum=0.5)`` (notebooks/ml/Experiment/PyTorch/mnist.ipynb:207),
+Keras ``Adam`` / ``RMSprop(0.2)`` (notebooks/ml/Benchmarks/benchmark.ipynb:154),
+TF ``FtrlOptimizer`` for the census LinearClassifier (feature-bias-whatif.ipynb:458-463).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .ops._C import OPTIM
+from .runtime.arena import ParamArena
+
+
+def _arena_of(obj) -> ParamArena:
+    if isinstance(obj, ParamArena):
+        return obj
+    if isinstance(obj, torch.nn.Module):
+        a = getattr(obj, "_hx_arena", None)
+        return a if a is not None else ParamArena.from_module(obj)
+    params = list(obj)
+    arenas = {id(getattr(p, "_hx_arena", None)) for p in params}
+    if len(arenas) == 1 and getattr(params[0], "_hx_arena", None) is not None:
+        return params[0]._hx_arena
+    return ParamArena(params)
+
+
+class FusedOptimizer:
+    kind = "sgd"
+    nstate = 0
+
+    def __init__(self, params, lr, weight_decay=0.0, **hp):
+        self.arena = _arena_of(params)
+        self.lr = float(lr)
+        self.weight_decay = float(weight_decay)
+        self.hp = hp
+        self.grad_scale = 1.0
+        dev = self.arena.device
+        self.step_count = torch.zeros(1, device=dev, dtype=torch.float32)
+        self._arrive = torch.zeros(1, device=dev, dtype=torch.int32)
+        # device RNG state advanced by the optimizer kernel's last workgroup (dropout masks)
+        self.rng = None
+        if dev.type == "cuda":
+            from .ops.functional import rng_state
+
+            self.rng = rng_state(dev)
+        self._states = [self.arena.state(f"{self.kind}_s{i}") for i in range(self.nstate)]
+        self.param_groups = [{"params": self.arena.params, "lr": self.lr}]
+
+    # hyper-parameter vector in the kernel's layout: lr, gscale, wd, a..e
+    def _hp(self) -> list[float]:
+        raise NotImplementedError
+
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.lr = self.param_groups[0]["lr"]
+        a = self.arena
+        s = self._states + [None] * (3 - len(self._states))
+        if a.device.type == "cuda":
+            from .ops import kernels as K
+
+            K.optim_step(OPTIM[self.kind], a.master, a.grad, s[0], s[1], s[2], a.shadow, self._hp(), self.step_count,
+                         zero_grad=True, arrive=self._arrive, rng=self.rng)
+        else:
+            self.step_count += 1
+            with torch.no_grad():
+                self._cpu_step(a.master, a.grad * self.grad_scale, s, float(self.step_count.item()))
+                a.grad.zero_()
+            if a.shadow is not None:
+                a.refresh_shadow()
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.arena.zero_grad()
+
+    def state_dict(self):
+        return {"step": self.step_count.cpu(), "lr": self.lr, "states": [t.cpu() for t in self._states]}
+
+    def load_state_dict(self, sd):
+        self.step_count.copy_(sd["step"])
+        self.lr = sd["lr"]
+        self.param_groups[0]["lr"] = self.lr
+        for t, v in zip(self._states, sd["states"]):
+            t.copy_(v)
+
+    def _cpu_step(self, p, g, s, t):  # pragma: no cover - overridden
+        raise NotImplementedError
+
+
+class SGD(FusedOptimizer):
+    kind, nstate = "sgd", 1
+
+    def __init__(self, params, lr=0.01, momentum=0.0, dampening=0.0, nesterov=False, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay, momentum=momentum, dampening=dampening, nesterov=nesterov)
+
+    def _hp(self):
+        h = self.hp
+        return [self.lr, self.grad_scale, self.weight_decay, h["momentum"], h["dampening"], float(h["nesterov"])]
+
+    def _cpu_step(self, p, g, s, t):
+        h = self.hp
+        g = g + self.weight_decay * p
+        if h["momentum"]:
+            s[0].mul_(h["momentum"]).add_(g, alpha=1 - h["dampening"])
+            g = g + h["momentum"] * s[0] if h["nesterov"] else s[0]
+        p.sub_(self.lr * g)
+
+
+class Adam(FusedOptimizer):
+    kind, nstate = "adam", 2
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay, b1=betas[0], b2=betas[1], eps=eps)
+
+    def _hp(self):
+        h = self.hp
+        return [self.lr, self.grad_scale, self.weight_decay, h["b1"], h["b2"], h["eps"]]
+
+    def _cpu_step(self, p, g, s, t):
+        h = self.hp
+        if self.kind == "adam":
+            g = g + self.weight_decay * p
+        else:
+            p.mul_(1 - self.lr * self.weight_decay)
+        s[0].mul_(h["b1"]).add_(g, alpha=1 - h["b1"])
+        s[1].mul_(h["b2"]).addcmul_(g, g, value=1 - h["b2"])
+        bc1, bc2 = 1 - h["b1"] ** t, 1 - h["b2"] ** t
+        p.sub_(self.lr * (s[0] / bc1) / ((s[1] / bc2).sqrt() + h["eps"]))
+
+
+class AdamW(Adam):
+    kind = "adamw"
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+
+class Adadelta(FusedOptimizer):
+    kind, nstate = "adadelta", 2
+
+    def __init__(self, params, lr=1.0, rho=0.95, eps=1e-7, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay, rho=rho, eps=eps)
+
+    def _hp(self):
+        return [self.lr, self.grad_scale, self.weight_decay, self.hp["rho"], self.hp["eps"]]
+
+    def _cpu_step(self, p, g, s, t):
+        rho, eps = self.hp["rho"], self.hp["eps"]
+        g = g + self.weight_decay * p
+        s[0].mul_(rho).addcmul_(g, g, value=1 - rho)
+        delta = (s[1] + eps).sqrt() / (s[0] + eps).sqrt() * g
+        s[1].mul_(rho).addcmul_(delta, delta, value=1 - rho)
+        p.sub_(self.lr * delta)
+
+
+class RMSprop(FusedOptimizer):
+    kind, nstate = "rmsprop", 3
+
+    def __init__(self, params, lr=1e-3, alpha=0.9, eps=1e-7, momentum=0.0, centered=False, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay, alpha=alpha, eps=eps, momentum=momentum, centered=centered)
+
+    def _hp(self):
+        h = self.hp
+        return [self.lr, self.grad_scale, self.weight_decay, h["alpha"], h["eps"], h["momentum"], float(h["centered"])]
+
+    def _cpu_step(self, p, g, s, t):
+        h = self.hp
+        g = g + self.weight_decay * p
+        s[0].mul_(h["alpha"]).addcmul_(g, g, value=1 - h["alpha"])
+        if h["centered"]:
+            s[2].mul_(h["alpha"]).add_(g, alpha=1 - h["alpha"])
+            avg = (s[0] - s[2] * s[2]).clamp_min(0).sqrt() + h["eps"]
+        else:
+            avg = s[0].sqrt() + h["eps"]
+        if h["momentum"]:
+            s[1].mul_(h["momentum"]).add_(g / avg)
+            p.sub_(self.lr * s[1])
+        else:
+            p.sub_(self.lr * g / avg)
+
+
+class Adagrad(FusedOptimizer):
+    kind, nstate = "adagrad", 1
+
+    def __init__(self, params, lr=0.01, eps=1e-10, initial_accumulator_value=0.0, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay, eps=eps)
+        if initial_accumulator_value:
+            self._states[0].fill_(initial_accumulator_value)
+
+    def _hp(self):
+        return [self.lr, self.grad_scale, self.weight_decay, self.hp["eps"]]
+
+    def _cpu_step(self, p, g, s, t):
+        g = g + self.weight_decay * p
+        s[0].addcmul_(g, g)
+        p.sub_(self.lr * g / (s[0].sqrt() + self.hp["eps"]))
+
+
+class Ftrl(FusedOptimizer):
+    """FTRL-proximal with lr_power = -0.5 (TF FtrlOptimizer defaults)."""
+
+    kind, nstate = "ftrl", 2
+
+    def __init__(self, params, lr=0.2, l1=0.0, l2=0.0, beta=0.0, initial_accumulator_value=0.1):
+        super().__init__(params, lr, 0.0, l1=l1, l2=l2, beta=beta)
+        self._states[1].fill_(initial_accumulator_value)
+
+    def _hp(self):
+        h = self.hp
+        return [self.lr, self.grad_scale, 0.0, h["l1"], h["l2"], h["beta"]]
+
+    def _cpu_step(self, p, g, s, t):
+        h = self.hp
+        nn_ = s[1] + g * g
+        sigma = (nn_.sqrt() - s[1].sqrt()) / self.lr
+        s[0].add_(g - sigma * p)
+        s[1].copy_(nn_)
+        z = s[0]
+        new = -(z - torch.sign(z) * h["l1"]) / ((h["beta"] + nn_.sqrt()) / self.lr + 2 * h["l2"])
+        p.copy_(torch.where(z.abs() <= h["l1"], torch.zeros_like(p), new))
+
+
+_BY_NAME = {"sgd": SGD, "adam": Adam, "adamw": AdamW, "adadelta": Adadelta, "rmsprop": RMSprop, "adagrad": Adagrad,
+            "ftrl": Ftrl}
+
+
+def get(name: str, params, **kw) -> FusedOptimizer:
+    return _BY_NAME[name.lower()](params, **kw)
+
+
+def cosine_lr(base, step, total, warmup=0):
+    if step < warmup:
+        return base * (step + 1) / warmup
+    return 0.5 * base * (1 + math.cos(math.pi * (step - warmup) / max(1, total - warmup)))

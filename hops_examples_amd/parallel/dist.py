@@ -1,0 +1,101 @@
+"""Process-group bootstrap: one process per GPU, RCCL over xGMI on MI355X
+(``backend="nccl"`` is RCCL on ROCm), gloo on CPU.
+
+Reads the torchrun contract (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT).  This replaces TF's TF_CONFIG cluster spec that
+``experiment.mirrored`` builds for MultiWorkerMirroredStrategy in the reference
+(notebooks/ml/Distributed_Training/multiworker_mirrored_strategy/multiworkermirroredstrategy_mnist_example.ipynb:137).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def init(backend: str | None = None, timeout_s: float = 600.0) -> tuple[int, int, int]:
+    """Initialise the default process group if WORLD_SIZE > 1 (idempotent).
+
+    Returns (rank, local_rank, world_size) and pins this process to cuda:local_rank.
+    """
+    rank, local_rank, world = env_world()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, local_rank, world
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_dist() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_dist() else 1
+
+
+def barrier() -> None:
+    if is_dist():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def device() -> torch.device:
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    if is_dist():
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+    return t
+
+
+def all_reduce_scalar(v: float, op: str = "sum") -> float:
+    if not is_dist():
+        return float(v)
+    t = torch.tensor([float(v)], dtype=torch.float64, device=device())
+    return float(all_reduce_(t, op).item())
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if is_dist():
+        dist.broadcast(t, src)
+    return t
+
+
+def self_test() -> bool:
+    """All-reduce checksum self-test: every rank contributes rank+1."""
+    n = world_size()
+    t = torch.full((1024,), float(rank() + 1), device=device())
+    all_reduce_(t)
+    ok = bool(torch.all(t == n * (n + 1) / 2).item())
+    return ok
+
+
+def shutdown() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()

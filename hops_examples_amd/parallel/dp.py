@@ -1,0 +1,138 @@
+"""Data-parallel engine: bucketed gradient all-reduce over RCCL, overlapped with backward.
+
+The gradients of a model live in ONE flat fp32 buffer (ParamArena), laid out in
+forward order.  Backward produces them roughly in reverse, so buckets are cut
+walking the parameters backwards: each bucket is a CONTIGUOUS slice of the
+grad buffer — no pack/unpack copies, and the all-reduce is issued the moment
+the bucket's last gradient kernel has been enqueued (hopsx kernels notify via
+runtime.hooks.grad_ready).  RCCL runs on its own stream, so the collective of
+bucket i overlaps the backward kernels of buckets i+1..
+
+Bucket sizing for MI355X xGMI: a ring all-reduce is bound per
+link (~153 GB/s x 7 links per GPU); below ~10 MB the per-collective latency
+dominates, so models under ~10 M params (every reference CNN) get ONE bucket
+and ResNet50-class models 4-8 buckets of >= 16 MB.
+
+Modes (the three strategies the reference names):
+  * ``mirrored`` / ``collective_allreduce`` — synchronous all-reduce (this class);
+  * ``parameter_server`` — see parallel/ps.py (reduce-scatter to shard owners +
+    all-gather, i.e. a sharded PS over the same RCCL communicator).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..runtime import hooks
+from ..runtime.arena import ParamArena
+from . import dist as hdist
+
+MB = 1 << 20
+
+
+def plan_buckets(arena: ParamArena, bucket_mb: float, first_bucket_mb: float | None = None):
+    """Contiguous [start, end) slices of the flat grad buffer, in backward order."""
+    ranges = arena.ranges()
+    total_bytes = arena.numel * 4
+    if total_bytes <= 10 * MB or bucket_mb <= 0:
+        return [(0, arena.numel, [id(p) for p, _, _ in ranges])]
+    cap = int(bucket_mb * MB / 4)
+    first_cap = int((first_bucket_mb or bucket_mb) * MB / 4)
+    buckets = []
+    end = arena.numel
+    cur_ids, cur_start = [], arena.numel
+    limit = first_cap
+    for p, off, n in reversed(ranges):
+        cur_ids.append(id(p))
+        cur_start = off
+        if end - cur_start >= limit:
+            buckets.append((cur_start, end, cur_ids))
+            end, cur_ids, limit = cur_start, [], cap
+    if cur_ids:
+        buckets.append((0, end, cur_ids))
+    elif buckets and buckets[-1][0] != 0:
+        s, e, ids = buckets[-1]
+        buckets[-1] = (0, e, ids)
+    return buckets
+
+
+class DataParallel:
+    def __init__(self, model_or_arena, bucket_mb: float = 25.0, overlap: bool = True, broadcast: bool = True,
+                 grad_dtype: torch.dtype = torch.float32):
+        if isinstance(model_or_arena, ParamArena):
+            self.arena = model_or_arena
+        else:
+            self.arena = getattr(model_or_arena, "_hx_arena", None) or ParamArena.from_module(model_or_arena)
+        self.world = hdist.world_size()
+        self.overlap = overlap and self.world > 1
+        self.buckets = plan_buckets(self.arena, bucket_mb)
+        self._owner = {}
+        for bi, (_, _, ids) in enumerate(self.buckets):
+            for i in ids:
+                self._owner[i] = bi
+        self._pending = [len(ids) for _, _, ids in self.buckets]
+        self._handles: list = []
+        self._launched = [False] * len(self.buckets)
+        self.grad_dtype = grad_dtype
+        if broadcast and self.world > 1:
+            self.broadcast_params()
+        if self.overlap:
+            hooks.subscribe(self._on_ready)
+
+    def broadcast_params(self) -> None:
+        hdist.broadcast_(self.arena.master, 0)
+        self.arena.refresh_shadow()
+
+    # -------------------------------------------------------------- backward
+    def _launch(self, bi: int) -> None:
+        if self._launched[bi]:
+            return
+        s, e, _ = self._launched_bucket(bi)
+        view = self.arena.grad[s:e]
+        if self.grad_dtype == torch.bfloat16:
+            # compressed all-reduce: bf16 on the wire, fp32 master accumulate
+            tmp = view.to(torch.bfloat16)
+            h = dist.all_reduce(tmp, async_op=True)
+            self._handles.append((h, view, tmp))
+        else:
+            self._handles.append((dist.all_reduce(view, async_op=True), None, None))
+        self._launched[bi] = True
+
+    def _launched_bucket(self, bi):
+        return self.buckets[bi]
+
+    def _on_ready(self, p) -> None:
+        bi = self._owner.get(id(p))
+        if bi is None:
+            return
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def finish(self) -> None:
+        """Complete the gradient all-reduce (called after loss.backward())."""
+        if self.world <= 1:
+            return
+        for bi in range(len(self.buckets)):
+            if not self._launched[bi]:
+                self._launch(bi)
+        for h, view, tmp in self._handles:
+            h.wait()
+            if tmp is not None:
+                view.copy_(tmp)
+        self._handles.clear()
+        self._pending = [len(ids) for _, _, ids in self.buckets]
+        self._launched = [False] * len(self.buckets)
+
+    def allreduce_all(self) -> None:
+        """Non-overlapped path (used between captured graph segments)."""
+        if self.world <= 1:
+            return
+        for s, e, _ in self.buckets:
+            dist.all_reduce(self.arena.grad[s:e])
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+    def close(self) -> None:
+        hooks.unsubscribe(self._on_ready)

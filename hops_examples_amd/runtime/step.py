@@ -1,0 +1,106 @@
+"""TrainStep: a training step (forward, fused loss, backward, gradient all-reduce,
+fused optimizer, RNG advance) that is captured into hipGraphs after warm-up.
+
+The reference runs the equivalent step inside ``model.fit`` (TF) or a Python
+loop (PyTorch) — notebooks/ml/Experiment/PyTorch/mnist.ipynb:136-154.  On
+MI355X the small reference models are launch-bound (a 32-image MNIST step is
+~1-3 GFLOP), so after warm-up the whole step is replayed from a hipGraph: one
+host call per step instead of ~30 kernel launches plus autograd bookkeeping.
+
+world_size == 1 : one graph  = fwd + bwd + optimizer + rng
+world_size  > 1 : graph A    = fwd + bwd            (RCCL all-reduce of the flat
+                  grad buckets runs between the graphs, on RCCL's stream)
+                  graph B    = optimizer + rng
+                  HOPSX_GRAPH_COLLECTIVES=1 captures the all-reduce too (one graph).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..ops import functional as HF
+from ..parallel import dist as hdist
+
+
+class TrainStep:
+    def __init__(self, model, optimizer, loss_kind: str = "sparse_ce", dp=None, graph: bool = True, warmup: int = 3,
+                 forward_fn=None):
+        self.model, self.opt, self.loss_kind, self.dp = model, optimizer, loss_kind, dp
+        self.forward_fn = forward_fn or (lambda m, x: m(x))
+        dev = optimizer.arena.device
+        self.device = dev
+        self.use_graph = bool(graph) and dev.type == "cuda" and os.environ.get("HOPSX_GRAPH", "1") == "1"
+        self.warmup = warmup
+        self.graph_collectives = os.environ.get("HOPSX_GRAPH_COLLECTIVES", "0") == "1"
+        self._n = 0
+        self._g1 = self._g2 = None
+        self._sx = self._sy = None
+        self._out = None
+        if dp is not None:
+            optimizer.grad_scale = dp.grad_scale()
+
+    # ------------------------------------------------------------- eager path
+    def _fwd_bwd(self, x, y):
+        out = self.forward_fn(self.model, x)
+        loss, correct, count, dl = HF.loss_and_grad(out, y, self.loss_kind)
+        out.backward(dl)
+        return {"loss": loss, "correct": correct, "count": count}
+
+    def _opt(self):
+        self.opt.step()
+        if self.device.type != "cuda" or getattr(self.opt, "rng", None) is None:
+            HF.advance_rng(self.device)  # on the GPU the optimizer kernel advances the RNG itself
+
+    def eager(self, x, y):
+        r = self._fwd_bwd(x, y)
+        if self.dp is not None:
+            self.dp.finish()
+        self._opt()
+        return r
+
+    # ------------------------------------------------------------- graph path
+    def _capture(self, x, y):
+        self._sx = x.clone()
+        self._sy = y.clone()
+        world = hdist.world_size()
+        overlap = None
+        if self.dp is not None:
+            overlap, self.dp.overlap = self.dp.overlap, False
+            from . import hooks
+
+            hooks.unsubscribe(self.dp._on_ready)
+        pool = torch.cuda.graph_pool_handle()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=pool):
+            out = self._fwd_bwd(self._sx, self._sy)
+            if world == 1 or self.dp is None or self.graph_collectives:
+                if self.dp is not None:
+                    self.dp.allreduce_all()
+                self._opt()
+        self._g1 = g1
+        if world > 1 and self.dp is not None and not self.graph_collectives:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=pool):
+                self._opt()
+            self._g2 = g2
+        self._out = out
+        if overlap is not None:
+            self.dp.overlap = overlap
+
+    def __call__(self, x, y):
+        self._n += 1
+        if not self.use_graph or self._n <= self.warmup:
+            return self.eager(x, y)
+        if self._g1 is None:
+            torch.cuda.synchronize()
+            self._capture(x, y)
+            torch.cuda.synchronize()
+        if x.data_ptr() != self._sx.data_ptr():
+            self._sx.copy_(x, non_blocking=True)
+            self._sy.copy_(y, non_blocking=True)
+        self._g1.replay()
+        if self._g2 is not None:
+            self.dp.allreduce_all()
+            self._g2.replay()
+        return self._out
