@@ -83,3 +83,12 @@ __device__ __forceinline__ float act_grad_from_out(float y, int act) {
 }
 
 #define HOPSX_CHECK_LAUNCH() (void)hipGetLastError()
+
+#include <cstdlib>
+#include <cstring>
+// Host-side kill switch for specialised fast paths, for A/B checks:
+// HOPSX_DISABLE=direct_conv,pool8,rowreduce,loss_thread,splitk
+static inline bool hopsx_disabled(const char* name) {
+  static const char* env = std::getenv("HOPSX_DISABLE");
+  return env && std::strstr(env, name) != nullptr;
+}

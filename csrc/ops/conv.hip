@@ -116,7 +116,7 @@ __global__ __launch_bounds__(1024) void conv_direct_wgrad_k(const bf16_raw* __re
 
 static bool direct_ok(const ConvGeom& g) {
   const int K = g.KH * g.KW * g.C;
-  return K <= 64 && g.CO % 4 == 0 && g.CO <= 256 && K * g.CO <= 1024;
+  return K <= 64 && g.CO % 4 == 0 && g.CO <= 256 && K * g.CO <= 1024 && !hopsx_disabled("direct_conv");
 }
 
 extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out,
@@ -166,8 +166,9 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
   const int M = g.CO, N = g.KH * g.KW * g.C, K = g.B * g.OH * g.OW;
   if (direct_ok(g)) {
     const int threads = ((N * M + 63) / 64) * 64;
-    long blocks = (K + 2047) / 2048;
-    if (blocks > 1024) blocks = 1024;
+    // ~2 workgroups per CU; each handles >= 64 pixels (one LDS tile)
+    long blocks = (K + 63) / 64;
+    if (blocks > 512) blocks = 512;
     if (blocks < 1) blocks = 1;
     const int ppb = (int)((K + blocks - 1) / blocks);
     const size_t shm = (size_t)64 * (M + N) * sizeof(float);

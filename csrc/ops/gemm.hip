@@ -13,12 +13,14 @@ __global__ __launch_bounds__(256) void splitk_finish_k(const float* __restrict__
                                                        float alpha, float beta, int act,
                                                        const bf16_raw* __restrict__ aux, long ldaux,
                                                        float* __restrict__ colsum, int rows_per_block) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  const int m0 = blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
-  const float b = bias ? bias[n] : 0.f;
+  // block = 4 rows x 64 columns; every thread handles ONE element per row group so
+  // the loads are independent (a serial per-column row loop was L2-latency bound)
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int m = blockIdx.y * 4 + (threadIdx.x >> 6);
+  __shared__ float red[4][64];
   float cs = 0.f;
-  for (int m = m0; m < m1; ++m) {
+  if (n < N && m < M) {
+    const float b = bias ? bias[n] : 0.f;
     float v = ws[(long)m * N + n];
     if (epi == EPI_DACT_BF16) {
       if (aux) v *= act_grad_from_out(bf2f(aux[(long)m * ldaux + n]), act);
@@ -33,9 +35,13 @@ __global__ __launch_bounds__(256) void splitk_finish_k(const float* __restrict__
         *o = v;
       }
     }
-    cs += v;
+    cs = v;
   }
-  if (colsum) atomicAdd(colsum + n, cs);
+  if (!colsum) return;
+  red[threadIdx.x >> 6][threadIdx.x & 63] = cs;
+  __syncthreads();
+  if (threadIdx.x < 64 && n < N)
+    atomicAdd(colsum + n, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
 // Small-M / long-K GEMMs (e.g. the MNIST Dense(128) over 10816 features at batch
@@ -44,7 +50,7 @@ __global__ __launch_bounds__(256) void splitk_finish_k(const float* __restrict__
 // GEMM + finishing pass (all graph-capturable).
 static bool want_splitk(int M, int N, int K) {
   GemmPlan p = plan_gemm(M, N, K, true);
-  return p.split >= 4;
+  return p.split >= 4 && !hopsx_disabled("splitk");
 }
 
 template <bool AK, bool BK_>
@@ -88,12 +94,10 @@ extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long
     int rc = hopsx_gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, EPI_ATOMIC_F32, ws, N, nullptr, 1.f, 0.f, 0, nullptr, 0,
                         nullptr, nullptr, 0, st);
     if (rc) return rc;
-    const int gx = (N + 255) / 256;
-    int gy = (M + 63) / 64;
-    if (gy < 1) gy = 1;
-    const int rpb = (M + gy - 1) / gy;
+    const int gx = (N + 63) / 64;
+    const int gy = (M + 3) / 4;
     hipLaunchKernelGGL(splitk_finish_k, dim3(gx, gy), dim3(256), 0, st, ws, M, N, epi, out, ldo, bias, alpha, beta,
-                       act, (const bf16_raw*)aux, ldaux, colsum, rpb);
+                       act, (const bf16_raw*)aux, ldaux, colsum, 4);
     return (int)hipGetLastError();
   }
   if (a_kc && b_kc)

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(1024) void loss_k(int kind, const void* __restrict_
 extern "C" int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
                                   float grad_scale, float* loss_sum, int* correct, void* dlogits, int dlogits_f32,
                                   hipStream_t st) {
-  const int per_thread = C <= 32;
+  const int per_thread = C <= 32 && !hopsx_disabled("loss_thread");
   int grid, block;
   if (per_thread) {
     block = B <= 1024 ? ((B + 63) / 64) * 64 : 256;

@@ -239,7 +239,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_k(const bf16_raw* __restrict
 
 static bool pool_fast(int C, int KH, int KW, int sh, int sw, int ph, int pw, const void* a, const void* b,
                       const void* c, const void* d) {
-  return C % 8 == 0 && (256 % (C / 8) == 0) && sh == KH && sw == KW && ph == 0 && pw == 0 && KH * KW <= 255 &&
+  return !hopsx_disabled("pool8") && C % 8 == 0 && (256 % (C / 8) == 0) && sh == KH && sw == KW && ph == 0 &&
+         pw == 0 && KH * KW <= 255 &&
          (((uintptr_t)a | (uintptr_t)b | (uintptr_t)d) % 16 == 0) && ((uintptr_t)c % 8 == 0);
 }
 

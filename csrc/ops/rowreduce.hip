@@ -58,8 +58,8 @@ static int launch_rowreduce(const void* dy, const void* y, void* dx, int M, int 
                             hipStream_t st) {
   const int g = N / 8;
   const int rpp = 256 / g;
-  // ~2 workgroups per CU at most, >= 16 rows per lane-row per workgroup
-  long blocks = (M + rpp * 16 - 1) / (rpp * 16);
+  // ~2 workgroups per CU at most, >= 4 rows per lane-row per workgroup
+  long blocks = (M + rpp * 4 - 1) / (rpp * 4);
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
   const int rpb = (int)((M + blocks - 1) / blocks);
@@ -75,7 +75,8 @@ static int launch_rowreduce(const void* dy, const void* y, void* dx, int M, int 
 }
 
 static bool vec8_ok(int N, const void* a, const void* b, const void* c) {
-  return N % 8 == 0 && N / 8 <= 256 && ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 == 0;
+  return N % 8 == 0 && N / 8 <= 256 && ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16 == 0 &&
+         !hopsx_disabled("rowreduce");
 }
 
 extern "C" int hopsx_colsum_bf16(const void* x, float* out, int M, int N, hipStream_t st) {

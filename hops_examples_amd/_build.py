@@ -77,7 +77,7 @@ def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra
                     cmd.insert(1, "-x")
                     cmd.insert(2, "hip")
             else:
-                cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-march=x86-64-v2", "-pthread",
+                cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-march=x86-64-v2", "-msse4.2", "-pthread",
                        *_py_includes(), f"-I{srcdir}", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
                        "-c", str(s), "-o", str(o)]
             jobs_list.append(cmd)
@@ -100,7 +100,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     outs.append(_build_lib("_hopsx_ops", ROOT / "csrc" / "ops", "hip", force, jobs, []))
     if (ROOT / "csrc" / "io").exists() and any((ROOT / "csrc" / "io").glob("*.cpp")):
         outs.append(_build_lib("_hopsx_io", ROOT / "csrc" / "io", "cpp", force, jobs,
-                               ["-L/opt/rocm/lib", "-lamdhip64"]))
+                               []))
     if (ROOT / "csrc" / "comm").exists() and any((ROOT / "csrc" / "comm").glob("*.hip")):
         outs.append(_build_lib("_hopsx_comm", ROOT / "csrc" / "comm", "hip", force, jobs, []))
     if verbose:
