@@ -23,20 +23,23 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   m.attr("ARCH") = "gfx950";
 
   m.def("gemm", [](u A, long lda, int akc, u B, long ldb, int bkc, int M, int N, int K, int epi, u out, long ldo,
-                   u bias, float alpha, float beta, int act, u aux, long ldaux, u colsum, u ws, long ws_elems, u st) {
+                   u bias, float alpha, float beta, int act, u aux, long ldaux, u colsum, u ws, long ws_elems, u ay,
+                   int aact, u arowsum, u st) {
     return hopsx_gemm(P<void>(A), lda, akc, P<void>(B), ldb, bkc, M, N, K, epi, P<void>(out), ldo, P<float>(bias),
-                      alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), P<float>(ws), ws_elems, S(st));
+                      alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), P<float>(ws), ws_elems, P<void>(ay), aact,
+                      P<float>(arowsum), S(st));
   });
   m.def("conv2d_fwd", [](u x, u w, std::vector<int> g, int epi, u out, u bias, int act, u colsum, u st) {
     return hopsx_conv2d_fwd(P<void>(x), P<void>(w), g.data(), epi, P<void>(out), P<float>(bias), act,
                             P<float>(colsum), S(st));
   });
-  m.def("conv2d_dgrad", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u st) {
+  m.def("conv2d_dgrad", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact, u st) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
-                              S(st));
+                              P<void>(y), yact, S(st));
   });
-  m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u st) {
-    return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), S(st));
+  m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems, u st) {
+    return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,
+                              P<float>(ws), ws_elems, S(st));
   });
   m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
                             int sw, int ph, int pw, float p, u rng, unsigned salt, u st) {

@@ -14,6 +14,7 @@ static ConvGeom make_geom(const int* g) {
   c.B = g[0]; c.H = g[1]; c.W = g[2]; c.C = g[3];
   c.OH = g[4]; c.OW = g[5]; c.CO = g[6];
   c.KH = g[7]; c.KW = g[8]; c.sh = g[9]; c.sw = g[10]; c.ph = g[11]; c.pw = g[12]; c.dh = g[13]; c.dw = g[14];
+  c.init_div();
   return c;
 }
 
@@ -68,50 +69,99 @@ __global__ __launch_bounds__(256) void conv_direct_fwd_k(const bf16_raw* __restr
   }
 }
 
-// dW[co][k] += sum_m dY[m][co] * im2col(X)[m][k] for K*CO <= 1024: one thread per
-// (k, co) output, pixel tiles of 64 staged in LDS, ONE atomic per thread per workgroup.
+// dW[co][k] += sum_m dY'[m][co] * im2col(X)[m][k] for K*CO <= 1024 (dY' = dY * act'(y)
+// when y is given; dbias[co] += sum_m dY'[m][co]).  Threads = R replicas x K x CO;
+// each thread walks a strided pixel subset straight from global memory with an
+// incremental (b, oh, ow) decode (no divisions in the loop, no LDS staging, no
+// barriers), replicas are reduced through LDS and every (co, k) gets ONE atomic
+// per workgroup.
 __global__ __launch_bounds__(1024) void conv_direct_wgrad_k(const bf16_raw* __restrict__ dy,
                                                             const bf16_raw* __restrict__ x, float* __restrict__ dw,
-                                                            ConvGeom g, int pix_per_block) {
-  constexpr int TP = 64;
-  extern __shared__ float sm[];
+                                                            float* __restrict__ dbias, const bf16_raw* __restrict__ y,
+                                                            int yact, ConvGeom g, int pix_per_block, int R,
+                                                            float* __restrict__ slab) {
+  extern __shared__ float red[];  // [R][K*CO + CO]
   const int K = g.KH * g.KW * g.C;
-  float* sdy = sm;             // [TP][CO]
-  float* sx = sm + TP * g.CO;  // [TP][K]
+  const int KC = K * g.CO;
+  const int tid = threadIdx.x;
+  const int rep = tid / KC, r = tid % KC;
+  const int co = r % g.CO, k = r / g.CO;
   const int M = g.B * g.OH * g.OW;
   const int m0 = blockIdx.x * pix_per_block, m1 = min(M, m0 + pix_per_block);
-  const int tid = threadIdx.x;
-  const int co = tid % g.CO, k = tid / g.CO;
-  const bool active = k < K;
-  float acc = 0.f;
-  for (int mb = m0; mb < m1; mb += TP) {
-    const int np = min(TP, m1 - mb);
-    for (int i = tid; i < TP * g.CO; i += blockDim.x) {
-      const int p = i / g.CO, c = i % g.CO;
-      sdy[i] = p < np ? bf2f(dy[(long)(mb + p) * g.CO + c]) : 0.f;
-    }
-    for (int i = tid; i < TP * K; i += blockDim.x) {
-      const int p = i / K, kk = i % K;
-      float v = 0.f;
-      if (p < np) {
-        const int m = mb + p;
-        const int ohw = g.OH * g.OW;
-        const int b = m / ohw, rem = m - b * ohw;
-        const int oh = rem / g.OW, ow = rem - oh * g.OW;
-        const int ci = kk % g.C, t = kk / g.C;
-        const int kw = t % g.KW, kh = t / g.KW;
-        const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
-        if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) v = bf2f(x[(((long)b * g.H + ih) * g.W + iw) * g.C + ci]);
+  float acc0 = 0.f, acc1 = 0.f, b0 = 0.f, b1 = 0.f;
+  if (rep < R) {
+    const int ci = k % g.C, t = k / g.C;
+    const int kw = t % g.KW, kh = t / g.KW;
+    // two independent pixel streams per thread (m and m + R) for memory-level parallelism
+    int m = m0 + rep;
+    const int ohw = g.OH * g.OW;
+    int b = m / ohw, rem = m - b * ohw;
+    int oh = rem / g.OW, ow = rem - oh * g.OW;
+    auto advance = [&](int step) {
+      ow += step;
+      while (ow >= g.OW) {
+        ow -= g.OW;
+        if (++oh == g.OH) { oh = 0; ++b; }
       }
-      sx[i] = v;
+    };
+    auto term = [&](int mm, int bb, int hh, int ww, float& acc, float& bacc) {
+      float d = bf2f(dy[(long)mm * g.CO + co]);
+      if (y) d *= act_grad_from_out(bf2f(y[(long)mm * g.CO + co]), yact);
+      const int ih = hh * g.sh - g.ph + kh * g.dh, iw = ww * g.sw - g.pw + kw * g.dw;
+      const float xv = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
+                           ? bf2f(x[(((long)bb * g.H + ih) * g.W + iw) * g.C + ci]) : 0.f;
+      acc += d * xv;
+      bacc += d;
+    };
+    for (; m + R < m1; m += 2 * R) {
+      const int bA = b, hA = oh, wA = ow;
+      advance(R);
+      term(m, bA, hA, wA, acc0, b0);
+      term(m + R, b, oh, ow, acc1, b1);
+      advance(R);
     }
-    __syncthreads();
-    if (active)
-#pragma unroll 8
-      for (int p = 0; p < TP; ++p) acc += sdy[p * g.CO + co] * sx[p * K + k];
-    __syncthreads();
+    if (m < m1) term(m, b, oh, ow, acc0, b0);
+    red[rep * (KC + g.CO) + r] = acc0 + acc1;
+    if (k == 0) red[rep * (KC + g.CO) + KC + co] = b0 + b1;
   }
-  if (active && acc != 0.f) atomicAdd(dw + (long)co * K + k, acc);
+  __syncthreads();
+  if (rep == 0) {
+    float s = 0.f, sb = 0.f;
+    for (int q = 0; q < R; ++q) {
+      s += red[q * (KC + g.CO) + r];
+      if (k == 0) sb += red[q * (KC + g.CO) + KC + co];
+    }
+    if (slab) {  // plain stores; slab_reduce_k sums the workgroups (no same-address atomics)
+      slab[(long)blockIdx.x * (KC + g.CO) + r] = s;
+      if (k == 0) slab[(long)blockIdx.x * (KC + g.CO) + KC + co] = sb;
+    } else {
+      if (s != 0.f) atomicAdd(dw + (long)co * K + k, s);
+      if (dbias && k == 0 && sb != 0.f) atomicAdd(dbias + co, sb);
+    }
+  }
+}
+
+// sums the per-workgroup partials: element e < KC is dW[co][k] (slab index r = k*CO + co),
+// e >= KC the bias of channel e - KC
+// one workgroup per output element: 256 lanes stride over the workgroup partials
+// (coalescing is poor but every load is independent), wave + LDS tree reduction
+__global__ __launch_bounds__(256) void slab_reduce_k(const float* __restrict__ slab, int nblk, int KC, int CO, int K,
+                                                     float* __restrict__ dw, float* __restrict__ dbias) {
+  const int e = blockIdx.x;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) s += slab[(long)b * (KC + CO) + e];
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s = red[0] + red[1] + red[2] + red[3];
+  if (e < KC) {
+    const int co = e % CO, k = e / CO;
+    dw[(long)co * K + k] += s;
+  } else if (dbias) {
+    dbias[e - KC] += s;
+  }
 }
 
 static bool direct_ok(const ConvGeom& g) {
@@ -149,10 +199,12 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
 // act'(yprev) — the backward of the activation that produced this conv's input
 // — and `colsum` receives that layer's bias gradient.
 extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
-                                  int act, float* colsum, hipStream_t st) {
+                                  int act, float* colsum, const void* y, int yact, hipStream_t st) {
   ConvGeom g = make_geom(geom);
   const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
-  ConvDgradALoader al{(const bf16_raw*)dy, g, (g.CO % 8 == 0) && ((uintptr_t)dy % 16 == 0)};
+  ConvDgradALoader al{(const bf16_raw*)dy, g,
+                      (g.CO % 8 == 0) && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)y % 16 == 0),
+                      (const bf16_raw*)y, yact};
   ConvWeightTLoader bl{(const bf16_raw*)w, g, (g.C % 8 == 0) && ((uintptr_t)w % 16 == 0)};
   EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act, colsum};
   launch_gemm<true, false>(al, bl, e, M, N, K, false, st);
@@ -161,25 +213,37 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
 
 // dW[co][k] += sum_m dY[m][co] * im2col(X)[m][k]; db[co] += sum_m dY[m][co] when colsum given
 extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias,
-                                  hipStream_t st) {
+                                  const void* y, int yact, float* ws, long ws_elems, hipStream_t st) {
   ConvGeom g = make_geom(geom);
   const int M = g.CO, N = g.KH * g.KW * g.C, K = g.B * g.OH * g.OW;
   if (direct_ok(g)) {
-    const int threads = ((N * M + 63) / 64) * 64;
-    // ~2 workgroups per CU; each handles >= 64 pixels (one LDS tile)
-    long blocks = (K + 63) / 64;
-    if (blocks > 512) blocks = 512;
+    const int KC = N * M;
+    int R = 1024 / KC;
+    if (R > 8) R = 8;
+    if (R < 1) R = 1;
+    const int threads = ((KC * R + 63) / 64) * 64;
+    // with a slab workspace: up to 1024 workgroups of >= 128 pixels, partials reduced by
+    // a second pass; without one: <= 128 workgroups so same-address atomics stay cheap
+    const bool use_slab = ws && ws_elems >= 1024L * (KC + M);
+    const long cap = use_slab ? 1024 : 128;
+    long blocks = (K + 127) / 128;
+    if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const int ppb = (int)((K + blocks - 1) / blocks);
-    const size_t shm = (size_t)64 * (M + N) * sizeof(float);
+    blocks = (K + ppb - 1) / ppb;
+    const size_t shm = (size_t)R * (KC + M) * sizeof(float);
     hipLaunchKernelGGL(conv_direct_wgrad_k, dim3(blocks), dim3(threads), shm, st, (const bf16_raw*)dy,
-                       (const bf16_raw*)x, dw, g, ppb);
+                       (const bf16_raw*)x, dw, dbias, (const bf16_raw*)y, yact, g, ppb, R, use_slab ? ws : nullptr);
+    if (use_slab)
+      hipLaunchKernelGGL(slab_reduce_k, dim3(KC + M), dim3(256), 0, st, ws, (int)blocks, KC, M, N, dw,
+                         dbias);
     return (int)hipGetLastError();
   }
-  DenseLoader al{(const bf16_raw*)dy, g.CO, is_vec_ok(dy, g.CO)};
+  DenseLoader al{(const bf16_raw*)dy, g.CO, is_vec_ok(dy, g.CO) && is_vec_ok(y ? y : dy, g.CO), (const bf16_raw*)y,
+                 yact};
   Im2colLoader bl{(const bf16_raw*)x, g, (g.C % 8 == 0) && ((uintptr_t)x % 16 == 0)};
   EpiAtomicF32 e{dw, N, 1.f, nullptr};
-  launch_gemm<false, false>(al, bl, e, M, N, K, true, st);
-  (void)dbias;  // bias gradient of a conv is produced by the consumer's fused column sum
+  // A = dY^T is staged as an RC image: its row sums are the conv bias gradient
+  launch_gemm<false, false>(al, bl, e, M, N, K, true, st, dbias);
   return (int)hipGetLastError();
 }

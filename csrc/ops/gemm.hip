@@ -56,26 +56,26 @@ static bool want_splitk(int M, int N, int K) {
 template <bool AK, bool BK_>
 static int dispatch_epi(const DenseLoader& al, const DenseLoader& bl, int M, int N, int K, int epi, void* out,
                         long ldo, const float* bias, float alpha, float beta, int act, const void* aux, long ldaux,
-                        float* colsum, hipStream_t st) {
+                        float* colsum, hipStream_t st, float* rowsum_a) {
   switch (epi) {
     case EPI_STORE_BF16: {
       EpiStoreBF16 e{(bf16_raw*)out, ldo, bias, alpha, act, colsum};
-      launch_gemm<AK, BK_>(al, bl, e, M, N, K, false, st);
+      launch_gemm<AK, BK_>(al, bl, e, M, N, K, false, st, rowsum_a);
       break;
     }
     case EPI_STORE_F32: {
       EpiStoreF32 e{(float*)out, ldo, bias, alpha, beta, act, colsum};
-      launch_gemm<AK, BK_>(al, bl, e, M, N, K, false, st);
+      launch_gemm<AK, BK_>(al, bl, e, M, N, K, false, st, rowsum_a);
       break;
     }
     case EPI_ATOMIC_F32: {
       EpiAtomicF32 e{(float*)out, ldo, alpha, colsum};
-      launch_gemm<AK, BK_>(al, bl, e, M, N, K, true, st);
+      launch_gemm<AK, BK_>(al, bl, e, M, N, K, true, st, rowsum_a);
       break;
     }
     case EPI_DACT_BF16: {
       EpiDActBF16 e{(bf16_raw*)out, ldo, (const bf16_raw*)aux, ldaux, act, colsum};
-      launch_gemm<AK, BK_>(al, bl, e, M, N, K, false, st);
+      launch_gemm<AK, BK_>(al, bl, e, M, N, K, false, st, rowsum_a);
       break;
     }
     default:
@@ -86,13 +86,17 @@ static int dispatch_epi(const DenseLoader& al, const DenseLoader& bl, int M, int
 
 extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K,
                           int epi, void* out, long ldo, const float* bias, float alpha, float beta, int act,
-                          const void* aux, long ldaux, float* colsum, float* ws, long ws_elems, hipStream_t st) {
-  DenseLoader al{(const bf16_raw*)A, lda, is_vec_ok(A, lda)};
+                          const void* aux, long ldaux, float* colsum, float* ws, long ws_elems, const void* ay,
+                          int aact, float* arowsum, hipStream_t st) {
+  // ay/aact: fused act' mask on the A operand (same layout as A); arowsum: row sums of
+  // the (masked) A operand — the bias gradient when A = dY^T in a weight-gradient GEMM
+  DenseLoader al{(const bf16_raw*)A, lda, is_vec_ok(A, lda) && is_vec_ok(ay ? ay : A, lda), (const bf16_raw*)ay,
+                 aact};
   DenseLoader bl{(const bf16_raw*)B, ldb, is_vec_ok(B, ldb)};
   if (ws && epi != EPI_ATOMIC_F32 && (long)M * N <= ws_elems && want_splitk(M, N, K)) {
     hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), st);
     int rc = hopsx_gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, EPI_ATOMIC_F32, ws, N, nullptr, 1.f, 0.f, 0, nullptr, 0,
-                        nullptr, nullptr, 0, st);
+                        nullptr, nullptr, 0, ay, aact, arowsum, st);
     if (rc) return rc;
     const int gx = (N + 63) / 64;
     const int gy = (M + 3) / 4;
@@ -101,11 +105,11 @@ extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long
     return (int)hipGetLastError();
   }
   if (a_kc && b_kc)
-    return dispatch_epi<true, true>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st);
+    return dispatch_epi<true, true>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st, arowsum);
   if (a_kc && !b_kc)
-    return dispatch_epi<true, false>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st);
+    return dispatch_epi<true, false>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st, arowsum);
   if (!a_kc && !b_kc)
     return dispatch_epi<false, false>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum,
-                                      st);
-  return dispatch_epi<false, true>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st);
+                                      st, arowsum);
+  return dispatch_epi<false, true>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st, arowsum);
 }

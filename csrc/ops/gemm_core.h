@@ -43,18 +43,61 @@ __device__ __forceinline__ int rc_swz(int k, int cpr) {
 // (outer, inner .. inner+7) — 8 consecutive along the contiguous axis, zero
 // outside [0, lim).  inner is always a multiple of 8.
 // ----------------------------------------------------------------------------
+// Prologue fusion: multiply a loaded operand by act'(y) (y = the activation
+// output with the operand's layout) so backward GEMMs consume dY directly and
+// the separate activation-backward pass disappears.
+__device__ __forceinline__ void mask8(bf16x8& v, const bf16x8& y, int act) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (act == ACT_RELU) {
+      v[j] = (bf2f((uint16_t)y[j]) > 0.f) ? v[j] : (short)0;
+    } else {
+      v[j] = (short)f2bf(bf2f((uint16_t)v[j]) * act_grad_from_out(bf2f((uint16_t)y[j]), act));
+    }
+  }
+}
+
 struct DenseLoader {
   const bf16_raw* p;
   long ld;
-  int vec;  // ld % 8 == 0 and base 16-B aligned
+  int vec;               // ld % 8 == 0 and base 16-B aligned
+  const bf16_raw* y;     // optional activation output for the fused act' mask (same layout as p)
+  int act;
   __device__ __forceinline__ bf16x8 load(int o, int i, int olim, int ilim) const {
     bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
     if (o >= olim) return r;
-    const bf16_raw* q = p + (long)o * ld + i;
-    if (vec && i + 8 <= ilim) return *(const bf16x8*)q;
+    const long off = (long)o * ld + i;
+    const bf16_raw* q = p + off;
+    if (vec && i + 8 <= ilim) {
+      r = *(const bf16x8*)q;
+      if (y) mask8(r, *(const bf16x8*)(y + off), act);
+      return r;
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (i + j < ilim) ? (short)q[j] : (short)0;
+    for (int j = 0; j < 8; ++j) {
+      if (i + j < ilim) {
+        if (y) r[j] = (short)f2bf(bf2f(q[j]) * act_grad_from_out(bf2f(y[off + j]), act));
+        else r[j] = (short)q[j];
+      }
+    }
     return r;
+  }
+};
+
+// Multiply-high "magic number" division (Granlund-Montgomery): the im2col /
+// transposed-conv gathers decode (b, oh, ow) and (kh, kw, ci) for every staged
+// element; hardware has no integer divider, so a generic '/' costs ~40 VALU
+// ops while this costs 3.
+struct FastDiv {
+  uint32_t d, mul, shift;
+  void init(uint32_t dd) {
+    d = dd ? dd : 1;
+    shift = 0;
+    while ((1ull << shift) < d) ++shift;
+    mul = (uint32_t)((((1ull << 32) * ((1ull << shift) - d)) / d) + 1);
+  }
+  __device__ __forceinline__ int div(int n) const {
+    return (int)((((uint64_t)__umulhi((uint32_t)n, mul)) + (uint32_t)n) >> shift);
   }
 };
 
@@ -62,6 +105,11 @@ struct ConvGeom {
   int B, H, W, C;      // input NHWC
   int OH, OW, CO;      // output NHWC
   int KH, KW, sh, sw, ph, pw, dh, dw;
+  FastDiv fC, fCO, fKW, fOW, fOHW, fW, fHW, fSH, fSW;
+  void init_div() {
+    fC.init(C); fCO.init(CO); fKW.init(KW); fOW.init(OW); fOHW.init(OH * OW);
+    fW.init(W); fHW.init(H * W); fSH.init(sh); fSW.init(sw);
+  }
 };
 
 // im2col view of X: (outer = output pixel m, inner = k = (kh, kw, ci))
@@ -70,9 +118,9 @@ struct Im2colLoader {
   ConvGeom g;
   int vec;  // C % 8 == 0 and aligned
   __device__ __forceinline__ short at(int b, int oh, int ow, int k) const {
-    const int ci = k % g.C;
-    const int t = k / g.C;
-    const int kw = t % g.KW, kh = t / g.KW;
+    const int t = g.fC.div(k);
+    const int ci = k - t * g.C;
+    const int kh = g.fKW.div(t), kw = t - kh * g.KW;
     const int ih = oh * g.sh - g.ph + kh * g.dh;
     const int iw = ow * g.sw - g.pw + kw * g.dw;
     if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return 0;
@@ -82,12 +130,12 @@ struct Im2colLoader {
     bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
     if (m >= olim) return r;
     const int ohw = g.OH * g.OW;
-    const int b = m / ohw, rem = m - b * ohw;
-    const int oh = rem / g.OW, ow = rem - oh * g.OW;
+    const int b = g.fOHW.div(m), rem = m - b * ohw;
+    const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
     if (vec && k + 8 <= ilim) {
-      const int ci = k % g.C;
-      const int t = k / g.C;
-      const int kw = t % g.KW, kh = t / g.KW;
+      const int t = g.fC.div(k);
+      const int ci = k - t * g.C;
+      const int kh = g.fKW.div(t), kw = t - kh * g.KW;
       const int ih = oh * g.sh - g.ph + kh * g.dh;
       const int iw = ow * g.sw - g.pw + kw * g.dw;
       if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return r;
@@ -104,32 +152,39 @@ struct Im2colLoader {
 struct ConvDgradALoader {
   const bf16_raw* dy;
   ConvGeom g;
-  int vec;  // CO % 8 == 0 and aligned
+  int vec;            // CO % 8 == 0 and aligned
+  const bf16_raw* y;  // optional: this conv's activation output -> fused act' mask on dY
+  int act;
   __device__ __forceinline__ short at(int b, int ih, int iw, int k) const {
-    const int co = k % g.CO;
-    const int t = k / g.CO;
-    const int kw = t % g.KW, kh = t / g.KW;
+    const int t = g.fCO.div(k);
+    const int co = k - t * g.CO;
+    const int kh = g.fKW.div(t), kw = t - kh * g.KW;
     const int hn = ih + g.ph - kh * g.dh, wn = iw + g.pw - kw * g.dw;
     if (hn < 0 || wn < 0) return 0;
-    const int oh = hn / g.sh, ow = wn / g.sw;
+    const int oh = g.fSH.div(hn), ow = g.fSW.div(wn);
     if (oh * g.sh != hn || ow * g.sw != wn || oh >= g.OH || ow >= g.OW) return 0;
-    return (short)dy[(((long)b * g.OH + oh) * g.OW + ow) * g.CO + co];
+    const long o = (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co;
+    if (y) return (short)f2bf(bf2f(dy[o]) * act_grad_from_out(bf2f(y[o]), act));
+    return (short)dy[o];
   }
   __device__ __forceinline__ bf16x8 load(int m, int k, int olim, int ilim) const {
     bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
     if (m >= olim) return r;
     const int hw = g.H * g.W;
-    const int b = m / hw, rem = m - b * hw;
-    const int ih = rem / g.W, iw = rem - ih * g.W;
+    const int b = g.fHW.div(m), rem = m - b * hw;
+    const int ih = g.fW.div(rem), iw = rem - ih * g.W;
     if (vec && k + 8 <= ilim) {
-      const int co = k % g.CO;
-      const int t = k / g.CO;
-      const int kw = t % g.KW, kh = t / g.KW;
+      const int t = g.fCO.div(k);
+      const int co = k - t * g.CO;
+      const int kh = g.fKW.div(t), kw = t - kh * g.KW;
       const int hn = ih + g.ph - kh * g.dh, wn = iw + g.pw - kw * g.dw;
       if (hn < 0 || wn < 0) return r;
-      const int oh = hn / g.sh, ow = wn / g.sw;
+      const int oh = g.fSH.div(hn), ow = g.fSW.div(wn);
       if (oh * g.sh != hn || ow * g.sw != wn || oh >= g.OH || ow >= g.OW) return r;
-      return *(const bf16x8*)(dy + (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co);
+      const long o = (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co;
+      r = *(const bf16x8*)(dy + o);
+      if (y) mask8(r, *(const bf16x8*)(y + o), act);
+      return r;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = (k + j < ilim) ? at(b, ih, iw, k + j) : (short)0;
@@ -145,9 +200,9 @@ struct ConvWeightTLoader {
   __device__ __forceinline__ bf16x8 load(int k, int ci, int olim, int ilim) const {
     bf16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
     if (k >= olim) return r;
-    const int co = k % g.CO;
-    const int t = k / g.CO;
-    const int kw = t % g.KW, kh = t / g.KW;
+    const int t = g.fCO.div(k);
+    const int co = k - t * g.CO;
+    const int kh = g.fKW.div(t), kw = t - kh * g.KW;
     const bf16_raw* q = w + (((long)co * g.KH + kh) * g.KW + kw) * g.C + ci;
     if (vec && ci + 8 <= ilim) return *(const bf16x8*)q;
 #pragma unroll
@@ -224,7 +279,10 @@ struct EpiDActBF16 {
 // ----------------------------------------------------------------------------
 template <int BM, int BN, int WAVES_M, bool A_KC, bool B_KC, class AL, class BL, class EP>
 __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl, const EP ep, int M, int N,
-                                                       int K, int kps) {
+                                                       int K, int kps, float* rowsum_a) {
+  // rowsum_a (RC-A only): rowsum_a[m] += sum_k A[m][k] of the staged (masked) A
+  // operand — in wgrad dW = dY^T X that is the bias gradient sum_b dY[b][m],
+  // accumulated while the tiles pass through registers, by the tn == 0 blocks.
   constexpr int BK = GEMM_BK;
   constexpr int WAVES_N = 4 / WAVES_M;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
@@ -251,6 +309,12 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
   const int nt = (kend - kbeg + BK - 1) / BK;
 
   bf16x8 ra[A_PT], rb[B_PT];
+  const bool do_rs = !A_KC && rowsum_a != nullptr && tn == 0;
+  float rs[A_PT][8];
+#pragma unroll
+  for (int i = 0; i < A_PT; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs[i][j] = 0.f;
 
   auto gload = [&](int k0) {
 #pragma unroll
@@ -299,6 +363,9 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
           off = kr * BM + 8 * (c ^ rc_swz(kr, cpr));
         }
         *(bf16x8*)(sa + off) = ra[i];
+        if (!A_KC && do_rs)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rs[i][j] += bf2f((uint16_t)ra[i][j]);
       }
     }
 #pragma unroll
@@ -378,6 +445,28 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
     cur ^= 1;
   }
 
+  if (!A_KC && do_rs) {
+    // reduce the per-thread row sums over the k-rows of the RC image through LDS
+    // (the staging buffers are free after the last barrier of the main loop)
+    float* red = (float*)smem;  // [BK][BM] floats = 2*BK*BM*2 bytes <= smem size
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < A_CH) {
+        const int cpr = BM / 8;
+        const int kr = idx / cpr, c = idx - kr * cpr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[kr * BM + 8 * c + j] = rs[i][j];
+      }
+    }
+    __syncthreads();
+    for (int m = tid; m < BM; m += 256) {
+      float s = 0.f;
+      for (int kr = 0; kr < BK; ++kr) s += red[kr * BM + m];
+      if (m0 + m < M && s != 0.f) atomicAdd(rowsum_a + m0 + m, s);
+    }
+  }
+
   // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + reg
   float cs[FN];
 #pragma unroll
@@ -422,6 +511,10 @@ inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu =
   if (M >= 128 && N >= 128 && t128 >= num_cu) p.cfg = 0;
   else if (M >= 48 && N >= 48 && t64 >= num_cu / 2) p.cfg = 1;
   else if (M > 32 && N > 32 && t64 >= 32) p.cfg = 1;
+  // split-K GEMMs (weight gradients, K = batch*pixels) get their parallelism from
+  // the K split, so use the bigger tile: every operand element is then fetched by
+  // fewer workgroups (64x64 halves the operand traffic of 32x32 tiles)
+  else if (allow_split && M >= 48 && N >= 48 && K >= 8192) p.cfg = 1;
   else p.cfg = 2;
   const int bm = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
   const long tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm);
@@ -446,7 +539,7 @@ inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu =
 
 template <bool A_KC, bool B_KC, class AL, class BL, class EP>
 inline void launch_gemm(const AL& al, const BL& bl, const EP& ep, int M, int N, int K, bool allow_split,
-                        hipStream_t st) {
+                        hipStream_t st, float* rowsum_a = nullptr) {
   if (M <= 0 || N <= 0) return;
   if (K <= 0) K = 1;  // degenerate: zero-length reduction still runs the epilogue
   GemmPlan p = plan_gemm(M, N, K, allow_split);
@@ -456,15 +549,15 @@ inline void launch_gemm(const AL& al, const BL& bl, const EP& ep, int M, int N, 
   switch (p.cfg) {
     case 0:
       hipLaunchKernelGGL((mfma_gemm_kernel<128, 128, 2, A_KC, B_KC, AL, BL, EP>), grid, dim3(256), 0, st, al, bl,
-                         ep, M, N, K, p.kps);
+                         ep, M, N, K, p.kps, rowsum_a);
       break;
     case 1:
       hipLaunchKernelGGL((mfma_gemm_kernel<64, 64, 2, A_KC, B_KC, AL, BL, EP>), grid, dim3(256), 0, st, al, bl, ep,
-                         M, N, K, p.kps);
+                         M, N, K, p.kps, rowsum_a);
       break;
     default:
       hipLaunchKernelGGL((mfma_gemm_kernel<32, 32, 2, A_KC, B_KC, AL, BL, EP>), grid, dim3(256), 0, st, al, bl, ep,
-                         M, N, K, p.kps);
+                         M, N, K, p.kps, rowsum_a);
       break;
   }
 }

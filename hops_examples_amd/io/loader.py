@@ -1,0 +1,109 @@
+"""DeviceLoader: host arrays -> shuffled mini-batches -> HBM, overlapped with compute.
+
+The path the SURVEY asks for (§1.2 DATA, BASELINE north star "Parquet on
+HopsFS -> tensor streams into 288 GB HBM via pinned hipMemcpyAsync on a side
+stream"):
+
+  * batch assembly: rows gathered by index into a PINNED host slot by the C++
+    thread pool (``_hopsx_io.gather_rows``; no Python per row);
+  * transfer: ``copy_`` with ``non_blocking=True`` on a dedicated copy stream
+    (hipMemcpyAsync from pinned memory, DMA engine, no SM time);
+  * hand-off: the consumer stream waits on a per-slot event, and the slot is
+    recycled only after the transfer that read it has completed;
+  * ``resident=True`` (default when it fits) keeps the WHOLE dataset in HBM —
+    with 288 GB per MI355X every reference dataset fits — and batches are then
+    device-side index gathers with no host traffic at all;
+  * sharding (petastorm's ``shard_count``/``cur_shard``) splits rows per rank.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import gather_rows
+
+
+class DeviceLoader:
+    def __init__(self, x: np.ndarray, y: np.ndarray | None, batch_size: int, shuffle: bool = True,
+                 drop_last: bool = True, device=None, shard: tuple[int, int] | None = None, seed: int | None = None,
+                 resident: bool | None = None, depth: int = 3, x_dtype=None):
+        if shard is not None:
+            n, i = shard
+            sel = np.arange(len(x))[i::n]
+            x = x[sel]
+            y = y[sel] if y is not None else None
+        self.x = np.ascontiguousarray(x)
+        self.y = None if y is None else np.ascontiguousarray(y)
+        self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        self.rng = np.random.default_rng(seed)
+        self.depth = depth
+        nbytes = self.x.nbytes + (0 if self.y is None else self.y.nbytes)
+        if resident is None:
+            resident = self.device.type == "cuda" and nbytes < (8 << 30)
+        self.resident = resident and self.device.type == "cuda"
+        self._x_dev = self._y_dev = None
+        if self.resident:
+            self._x_dev = torch.from_numpy(self.x).to(self.device, non_blocking=False)
+            if x_dtype is not None:
+                self._x_dev = self._x_dev.to(x_dtype)
+            if self.y is not None:
+                self._y_dev = torch.from_numpy(self.y).to(self.device)
+        elif self.device.type == "cuda":
+            self._stream = torch.cuda.Stream(self.device)
+            self._slots = []
+            for _ in range(depth):
+                hx = torch.empty((batch_size,) + self.x.shape[1:], dtype=torch.from_numpy(self.x[:1]).dtype).pin_memory()
+                hy = None if self.y is None else torch.empty((batch_size,) + self.y.shape[1:],
+                                                             dtype=torch.from_numpy(self.y[:1]).dtype).pin_memory()
+                self._slots.append([hx, hy, None])
+
+    def __len__(self):
+        n = len(self.x)
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def _order(self):
+        return self.rng.permutation(len(self.x)) if self.shuffle else np.arange(len(self.x))
+
+    def __iter__(self):
+        order = self._order()
+        nb = len(self)
+        if self.resident:
+            perm = torch.from_numpy(order).to(self.device)
+            for b in range(nb):
+                idx = perm[b * self.batch_size:(b + 1) * self.batch_size]
+                yield (self._x_dev.index_select(0, idx),
+                       None if self._y_dev is None else self._y_dev.index_select(0, idx))
+            return
+        if self.device.type != "cuda":
+            for b in range(nb):
+                idx = order[b * self.batch_size:(b + 1) * self.batch_size]
+                yield torch.from_numpy(self.x[idx]), (None if self.y is None else torch.from_numpy(self.y[idx]))
+            return
+        cur = torch.cuda.current_stream(self.device)
+        pending = []
+        for b in range(nb):
+            slot = self._slots[b % self.depth]
+            if slot[2] is not None:
+                slot[2].synchronize()  # the H2D that last read this pinned slot is done
+            idx = order[b * self.batch_size:(b + 1) * self.batch_size]
+            k = len(idx)
+            gather_rows(self.x, idx, slot[0].numpy())
+            if self.y is not None:
+                gather_rows(self.y, idx, slot[1].numpy())
+            with torch.cuda.stream(self._stream):
+                dx = slot[0][:k].to(self.device, non_blocking=True)
+                dy = None if self.y is None else slot[1][:k].to(self.device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+            slot[2] = ev
+            pending.append((dx, dy, ev))
+            if len(pending) >= 2 or b == nb - 1:
+                while pending:
+                    px, py, pev = pending.pop(0)
+                    cur.wait_event(pev)
+                    px.record_stream(cur)
+                    if py is not None:
+                        py.record_stream(cur)
+                    yield px, py

@@ -77,16 +77,14 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2.to(BF16)
         dy2 = dy2.contiguous()
         gb = _wgrad_buf(b) if b is not None else None
-        if act and y.dtype == BF16:
-            # activation backward + bias gradient in one pass
-            dy2 = K.act_bwd_colsum(dy2, y, act, gb)
-        elif gb is not None:
-            K.colsum(dy2, gb)
+        # the activation backward is fused into the A-operand staging of both GEMMs and
+        # the bias gradient falls out of the weight-gradient GEMM (no elementwise passes)
+        ymask = y if (act and y.dtype == BF16) else None
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = K.linear_dgrad(dy2, _arena.weight_bf16(w)).view(ctx.xshape)
+            dx = K.linear_dgrad(dy2, _arena.weight_bf16(w), y=ymask, act=act).view(ctx.xshape)
         gw = _wgrad_buf(w)
-        K.linear_wgrad(dy2, x2, gw)
+        K.linear_wgrad(dy2, x2, gw, y=ymask, act=act, dbias=gb)
         return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None
 
 
@@ -120,15 +118,12 @@ class _Conv2dFn(torch.autograd.Function):
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
         gb = _wgrad_buf(b) if b is not None else None
-        if act:
-            dy = K.act_bwd_colsum(dy, y, act, gb)
-        elif gb is not None:
-            K.colsum(dy.view(-1, dy.shape[-1]), gb)
+        ymask = y if act else None
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g)
+            dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act)
         gw = _wgrad_buf(w)
-        K.conv2d_wgrad(dy, x, g, gw)
+        K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act)
         return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None
 
 

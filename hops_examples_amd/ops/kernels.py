@@ -31,11 +31,13 @@ def act_id(act) -> int:
 
 # ---------------------------------------------------------------- dense GEMM
 def gemm_raw(a, lda, a_kc, b, ldb, b_kc, M, N, K, epi, out, ldo, bias=None, alpha=1.0, beta=0.0, act=0, aux=None,
-             ldaux=0, colsum=None, ws=None):
-    """ws: optional fp32 workspace (>= M*N) enabling split-K for small-M/long-K store epilogues."""
+             ldaux=0, colsum=None, ws=None, a_mask_y=None, a_mask_act=0, a_rowsum=None):
+    """ws: optional fp32 workspace (>= M*N) enabling split-K for small-M/long-K store epilogues.
+    a_mask_y/a_mask_act: multiply the A operand by act'(y) while staging it (prologue fusion).
+    a_rowsum: accumulate the row sums of the (masked) A operand (RC-A only; bias gradients)."""
     rc = _C.ext().gemm(ptr(a), lda, int(a_kc), ptr(b), ldb, int(b_kc), M, N, K, epi, ptr(out), ldo, ptr(bias),
                        float(alpha), float(beta), act_id(act), ptr(aux), ldaux, ptr(colsum), ptr(ws),
-                       0 if ws is None else ws.numel(), stream())
+                       0 if ws is None else ws.numel(), ptr(a_mask_y), act_id(a_mask_act), ptr(a_rowsum), stream())
     check(rc, "gemm")
 
 
@@ -61,8 +63,9 @@ def linear_fwd(x, w, bias=None, act=0, out=None, out_f32=False, colsum=None):
     return out
 
 
-def linear_dgrad(dy, w, yprev=None, act_prev=0, out=None, colsum=None):
-    """dx[M,K] = (dy[M,N] @ w[N,K]) * act'(yprev)  (+ column sum -> previous layer's bias grad)."""
+def linear_dgrad(dy, w, yprev=None, act_prev=0, out=None, colsum=None, y=None, act=0):
+    """dx[M,K] = ((dy * act'(y)) [M,N] @ w[N,K]) * act'(yprev)  (+ column sum -> previous layer's bias grad).
+    y/act: this layer's own activation output (mask fused into the A-operand staging)."""
     M, N = dy.shape
     K = w.shape[1]
     _req(dy, BF16, "dy")
@@ -70,18 +73,20 @@ def linear_dgrad(dy, w, yprev=None, act_prev=0, out=None, colsum=None):
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=BF16)
     gemm_raw(dy, N, True, w, K, False, M, K, N, EPI_DACT_BF16, out, K, act=act_prev if yprev is not None else 0,
-             aux=yprev, ldaux=K, colsum=colsum, ws=_splitk_ws(M, K, N, dy.device))
+             aux=yprev, ldaux=K, colsum=colsum, ws=_splitk_ws(M, K, N, dy.device), a_mask_y=y, a_mask_act=act)
     return out
 
 
-def linear_wgrad(dy, x, dw, alpha=1.0):
-    """dw[N,K] += dy[M,N]^T @ x[M,K]  (fp32 atomics, split-K over the batch)."""
+def linear_wgrad(dy, x, dw, alpha=1.0, y=None, act=0, dbias=None):
+    """dw[N,K] += (dy * act'(y))[M,N]^T @ x[M,K]  (fp32 atomics, split-K over the batch);
+    dbias[N] += column sums of the masked dy, computed while dy^T is staged."""
     M, N = dy.shape
     K = x.shape[1]
     _req(dy, BF16, "dy")
     _req(x, BF16, "x")
     _req(dw, F32, "dw")
-    gemm_raw(dy, N, False, x, K, False, N, K, M, EPI_ATOMIC_F32, dw, K, alpha=alpha)
+    gemm_raw(dy, N, False, x, K, False, N, K, M, EPI_ATOMIC_F32, dw, K, alpha=alpha, a_mask_y=y, a_mask_act=act,
+             a_rowsum=dbias)
     return dw
 
 
@@ -118,21 +123,27 @@ def conv2d_fwd(x, w, geom, bias=None, act=0, out=None, colsum=None):
     return out
 
 
-def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None):
+def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=None, act=0):
     _req(dy, BF16, "dy")
     B, H, W, C = geom[:4]
     if out is None:
         out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
     check(_C.ext().conv2d_dgrad(ptr(dy), ptr(w), geom, ptr(out), ptr(yprev), act_id(act_prev) if yprev is not None
-                                else 0, ptr(colsum), stream()), "conv2d_dgrad")
+                                else 0, ptr(colsum), ptr(y), act_id(act), stream()), "conv2d_dgrad")
     return out
 
 
-def conv2d_wgrad(dy, x, geom, dw):
+def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0):
+    """dw += (dy * act'(y))^T . im2col(x); dbias += per-channel sums of the masked dy."""
     _req(dy, BF16, "dy")
     _req(x, BF16, "x")
     _req(dw, F32, "dw")
-    check(_C.ext().conv2d_wgrad(ptr(dy), ptr(x), geom, ptr(dw), 0, stream()), "conv2d_wgrad")
+    KC = geom[7] * geom[8] * geom[3] * geom[6]
+    ws = None
+    if geom[7] * geom[8] * geom[3] <= 64 and KC <= 1024:  # small-K direct kernel: slab workspace
+        ws = torch.empty(1024 * (KC + geom[6]), device=dy.device, dtype=F32)
+    check(_C.ext().conv2d_wgrad(ptr(dy), ptr(x), geom, ptr(dw), ptr(dbias), ptr(y), act_id(act), ptr(ws),
+                                0 if ws is None else ws.numel(), stream()), "conv2d_wgrad")
     return dw
 
 

@@ -90,8 +90,9 @@ class TrainStep:
 
     def __call__(self, x, y):
         self._n += 1
-        if not self.use_graph or self._n <= self.warmup:
-            return self.eager(x, y)
+        if not self.use_graph or self._n <= self.warmup or (
+                self._sx is not None and (x.shape != self._sx.shape or y.shape != self._sy.shape)):
+            return self.eager(x, y)  # warm-up, or a ragged (e.g. last) batch the graph was not captured for
         if self._g1 is None:
             torch.cuda.synchronize()
             self._capture(x, y)

@@ -2,10 +2,13 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-out=gpurun_out/diag.log; : > $out
-for D in "" "direct_conv" "pool8" "rowreduce" "loss_thread" "splitk" "direct_conv,pool8,rowreduce,loss_thread,splitk"; do
-  HOPSX_DISABLE="$D" timeout -k 10 120 python tools/diag_div.py 256 1 >> $out 2>&1 || { echo "fail $D" >> $out; exit 1; }
-done
-timeout -k 10 120 python tools/diag_div.py 256 0 >> $out 2>&1 || exit 1
-timeout -k 10 120 python tools/diag_div.py 32 1 >> $out 2>&1 || exit 1
-bash tools/gpu_iter.sh it4
+out=gpurun_out/diag3.log; : > $out
+run() { timeout -k 10 150 python tools/diag_div2.py "$@" >> $out 2>&1 || { echo "fail $*" >> $out; exit 1; }; }
+run 32 1 400 0
+run 32 1 400 1
+run 32 0 400 0
+HOPSX_DISABLE=direct_conv run 32 1 400 0
+HOPSX_DISABLE=splitk run 32 1 400 0
+HOPSX_DISABLE=pool8 run 32 1 400 0
+HOPSX_DISABLE=direct_conv,pool8,splitk,loss_thread,rowreduce run 32 1 400 0
+run 256 1 400 0
