@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("HOPSX_BENCH_BATCH", "32")))
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-taxi", action="store_true")
-    ap.add_argument("--taxi-batch", type=int, default=512)
+    ap.add_argument("--taxi-batch", type=int, default=40)  # TFX taxi trainer batch
     return ap.parse_args()
 
 

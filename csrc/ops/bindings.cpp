@@ -106,15 +106,15 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_bn_bwd(P<void>(dy), P<void>(x), P<void>(y), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
                         P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), S(st));
   });
-  m.def("embedding_bag_fwd", [](u table, u idx, u offs, int nbags, int dim, long nidx, int mode, u out, int of32,
-                                long ldo, u st) {
-    return hopsx_embedding_bag_fwd(P<float>(table), P<long>(idx), P<long>(offs), nbags, dim, nidx, mode, P<void>(out),
-                                   of32, ldo, S(st));
+  m.def("embedding_bag_fwd", [](u table, u idx, u offs, int nbags, int dim, long nidx, int bag_len, int mode, u out,
+                                int of32, long ldo, u st) {
+    return hopsx_embedding_bag_fwd(P<float>(table), P<long>(idx), P<long>(offs), nbags, dim, nidx, bag_len, mode,
+                                   P<void>(out), of32, ldo, S(st));
   });
-  m.def("embedding_bag_bwd", [](u dout, int df32, long ldo, u idx, u offs, int nbags, int dim, long nidx, int mode,
-                                u dtable, u st) {
-    return hopsx_embedding_bag_bwd(P<void>(dout), df32, ldo, P<long>(idx), P<long>(offs), nbags, dim, nidx, mode,
-                                   P<float>(dtable), S(st));
+  m.def("embedding_bag_bwd", [](u dout, int df32, long ldo, u idx, u offs, int nbags, int dim, long nidx,
+                                int bag_len, int mode, u dtable, u st) {
+    return hopsx_embedding_bag_bwd(P<void>(dout), df32, ldo, P<long>(idx), P<long>(offs), nbags, dim, nidx, bag_len,
+                                   mode, P<float>(dtable), S(st));
   });
   m.def("column_stats", [](u x, int rows, int cols, u out, u st) {
     return hopsx_column_stats(P<float>(x), rows, cols, P<float>(out), S(st));

@@ -1,0 +1,144 @@
+"""Chicago-taxi wide & deep classifier ("big tipper": tips > 20% of the fare).
+
+The reference README names a TFX Chicago-taxi pipeline (README.md:99-112) whose
+notebooks are absent from the repo, so the model follows the public
+TFX taxi trainer it points to:
+
+* dense (DNN) inputs: trip_miles, fare, trip_seconds — z-scored by the Transform stage;
+* wide (linear) inputs: 13 identity-categorical columns —
+  4 bucketized lat/long columns (10 buckets each), 2 vocabulary columns
+  (payment_type, company: 1000 vocab + 10 OOV buckets) and 7 categorical columns
+  (trip_start_hour 24, trip_start_day 31, trip_start_month 12, pickup/dropoff census
+  tract 2000, pickup/dropoff community area 80) — 6,287 one-hot slots in total;
+* DNN hidden units [100, 70, 48, 34] (first_dnn_layer_size=100, num_dnn_layers=4,
+  dnn_decay_factor=0.7), logits = wide + deep, sigmoid cross-entropy;
+* optimizers as tf.estimator.DNNLinearCombinedClassifier: FTRL (lr 0.2) on the wide
+  part, Adagrad (lr 0.05, accumulator 0.1) on the deep part; train batch 40.
+
+MI355X mapping: the wide part is a fixed-length embedding-bag (13 rows of a
+[6287, 1] table per example, thread-per-bag gather / atomic scatter-add kernel);
+the deep part runs on the MFMA linear kernels with fused bias+ReLU epilogues; the
+two optimizers are single fused kernels over two slices of ONE parameter arena
+(so data parallelism all-reduces one flat buffer); the whole step is one hipGraph.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import nn as hnn
+from ..ops import functional as HF
+
+DENSE_FLOAT_FEATURE_KEYS = ["trip_miles", "fare", "trip_seconds"]
+BUCKET_FEATURE_KEYS = ["pickup_latitude", "pickup_longitude", "dropoff_latitude", "dropoff_longitude"]
+FEATURE_BUCKET_COUNT = 10
+VOCAB_FEATURE_KEYS = ["payment_type", "company"]
+VOCAB_SIZE, OOV_SIZE = 1000, 10
+CATEGORICAL_FEATURE_KEYS = ["trip_start_hour", "trip_start_day", "trip_start_month", "pickup_census_tract",
+                            "dropoff_census_tract", "pickup_community_area", "dropoff_community_area"]
+MAX_CATEGORICAL_FEATURE_VALUES = [24, 31, 12, 2000, 2000, 80, 80]
+LABEL_KEY = "tips"
+TRAIN_BATCH_SIZE = 40
+
+
+def hidden_units(first: int = 100, num_layers: int = 4, decay: float = 0.7) -> list[int]:
+    return [max(2, int(first * decay ** i)) for i in range(num_layers)]
+
+
+def wide_cardinalities() -> list[int]:
+    return ([FEATURE_BUCKET_COUNT] * len(BUCKET_FEATURE_KEYS) + [VOCAB_SIZE + OOV_SIZE] * len(VOCAB_FEATURE_KEYS)
+            + list(MAX_CATEGORICAL_FEATURE_VALUES))
+
+
+def wide_offsets() -> np.ndarray:
+    c = wide_cardinalities()
+    return np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64)
+
+
+WIDE_ROWS = int(sum(wide_cardinalities()))  # 6287
+N_WIDE = len(wide_cardinalities())  # 13
+
+
+class TaxiWideDeep(nn.Module):
+    def __init__(self, hidden=None):
+        super().__init__()
+        hidden = hidden or hidden_units()
+        # wide part first, deep part second: each is one contiguous slice of the arena
+        self.wide = nn.Module()
+        self.wide.weight = nn.Parameter(torch.zeros(WIDE_ROWS, 1))  # linear model init = 0 (tf.estimator)
+        layers, d = [], len(DENSE_FLOAT_FEATURE_KEYS)
+        for h in hidden:
+            layers.append(hnn.Linear(d, h, activation="relu"))
+            d = h
+        layers.append(hnn.Linear(d, 1, out_f32=True))
+        self.deep = nn.Sequential(*layers)
+
+    def forward(self, dense, cat):
+        """dense: [B, 3] z-scored floats; cat: [B, 13] int64 ids, already offset into the
+        concatenated one-hot space (see ``wide_offsets``). Returns fp32 logits [B, 1]."""
+        deep = self.deep(dense if not dense.is_cuda else HF.to_compute(dense))
+        wide = HF.embedding_bag(cat, self.wide.weight)
+        return deep.float() + wide
+
+
+def make_optimizer(model: TaxiWideDeep, ftrl_lr: float = 0.2, adagrad_lr: float = 0.05):
+    from .. import optim
+
+    return optim.Chain(optim.Ftrl(model.wide, lr=min(ftrl_lr, 1.0 / math.sqrt(N_WIDE))),
+                       optim.Adagrad(model.deep, lr=adagrad_lr, initial_accumulator_value=0.1))
+
+
+def synth_taxi(n: int, seed: int = 0, device="cpu"):
+    """Transformed-feature synthetic taxi trips with a learnable tip rule.
+    Returns dense [n, 3] f32, cat [n, 13] int64 (global one-hot ids), label [n, 1] f32."""
+    g = torch.Generator().manual_seed(seed)
+    dense = torch.randn(n, len(DENSE_FLOAT_FEATURE_KEYS), generator=g)
+    card = wide_cardinalities()
+    cols = []
+    for c in card:
+        if c == VOCAB_SIZE + OOV_SIZE:  # vocabulary columns are heavy-tailed
+            r = torch.rand(n, generator=g)
+            cols.append(torch.clamp((c * r ** 3).long(), max=c - 1))
+        else:
+            cols.append(torch.randint(0, c, (n,), generator=g))
+    cat = torch.stack(cols, 1) + torch.from_numpy(wide_offsets())
+    w_true = torch.randn(WIDE_ROWS, generator=g) * 0.5
+    logit = dense @ torch.tensor([0.8, -0.6, 0.3]) + w_true[cat].sum(1) * 0.5
+    label = (torch.rand(n, generator=g) < torch.sigmoid(logit)).float().unsqueeze(1)
+    dev = torch.device(device)
+    return dense.to(dev), cat.to(dev), label.to(dev)
+
+
+def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, graph: bool = True,
+               pool_examples: int = 200_000) -> dict:
+    """Steps/sec of the taxi trainer (per-GPU batch ``batch``; DP all-reduce when world > 1)."""
+    from ..parallel.dp import DataParallel
+    from ..runtime.arena import ParamArena
+    from ..runtime.step import TrainStep
+
+    model = TaxiWideDeep().to(dev)
+    ParamArena.from_module(model, dev)
+    opt = make_optimizer(model)
+    dp = DataParallel(model) if world > 1 else None
+    step = TrainStep(model, opt, "bce_logits", dp=dp, graph=graph, forward_fn=lambda m, x: m(*x))
+    nb = max(8, -(-pool_examples // batch))
+    dense, cat, label = synth_taxi(nb * batch, seed=7, device=dev)
+    dense = dense.to(torch.bfloat16).view(nb, batch, -1)
+    cat = cat.view(nb, batch, -1)
+    label = label.view(nb, batch, 1)
+    out = {}
+
+    def run(i):
+        j = i % nb
+        out["r"] = step((dense[j], cat[j]), label[j])
+
+    for i in range(warmup):
+        run(i)
+    el = timed(run, steps, dev)
+    loss = float(out["r"]["loss"].reshape(-1)[0])
+    return {"steps_per_sec": round(steps / el, 1), "examples_per_sec": round(batch * world * steps / el, 1),
+            "ms_per_step": round(el / steps * 1e3, 4), "batch_per_gpu": batch, "loss": round(loss, 4),
+            "params": sum(p.numel() for p in model.parameters()), "hidden_units": hidden_units()}

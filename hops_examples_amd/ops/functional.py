@@ -298,32 +298,39 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentu
 # ============================================================== embedding bag
 class _EmbagFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, idx, offsets, table, mode, nbags):
+    def forward(ctx, idx, offsets, table, mode, nbags, bag_len):
         out = torch.empty(nbags, table.shape[1], device=table.device, dtype=torch.float32)
-        K.embedding_bag_fwd(table.detach(), idx, offsets, mode, out)
+        K.embedding_bag_fwd(table.detach(), idx, offsets, mode, out, bag_len=bag_len)
         ctx.save_for_backward(idx, offsets if offsets is not None else torch.empty(0, device=idx.device))
-        ctx.p = (table, mode, nbags, offsets is not None)
+        ctx.p = (table, mode, nbags, offsets is not None, bag_len)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         idx, offs = ctx.saved_tensors
-        table, mode, nbags, has_offs = ctx.p
+        table, mode, nbags, has_offs, bag_len = ctx.p
         g = _wgrad_buf(table)
-        K.embedding_bag_bwd(dout.float().contiguous(), idx, offs if has_offs else None, mode, g, nbags)
-        return None, None, _ret_grad(table, g), None, None
+        K.embedding_bag_bwd(dout.float().contiguous(), idx, offs if has_offs else None, mode, g, nbags,
+                            bag_len=bag_len)
+        return None, None, _ret_grad(table, g), None, None, None
 
 
 def embedding_bag(idx, table, offsets=None, mode="sum"):
-    """idx: 1-D int64 (with offsets) or [B] (one index per bag). Returns fp32 [bags, dim]."""
+    """Sum/mean of embedding rows per bag -> fp32 [bags, dim].
+
+    idx: 1-D int64 with ``offsets`` (variable-length bags), [B] (one row per bag), or
+    [B, L] (fixed-length bags of L rows, e.g. the L categorical columns of a wide model)."""
     m = {"sum": 0, "mean": 1}[mode]
     if not table.is_cuda:
         if offsets is None:
-            return F.embedding(idx, table)
+            e = F.embedding(idx, table)
+            return e if idx.dim() == 1 else (e.sum(1) if m == 0 else e.mean(1))
         return F.embedding_bag(idx, table, offsets, mode=mode)
+    bag_len = idx.shape[1] if (offsets is None and idx.dim() == 2) else 1
     idx = idx.long().contiguous()
-    nb = idx.numel() if offsets is None else offsets.numel()
-    return _EmbagFn.apply(idx, None if offsets is None else offsets.long().contiguous(), table, m, nb)
+    nb = (idx.numel() // bag_len) if offsets is None else offsets.numel()
+    return _EmbagFn.apply(idx.reshape(-1), None if offsets is None else offsets.long().contiguous(), table, m, nb,
+                          bag_len)
 
 
 # ===================================================================== losses

@@ -298,19 +298,23 @@ def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None
 
 
 # ------------------------------------------------------------ embedding bag
-def embedding_bag_fwd(table, idx, offsets, mode, out, ldo=None):
+def embedding_bag_fwd(table, idx, offsets, mode, out, ldo=None, bag_len=1):
+    """Bags are given by ``offsets`` or, without offsets, by a fixed ``bag_len`` (idx [bags, bag_len])."""
     nb = out.shape[0] if offsets is None else offsets.numel()
     dim = table.shape[1]
-    check(_C.ext().embedding_bag_fwd(ptr(table), ptr(idx), ptr(offsets), nb, dim, idx.numel(), mode, ptr(out),
+    assert offsets is not None or idx.numel() == nb * bag_len, "idx / bag_len / out shape mismatch"
+    check(_C.ext().embedding_bag_fwd(ptr(table), ptr(idx), ptr(offsets), nb, dim, idx.numel(), bag_len, mode, ptr(out),
                                      int(out.dtype == F32), ldo if ldo is not None else out.stride(0), stream()),
           "embedding_bag_fwd")
     return out
 
 
-def embedding_bag_bwd(dout, idx, offsets, mode, dtable, nbags, ldo=None):
+def embedding_bag_bwd(dout, idx, offsets, mode, dtable, nbags, ldo=None, bag_len=1):
     dim = dtable.shape[1]
+    assert offsets is not None or idx.numel() == nbags * bag_len, "idx / bag_len mismatch"
     check(_C.ext().embedding_bag_bwd(ptr(dout), int(dout.dtype == F32), ldo if ldo is not None else dout.stride(0),
-                                     ptr(idx), ptr(offsets), nbags, dim, idx.numel(), mode, ptr(dtable), stream()),
+                                     ptr(idx), ptr(offsets), nbags, dim, idx.numel(), bag_len, mode, ptr(dtable),
+                                     stream()),
           "embedding_bag_bwd")
     return dtable
 

@@ -15,7 +15,7 @@ import math
 import torch
 
 from .ops._C import OPTIM
-from .runtime.arena import ParamArena
+from .runtime.arena import ALIGN, ParamArena
 
 
 def _arena_of(obj) -> ParamArena:
@@ -23,12 +23,36 @@ def _arena_of(obj) -> ParamArena:
         return obj
     if isinstance(obj, torch.nn.Module):
         a = getattr(obj, "_hx_arena", None)
-        return a if a is not None else ParamArena.from_module(obj)
+        if a is not None:
+            return a
+        params = [p for p in obj.parameters() if p.requires_grad]
+        a = getattr(params[0], "_hx_arena", None) if params else None
+        if a is not None and all(getattr(p, "_hx_arena", None) is a for p in params):
+            return a  # a sub-module of a model whose arena already exists
+        return ParamArena.from_module(obj)
     params = list(obj)
     arenas = {id(getattr(p, "_hx_arena", None)) for p in params}
     if len(arenas) == 1 and getattr(params[0], "_hx_arena", None) is not None:
         return params[0]._hx_arena
     return ParamArena(params)
+
+
+def _range_of(arena: ParamArena, obj) -> slice:
+    """The contiguous slice of the arena an optimizer owns: everything, or the span of a
+    sub-module / parameter subset (wide & deep: FTRL on the wide part, Adagrad on the deep)."""
+    if isinstance(obj, ParamArena) or (isinstance(obj, torch.nn.Module) and getattr(obj, "_hx_arena", None) is arena):
+        return slice(0, arena.numel)
+    params = [p for p in (obj.parameters() if isinstance(obj, torch.nn.Module) else obj) if p.requires_grad]
+    ids = {id(p) for p in params}
+    if ids == {id(p) for p in arena.params}:
+        return slice(0, arena.numel)
+    lo = min(p._hx_off for p in params)
+    hi = max(p._hx_off + -(-p.numel() // ALIGN) * ALIGN for p in params)
+    for p, o, _ in arena.ranges():
+        if lo <= o < hi and id(p) not in ids:
+            raise ValueError("optimizer parameter subset must be contiguous in the arena (register it as one "
+                             "sub-module)")
+    return slice(lo, hi)
 
 
 class FusedOptimizer:
@@ -37,6 +61,7 @@ class FusedOptimizer:
 
     def __init__(self, params, lr, weight_decay=0.0, **hp):
         self.arena = _arena_of(params)
+        self._sl = _range_of(self.arena, params)
         self.lr = float(lr)
         self.weight_decay = float(weight_decay)
         self.hp = hp
@@ -50,7 +75,7 @@ class FusedOptimizer:
             from .ops.functional import rng_state
 
             self.rng = rng_state(dev)
-        self._states = [self.arena.state(f"{self.kind}_s{i}") for i in range(self.nstate)]
+        self._states = [self.arena.state(f"{self.kind}_s{i}")[self._sl] for i in range(self.nstate)]
         self.param_groups = [{"params": self.arena.params, "lr": self.lr}]
 
     # hyper-parameter vector in the kernel's layout: lr, gscale, wd, a..e
@@ -65,13 +90,16 @@ class FusedOptimizer:
         if a.device.type == "cuda":
             from .ops import kernels as K
 
-            K.optim_step(OPTIM[self.kind], a.master, a.grad, s[0], s[1], s[2], a.shadow, self._hp(), self.step_count,
+            sl = self._sl
+            K.optim_step(OPTIM[self.kind], a.master[sl], a.grad[sl], s[0], s[1], s[2],
+                         a.shadow[sl] if a.shadow is not None else None, self._hp(), self.step_count,
                          zero_grad=True, arrive=self._arrive, rng=self.rng)
         else:
             self.step_count += 1
+            sl = self._sl
             with torch.no_grad():
-                self._cpu_step(a.master, a.grad * self.grad_scale, s, float(self.step_count.item()))
-                a.grad.zero_()
+                self._cpu_step(a.master[sl], a.grad[sl] * self.grad_scale, s, float(self.step_count.item()))
+                a.grad[sl].zero_()
             if a.shadow is not None:
                 a.refresh_shadow()
         return loss
@@ -224,6 +252,42 @@ class Ftrl(FusedOptimizer):
         z = s[0]
         new = -(z - torch.sign(z) * h["l1"]) / ((h["beta"] + nn_.sqrt()) / self.lr + 2 * h["l2"])
         p.copy_(torch.where(z.abs() <= h["l1"], torch.zeros_like(p), new))
+
+
+class Chain:
+    """Several fused optimizers over disjoint slices of one arena, stepped together
+    (one kernel launch each) — e.g. FTRL for a wide part + Adagrad for a deep part."""
+
+    def __init__(self, *opts: FusedOptimizer):
+        self.opts = list(opts)
+        self.arena = opts[0].arena
+        self.rng = opts[0].rng
+        self.param_groups = [g for o in opts for g in o.param_groups]
+
+    @property
+    def grad_scale(self):
+        return self.opts[0].grad_scale
+
+    @grad_scale.setter
+    def grad_scale(self, v):
+        for o in self.opts:
+            o.grad_scale = v
+
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for o in self.opts:
+            o.step()
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.arena.zero_grad()
+
+    def state_dict(self):
+        return {"opts": [o.state_dict() for o in self.opts]}
+
+    def load_state_dict(self, sd):
+        for o, s in zip(self.opts, sd["opts"]):
+            o.load_state_dict(s)
 
 
 _BY_NAME = {"sgd": SGD, "adam": Adam, "adamw": AdamW, "adadelta": Adadelta, "rmsprop": RMSprop, "adagrad": Adagrad,

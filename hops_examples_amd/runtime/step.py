@@ -23,7 +23,31 @@ from ..ops import functional as HF
 from ..parallel import dist as hdist
 
 
+def _clone(x):
+    return tuple(t.clone() for t in x) if isinstance(x, (tuple, list)) else x.clone()
+
+
+def _shape(x):
+    return tuple(t.shape for t in x) if isinstance(x, (tuple, list)) else x.shape
+
+
+def _same_storage(a, b):
+    if isinstance(a, (tuple, list)):
+        return all(u.data_ptr() == v.data_ptr() for u, v in zip(a, b))
+    return a.data_ptr() == b.data_ptr()
+
+
+def _copy_into(dst, src):
+    if isinstance(dst, (tuple, list)):
+        for d, s_ in zip(dst, src):
+            d.copy_(s_, non_blocking=True)
+    else:
+        dst.copy_(src, non_blocking=True)
+
+
 class TrainStep:
+    """``x`` may be a tensor or a tuple of tensors (e.g. dense + categorical inputs)."""
+
     def __init__(self, model, optimizer, loss_kind: str = "sparse_ce", dp=None, graph: bool = True, warmup: int = 3,
                  forward_fn=None):
         self.model, self.opt, self.loss_kind, self.dp = model, optimizer, loss_kind, dp
@@ -61,7 +85,7 @@ class TrainStep:
 
     # ------------------------------------------------------------- graph path
     def _capture(self, x, y):
-        self._sx = x.clone()
+        self._sx = _clone(x)
         self._sy = y.clone()
         world = hdist.world_size()
         overlap = None
@@ -91,14 +115,14 @@ class TrainStep:
     def __call__(self, x, y):
         self._n += 1
         if not self.use_graph or self._n <= self.warmup or (
-                self._sx is not None and (x.shape != self._sx.shape or y.shape != self._sy.shape)):
+                self._sx is not None and (_shape(x) != _shape(self._sx) or y.shape != self._sy.shape)):
             return self.eager(x, y)  # warm-up, or a ragged (e.g. last) batch the graph was not captured for
         if self._g1 is None:
             torch.cuda.synchronize()
             self._capture(x, y)
             torch.cuda.synchronize()
-        if x.data_ptr() != self._sx.data_ptr():
-            self._sx.copy_(x, non_blocking=True)
+        if not _same_storage(x, self._sx):
+            _copy_into(self._sx, x)
             self._sy.copy_(y, non_blocking=True)
         self._g1.replay()
         if self._g2 is not None:
