@@ -78,6 +78,12 @@ class FusedOptimizer:
         self._states = [self.arena.state(f"{self.kind}_s{i}")[self._sl] for i in range(self.nstate)]
         self.param_groups = [{"params": self.arena.params, "lr": self.lr}]
 
+    def restrict(self, sl: slice) -> "FusedOptimizer":
+        """Own only ``sl`` of the arena (sharded parameter-server mode: each rank updates its shard)."""
+        self._sl = sl
+        self._states = [self.arena.state(f"{self.kind}_s{i}")[sl] for i in range(self.nstate)]
+        return self
+
     # hyper-parameter vector in the kernel's layout: lr, gscale, wd, a..e
     def _hp(self) -> list[float]:
         raise NotImplementedError
@@ -87,6 +93,9 @@ class FusedOptimizer:
         self.lr = self.param_groups[0]["lr"]
         a = self.arena
         s = self._states + [None] * (3 - len(self._states))
+        if self._sl.stop <= self._sl.start:  # empty shard (sharded PS mode): nothing to update
+            self.step_count += 1
+            return loss
         if a.device.type == "cuda":
             from .ops import kernels as K
 
@@ -272,6 +281,12 @@ class Chain:
     def grad_scale(self, v):
         for o in self.opts:
             o.grad_scale = v
+
+    def restrict(self, sl: slice) -> "Chain":
+        for o in self.opts:
+            lo, hi = max(o._sl.start, sl.start), min(o._sl.stop, sl.stop)
+            o.restrict(slice(lo, max(lo, hi)))
+        return self
 
     def step(self, closure=None):
         loss = closure() if closure is not None else None

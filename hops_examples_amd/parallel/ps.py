@@ -1,0 +1,118 @@
+"""Parameter-server mode as a sharded update over RCCL (``experiment.parameter_server``;
+the reference names it in prose and sets ``spark.tensorflow.num.ps``,
+notebooks/ml/Experiment/Tensorflow/mnist.ipynb:52, jobs-client/spark/job_config.json:13).
+
+A TF parameter server owns a slice of the variables, receives every worker's
+gradients for that slice, applies the optimizer and serves the new values.  On one
+MI355X node the same data flow maps onto collectives with every GPU acting as both
+worker and server for 1/world of the flat parameter arena:
+
+  1. reduce-scatter the fp32 gradient buffer  -> rank r holds the summed grads of shard r
+  2. the fused optimizer kernel updates ONLY shard r (fp32 master + optimizer state of
+     that shard live only meaningfully on its owner: optimizer memory / world)
+  3. all-gather the updated bf16 compute weights (2 bytes/param on the wire, half of
+     an fp32 all-reduce's second phase)
+
+Bytes per step per GPU: ~ (world-1)/world * (4N + 2N) vs 2*(world-1)/world * 4N for a
+ring all-reduce — 25% less traffic on the xGMI links, and the optimizer runs on 1/world
+of the parameters.  fp32 masters of non-owned shards go stale; ``gather_master()``
+reassembles them for checkpoints.  Requires an arena padded to world*ALIGN
+(``ParamArena.from_module(m, pad_multiple=world * ALIGN)``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..runtime.arena import ALIGN, ParamArena
+from . import dist as hdist
+
+
+class ShardedPS:
+    def __init__(self, model_or_arena, optimizer=None):
+        self.arena: ParamArena = model_or_arena if isinstance(model_or_arena, ParamArena) else \
+            model_or_arena._hx_arena
+        self.world = hdist.world_size()
+        self.rank = hdist.rank()
+        n = self.arena.numel
+        if n % (self.world * ALIGN):
+            raise ValueError(f"arena of {n} elements is not padded to world*{ALIGN}; build it with "
+                             f"pad_multiple={self.world * ALIGN}")
+        self.shard = n // self.world
+        self.sl = slice(self.rank * self.shard, (self.rank + 1) * self.shard)
+        self.overlap = False
+        self._gloo = dist.is_initialized() and dist.get_backend() == "gloo"
+        if self.world > 1:
+            hdist.broadcast_(self.arena.master, 0)
+            self.arena.refresh_shadow()
+        if optimizer is not None:
+            self.attach(optimizer)
+
+    def attach(self, optimizer):
+        optimizer.restrict(self.sl)
+        optimizer.grad_scale = self.grad_scale()
+        return optimizer
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+    # ---- step phases (TrainStep calls finish()/allreduce_all() then the optimizer then post_step())
+    def _reduce_scatter(self):
+        if self.world <= 1:
+            return
+        g = self.arena.grad
+        if self._gloo:  # gloo has no reduce-scatter: all-reduce, keep the owned shard
+            dist.all_reduce(g)
+        else:
+            dist.reduce_scatter_tensor(g[self.sl], g)
+
+    def finish(self):
+        self._reduce_scatter()
+
+    allreduce_all = finish
+
+    def post_step(self):
+        a = self.arena
+        if self.world > 1:
+            # non-owned grad shards were consumed by their owners; clear ours for the next step
+            a.grad.zero_()
+            if a.shadow is not None:
+                if self._gloo:
+                    parts = list(a.shadow.float().chunk(self.world))
+                    dist.all_gather(parts, a.shadow[self.sl].float())
+                    a.shadow.copy_(torch.cat(parts))
+                else:
+                    dist.all_gather_into_tensor(a.shadow, a.shadow[self.sl].clone())
+            else:  # CPU arenas have no shadow: gather the fp32 masters (= the compute weights)
+                self._gather(a.master)
+
+    def _gather(self, t):
+        if self._gloo:
+            parts = list(t.chunk(self.world))
+            dist.all_gather(parts, t[self.sl].clone())
+            t.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(t, t[self.sl].clone())
+
+    def gather_master(self) -> torch.Tensor:
+        if self.world > 1:
+            self._gather(self.arena.master)
+        return self.arena.master
+
+    def close(self):
+        pass
+
+
+def make(model, optimizer, mode: str | None = None):
+    """The data-parallel engine for ``HOPSX_DP_MODE`` (mirrored / collective_allreduce -> DataParallel,
+    parameter_server -> ShardedPS)."""
+    import os
+
+    from .dp import DataParallel
+
+    mode = mode or os.environ.get("HOPSX_DP_MODE", "mirrored")
+    if hdist.world_size() <= 1:
+        return None
+    if mode == "parameter_server":
+        return ShardedPS(model, optimizer)
+    return DataParallel(model)

@@ -22,7 +22,7 @@ ALIGN = 64
 
 
 class ParamArena:
-    def __init__(self, params, device=None, shadow: bool | None = None):
+    def __init__(self, params, device=None, shadow: bool | None = None, pad_multiple: int = ALIGN):
         params = [p for p in params if p.requires_grad]
         seen, uniq = set(), []
         for p in params:
@@ -37,7 +37,8 @@ class ParamArena:
         for p in uniq:
             offs.append(n)
             n += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-        self.numel = max(n, ALIGN)
+        pad = max(ALIGN, int(pad_multiple))
+        self.numel = max(-(-n // pad) * pad, pad)  # sharded (PS) modes need numel % (world*ALIGN) == 0
         self.offsets = offs
         self.master = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
         self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
@@ -65,10 +66,10 @@ class ParamArena:
 
     # ------------------------------------------------------------------ api
     @classmethod
-    def from_module(cls, module: torch.nn.Module, device=None) -> "ParamArena":
+    def from_module(cls, module: torch.nn.Module, device=None, pad_multiple: int = ALIGN) -> "ParamArena":
         if device is not None:
             module.to(device)
-        arena = cls(list(module.parameters()), device=device)
+        arena = cls(list(module.parameters()), device=device, pad_multiple=pad_multiple)
         module._hx_arena = arena
         return arena
 

@@ -76,11 +76,16 @@ class TrainStep:
         if self.device.type != "cuda" or getattr(self.opt, "rng", None) is None:
             HF.advance_rng(self.device)  # on the GPU the optimizer kernel advances the RNG itself
 
+    def _post(self):
+        if self.dp is not None and hasattr(self.dp, "post_step"):
+            self.dp.post_step()  # sharded PS: all-gather the updated weights
+
     def eager(self, x, y):
         r = self._fwd_bwd(x, y)
         if self.dp is not None:
             self.dp.finish()
         self._opt()
+        self._post()
         return r
 
     # ------------------------------------------------------------- graph path
@@ -89,7 +94,7 @@ class TrainStep:
         self._sy = y.clone()
         world = hdist.world_size()
         overlap = None
-        if self.dp is not None:
+        if self.dp is not None and hasattr(self.dp, "_on_ready"):
             overlap, self.dp.overlap = self.dp.overlap, False
             from . import hooks
 
@@ -102,6 +107,8 @@ class TrainStep:
                 if self.dp is not None:
                     self.dp.allreduce_all()
                 self._opt()
+                if self.graph_collectives:
+                    self._post()
         self._g1 = g1
         if world > 1 and self.dp is not None and not self.graph_collectives:
             g2 = torch.cuda.CUDAGraph()
@@ -128,4 +135,5 @@ class TrainStep:
         if self._g2 is not None:
             self.dp.allreduce_all()
             self._g2.replay()
+            self._post()
         return self._out

@@ -1,0 +1,105 @@
+"""Data-parallel engines on CPU with gloo, world_size 2: bucket planning,
+DataParallel gradient averaging == single-process large-batch gradients, sharded parameter
+server == DataParallel trajectory, dist self-test."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+
+
+def _data(rank):
+    g = torch.Generator().manual_seed(100 + rank)
+    return torch.randn(16, 8, generator=g), torch.randint(0, 4, (16,), generator=g)
+
+
+def _worker(rank, world, port, mode, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from hops_examples_amd import optim
+    from hops_examples_amd.parallel import dist as hdist
+    from hops_examples_amd.parallel import ps as P
+    from hops_examples_amd.parallel.dp import DataParallel
+    from hops_examples_amd.runtime.arena import ALIGN, ParamArena
+    from hops_examples_amd.runtime.step import TrainStep
+
+    hdist.init(backend="gloo")
+    assert hdist.self_test()
+    m = _model()
+    ParamArena.from_module(m, pad_multiple=world * ALIGN)
+    opt = optim.Adam(m, lr=0.01)
+    dp = P.make(m, opt, mode)
+    assert isinstance(dp, P.ShardedPS if mode == "parameter_server" else DataParallel)
+    step = TrainStep(m, opt, "sparse_ce", dp=dp, graph=False)
+    x, y = _data(rank)
+    for _ in range(5):
+        step(x, y)
+    master = dp.gather_master() if hasattr(dp, "gather_master") else m._hx_arena.master
+    q.put((rank, master.clone()))
+    hdist.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def _run(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+def _single_process_reference():
+    from hops_examples_amd import optim
+    from hops_examples_amd.runtime.arena import ParamArena
+    from hops_examples_amd.runtime.step import TrainStep
+
+    m = _model()
+    ParamArena.from_module(m, pad_multiple=128)
+    opt = optim.Adam(m, lr=0.01)
+    step = TrainStep(m, opt, "sparse_ce", graph=False)
+    (x0, y0), (x1, y1) = _data(0), _data(1)
+    x, y = torch.cat([x0, x1]), torch.cat([y0, y1])
+    for _ in range(5):
+        step(x, y)
+    return m._hx_arena.master.clone()
+
+
+@pytest.mark.parametrize("mode", ["mirrored", "parameter_server"])
+def test_dp_matches_large_batch(mode):
+    res = _run(mode)
+    ref = _single_process_reference()
+    torch.testing.assert_close(res[0], res[1])  # replicas stay identical
+    torch.testing.assert_close(res[0], ref, atol=1e-5, rtol=1e-4)
+
+
+def test_bucket_plan():
+    from hops_examples_amd.parallel.dp import plan_buckets
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    small = ParamArena(list(_model().parameters()))
+    assert len(plan_buckets(small, 25.0)) == 1  # < 10 MB: one bucket
+    big = ParamArena([torch.nn.Parameter(torch.zeros(1 << 20)) for _ in range(12)])  # 48 MB
+    b = plan_buckets(big, 16.0)
+    assert b[-1][0] == 0 and b[0][1] == big.numel
+    assert all(s < e for s, e, _ in b) and all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
+    assert 2 <= len(b) <= 4
