@@ -1,0 +1,46 @@
+"""Image inference helpers and sharded batch inference (notebooks/ml/Inference/*) on CPU with
+a small CIFAR ResNet: preprocessing, decode_predictions ordering, per-shard Parquet output,
+malformed images skipped."""
+import numpy as np
+import pytest
+
+
+def _tiny_resnet():
+    import functools
+
+    from hops_examples_amd.models.resnet import cifar_resnet
+
+    return functools.partial(cifar_resnet, 8, num_classes=5)  # importable builder for the worker processes
+
+
+def test_decode_and_preprocess():
+    from hops_examples_amd import inference as I
+
+    p = np.array([[0.1, 0.7, 0.2], [0.5, 0.2, 0.3]])
+    d = I.decode_predictions(p, top=2)
+    assert [x[1] for x in d[0]] == ["class_1", "class_2"] and d[1][0][2] == 0.5
+    x = I.preprocess_input(np.zeros((1, 2, 2, 3), np.uint8) + np.array([1, 2, 3], np.uint8))
+    assert np.allclose(x[0, 0, 0], [3 - 103.939, 2 - 116.779, 1 - 123.68])
+
+
+def test_batch_predict_shards(project_root, monkeypatch):
+    from PIL import Image
+
+    from hops_examples_amd import inference as I
+
+    monkeypatch.setenv("HOPSX_NUM_GPUS", "0")
+    d = project_root / "images"
+    d.mkdir(parents=True)
+    rng = np.random.default_rng(0)
+    paths = []
+    for i in range(7):
+        p = d / f"img_{i}.png"
+        Image.fromarray(rng.integers(0, 255, (40, 48, 3), dtype=np.uint8)).save(p)
+        paths.append(str(p))
+    (d / "broken.png").write_bytes(b"not an image")
+    paths.append(str(d / "broken.png"))
+    df = I.batch_predict(_tiny_resnet(), paths, "Resources/labels.parquet", batch_size=3, num_workers=2)
+    assert sorted(df.image_path) == sorted(paths[:7])
+    assert {"top1_label", "top2_label", "top3_label"} <= set(df.columns)
+    assert (df.top1_score >= df.top2_score).all()
+    assert len(list((project_root / "Resources" / "labels.parquet").glob("part-*.parquet"))) == 2
