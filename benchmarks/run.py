@@ -1,0 +1,249 @@
+"""Benchmark harness for every BASELINE.json config (+ the reference's ResNet-50 benchmark notebook).
+
+    python benchmarks/run.py <config> [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 benchmarks/run.py <config>
+
+configs:
+  mnist_launch_cpu   MNIST 2-layer CNN through experiment.launch on CPU (plumbing; images/s)
+  mnist_mirrored     MNIST CNN (E3, 1.39M params) bf16, DP over RCCL (images/s)       == bench.py
+  taxi               Chicago-taxi wide & deep trainer (steps/s)
+  titanic            Titanic TD (Parquet) -> HBM ingest (GB/s) + 7.8k-param DNN (steps/s)
+  cifar_resnet       CIFAR-10 ResNet-20/56, collective all-reduce (images/s)
+  resnet50           ResNet-50 224x224, RMSprop(0.2), batch 8/GPU as benchmark.ipynb (images/s)
+
+Every run prints one JSON line (rank 0) with the whole-job value; data are synthetic with the
+real shapes, weights random-init.  Timing: warmup untimed, then K steps between a barrier +
+device synchronize on both sides, max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from hops_examples_amd.parallel import dist as hdist  # noqa: E402
+
+
+def timed(fn, n, dev):
+    hdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(n):
+        fn(i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    hdist.barrier()
+    return hdist.all_reduce_scalar(time.perf_counter() - t0, "max")
+
+
+def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=None):
+    from hops_examples_amd.parallel import ps as P
+    from hops_examples_amd.runtime.step import TrainStep
+
+    dp = P.make(model, opt) if world > 1 else None
+    st = TrainStep(model, opt, kind, dp=dp, graph=dev.type == "cuda", forward_fn=forward_fn)
+    nb = len(xs)
+    box = {}
+
+    def run(i):
+        box["r"] = st(xs[i % nb], ys[i % nb])
+
+    for i in range(warmup):
+        run(i)
+    el = timed(run, steps, dev)
+    return el, float(box["r"]["loss"].reshape(-1)[0])
+
+
+def _emit(rank, metric, value, unit, steps, warmup, el, world, cfg, extra=None):
+    if rank != 0:
+        return
+    rec = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": steps,
+           "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "dtype": "bf16", "data": "synthetic", "config": cfg}
+    if extra:
+        rec.update(extra)
+    print(json.dumps(rec), flush=True)
+
+
+def cfg_mnist_mirrored(a, dev, rank, world):
+    from hops_examples_amd import optim
+    from hops_examples_amd.models.mnist import MirroredMnistCNN
+    from hops_examples_amd.runtime.arena import ALIGN, ParamArena
+
+    B = a.batch or 32
+    m = MirroredMnistCNN().to(dev)
+    ParamArena.from_module(m, dev, pad_multiple=max(1, world) * ALIGN)
+    opt = optim.Adadelta(m, lr=1.0)
+    nb = max(8, -(-61440 // B))
+    xs = torch.randint(0, 256, (nb, B, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (nb, B), device=dev)
+    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world)
+    _emit(rank, "images/sec MNIST CNN (E3) DP", B * world * a.steps / el, "images/sec", a.steps, a.warmup, el, world,
+          {"model": "MirroredMnistCNN 1,394,282 params", "per_gpu_batch": B, "parallelism": f"dp{world}"},
+          {"final_loss": round(loss, 4)})
+
+
+def cfg_mnist_launch_cpu(a, dev, rank, world):
+    from hops_examples_amd import experiment
+
+    steps, B = a.steps, a.batch or 32
+
+    def train():
+        import time as _t
+
+        import torch as _torch
+
+        from hops_examples_amd import optim as _optim
+        from hops_examples_amd.models.mnist import KerasMnistCNN
+        from hops_examples_amd.runtime.arena import ParamArena as _PA
+        from hops_examples_amd.runtime.step import TrainStep as _TS
+
+        _torch.set_num_threads(max(1, (os.cpu_count() or 2) // 2))
+        m = KerasMnistCNN()
+        _PA.from_module(m)
+        st = _TS(m, _optim.Adadelta(m, lr=1.0), "sparse_ce", graph=False)
+        x = _torch.randint(0, 256, (B, 28, 28, 1), dtype=_torch.uint8)
+        y = _torch.randint(0, 10, (B,))
+        for _ in range(2):
+            st(x, y)
+        t0 = _t.perf_counter()
+        for _ in range(steps):
+            r = st(x, y)
+        el = _t.perf_counter() - t0
+        return {"images_per_sec": B * steps / el, "elapsed": el, "loss": float(r["loss"])}
+
+    os.environ.setdefault("HOPSX_NUM_GPUS", "0")
+    t0 = time.perf_counter()
+    _, res = experiment.launch(train, name="mnist_launch_cpu")
+    wall = time.perf_counter() - t0
+    _emit(rank, "images/sec MNIST 2-layer CNN via experiment.launch on CPU", res["images_per_sec"], "images/sec",
+          steps, 2, res["elapsed"], 1, {"model": "KerasMnistCNN 239,594 params", "per_gpu_batch": B,
+                                        "parallelism": "cpu"},
+          {"dtype": "fp32", "launch_wall_s": round(wall, 2)})
+
+
+def cfg_taxi(a, dev, rank, world):
+    from hops_examples_amd.models.widedeep import TRAIN_BATCH_SIZE, bench_taxi
+
+    B = a.batch or TRAIN_BATCH_SIZE
+    r = bench_taxi(dev, B, a.steps, a.warmup, timed, world, graph=dev.type == "cuda")
+    _emit(rank, "steps/sec Chicago-taxi wide&deep", r["steps_per_sec"], "steps/sec", a.steps, a.warmup,
+          r["ms_per_step"] * a.steps / 1e3, world, {"model": f"TaxiWideDeep {r['params']} params", "per_gpu_batch": B,
+                                                     "parallelism": f"dp{world}"},
+          {"examples_per_sec": r["examples_per_sec"], "final_loss": r["loss"]})
+
+
+def cfg_titanic(a, dev, rank, world):
+    """Parquet TD -> pinned host -> HBM ingest rate, then DNN training steps/s on the resident data."""
+    import numpy as np
+    import pandas as pd
+
+    from hops_examples_amd import keras, optim
+    from hops_examples_amd.models.zoo import titanic_dnn
+    from hops_examples_amd.runtime.arena import ALIGN, ParamArena
+
+    B = a.batch or 10
+    n = a.rows
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"hopsx_titanic_{n}_{rank}.parquet")
+    if not os.path.exists(path):
+        rng = np.random.default_rng(rank)
+        df = pd.DataFrame({"pclass": rng.integers(1, 4, n), "sex": rng.integers(0, 2, n),
+                           "fare": rng.gamma(2.0, 16.0, n).astype(np.float32), "age": rng.normal(30, 12, n),
+                           "sibsp": rng.integers(0, 5, n), "parch": rng.integers(0, 4, n)})
+        df["survived"] = ((df.sex == 1) ^ (rng.random(n) < 0.2)).astype(np.float32)
+        df.to_parquet(path, index=False)
+    hdist.barrier()
+    import pyarrow.parquet as pq
+
+    t0 = time.perf_counter()
+    tbl = pq.read_table(path)
+    feats = np.stack([tbl.column(c).to_numpy().astype(np.float32) for c in
+                      ["pclass", "sex", "fare", "age", "sibsp", "parch"]], 1)
+    lab = tbl.column("survived").to_numpy().astype(np.float32)
+    host = torch.from_numpy(feats).pin_memory() if dev.type == "cuda" else torch.from_numpy(feats)
+    xd = host.to(dev, non_blocking=True)
+    yd = torch.from_numpy(lab).to(dev, non_blocking=True)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    ingest = time.perf_counter() - t0
+    gbps = (feats.nbytes + lab.nbytes) / ingest / 1e9
+    m = titanic_dnn()
+    m.build((6,))
+    net = m.net.to(dev)
+    ParamArena.from_module(net, dev, pad_multiple=max(1, world) * ALIGN)
+    opt = optim.Adam(net, lr=1e-3, eps=1e-7)
+    nb = n // B
+    xs = xd[: nb * B].view(nb, B, 6)
+    ys = yd[: nb * B].view(nb, B, 1)
+    el, loss = _train_loop(net, opt, "bce", xs, ys, a.steps, a.warmup, dev, world)
+    _emit(rank, "steps/sec Titanic TD -> DNN", a.steps / el, "steps/sec", a.steps, a.warmup, el, world,
+          {"model": f"titanic_dnn {m.count_params()} params", "per_gpu_batch": B, "parallelism": f"dp{world}",
+           "rows": n}, {"ingest_GBps_parquet_to_hbm": round(gbps, 3), "final_loss": round(loss, 4)})
+    _ = keras
+
+
+def cfg_cifar_resnet(a, dev, rank, world):
+    from hops_examples_amd import optim
+    from hops_examples_amd.models.resnet import cifar_resnet
+    from hops_examples_amd.runtime.arena import ALIGN, ParamArena
+
+    B = a.batch or 128
+    m = cifar_resnet(a.depth).to(dev)
+    ParamArena.from_module(m, dev, pad_multiple=max(1, world) * ALIGN)
+    opt = optim.SGD(m, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    nb = 16
+    xs = torch.randint(0, 256, (nb, B, 32, 32, 3), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (nb, B), device=dev)
+    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world)
+    _emit(rank, f"images/sec CIFAR-10 ResNet-{a.depth} collective all-reduce", B * world * a.steps / el, "images/sec",
+          a.steps, a.warmup, el, world, {"model": f"ResNet-{a.depth}", "per_gpu_batch": B,
+                                          "parallelism": f"dp{world}"}, {"final_loss": round(loss, 4)})
+
+
+def cfg_resnet50(a, dev, rank, world):
+    from hops_examples_amd import optim
+    from hops_examples_amd.models.resnet import resnet50
+    from hops_examples_amd.runtime.arena import ALIGN, ParamArena
+
+    B = a.batch or 8
+    m = resnet50().to(dev)
+    ParamArena.from_module(m, dev, pad_multiple=max(1, world) * ALIGN)
+    opt = optim.RMSprop(m, lr=0.2)
+    nb = 4
+    xs = torch.randint(0, 256, (nb, B, 224, 224, 3), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 1000, (nb, B), device=dev)
+    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world)
+    _emit(rank, "images/sec ResNet-50 224x224 (benchmark.ipynb)", B * world * a.steps / el, "images/sec", a.steps,
+          a.warmup, el, world, {"model": "ResNet-50 25,557,032 params", "per_gpu_batch": B,
+                                "parallelism": f"dp{world}"}, {"final_loss": round(loss, 4)})
+
+
+CONFIGS = {"mnist_launch_cpu": cfg_mnist_launch_cpu, "mnist_mirrored": cfg_mnist_mirrored, "taxi": cfg_taxi,
+           "titanic": cfg_titanic, "cifar_resnet": cfg_cifar_resnet, "resnet50": cfg_resnet50}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--depth", type=int, default=20)
+    ap.add_argument("--rows", type=int, default=891 * 1000)
+    a = ap.parse_args()
+    rank, _, world = hdist.init()
+    dev = hdist.device()
+    torch.manual_seed(1234 + rank)
+    CONFIGS[a.config](a, dev, rank, world)
+
+
+if __name__ == "__main__":
+    main()

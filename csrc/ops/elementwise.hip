@@ -167,3 +167,26 @@ extern "C" int hopsx_add_bf16(const void* a, const void* b, void* out, long n, i
                      (bf16_raw*)out, n, act);
   return (int)hipGetLastError();
 }
+
+
+// Zero-fill as a KERNEL node.  hipMemsetAsync inside a captured hipGraph becomes a runtime
+// blit node; replays showed it intermittently not ordered before the split-K atomics that
+// follow it (garbage accumulators -> exploding logits), so every in-graph clear goes through
+// this kernel instead.
+__global__ __launch_bounds__(256) void zero_k(uint32_t* __restrict__ p, long n32) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n128 = ((uintptr_t)p % 16 == 0) ? (n32 >> 2) : 0;
+  for (long j = i; j < n128; j += stride) ((uint4*)p)[j] = make_uint4(0u, 0u, 0u, 0u);
+  for (long j = (n128 << 2) + i; j < n32; j += stride) p[j] = 0u;
+}
+
+extern "C" int hopsx_zero(void* p, long bytes, hipStream_t st) {
+  if (!p || bytes <= 0) return 0;
+  const long n32 = bytes / 4;  // callers clear fp32 / int32 buffers
+  long g = (n32 / 4 + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(zero_k, dim3(g), dim3(256), 0, st, (uint32_t*)p, n32);
+  return (int)hipGetLastError();
+}

@@ -94,7 +94,7 @@ extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long
                  aact};
   DenseLoader bl{(const bf16_raw*)B, ldb, is_vec_ok(B, ldb)};
   if (ws && epi != EPI_ATOMIC_F32 && (long)M * N <= ws_elems && want_splitk(M, N, K)) {
-    hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), st);
+    hopsx_zero(ws, (long)M * N * sizeof(float), st);
     int rc = hopsx_gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, EPI_ATOMIC_F32, ws, N, nullptr, 1.f, 0.f, 0, nullptr, 0,
                         nullptr, nullptr, 0, ay, aact, arowsum, st);
     if (rc) return rc;

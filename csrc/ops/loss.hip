@@ -235,8 +235,8 @@ extern "C" int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, 
     if (grid > 1024) grid = 1024;
   }
   if (grid > 1) {
-    if (loss_sum) hipMemsetAsync(loss_sum, 0, sizeof(float), st);
-    if (correct) hipMemsetAsync(correct, 0, sizeof(int), st);
+    if (loss_sum) hopsx_zero(loss_sum, sizeof(float), st);
+    if (correct) hopsx_zero(correct, sizeof(int), st);
   }
   hipLaunchKernelGGL(loss_k, dim3(grid), dim3(block), 0, st, kind, logits, logits_f32, target, B, C, grad_scale,
                      loss_sum, correct, dlogits, dlogits_f32, per_thread);

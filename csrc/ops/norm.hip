@@ -127,8 +127,8 @@ static int ew_grid(long n) {
 extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
                                   float* rstd_out, float* running_mean, float* running_var, float momentum,
                                   float eps, int M, int C, const void* residual, int act, hipStream_t st) {
-  hipMemsetAsync(mean_out, 0, C * sizeof(float), st);
-  hipMemsetAsync(rstd_out, 0, C * sizeof(float), st);
+  hopsx_zero(mean_out, C * sizeof(float), st);
+  hopsx_zero(rstd_out, C * sizeof(float), st);
   int gx, gy, rpb;
   slab_grid(M, C, gx, gy, rpb);
   hipLaunchKernelGGL(bn_stats_k, dim3(gx, gy), dim3(256), 0, st, (const bf16_raw*)x, mean_out, rstd_out, M, C, rpb);
@@ -152,7 +152,7 @@ extern "C" int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, co
 extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                             const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C,
                             int act, void* dresidual, hipStream_t st) {
-  hipMemsetAsync(ws, 0, 2 * C * sizeof(float), st);
+  hopsx_zero(ws, 2 * C * sizeof(float), st);
   int gx, gy, rpb;
   slab_grid(M, C, gx, gy, rpb);
   hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(gx, gy), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,

@@ -74,6 +74,9 @@ int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamm
                  const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
                  void* dresidual, hipStream_t st);
 
+// ---- zero-fill kernel (elementwise.hip): graph-safe replacement for hipMemsetAsync ----
+int hopsx_zero(void* p, long bytes, hipStream_t st);
+
 // ---- embedding bag (embedding.hip) ----
 int hopsx_embedding_bag_fwd(const float* table, const long* idx, const long* offsets, int nbags, int dim,
                             long nidx, int bag_len, int mode, void* out, int out_f32, long ldo, hipStream_t st);

@@ -45,7 +45,9 @@ def export(model_path: str, model_name: str, model_version: int | None = None, o
            metrics: dict | None = None, description: str | None = None, synchronous: bool = True,
            synchronous_timeout: int = 120, project: str | None = None) -> str:
     """Copy a model file/directory into the registry as a new (or given) version."""
-    src = Path(hdfs.abs_path(model_path)) if not os.path.isabs(str(model_path)) else Path(model_path)
+    # a local (cwd-relative) path first, as the reference exports from the executor's local dir,
+    # then the project filesystem
+    src = Path(model_path) if Path(model_path).exists() else Path(hdfs.abs_path(model_path))
     if not src.exists():
         raise FileNotFoundError(model_path)
     versions = _versions(model_name)

@@ -66,3 +66,10 @@ def fashion_mnist_cnn(kernel: int = 3, pool: int = 2, dropout: float = 0.45) -> 
         K.layers.Dropout(dropout),
         K.layers.Dense(10),
     ])
+
+
+def mnist_mlp_net():
+    """The built module of :func:`mnist_mlp` (serving rebuilds exported models from this)."""
+    m = mnist_mlp()
+    m.build()
+    return m.net

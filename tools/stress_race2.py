@@ -26,7 +26,7 @@ g = torch.cuda.CUDAGraph()
 with torch.cuda.graph(g):
     fb()
 a.grad.zero_(); g.replay(); torch.cuda.synchronize()
-ref, oref = a.grad.clone(), box["out"].float().clone()
+ref, oref = a.grad.clone(), box["out"].detach().float().clone()
 m0, s0, x0 = a.master.clone(), a.shadow.clone(), x.clone()
 dbuf = torch.empty_like(ref); dmax = torch.zeros(N, device=dev); omax = torch.zeros(N, device=dev)
 obuf = torch.empty_like(oref)
@@ -36,11 +36,11 @@ for i in range(N):
     if variant == "noalloc":
         torch.sub(a.grad, ref, out=dbuf); dbuf.abs_()
         torch.amax(dbuf, dim=0, out=dmax[i])
-        obuf.copy_(box["out"]); obuf.sub_(oref).abs_()
+        obuf.copy_(box["out"].detach()); obuf.sub_(oref).abs_()
         torch.amax(obuf.view(-1), dim=0, out=omax[i])
     else:
         dmax[i] = (a.grad - ref).abs().max()
-        omax[i] = (box["out"].float() - oref).abs().max()
+        omax[i] = (box["out"].detach().float() - oref).abs().max()
         if variant == "poison":
             p = torch.full((16 << 20,), float("nan"), device=dev)
             del p
