@@ -114,8 +114,9 @@ class StorageConnector:
     def read(self, query: str | None = None, data_format: str | None = None, path: str | None = None):
         if self.connector_type in ("JDBC", "REDSHIFT", "SNOWFLAKE", "SQLITE"):
             db = self.connection_string or self.path
-            if db and db.startswith("jdbc:sqlite:"):
-                db = db[len("jdbc:sqlite:"):]
+            for pre in ("jdbc:sqlite:", "sqlite:///"):
+                if db and db.startswith(pre):
+                    db = db[len(pre):]
             with sqlite3.connect(db) as c:
                 return pd.read_sql_query(query, c)
         p = Path(path or self.path)

@@ -75,9 +75,10 @@ class CifarResNet(nn.Module):
         self.pool = hnn.GlobalAvgPool2d()
         self.fc = hnn.Linear(cin, num_classes, init="torch", out_f32=True)
         self.depth = depth
+        _norm_buffers(self)
 
     def forward(self, x):
-        x = _as_nhwc_image(x)
+        x = _as_nhwc_image(x, self.img_shift, self.img_scale)
         return self.fc(self.pool(self.blocks(self.stem(x))))
 
 
@@ -94,9 +95,10 @@ class ResNet50(nn.Module):
         self.blocks = nn.Sequential(*blocks)
         self.pool = hnn.GlobalAvgPool2d()
         self.fc = hnn.Linear(cin, num_classes, init="torch", out_f32=True)
+        _norm_buffers(self)
 
     def forward(self, x):
-        x = _as_nhwc_image(x)
+        x = _as_nhwc_image(x, self.img_shift, self.img_scale)
         return self.fc(self.pool(self.blocks(self.maxpool(self.stem(x)))))
 
 
@@ -104,14 +106,22 @@ _MEAN = (0.4914, 0.4822, 0.4465)
 _STD = (0.2470, 0.2435, 0.2616)
 
 
-def _as_nhwc_image(x):
+def _norm_buffers(m):
+    """Per-channel (x/255 - mean)/std folded into one scale/shift pair, kept as buffers so the
+    normalisation is capture-safe (no host->device constants inside a hipGraph)."""
+    import torch
+
+    std = torch.tensor(_STD)
+    m.register_buffer("img_scale", 1.0 / (255.0 * std), persistent=False)
+    m.register_buffer("img_shift", -torch.tensor(_MEAN) / std, persistent=False)
+
+
+def _as_nhwc_image(x, shift, scale):
     """uint8 NHWC images are normalised per channel on the device; float inputs pass through."""
     import torch
 
     if x.dtype == torch.uint8:
-        mean = torch.tensor(_MEAN, device=x.device) * 255
-        inv = 1.0 / (torch.tensor(_STD, device=x.device) * 255)
-        y = (x.float() - mean) * inv
+        y = torch.addcmul(shift, x, scale)  # one fused elementwise pass: shift + x * scale
         return y.to(torch.bfloat16) if x.is_cuda else y
     return x
 
