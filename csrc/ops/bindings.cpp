@@ -29,17 +29,19 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                       alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), P<float>(ws), ws_elems, P<void>(ay), aact,
                       P<float>(arowsum), S(st));
   });
-  m.def("conv2d_fwd", [](u x, u w, std::vector<int> g, int epi, u out, u bias, int act, u colsum, u st) {
+  m.def("conv2d_fwd", [](u x, u w, std::vector<int> g, int epi, u out, u bias, int act, u colsum, float xscale,
+                         float xshift, u st) {
     return hopsx_conv2d_fwd(P<void>(x), P<void>(w), g.data(), epi, P<void>(out), P<float>(bias), act,
-                            P<float>(colsum), S(st));
+                            P<float>(colsum), xscale, xshift, S(st));
   });
   m.def("conv2d_dgrad", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact, u st) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
                               P<void>(y), yact, S(st));
   });
-  m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems, u st) {
+  m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
+                           float xscale, float xshift, u st) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,
-                              P<float>(ws), ws_elems, S(st));
+                              P<float>(ws), ws_elems, xscale, xshift, S(st));
   });
   m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
                             int sw, int ph, int pw, float p, u rng, unsigned salt, u st) {

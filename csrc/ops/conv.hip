@@ -25,7 +25,13 @@ static ConvGeom make_geom(const int* g) {
 // gather per element; here each thread owns (pixel, 4 output channels), the
 // weights sit in LDS as fp32, and outputs leave as 8-byte stores.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void conv_direct_fwd_k(const bf16_raw* __restrict__ x,
+// Input element of the direct kernels: bf16 activations, or raw uint8 pixels scaled on
+// the fly (the u8->[0,1] normalisation of the input layer fused away: xscale != 0).
+__device__ __forceinline__ float in_at(const void* x, float xscale, float xshift, long i) {
+  return xscale != 0.f ? fmaf((float)((const uint8_t*)x)[i], xscale, xshift) : bf2f(((const bf16_raw*)x)[i]);
+}
+
+__global__ __launch_bounds__(256) void conv_direct_fwd_k(const void* __restrict__ x, float xscale, float xshift,
                                                          const bf16_raw* __restrict__ w,
                                                          const float* __restrict__ bias, bf16_raw* __restrict__ y,
                                                          ConvGeom g, int act) {
@@ -54,9 +60,9 @@ __global__ __launch_bounds__(256) void conv_direct_fwd_k(const bf16_raw* __restr
       for (int kw = 0; kw < g.KW; ++kw) {
         const int iw = ow * g.sw - g.pw + kw * g.dw;
         const bool in = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        const bf16_raw* xp = x + (((long)b * g.H + ih) * g.W + iw) * g.C;
+        const long xo = (((long)b * g.H + ih) * g.W + iw) * g.C;
         for (int ci = 0; ci < g.C; ++ci, ++k) {
-          const float xv = in ? bf2f(xp[ci]) : 0.f;
+          const float xv = in ? in_at(x, xscale, xshift, xo + ci) : 0.f;
           const float* wr = sw + k * g.CO + cg * 4;
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[j] += xv * wr[j];
@@ -141,6 +147,90 @@ __global__ __launch_bounds__(1024) void conv_direct_wgrad_k(const bf16_raw* __re
   }
 }
 
+// Small-K weight gradient (K = KH*KW*C <= 16, CO % 8 == 0): the input layers of the MNIST
+// models.  Work item = (output pixel, group of 8 output channels); a thread owns one channel
+// group for its whole life (the grid stride is a multiple of CO/8), loads dY (and y for the
+// fused act' mask) as 16-B vectors, keeps acc[8][K+1] (last column = bias) in registers and
+// processes UNROLL items per trip with all loads issued up front, so the loads are
+// independent (the old (k, co)-per-thread walk was a chain of dependent L2 round trips).
+// Lanes with the same channel group are reduced with xor-shuffles, waves through LDS, and
+// each workgroup adds its partial into dW/db with one fp32 atomic per element (<= 128
+// workgroups, so same-address contention stays small).
+template <int KK>
+__global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __restrict__ dy, const void* __restrict__ x,
+                                                          float xscale, float xshift, float* __restrict__ dw,
+                                                          float* __restrict__ dbias, const bf16_raw* __restrict__ y,
+                                                          int yact, ConvGeom g, long total) {
+  constexpr int UNROLL = 4;
+  const int G = g.CO >> 3;
+  const int cg = threadIdx.x % G;
+  float acc[8][KK + 1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int k = 0; k <= KK; ++k) acc[j][k] = 0.f;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long base = (long)blockIdx.x * blockDim.x + threadIdx.x; base < total; base += UNROLL * stride) {
+    bf16x8 dv[UNROLL], yv[UNROLL];
+    float xv[UNROLL][KK];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const long idx = base + u * stride;
+      const bool ok = idx < total;
+      const long p = ok ? idx / G : 0;
+      dv[u] = ok ? *(const bf16x8*)(dy + p * g.CO + cg * 8) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (y) yv[u] = ok ? *(const bf16x8*)(y + p * g.CO + cg * 8) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      const int pi = (int)p;
+      const int b = g.fOHW.div(pi), rem = pi - b * (g.OH * g.OW);
+      const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
+#pragma unroll
+      for (int k = 0; k < KK; ++k) {
+        const int ci = k % g.C, t = k / g.C;  // KK is small; the compiler folds what it can
+        const int kw = t % g.KW, kh = t / g.KW;
+        const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
+        const bool in = ok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        xv[u][k] = in ? in_at(x, xscale, xshift, (((long)b * g.H + ih) * g.W + iw) * g.C + ci) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = bf2f((uint16_t)dv[u][j]);
+        if (y) d *= act_grad_from_out(bf2f((uint16_t)yv[u][j]), yact);
+#pragma unroll
+        for (int k = 0; k < KK; ++k) acc[j][k] += d * xv[u][k];
+        acc[j][KK] += d;
+      }
+    }
+  }
+  // lanes l, l+G, l+2G, ... hold the same channel group
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int k = 0; k <= KK; ++k)
+      for (int o = G; o < 64; o <<= 1) acc[j][k] += __shfl_xor(acc[j][k], o, 64);
+  __shared__ float red[4][32][8 * (KK + 1)];  // [wave][channel group][8*(K+1)], G <= 32
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane < G) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int k = 0; k <= KK; ++k) red[wave][lane][j * (KK + 1) + k] = acc[j][k];
+  }
+  __syncthreads();
+  const int nel = G * 8 * (KK + 1);
+  for (int e = threadIdx.x; e < nel; e += blockDim.x) {
+    const int grp = e / (8 * (KK + 1)), r = e - grp * (8 * (KK + 1));
+    const float s = red[0][grp][r] + red[1][grp][r] + red[2][grp][r] + red[3][grp][r];
+    const int j = r / (KK + 1), k = r - j * (KK + 1);
+    const int co = grp * 8 + j;
+    if (s == 0.f) continue;
+    if (k < KK) atomicAdd(dw + (long)co * KK + k, s);
+    else if (dbias) atomicAdd(dbias + co, s);
+  }
+}
+
 // sums the per-workgroup partials: element e < KC is dW[co][k] (slab index r = k*CO + co),
 // e >= KC the bias of channel e - KC
 // one workgroup per output element: 256 lanes stride over the workgroup partials
@@ -170,15 +260,18 @@ static bool direct_ok(const ConvGeom& g) {
 }
 
 extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out,
-                                const float* bias, int act, float* colsum, hipStream_t st) {
+                                const float* bias, int act, float* colsum, float xscale, float xshift,
+                                hipStream_t st) {
   ConvGeom g = make_geom(geom);
   const int M = g.B * g.OH * g.OW, N = g.CO, K = g.KH * g.KW * g.C;
-  if (epi == EPI_STORE_BF16 && !colsum && direct_ok(g) && ((uintptr_t)out % 8 == 0)) {
+  const bool direct = epi == EPI_STORE_BF16 && !colsum && direct_ok(g) && ((uintptr_t)out % 8 == 0);
+  if (xscale != 0.f && !direct) return -3;  // uint8 inputs are only fused into the direct kernel
+  if (direct) {
     long total = (long)M * (N / 4);
     long grid = (total + 255) / 256;
     if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(conv_direct_fwd_k, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), st,
-                       (const bf16_raw*)x, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act);
+    hipLaunchKernelGGL(conv_direct_fwd_k, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), st, x, xscale,
+                       xshift, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act);
     return (int)hipGetLastError();
   }
   Im2colLoader al{(const bf16_raw*)x, g, (g.C % 8 == 0) && ((uintptr_t)x % 16 == 0)};
@@ -212,10 +305,32 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
 }
 
 // dW[co][k] += sum_m dY[m][co] * im2col(X)[m][k]; db[co] += sum_m dY[m][co] when colsum given
+static bool smallk_ok(const ConvGeom& g, const void* dy, const void* y) {
+  const int K = g.KH * g.KW * g.C;
+  return (K == 4 || K == 9 || K == 16) && g.CO % 8 == 0 && g.CO <= 256 && ((uintptr_t)dy % 16 == 0) &&
+         ((uintptr_t)y % 16 == 0) && !hopsx_disabled("smallk_wgrad");
+}
+
 extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias,
-                                  const void* y, int yact, float* ws, long ws_elems, hipStream_t st) {
+                                  const void* y, int yact, float* ws, long ws_elems, float xscale, float xshift,
+                                  hipStream_t st) {
   ConvGeom g = make_geom(geom);
   const int M = g.CO, N = g.KH * g.KW * g.C, K = g.B * g.OH * g.OW;
+  if (smallk_ok(g, dy, y)) {
+    const long total = (long)K * (g.CO / 8);
+    long blocks = (total + 1023) / 1024;  // >= 4 work items per thread
+    if (blocks > 128) blocks = 128;
+    if (blocks < 1) blocks = 1;
+#define HOPSX_SMALLK(KK)                                                                                      \
+  hipLaunchKernelGGL(conv_wgrad_smallk_k<KK>, dim3(blocks), dim3(256), 0, st, (const bf16_raw*)dy, x, xscale, xshift, dw, \
+                     dbias, (const bf16_raw*)y, yact, g, total)
+    if (N == 4) HOPSX_SMALLK(4);
+    else if (N == 9) HOPSX_SMALLK(9);
+    else HOPSX_SMALLK(16);
+#undef HOPSX_SMALLK
+    return (int)hipGetLastError();
+  }
+  if (xscale != 0.f) return -3;
   if (direct_ok(g)) {
     const int KC = N * M;
     int R = 1024 / KC;

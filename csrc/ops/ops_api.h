@@ -12,15 +12,16 @@ extern "C" {
 int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K, int epi,
                void* out, long ldo, const float* bias, float alpha, float beta, int act, const void* aux, long ldaux,
                float* colsum, float* ws, long ws_elems, const void* ay, int aact, float* arowsum, hipStream_t st);
+// xscale != 0: x is uint8 and is read as x * xscale + xshift (input-layer normalisation fused; direct kernel only)
 int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out, const float* bias, int act,
-                     float* colsum, hipStream_t st);
+                     float* colsum, float xscale, float xshift, hipStream_t st);
 // y/yact: this conv's activation output -> fused act' mask on dY (prologue fusion)
 int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act,
                        float* colsum, const void* y, int yact, hipStream_t st);
 // dbias (optional) receives sum over pixels of the (masked) dY = the conv bias gradient
 // ws (optional, >= 1024*(K*CO+CO) floats): slab workspace for the small-K direct kernel
 int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias, const void* y,
-                       int yact, float* ws, long ws_elems, hipStream_t st);
+                       int yact, float* ws, long ws_elems, float xscale, float xshift, hipStream_t st);
 
 // ---- pooling (pool.hip) ----
 // optional fused dropout on the pooled output (p > 0, rng/salt as hopsx_dropout_fwd)

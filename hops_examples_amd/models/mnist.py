@@ -26,24 +26,29 @@ from ..ops import functional as HF
 from ..ops import kernels as K
 
 
-def _as_nhwc(x: torch.Tensor, scale: float, shift: float) -> torch.Tensor:
+def _as_nhwc(x: torch.Tensor) -> torch.Tensor:
     if x.dim() == 2:
         x = x.view(x.shape[0], 28, 28, 1)
     elif x.dim() == 3:
         x = x.unsqueeze(-1)
-    if x.dtype == torch.uint8:
-        if x.is_cuda:
-            return K.u8_normalize(x.contiguous(), scale, shift)
-        return x.float() * scale + shift
     return x
 
 
 class _ImageModel(nn.Module):
+    """uint8 images go straight into conv1, which applies ``x * input_scale + input_shift``
+    itself (fused into its kernels on the GPU when the layer qualifies)."""
+
     input_scale = 1.0 / 255.0
     input_shift = 0.0
 
+    def __init__(self):
+        super().__init__()
+
+    def _set_input_affine(self):
+        self.conv1.in_affine = (self.input_scale, self.input_shift)
+
     def prep(self, x):
-        return _as_nhwc(x, self.input_scale, self.input_shift)
+        return _as_nhwc(x)
 
 
 class KerasMnistCNN(_ImageModel):
@@ -56,6 +61,7 @@ class KerasMnistCNN(_ImageModel):
         self.fc1 = hnn.Dense(s * s * 64, 128, activation="relu")
         self.drop2 = hnn.Dropout(dropout)
         self.fc2 = hnn.Dense(128, num_classes)
+        self._set_input_affine()
 
     def forward(self, x):
         x = self.conv2(self.conv1(self.prep(x)))
@@ -73,6 +79,7 @@ class MirroredMnistCNN(_ImageModel):
         self.pool = hnn.MaxPool2d(2, dropout=0.01)  # MaxPool2D + Dropout(0.01) fused
         self.fc1 = hnn.Dense(13 * 13 * 64, 128, activation="relu")
         self.fc2 = hnn.Dense(128, num_classes)
+        self._set_input_affine()
 
     def forward(self, x):
         x = self.conv2(self.conv1(self.prep(x)))
@@ -90,6 +97,7 @@ class FashionMnistCNN(_ImageModel):
         self.fc1 = hnn.Dense(s * s * 64, 128, activation="relu")
         self.drop2 = hnn.Dropout(dropout)
         self.fc2 = hnn.Dense(128, num_classes)
+        self._set_input_affine()
 
     def forward(self, x):
         x = self.conv2(self.conv1(self.prep(x)))
@@ -109,6 +117,7 @@ class TorchMnistNet(_ImageModel):
         self.conv2 = hnn.Conv2d(20, 50, 5, activation="relu", init="torch")
         self.fc1 = hnn.Linear(4 * 4 * 50, 500, activation="relu", init="torch")
         self.fc2 = hnn.Linear(500, num_classes, init="torch")
+        self._set_input_affine()
 
     def forward(self, x):
         x = HF.max_pool2d(self.conv1(self.prep(x)), 2)

@@ -73,6 +73,7 @@ class Conv2d(nn.Module):
         kh, kw = (kernel_size, kernel_size) if isinstance(kernel_size, int) else kernel_size
         self.cfg = dict(stride=stride, padding=padding, dilation=dilation)
         self.activation = activation
+        self.in_affine = None  # (scale, shift) when this layer receives raw uint8 pixels
         self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, (kh, kw)
         fan_in, fan_out = in_channels * kh * kw, out_channels * kh * kw
         if init == "glorot":
@@ -90,7 +91,7 @@ class Conv2d(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, x):
-        return HF.conv2d(x, self.weight, self.bias, act=self.activation, **self.cfg)
+        return HF.conv2d(x, self.weight, self.bias, act=self.activation, in_affine=self.in_affine, **self.cfg)
 
     def extra_repr(self):
         return f"{self.in_channels}, {self.out_channels}, k={self.kernel_size}, {self.cfg}, act={self.activation}"

@@ -103,13 +103,13 @@ def _pad_same(k, d=1):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, dilation, act):
+    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None):
         x = x.contiguous()
         wb = _arena.weight_bf16(w)
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
-        y = K.conv2d_fwd(x, wb, g, bias=b, act=act)
+        y = K.conv2d_fwd(x, wb, g, bias=b, act=act, in_affine=in_affine)
         ctx.save_for_backward(x, y)
-        ctx.w, ctx.b, ctx.g, ctx.act = w, b, g, act
+        ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine = w, b, g, act, in_affine
         return y
 
     @staticmethod
@@ -123,12 +123,16 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act)
         gw = _wgrad_buf(w)
-        K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act)
-        return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None
+        K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
+        return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None)
 
 
-def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None):
-    """NHWC conv. x [B,H,W,C], w [CO,KH,KW,C]. padding: int, tuple, 'valid' or 'same' (stride 1)."""
+def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None):
+    """NHWC conv. x [B,H,W,C], w [CO,KH,KW,C]. padding: int, tuple, 'valid' or 'same' (stride 1).
+
+    ``in_affine=(scale, shift)`` with a uint8 ``x``: the input layer's normalisation
+    ``x * scale + shift``; on the GPU it is fused into the conv kernels when the layer
+    qualifies (K.conv_u8_fusable), otherwise applied by one normalisation pass first."""
     st = (stride, stride) if isinstance(stride, int) else tuple(stride)
     dl = (dilation, dilation) if isinstance(dilation, int) else tuple(dilation)
     if padding == "valid":
@@ -138,6 +142,17 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None):
     else:
         pd = (padding, padding) if isinstance(padding, int) else tuple(padding)
     a = ACT[act] if not isinstance(act, int) else act
+    if x.dtype == torch.uint8:
+        sc, sh = in_affine or (1.0, 0.0)
+        if not x.is_cuda:
+            x = x.float() * sc + sh
+        elif padding != "same" or (w.shape[1] % 2 == 1 and w.shape[2] % 2 == 1):
+            g = K.conv_geom(x.shape, w.shape, st, pd, dl)
+            if K.conv_u8_fusable(g):
+                return _Conv2dFn.apply(x, w, b, st, pd, dl, a, (float(sc), float(sh)))
+            x = K.u8_normalize(x.contiguous(), float(sc), float(sh))
+        else:
+            x = K.u8_normalize(x.contiguous(), float(sc), float(sh))
     if not x.is_cuda:
         xr = x.float().permute(0, 3, 1, 2)
         if padding == "same" and (w.shape[1] % 2 == 0 or w.shape[2] % 2 == 0):
@@ -151,7 +166,7 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None):
         th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
         x = F.pad(to_compute(x), (0, 0, tw // 2, tw - tw // 2, th // 2, th - th // 2))
         pd = (0, 0)
-    return _Conv2dFn.apply(to_compute(x), w, b, st, pd, dl, a)
+    return _Conv2dFn.apply(to_compute(x), w, b, st, pd, dl, a, None)
 
 
 # ==================================================================== pooling

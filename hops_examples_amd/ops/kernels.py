@@ -7,6 +7,8 @@ the caller (the fused optimizers zero them after consuming them).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _C
@@ -111,15 +113,26 @@ def conv_geom(x_shape, w_shape, stride, padding, dilation):
     return [B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw, dh, dw]
 
 
-def conv2d_fwd(x, w, geom, bias=None, act=0, out=None, colsum=None):
-    _req(x, BF16, "x")
+def conv_u8_fusable(geom) -> bool:
+    """The uint8 input layer can skip its normalisation pass: the direct forward kernel and the
+    small-K weight-gradient kernel both read raw pixels (x * scale + shift) themselves."""
+    K = geom[7] * geom[8] * geom[3]
+    CO = geom[6]
+    return K in (4, 9, 16) and CO % 8 == 0 and CO <= 256 and K * CO <= 1024 and \
+        "u8_fuse" not in os.environ.get("HOPSX_DISABLE", "")
+
+
+def conv2d_fwd(x, w, geom, bias=None, act=0, out=None, colsum=None, in_affine=None):
+    """in_affine=(scale, shift): x is raw uint8 and is normalised inside the kernel."""
+    _req(x, torch.uint8 if in_affine else BF16, "x")
     _req(w, BF16, "w")
     B, OH, OW, CO = geom[0], geom[4], geom[5], geom[6]
     if out is None:
         out = torch.empty(B, OH, OW, CO, device=x.device, dtype=BF16)
     epi = EPI_STORE_F32 if out.dtype == F32 else EPI_STORE_BF16
-    check(_C.ext().conv2d_fwd(ptr(x), ptr(w), geom, epi, ptr(out), ptr(bias), act_id(act), ptr(colsum), stream()),
-          "conv2d_fwd")
+    sc, sh = (float(in_affine[0]), float(in_affine[1])) if in_affine else (0.0, 0.0)
+    check(_C.ext().conv2d_fwd(ptr(x), ptr(w), geom, epi, ptr(out), ptr(bias), act_id(act), ptr(colsum), sc, sh,
+                              stream()), "conv2d_fwd")
     return out
 
 
@@ -133,17 +146,22 @@ def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=N
     return out
 
 
-def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0):
-    """dw += (dy * act'(y))^T . im2col(x); dbias += per-channel sums of the masked dy."""
+def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0, in_affine=None):
+    """dw += (dy * act'(y))^T . im2col(x); dbias += per-channel sums of the masked dy.
+    in_affine=(scale, shift): x is the raw uint8 input (see conv_u8_fusable)."""
     _req(dy, BF16, "dy")
-    _req(x, BF16, "x")
+    _req(x, torch.uint8 if in_affine else BF16, "x")
     _req(dw, F32, "dw")
-    KC = geom[7] * geom[8] * geom[3] * geom[6]
+    K = geom[7] * geom[8] * geom[3]
+    KC = K * geom[6]
     ws = None
-    if geom[7] * geom[8] * geom[3] <= 64 and KC <= 1024:  # small-K direct kernel: slab workspace
+    smallk = K in (4, 9, 16) and geom[6] % 8 == 0 and geom[6] <= 256 and "smallk_wgrad" not in \
+        os.environ.get("HOPSX_DISABLE", "")
+    if not smallk and K <= 64 and KC <= 1024:  # older direct kernel: slab workspace
         ws = torch.empty(1024 * (KC + geom[6]), device=dy.device, dtype=F32)
+    sc, sh = (float(in_affine[0]), float(in_affine[1])) if in_affine else (0.0, 0.0)
     check(_C.ext().conv2d_wgrad(ptr(dy), ptr(x), geom, ptr(dw), ptr(dbias), ptr(y), act_id(act), ptr(ws),
-                                0 if ws is None else ws.numel(), stream()), "conv2d_wgrad")
+                                0 if ws is None else ws.numel(), sc, sh, stream()), "conv2d_wgrad")
     return dw
 
 

@@ -1,0 +1,85 @@
+"""Numerics of the second-generation kernels vs fp32 PyTorch references: small-K conv weight
+gradient (register-accumulated, shuffle/LDS reduced) with the fused act' mask, and the uint8
+input layer with its normalisation fused into the direct forward and the wgrad kernels."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from hops_examples_amd.ops import kernels as K  # noqa: E402
+
+dev = torch.device("cuda", 0)
+bf = torch.bfloat16
+
+
+def _ref_wgrad(dy, x, k, act_y=None):
+    # dy [B,OH,OW,CO] (bf16 values), x [B,H,W,C] float; returns dW [CO,KH,KW,C], db [CO]
+    d = dy.float()
+    if act_y is not None:
+        d = d * (act_y.float() > 0).float()
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(False)
+    CO = d.shape[-1]
+    w = torch.zeros(CO, x.shape[-1], k, k, device=dev, requires_grad=True)
+    out = F.conv2d(xr, w)
+    out.backward(d.permute(0, 3, 1, 2))
+    return w.grad.permute(0, 2, 3, 1).reshape(CO, -1), d.sum((0, 1, 2))
+
+
+@pytest.mark.parametrize("k,C,CO,B,H", [(2, 1, 32, 32, 28), (3, 1, 32, 7, 28), (4, 1, 32, 5, 28), (2, 4, 16, 3, 20),
+                                        (3, 1, 64, 2, 12)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_smallk_wgrad(k, C, CO, B, H, masked):
+    torch.manual_seed(0)
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    OH = H - k + 1
+    dy = torch.randn(B, OH, OH, CO, device=dev).to(bf)
+    y = torch.relu(torch.randn(B, OH, OH, CO, device=dev)).to(bf) if masked else None
+    g = K.conv_geom(x.shape, (CO, k, k, C), (1, 1), (0, 0), (1, 1))
+    dw = torch.zeros(CO, k * k * C, device=dev)
+    db = torch.zeros(CO, device=dev)
+    K.conv2d_wgrad(dy, x, g, dw, dbias=db, y=y, act="relu" if masked else 0)
+    rw, rb = _ref_wgrad(dy, x, k, y)
+    torch.testing.assert_close(dw, rw, atol=2e-2 * rw.abs().max().item(), rtol=1e-2)
+    torch.testing.assert_close(db, rb, atol=2e-2 * rb.abs().max().item() + 1e-3, rtol=1e-2)
+
+
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_u8_fused_input_layer(k):
+    torch.manual_seed(1)
+    B, H, CO = 16, 28, 32
+    xu = torch.randint(0, 256, (B, H, H, 1), dtype=torch.uint8, device=dev)
+    sc, sh = 1 / 255.0, -0.5
+    xf = xu.float() * sc + sh
+    w = (torch.randn(CO, k, k, 1, device=dev) * 0.3).to(bf)
+    b = torch.randn(CO, device=dev) * 0.1
+    g = K.conv_geom(xu.shape, w.shape, (1, 1), (0, 0), (1, 1))
+    assert K.conv_u8_fusable(g)
+    y = K.conv2d_fwd(xu, w, g, bias=b, act="relu", in_affine=(sc, sh))
+    ref = torch.relu(F.conv2d(xf.permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b)).permute(0, 2, 3, 1)
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+    dy = torch.randn_like(y)
+    dw = torch.zeros(CO, k * k, device=dev)
+    K.conv2d_wgrad(dy, xu, g, dw, y=y, act="relu", in_affine=(sc, sh))
+    rw, _ = _ref_wgrad(dy, xf, k, y)
+    torch.testing.assert_close(dw, rw, atol=2e-2 * rw.abs().max().item(), rtol=1e-2)
+
+
+def test_mnist_models_use_fused_input_path():
+    from hops_examples_amd.models.mnist import MirroredMnistCNN, TorchMnistNet
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    for cls in (MirroredMnistCNN, TorchMnistNet):  # fused (K=4) and unfused (K=25) input layers
+        torch.manual_seed(0)
+        cpu = cls()
+        gpu = cls().to(dev)
+        gpu.load_state_dict(cpu.state_dict())
+        ParamArena.from_module(gpu)
+        x = torch.randint(0, 256, (8, 28, 28, 1), dtype=torch.uint8)
+        y = torch.randint(0, 10, (8,))
+        lc = HF.loss(cpu.eval()(x), y)
+        lg = HF.loss(gpu.eval()(x.to(dev)), y.to(dev))
+        assert abs(lc.item() - lg.item()) < 0.03 * max(1.0, lc.item()), (cls.__name__, lc.item(), lg.item())
