@@ -24,10 +24,10 @@ PYBIND11_MODULE(_hopsx_ops, m) {
 
   m.def("gemm", [](u A, long lda, int akc, u B, long ldb, int bkc, int M, int N, int K, int epi, u out, long ldo,
                    u bias, float alpha, float beta, int act, u aux, long ldaux, u colsum, u ws, long ws_elems, u ay,
-                   int aact, u arowsum, u st) {
+                   int aact, u arowsum, u tickets, u st) {
     return hopsx_gemm(P<void>(A), lda, akc, P<void>(B), ldb, bkc, M, N, K, epi, P<void>(out), ldo, P<float>(bias),
                       alpha, beta, act, P<void>(aux), ldaux, P<float>(colsum), P<float>(ws), ws_elems, P<void>(ay), aact,
-                      P<float>(arowsum), S(st));
+                      P<float>(arowsum), P<unsigned>(tickets), S(st));
   });
   m.def("conv2d_fwd", [](u x, u w, std::vector<int> g, int epi, u out, u bias, int act, u colsum, float xscale,
                          float xshift, u st) {
@@ -39,9 +39,9 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                               P<void>(y), yact, S(st));
   });
   m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
-                           float xscale, float xshift, u st) {
+                           float xscale, float xshift, u counter, u st) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,
-                              P<float>(ws), ws_elems, xscale, xshift, S(st));
+                              P<float>(ws), ws_elems, xscale, xshift, P<unsigned>(counter), S(st));
   });
   m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
                             int sw, int ph, int pw, float p, u rng, unsigned salt, u st) {

@@ -12,6 +12,14 @@ typedef uint16_t bf16_raw;
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Branch-free masking for gathers: load from a clamped (always valid) address, then zero the
+// value unless `keep`.  A `cond ? load : 0` makes hipcc branch around each load and wait
+// vmcnt(0) per element, serialising what should be independent loads in flight.
+__device__ __forceinline__ bf16x8 zero_unless(bf16x8 v, bool keep) {
+  const short m = keep ? (short)-1 : (short)0;
+  return v & (bf16x8){m, m, m, m, m, m, m, m};
+}
 typedef __attribute__((address_space(3))) bf16x4* lds_v4_ptr;
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }

@@ -153,16 +153,19 @@ __global__ __launch_bounds__(1024) void conv_direct_wgrad_k(const bf16_raw* __re
 // fused act' mask) as 16-B vectors, keeps acc[8][K+1] (last column = bias) in registers and
 // processes UNROLL items per trip with all loads issued up front, so the loads are
 // independent (the old (k, co)-per-thread walk was a chain of dependent L2 round trips).
-// Lanes with the same channel group are reduced with xor-shuffles, waves through LDS, and
-// each workgroup adds its partial into dW/db with one fp32 atomic per element (<= 128
-// workgroups, so same-address contention stays small).
+// Lanes with the same channel group are reduced with xor-shuffles, waves through LDS, each
+// workgroup writes its partial row to a slab, and the last workgroup to finish (ticket
+// counter, agent-scope release/acquire) sums the rows into dW/db — no same-address atomics
+// (91+ workgroups hammering 160 addresses cost ~15 us) and no second kernel.
 template <int KK>
 __global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __restrict__ dy, const void* __restrict__ x,
                                                           float xscale, float xshift, float* __restrict__ dw,
                                                           float* __restrict__ dbias, const bf16_raw* __restrict__ y,
-                                                          int yact, ConvGeom g, long total) {
+                                                          int yact, ConvGeom g, long total, float* __restrict__ slab,
+                                                          unsigned* __restrict__ counter) {
   constexpr int UNROLL = 4;
   const int G = g.CO >> 3;
+  const bf16_raw* yp = y ? y : dy;
   const int cg = threadIdx.x % G;
   float acc[8][KK + 1];
 #pragma unroll
@@ -177,10 +180,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __res
     for (int u = 0; u < UNROLL; ++u) {
       const long idx = base + u * stride;
       const bool ok = idx < total;
-      const long p = ok ? idx / G : 0;
-      dv[u] = ok ? *(const bf16x8*)(dy + p * g.CO + cg * 8) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (y) yv[u] = ok ? *(const bf16x8*)(y + p * g.CO + cg * 8) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      const int pi = (int)p;
+      const int pi = ok ? (int)(idx / G) : 0;  // clamped: every load below is unconditional
+      dv[u] = zero_unless(*(const bf16x8*)(dy + (long)pi * g.CO + cg * 8), ok);
+      yv[u] = *(const bf16x8*)(yp + (long)pi * g.CO + cg * 8);  // unconditional (yp = y or dy)
       const int b = g.fOHW.div(pi), rem = pi - b * (g.OH * g.OW);
       const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
 #pragma unroll
@@ -189,7 +191,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __res
         const int kw = t % g.KW, kh = t / g.KW;
         const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
         const bool in = ok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        xv[u][k] = in ? in_at(x, xscale, xshift, (((long)b * g.H + ih) * g.W + iw) * g.C + ci) : 0.f;
+        const long xi = in ? (((long)b * g.H + ih) * g.W + iw) * g.C + ci : 0;
+        const float xval = in_at(x, xscale, xshift, xi);
+        xv[u][k] = in ? xval : 0.f;
       }
     }
 #pragma unroll
@@ -210,24 +214,46 @@ __global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __res
 #pragma unroll
     for (int k = 0; k <= KK; ++k)
       for (int o = G; o < 64; o <<= 1) acc[j][k] += __shfl_xor(acc[j][k], o, 64);
-  __shared__ float red[4][32][8 * (KK + 1)];  // [wave][channel group][8*(K+1)], G <= 32
+  __shared__ float red[4 * 32 * 8 * (KK + 1) + 1];  // [wave][group][8*(K+1)] + the "last arriver" flag
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = 32 * 8 * (KK + 1);
   if (lane < G) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int k = 0; k <= KK; ++k) red[wave][lane][j * (KK + 1) + k] = acc[j][k];
+      for (int k = 0; k <= KK; ++k) red[wave * per + lane * 8 * (KK + 1) + j * (KK + 1) + k] = acc[j][k];
   }
   __syncthreads();
-  const int nel = G * 8 * (KK + 1);
+  const int nel = G * 8 * (KK + 1);  // element e = grp*8*(K+1) + j*(K+1) + k
+  for (int e = threadIdx.x; e < nel; e += blockDim.x)
+    slab[(long)blockIdx.x * nel + e] = red[e] + red[per + e] + red[2 * per + e] + red[3 * per + e];
+  // in-launch combine (one agent-scope release per workgroup, one acquire in the last one):
+  // the last workgroup to draw a ticket sums every slab row; it also re-arms the counter
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    red[4 * per] = (t == gridDim.x - 1) ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (red[4 * per] == 0.f) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *counter = 0u;
+  }
+  __syncthreads();
   for (int e = threadIdx.x; e < nel; e += blockDim.x) {
+    float s = 0.f;
+#pragma unroll 16
+    for (int b = 0; b < (int)gridDim.x; ++b) s += slab[(long)b * nel + e];
     const int grp = e / (8 * (KK + 1)), r = e - grp * (8 * (KK + 1));
-    const float s = red[0][grp][r] + red[1][grp][r] + red[2][grp][r] + red[3][grp][r];
     const int j = r / (KK + 1), k = r - j * (KK + 1);
     const int co = grp * 8 + j;
-    if (s == 0.f) continue;
-    if (k < KK) atomicAdd(dw + (long)co * KK + k, s);
-    else if (dbias) atomicAdd(dbias + co, s);
+    if (k < KK) dw[(long)co * KK + k] += s;
+    else if (dbias) dbias[co] += s;
   }
 }
 
@@ -274,6 +300,9 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
                        xshift, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act);
     return (int)hipGetLastError();
   }
+  if (epi == EPI_STORE_BF16 && !colsum && hopsx_conv_fwd_mfma_ok(geom) && ((uintptr_t)x % 16 == 0) &&
+      ((uintptr_t)w % 16 == 0) && ((uintptr_t)out % 16 == 0))
+    return hopsx_conv2d_fwd_mfma(x, w, geom, out, bias, act, st);
   Im2colLoader al{(const bf16_raw*)x, g, (g.C % 8 == 0) && ((uintptr_t)x % 16 == 0)};
   DenseLoader bl{(const bf16_raw*)w, K, is_vec_ok(w, K)};
   if (epi == EPI_STORE_BF16) {
@@ -293,6 +322,9 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
 // — and `colsum` receives that layer's bias gradient.
 extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                   int act, float* colsum, const void* y, int yact, hipStream_t st) {
+  if (hopsx_conv_dgrad_mfma_ok(geom) && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
+      ((uintptr_t)dx % 16 == 0) && ((uintptr_t)yprev % 16 == 0))
+    return hopsx_conv2d_dgrad_mfma(dy, w, geom, dx, yprev, act, colsum, y, yact, st);
   ConvGeom g = make_geom(geom);
   const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
   ConvDgradALoader al{(const bf16_raw*)dy, g,
@@ -305,25 +337,29 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
 }
 
 // dW[co][k] += sum_m dY[m][co] * im2col(X)[m][k]; db[co] += sum_m dY[m][co] when colsum given
-static bool smallk_ok(const ConvGeom& g, const void* dy, const void* y) {
+static bool smallk_ok(const ConvGeom& g, const void* dy, const void* y, const float* ws, long ws_elems,
+                      const unsigned* counter) {
   const int K = g.KH * g.KW * g.C;
   return (K == 4 || K == 9 || K == 16) && g.CO % 8 == 0 && g.CO <= 256 && ((uintptr_t)dy % 16 == 0) &&
-         ((uintptr_t)y % 16 == 0) && !hopsx_disabled("smallk_wgrad");
+         ((uintptr_t)y % 16 == 0) && counter && ws && ws_elems >= 128L * g.CO * (K + 1) &&
+         !hopsx_disabled("smallk_wgrad");
 }
 
 extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias,
                                   const void* y, int yact, float* ws, long ws_elems, float xscale, float xshift,
-                                  hipStream_t st) {
+                                  unsigned* counter, hipStream_t st) {
   ConvGeom g = make_geom(geom);
   const int M = g.CO, N = g.KH * g.KW * g.C, K = g.B * g.OH * g.OW;
-  if (smallk_ok(g, dy, y)) {
+  if (smallk_ok(g, dy, y, ws, ws_elems, counter)) {
     const long total = (long)K * (g.CO / 8);
-    long blocks = (total + 1023) / 1024;  // >= 4 work items per thread
+    // ~16 work items per thread: the in-launch combine then reads only blocks x CO x (K+1)
+    // floats (one row per workgroup; ~23 rows at the MNIST batch of 32)
+    long blocks = (total + 4095) / 4096;
     if (blocks > 128) blocks = 128;
     if (blocks < 1) blocks = 1;
 #define HOPSX_SMALLK(KK)                                                                                      \
   hipLaunchKernelGGL(conv_wgrad_smallk_k<KK>, dim3(blocks), dim3(256), 0, st, (const bf16_raw*)dy, x, xscale, xshift, dw, \
-                     dbias, (const bf16_raw*)y, yact, g, total)
+                     dbias, (const bf16_raw*)y, yact, g, total, ws, counter)
     if (N == 4) HOPSX_SMALLK(4);
     else if (N == 9) HOPSX_SMALLK(9);
     else HOPSX_SMALLK(16);

@@ -1,0 +1,328 @@
+// Direct MFMA convolutions for short reductions (K = KH*KW*Cin <= 512, Cin % 8 == 0 for the
+// forward, Cout % 8 == 0 for dgrad; the 32->64 channel second conv of every MNIST model,
+// K = 128 / 288 / 512).  As an implicit GEMM these layers are latency-bound: 2-8 K-tiles per
+// workgroup, each paying an LDS staging round trip and two barriers.  Here:
+//   * the (tiny) weight matrix is staged ONCE per workgroup into LDS in MFMA B-fragment
+//     order (16-B chunks, XOR-swizzled so a 16-lane ds_read_b128 group hits 16 distinct slots),
+//   * each wave owns 16-pixel groups and loads its A fragments straight from global memory
+//     into registers — one 16-B im2col (fwd) / col2im (dgrad) gather per lane per 32-deep
+//     K-step, two groups in flight per trip, no barriers in the loop,
+//   * v_mfma_f32_16x16x32_bf16 over all Cout fragments, then a fused epilogue (bias + act
+//     for fwd; act'(yprev) mask + previous layer's bias gradient for dgrad) written through
+//     a per-wave LDS transpose so the stores leave as 16-B vectors.
+#include "gemm_core.h"
+#include "ops_api.h"
+
+using namespace hopsx;
+
+namespace {
+
+constexpr int CM_WAVES = 4;
+constexpr int CM_UN = 2;  // pixel groups per wave per trip
+
+// LDS row stride (in 16-B chunks) of a weight image with cpr chunks per row: rows of >= 16
+// chunks are padded to a multiple of 16 so the XOR swizzle below never leaves its row
+__host__ __device__ constexpr int cm_rs(int cpr) { return cpr >= 16 ? (cpr + 15) / 16 * 16 : cpr; }
+
+// swizzled chunk index for row `r` of a [rows][cpr chunks] LDS image: 16 consecutive rows
+// reading the same logical chunk land on 16 different 16-B slots of the 256-B bank row
+__device__ __forceinline__ int cm_swz(int r, int c, int cpr) {
+  if (cpr >= 16) return c ^ (r & 15);
+  const int rows_per_line = 16 / cpr;  // 2 (cpr 8), 4 (cpr 4)
+  return c ^ ((r / rows_per_line) & (cpr - 1));
+}
+
+// ---------------------------------------------------------------------------- forward
+template <int NF, int KS>
+__global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
+                                                      const float* __restrict__ bias, bf16_raw* __restrict__ y,
+                                                      ConvGeom g, int act, int K) {
+  constexpr int CO = NF * 16;
+  extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
+  constexpr int cpr = KS * 4;  // 16-B chunks per weight row (K padded to 32*KS)
+  constexpr int RS = cm_rs(cpr);  // row stride in chunks: the XOR swizzle stays inside the row
+  bf16_raw* sw = cm_smem;                                 // [CO][RS*8]
+  bf16_raw* scratch = cm_smem + CO * RS * 8;              // [waves][16][CO]
+  for (int i = threadIdx.x; i < CO * cpr; i += blockDim.x) {
+    const int co = i / cpr, c = i - co * cpr;
+    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (8 * c < K) v = *(const bf16x8*)(w + (long)co * K + 8 * c);  // K % 8 == 0 (Cin % 8 == 0)
+    *(bf16x8*)(sw + co * RS * 8 + 8 * cm_swz(co, c, cpr)) = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int M = g.B * g.OH * g.OW;
+  const int ngroups = (M + 15) / 16;
+  bf16_raw* sc = scratch + wave * 16 * CO;
+  float bv[NF];
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf) bv[nf] = bias ? bias[nf * 16 + fr] : 0.f;
+  for (int g0 = (blockIdx.x * CM_WAVES + wave) * CM_UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * CM_UN) {
+    bf16x8 a[CM_UN][KS];
+#pragma unroll
+    for (int u = 0; u < CM_UN; ++u) {
+      const int px = (g0 + u) * 16 + fr;
+      const bool pok = (g0 + u) < ngroups && px < M;
+      const int pp = pok ? px : 0;
+      const int b = g.fOHW.div(pp), rem = pp - b * (g.OH * g.OW);
+      const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int k0 = kk * 32 + 8 * fq;
+        const int kc = k0 < K ? k0 : 0;
+        const int t = g.fC.div(kc), ci = kc - t * g.C;
+        const int kh = g.fKW.div(t), kw = t - kh * g.KW;
+        const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
+        const bool ok = pok && k0 < K && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const long off = ok ? (((long)b * g.H + ih) * g.W + iw) * g.C + ci : 0;
+        a[u][kk] = zero_unless(*(const bf16x8*)(x + off), ok);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CM_UN; ++u) {
+      if (g0 + u >= ngroups) break;
+      f32x4 acc[NF];
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) acc[nf] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const int co = nf * 16 + fr;
+          const bf16x8 bfr = *(const bf16x8*)(sw + co * RS * 8 + 8 * cm_swz(co, kk * 4 + fq, cpr));
+          acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][kk], bfr, acc[nf], 0, 0, 0);
+        }
+      }
+      // epilogue through the wave's LDS scratch: C map col = lane&15 (co), row = (lane>>4)*4 + r (pixel)
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sc[(fq * 4 + r) * CO + nf * 16 + fr] = f2bf(apply_act(acc[nf][r] + bv[nf], act));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int base = (g0 + u) * 16;
+#pragma unroll
+      for (int c = lane; c < 16 * CO / 8; c += 64) {
+        const int row = c / (CO / 8), col = (c - row * (CO / 8)) * 8;
+        if (base + row < M) *(bf16x8*)(y + (long)(base + row) * CO + col) = *(const bf16x8*)(sc + row * CO + col);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- dgrad
+// dX[b,ih,iw,ci] = sum_{kh,kw,co} dY'[b,oh,ow,co] W[co,kh,kw,ci]  (stride 1:
+// oh = ih + ph - kh*dh), dY' = dY * act'(y); output masked by act'(yprev) and its
+// per-channel sums accumulated into `colsum` (the previous layer's bias gradient).
+template <int NF, int KS>
+__global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ w,
+                                                        bf16_raw* __restrict__ dx, const bf16_raw* __restrict__ yprev,
+                                                        int act_prev, float* __restrict__ colsum,
+                                                        const bf16_raw* __restrict__ y, int yact, ConvGeom g, int K) {
+  constexpr int CI = NF * 16;
+  extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
+  constexpr int cpr = KS * 4;
+  constexpr int RS = cm_rs(cpr);
+  bf16_raw* sw = cm_smem;                     // [CI][RS*8]: (ci, k=(kh,kw,co)) = W[co][kh][kw][ci]
+  bf16_raw* scratch = cm_smem + CI * RS * 8;  // [waves][16][CI]
+  float* csum = (float*)(scratch + CM_WAVES * 16 * CI);  // [CI]
+  // zero the K padding, then scatter W (read in its own order: coalesced) into the
+  // transposed image; the 2-B LDS writes are cheap next to strided global reads
+  for (int i = threadIdx.x; i < CI * (cpr * 8 - K); i += blockDim.x) {
+    const int ci = i / (cpr * 8 - K), kk = K + i - ci * (cpr * 8 - K);
+    sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = 0;
+  }
+  for (int i = threadIdx.x; i < K * CI; i += blockDim.x) {
+    const int ci = i % CI, r = i / CI;               // r = co*KH*KW + t  (source order [co][kh][kw][ci])
+    const int co = r / (g.KH * g.KW), t = r - co * (g.KH * g.KW);
+    const int kk = t * g.CO + co;                     // k = (kh, kw, co)
+    sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = w[i];
+  }
+  for (int i = threadIdx.x; i < CI; i += blockDim.x) csum[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int M = g.B * g.H * g.W;
+  const int ngroups = (M + 15) / 16;
+  const bf16_raw* yp = y ? y : dy;
+  const bf16_raw* ypp = yprev ? yprev : dx;
+  bf16_raw* sc = scratch + wave * 16 * CI;
+  float cacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int g0 = (blockIdx.x * CM_WAVES + wave) * CM_UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * CM_UN) {
+    bf16x8 a[CM_UN][KS];
+#pragma unroll
+    for (int u = 0; u < CM_UN; ++u) {
+      const int px = (g0 + u) * 16 + fr;
+      const bool pok = (g0 + u) < ngroups && px < M;
+      const int pp = pok ? px : 0;
+      const int b = g.fHW.div(pp), rem = pp - b * (g.H * g.W);
+      const int ih = g.fW.div(rem), iw = rem - ih * g.W;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int k0 = kk * 32 + 8 * fq;
+        const int kc = k0 < K ? k0 : 0;
+        const int t = g.fCO.div(kc), co = kc - t * g.CO;
+        const int kh = g.fKW.div(t), kw = t - kh * g.KW;
+        const int oh = ih + g.ph - kh * g.dh, ow = iw + g.pw - kw * g.dw;  // stride 1
+        const bool ok = pok && k0 < K && oh >= 0 && oh < g.OH && ow >= 0 && ow < g.OW;
+        const long o = ok ? (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co : 0;
+        bf16x8 v = zero_unless(*(const bf16x8*)(dy + o), ok);
+        const bf16x8 ym = *(const bf16x8*)(yp + o);  // unconditional load (yp = y or dy)
+        if (y) mask8(v, ym, yact);
+        a[u][kk] = v;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CM_UN; ++u) {
+      if (g0 + u >= ngroups) break;
+      f32x4 acc[NF];
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) acc[nf] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const int ci = nf * 16 + fr;
+          const bf16x8 bfr = *(const bf16x8*)(sw + ci * RS * 8 + 8 * cm_swz(ci, kk * 4 + fq, cpr));
+          acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][kk], bfr, acc[nf], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[(fq * 4 + r) * CI + nf * 16 + fr] = f2bf(acc[nf][r]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const int base = (g0 + u) * 16;
+#pragma unroll
+      for (int c = lane; c < 16 * CI / 8; c += 64) {  // a lane always lands on the same 8 columns
+        const int row = c / (CI / 8), col = (c - row * (CI / 8)) * 8;
+        if (base + row < M) {
+          bf16x8 v = *(const bf16x8*)(sc + row * CI + col);
+          const long o = (long)(base + row) * CI + col;
+          const bf16x8 pm = *(const bf16x8*)(ypp + o);  // unconditional (ypp = yprev or dx)
+          if (yprev) mask8(v, pm, act_prev);
+          *(bf16x8*)(dx + o) = v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cacc[j] += bf2f((uint16_t)v[j]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (colsum) {
+    // lanes l, l + CI/8, l + 2*CI/8, ... own the same 8 columns
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int off = CI / 8; off < 64; off <<= 1) cacc[j] += __shfl_xor(cacc[j], off, 64);
+    if (lane < CI / 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(csum + lane * 8 + j, cacc[j]);  // LDS atomics, 4 waves
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < CI; i += blockDim.x)
+      if (csum[i] != 0.f) atomicAdd(colsum + i, csum[i]);
+  }
+}
+
+// supported K-step counts (K is zero-padded up to one of them)
+int cm_ks(int ks) { return ks <= 2 ? 2 : ks <= 4 ? 4 : ks <= 8 ? 8 : ks <= 9 ? 9 : 16; }
+
+int cm_grid(long ngroups) {
+  long blocks = (ngroups + CM_WAVES * CM_UN - 1) / (CM_WAVES * CM_UN);
+  if (blocks > 1024) blocks = 1024;
+  return (int)(blocks < 1 ? 1 : blocks);
+}
+
+}  // namespace
+
+// K = KH*KW*C <= 512, C % 8 == 0, CO in {16, 32, 64, 128}
+bool hopsx_conv_fwd_mfma_ok(const int* geom) {
+  const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * C;
+  return C % 8 == 0 && K <= 512 && (CO == 16 || CO == 32 || CO == 64 || CO == 128) &&
+         !hopsx_disabled("conv_mfma");
+}
+
+// stride 1 only; K = KH*KW*CO <= 512, CO % 8 == 0, C in {16, 32, 64, 128}
+bool hopsx_conv_dgrad_mfma_ok(const int* geom) {
+  const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * CO;
+  return geom[9] == 1 && geom[10] == 1 && CO % 8 == 0 && K <= 512 && (C == 16 || C == 32 || C == 64 || C == 128) &&
+         !hopsx_disabled("conv_mfma");
+}
+
+extern "C" int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* out, const float* bias,
+                                     int act, hipStream_t st) {
+  ConvGeom g;
+  g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
+  g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
+  g.dh = geom[13]; g.dw = geom[14];
+  g.init_div();
+  const int K = g.KH * g.KW * g.C;
+  const int KS = cm_ks((K + 31) / 32);
+  const long M = (long)g.B * g.OH * g.OW;
+  const int grid = cm_grid((M + 15) / 16);
+  const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw);
+#define HOPSX_CMF(NF, KSV)                                                                                     \
+  hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,            \
+                     (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K)
+#define HOPSX_CMF_NF(NF)          \
+  switch (KS) {                   \
+    case 2: HOPSX_CMF(NF, 2); break;  \
+    case 4: HOPSX_CMF(NF, 4); break;  \
+    case 8: HOPSX_CMF(NF, 8); break;  \
+    case 9: HOPSX_CMF(NF, 9); break;  \
+    default: HOPSX_CMF(NF, 16); break; \
+  }
+  switch (g.CO / 16) {
+    case 1: HOPSX_CMF_NF(1); break;
+    case 2: HOPSX_CMF_NF(2); break;
+    case 4: HOPSX_CMF_NF(4); break;
+    case 8: HOPSX_CMF_NF(8); break;
+    default: return -2;
+  }
+#undef HOPSX_CMF_NF
+#undef HOPSX_CMF
+  return (int)hipGetLastError();
+}
+
+extern "C" int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                       int act_prev, float* colsum, const void* y, int yact, hipStream_t st) {
+  ConvGeom g;
+  g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
+  g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
+  g.dh = geom[13]; g.dw = geom[14];
+  g.init_div();
+  const int K = g.KH * g.KW * g.CO;
+  const int KS = cm_ks((K + 31) / 32);
+  const long M = (long)g.B * g.H * g.W;
+  long blocks = cm_grid((M + 15) / 16);
+  if (colsum && blocks > 256) blocks = 256;  // one colsum atomic per channel per workgroup
+  const size_t shm =
+      (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) + (size_t)g.C * sizeof(float);
+#define HOPSX_CMD(NF, KSV)                                                                                     \
+  hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy,       \
+                     (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,              \
+                     (const bf16_raw*)y, yact, g, K)
+#define HOPSX_CMD_NF(NF)          \
+  switch (KS) {                   \
+    case 2: HOPSX_CMD(NF, 2); break;  \
+    case 4: HOPSX_CMD(NF, 4); break;  \
+    case 8: HOPSX_CMD(NF, 8); break;  \
+    case 9: HOPSX_CMD(NF, 9); break;  \
+    default: HOPSX_CMD(NF, 16); break; \
+  }
+  switch (g.C / 16) {
+    case 1: HOPSX_CMD_NF(1); break;
+    case 2: HOPSX_CMD_NF(2); break;
+    case 4: HOPSX_CMD_NF(4); break;
+    case 8: HOPSX_CMD_NF(8); break;
+    default: return -2;
+  }
+#undef HOPSX_CMD_NF
+#undef HOPSX_CMD
+  return (int)hipGetLastError();
+}

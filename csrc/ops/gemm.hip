@@ -87,16 +87,27 @@ static int dispatch_epi(const DenseLoader& al, const DenseLoader& bl, int M, int
 extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K,
                           int epi, void* out, long ldo, const float* bias, float alpha, float beta, int act,
                           const void* aux, long ldaux, float* colsum, float* ws, long ws_elems, const void* ay,
-                          int aact, float* arowsum, hipStream_t st) {
+                          int aact, float* arowsum, unsigned* tickets, hipStream_t st) {
   // ay/aact: fused act' mask on the A operand (same layout as A); arowsum: row sums of
   // the (masked) A operand — the bias gradient when A = dY^T in a weight-gradient GEMM
   DenseLoader al{(const bf16_raw*)A, lda, is_vec_ok(A, lda) && is_vec_ok(ay ? ay : A, lda), (const bf16_raw*)ay,
                  aact};
   DenseLoader bl{(const bf16_raw*)B, ldb, is_vec_ok(B, ldb)};
+  if (ws && tickets && epi != EPI_ATOMIC_F32 && (long)M * N <= ws_elems && want_splitk(M, N, K) &&
+      !hopsx_disabled("splitk_ticket")) {
+    // ws is persistent and zero at rest (see EpiAtomicTicket)
+    SplitFinish f{tickets, epi, out, ldo, bias, alpha, beta, act, (const bf16_raw*)aux, ldaux, colsum};
+    EpiAtomicTicket e{ws, N, 1.f, nullptr, f};
+    if (a_kc && b_kc) launch_gemm<true, true>(al, bl, e, M, N, K, true, st, arowsum);
+    else if (a_kc) launch_gemm<true, false>(al, bl, e, M, N, K, true, st, arowsum);
+    else if (b_kc) launch_gemm<false, true>(al, bl, e, M, N, K, true, st, arowsum);
+    else launch_gemm<false, false>(al, bl, e, M, N, K, true, st, arowsum);
+    return (int)hipGetLastError();
+  }
   if (ws && epi != EPI_ATOMIC_F32 && (long)M * N <= ws_elems && want_splitk(M, N, K)) {
     hopsx_zero(ws, (long)M * N * sizeof(float), st);
     int rc = hopsx_gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, EPI_ATOMIC_F32, ws, N, nullptr, 1.f, 0.f, 0, nullptr, 0,
-                        nullptr, nullptr, 0, ay, aact, arowsum, st);
+                        nullptr, nullptr, 0, ay, aact, arowsum, nullptr, st);
     if (rc) return rc;
     const int gx = (N + 63) / 64;
     const int gy = (M + 3) / 4;

@@ -259,6 +259,44 @@ struct EpiAtomicF32 {  // out += alpha*acc (split-K safe)
   }
 };
 
+// Split-K with an in-launch finish: every K-slice adds into the fp32 workspace `out`
+// (persistent, zero at rest); the slice that draws the last ticket of its tile reads the
+// tile back, applies the real epilogue (bias/act/bf16 store, dact mask, colsum) and
+// re-zeroes the workspace tile and its counter — no memset node, no finishing kernel.
+// epilogue ids of ops_api.h's GemmEpi (this header does not depend on the C ABI header)
+constexpr int kEpiStoreBF16 = 0, kEpiStoreF32 = 1, kEpiDActBF16 = 3;
+
+struct SplitFinish {
+  unsigned* cnt;  // one counter per output tile, zero at rest
+  int epi;        // EPI_STORE_BF16 / EPI_STORE_F32 / EPI_DACT_BF16
+  void* out;
+  long ldo;
+  const float* bias;
+  float alpha, beta;
+  int act;
+  const bf16_raw* aux;
+  long ldaux;
+  float* colsum;
+};
+
+struct EpiAtomicTicket {
+  float* out;  // workspace [M][N]
+  long ldo;
+  float alpha;
+  float* colsum;  // unused in the slice pass
+  SplitFinish fin;
+  static constexpr bool kTicket = true;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    atomicAdd(out + (long)m * ldo + n, v);
+    return v;
+  }
+};
+
+template <class EP, class = void>
+struct has_ticket { static constexpr bool value = false; };
+template <class EP>
+struct has_ticket<EP, decltype((void)EP::kTicket)> { static constexpr bool value = EP::kTicket; };
+
 // out = acc * act'(y[m,n])  (backprop through the activation whose OUTPUT is y)
 struct EpiDActBF16 {
   bf16_raw* out;
@@ -483,14 +521,69 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
       }
     }
   }
-  if (ep.colsum) {
+  if constexpr (!has_ticket<EP>::value) {
+    if (ep.colsum) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float v = cs[j];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      const int n = n0 + wn * WTN + j * 16 + fr;
-      if (fq == 0 && n < N) atomicAdd(ep.colsum + n, v);
+      for (int j = 0; j < FN; ++j) {
+        float v = cs[j];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int n = n0 + wn * WTN + j * 16 + fr;
+        if (fq == 0 && n < N) atomicAdd(ep.colsum + n, v);
+      }
+    }
+  } else {
+    // ---- in-launch split-K finish (agent-scope release per slice, acquire in the last one)
+    int* flag = (int*)smem;  // the staging array is free now; never a second __shared__ object
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(ep.fin.cnt + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = (t == gridDim.y - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (flag[0] == 0) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ep.fin.cnt[bid] = 0u;
+    }
+    __syncthreads();
+    const SplitFinish& f = ep.fin;
+    const int c = tid % BN;  // BN divides 256: a thread keeps one column
+    float csum = 0.f;
+    for (int idx = tid; idx < BM * BN; idx += 256) {
+      const int m = m0 + idx / BN, n = n0 + c;
+      if (m >= M || n >= N) continue;
+      float* wp = ep.out + (long)m * ep.ldo + n;
+      float v = *wp;
+      *wp = 0.f;
+      if (f.epi == kEpiDActBF16) {
+        if (f.aux) v *= act_grad_from_out(bf2f(f.aux[(long)m * f.ldaux + n]), f.act);
+        ((bf16_raw*)f.out)[(long)m * f.ldo + n] = f2bf(v);
+      } else {
+        v = apply_act(v * f.alpha + (f.bias ? f.bias[n] : 0.f), f.act);
+        if (f.epi == kEpiStoreBF16) {
+          ((bf16_raw*)f.out)[(long)m * f.ldo + n] = f2bf(v);
+        } else {
+          float* o = (float*)f.out + (long)m * f.ldo + n;
+          *o = (f.beta != 0.f) ? v + f.beta * *o : v;
+        }
+      }
+      csum += v;
+    }
+    if (f.colsum) {
+      float* red = (float*)smem;
+      __syncthreads();
+      red[tid] = csum;
+      __syncthreads();
+      if (tid < BN && n0 + tid < N) {
+        float t = 0.f;
+        for (int q = tid; q < 256; q += BN) t += red[q];
+        atomicAdd(f.colsum + n0 + tid, t);
+      }
     }
   }
 }

@@ -11,7 +11,8 @@ extern "C" {
 // ---- GEMM / conv (gemm.hip, conv.hip) ----
 int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b_kc, int M, int N, int K, int epi,
                void* out, long ldo, const float* bias, float alpha, float beta, int act, const void* aux, long ldaux,
-               float* colsum, float* ws, long ws_elems, const void* ay, int aact, float* arowsum, hipStream_t st);
+               float* colsum, float* ws, long ws_elems, const void* ay, int aact, float* arowsum, unsigned* tickets,
+               hipStream_t st);
 // xscale != 0: x is uint8 and is read as x * xscale + xshift (input-layer normalisation fused; direct kernel only)
 int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out, const float* bias, int act,
                      float* colsum, float xscale, float xshift, hipStream_t st);
@@ -21,7 +22,8 @@ int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx,
 // dbias (optional) receives sum over pixels of the (masked) dY = the conv bias gradient
 // ws (optional, >= 1024*(K*CO+CO) floats): slab workspace for the small-K direct kernel
 int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias, const void* y,
-                       int yact, float* ws, long ws_elems, float xscale, float xshift, hipStream_t st);
+                       int yact, float* ws, long ws_elems, float xscale, float xshift, unsigned* counter,
+                       hipStream_t st);
 
 // ---- pooling (pool.hip) ----
 // optional fused dropout on the pooled output (p > 0, rng/salt as hopsx_dropout_fwd)
@@ -74,6 +76,14 @@ int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, const float* 
 int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                  const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
                  void* dresidual, hipStream_t st);
+
+// ---- direct MFMA convs for short reductions (conv_mfma.hip) ----
+bool hopsx_conv_fwd_mfma_ok(const int* geom);
+bool hopsx_conv_dgrad_mfma_ok(const int* geom);
+int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* out, const float* bias, int act,
+                          hipStream_t st);
+int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                            int act_prev, float* colsum, const void* y, int yact, hipStream_t st);
 
 // ---- zero-fill kernel (elementwise.hip): graph-safe replacement for hipMemsetAsync ----
 int hopsx_zero(void* p, long bytes, hipStream_t st);

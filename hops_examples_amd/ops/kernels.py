@@ -39,15 +39,28 @@ def gemm_raw(a, lda, a_kc, b, ldb, b_kc, M, N, K, epi, out, ldo, bias=None, alph
     a_rowsum: accumulate the row sums of the (masked) A operand (RC-A only; bias gradients)."""
     rc = _C.ext().gemm(ptr(a), lda, int(a_kc), ptr(b), ldb, int(b_kc), M, N, K, epi, ptr(out), ldo, ptr(bias),
                        float(alpha), float(beta), act_id(act), ptr(aux), ldaux, ptr(colsum), ptr(ws),
-                       0 if ws is None else ws.numel(), ptr(a_mask_y), act_id(a_mask_act), ptr(a_rowsum), stream())
+                       0 if ws is None else ws.numel(), ptr(a_mask_y), act_id(a_mask_act), ptr(a_rowsum),
+                       ptr(ticket(a.device)) if ws is not None else 0, stream())
     check(rc, "gemm")
 
 
+_SPLITK_WS: dict = {}
+
+
 def _splitk_ws(M, N, K, device):
+    """fp32 split-K accumulator: a persistent per-device buffer that is zero at rest (the
+    in-launch finish of each split-K GEMM re-zeroes the tiles it consumed), so no memset
+    node or finishing kernel runs per call.  Grown only outside graph capture."""
     # split-K pays when the output has few tiles but the reduction is long
-    if M * N <= (1 << 22) and K >= 1024 and (M <= 128 or N <= 128):
-        return torch.empty(M * N, device=device, dtype=F32)
-    return None
+    if not (M * N <= (1 << 22) and K >= 1024 and (M <= 128 or N <= 128)):
+        return None
+    buf = _SPLITK_WS.get(device)
+    if buf is None or buf.numel() < M * N:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("split-K workspace must be sized before graph capture (run an eager step first)")
+        buf = torch.zeros(max(M * N, 1 << 16), device=device, dtype=F32)
+        _SPLITK_WS[device] = buf
+    return buf[: M * N]
 
 
 def linear_fwd(x, w, bias=None, act=0, out=None, out_f32=False, colsum=None):
@@ -113,6 +126,22 @@ def conv_geom(x_shape, w_shape, stride, padding, dilation):
     return [B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw, dh, dw]
 
 
+_TICKETS: dict = {}
+
+
+def ticket(device) -> torch.Tensor:
+    """Per-device in-launch-reduction ticket counter (uint32, zero at rest: every kernel that
+    draws tickets has its last workgroup re-arm it, so it stays valid across graph replays).
+    Allocated outside any capture on first use (the eager warm-up steps)."""
+    t = _TICKETS.get(device)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("ticket counter must be created before graph capture (run an eager step first)")
+        t = torch.zeros(8192, device=device, dtype=torch.int32)
+        _TICKETS[device] = t
+    return t
+
+
 def conv_u8_fusable(geom) -> bool:
     """The uint8 input layer can skip its normalisation pass: the direct forward kernel and the
     small-K weight-gradient kernel both read raw pixels (x * scale + shift) themselves."""
@@ -157,11 +186,14 @@ def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0, in_affine=None):
     ws = None
     smallk = K in (4, 9, 16) and geom[6] % 8 == 0 and geom[6] <= 256 and "smallk_wgrad" not in \
         os.environ.get("HOPSX_DISABLE", "")
-    if not smallk and K <= 64 and KC <= 1024:  # older direct kernel: slab workspace
+    if smallk:  # per-workgroup partial rows (<= 128 workgroups), combined in-launch
+        ws = torch.empty(128 * geom[6] * (K + 1), device=dy.device, dtype=F32)
+    elif K <= 64 and KC <= 1024:  # older direct kernel: slab workspace
         ws = torch.empty(1024 * (KC + geom[6]), device=dy.device, dtype=F32)
     sc, sh = (float(in_affine[0]), float(in_affine[1])) if in_affine else (0.0, 0.0)
     check(_C.ext().conv2d_wgrad(ptr(dy), ptr(x), geom, ptr(dw), ptr(dbias), ptr(y), act_id(act), ptr(ws),
-                                0 if ws is None else ws.numel(), sc, sh, stream()), "conv2d_wgrad")
+                                0 if ws is None else ws.numel(), sc, sh, ptr(ticket(dy.device)), stream()),
+          "conv2d_wgrad")
     return dw
 
 

@@ -83,3 +83,42 @@ def test_mnist_models_use_fused_input_path():
         lc = HF.loss(cpu.eval()(x), y)
         lg = HF.loss(gpu.eval()(x.to(dev)), y.to(dev))
         assert abs(lc.item() - lg.item()) < 0.03 * max(1.0, lc.item()), (cls.__name__, lc.item(), lg.item())
+
+
+def _torch_conv(x, w, b, pad):
+    return F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=pad).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("k,C,CO,H,pad", [(2, 32, 64, 27, 0), (3, 32, 64, 28, 1), (4, 32, 64, 25, 0), (2, 16, 32, 9, 0),
+                                          (3, 64, 128, 10, 1), (1, 64, 16, 7, 0)])
+def test_conv_mfma_fwd(k, C, CO, H, pad):
+    torch.manual_seed(2)
+    B = 3
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    w = (torch.randn(CO, k, k, C, device=dev) * 0.1).to(bf)
+    b = torch.randn(CO, device=dev) * 0.1
+    g = K.conv_geom(x.shape, w.shape, (1, 1), (pad, pad), (1, 1))
+    y = K.conv2d_fwd(x, w, g, bias=b, act="relu")
+    ref = torch.relu(_torch_conv(x, w, b, pad))
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("k,C,CO,H,pad", [(2, 32, 64, 27, 0), (3, 32, 64, 14, 1), (4, 32, 64, 13, 0), (2, 16, 32, 9, 0)])
+def test_conv_mfma_dgrad_masks_colsum(k, C, CO, H, pad):
+    torch.manual_seed(3)
+    B = 2
+    xprev = torch.relu(torch.randn(B, H, H, C, device=dev)).to(bf)  # previous layer's activation output
+    w = (torch.randn(CO, k, k, C, device=dev) * 0.1).to(bf)
+    g = K.conv_geom(xprev.shape, w.shape, (1, 1), (pad, pad), (1, 1))
+    OH = g[4]
+    y = torch.relu(torch.randn(B, OH, OH, CO, device=dev)).to(bf)
+    dy = torch.randn(B, OH, OH, CO, device=dev).to(bf)
+    cs = torch.zeros(C, device=dev)
+    dx = K.conv2d_dgrad(dy, w, g, yprev=xprev, act_prev="relu", colsum=cs, y=y, act="relu")
+    xr = xprev.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    out = F.conv2d(xr, w.float().permute(0, 3, 1, 2), padding=pad)
+    out.backward((dy.float() * (y.float() > 0)).permute(0, 3, 1, 2))
+    ref = xr.grad.permute(0, 2, 3, 1) * (xprev.float() > 0)
+    torch.testing.assert_close(dx.float(), ref, atol=3e-2 * ref.abs().max().item(), rtol=2e-2)
+    torch.testing.assert_close(cs, ref.sum((0, 1, 2)), atol=3e-2 * ref.abs().sum((0, 1, 2)).max().item() + 1e-2,
+                               rtol=3e-2)
