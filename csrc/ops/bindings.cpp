@@ -38,6 +38,15 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
                               P<void>(y), yact, S(st));
   });
+  m.def("conv2d_dgrad_fused_wgrad_ok", [](std::vector<int> g, std::vector<int> g0) {
+    return hopsx_conv_dgrad_fused_wgrad_ok(g.data(), g0.data());
+  });
+  m.def("conv2d_dgrad_fused_wgrad", [](u dy, u w, std::vector<int> g, u yprev, int act, u colsum, u y, int yact,
+                                       std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u st) {
+    return hopsx_conv2d_dgrad_mfma_ex(P<void>(dy), P<void>(w), g.data(), nullptr, P<void>(yprev), act,
+                                      P<float>(colsum), P<void>(y), yact, g0.data(), P<void>(x0), xscale, xshift,
+                                      P<float>(dw0), S(st));
+  });
   m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
                            float xscale, float xshift, u counter, u st) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,

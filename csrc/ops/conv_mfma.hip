@@ -117,11 +117,20 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
 // dX[b,ih,iw,ci] = sum_{kh,kw,co} dY'[b,oh,ow,co] W[co,kh,kw,ci]  (stride 1:
 // oh = ih + ph - kh*dh), dY' = dY * act'(y); output masked by act'(yprev) and its
 // per-channel sums accumulated into `colsum` (the previous layer's bias gradient).
-template <int NF, int KS>
+//
+// K0 > 0 fuses the weight gradient of the PREVIOUS layer into the epilogue: when that layer is
+// the network's input layer (its input needs no gradient) with a K0 = KH0*KW0*1-tap reduction,
+// dX here is only ever consumed by that layer's wgrad, so instead of storing dX the epilogue
+// multiplies each masked dX row by the input layer's im2col row (K0 raw pixels, uint8 with the
+// fused affine or bf16) and accumulates dW0[ci][k] in registers; the previous layer's bias
+// gradient is the existing colsum.  Saves the dX write/re-read and a whole launch.
+template <int NF, int KS, int K0>
 __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ w,
                                                         bf16_raw* __restrict__ dx, const bf16_raw* __restrict__ yprev,
                                                         int act_prev, float* __restrict__ colsum,
-                                                        const bf16_raw* __restrict__ y, int yact, ConvGeom g, int K) {
+                                                        const bf16_raw* __restrict__ y, int yact, ConvGeom g, int K,
+                                                        int wvec, const void* __restrict__ x0, float xscale,
+                                                        float xshift, ConvGeom gi, float* __restrict__ dw0) {
   constexpr int CI = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
   constexpr int cpr = KS * 4;
@@ -135,13 +144,26 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
     const int ci = i / (cpr * 8 - K), kk = K + i - ci * (cpr * 8 - K);
     sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = 0;
   }
-  for (int i = threadIdx.x; i < K * CI; i += blockDim.x) {
-    const int ci = i % CI, r = i / CI;               // r = co*KH*KW + t  (source order [co][kh][kw][ci])
-    const int co = r / (g.KH * g.KW), t = r - co * (g.KH * g.KW);
-    const int kk = t * g.CO + co;                     // k = (kh, kw, co)
-    sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = w[i];
+  if (wvec) {  // 16-B loads of 8 consecutive ci (CI % 8 == 0, 16-B aligned W): 8x fewer global loads
+    for (int i = threadIdx.x; i < K * CI / 8; i += blockDim.x) {
+      const int r = i / (CI / 8), ci0 = (i - r * (CI / 8)) * 8;
+      const int co = r / (g.KH * g.KW), t = r - co * (g.KH * g.KW);
+      const int kk = t * g.CO + co;
+      const bf16x8 v = *(const bf16x8*)(w + (long)i * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sw[(ci0 + j) * RS * 8 + 8 * cm_swz(ci0 + j, kk >> 3, cpr) + (kk & 7)] = v[j];
+    }
+  } else {
+    for (int i = threadIdx.x; i < K * CI; i += blockDim.x) {
+      const int ci = i % CI, r = i / CI;               // r = co*KH*KW + t  (source order [co][kh][kw][ci])
+      const int co = r / (g.KH * g.KW), t = r - co * (g.KH * g.KW);
+      const int kk = t * g.CO + co;                     // k = (kh, kw, co)
+      sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = w[i];
+    }
   }
   for (int i = threadIdx.x; i < CI; i += blockDim.x) csum[i] = 0.f;
+  float* cwsum = csum + CI;  // [CI][K0] (K0 > 0)
+  for (int i = threadIdx.x; i < CI * K0; i += blockDim.x) cwsum[i] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -151,8 +173,18 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
   const bf16_raw* ypp = yprev ? yprev : dx;
   bf16_raw* sc = scratch + wave * 16 * CI;
   float cacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float cw[8][K0 > 0 ? K0 : 1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int k = 0; k < (K0 > 0 ? K0 : 1); ++k) cw[j][k] = 0.f;
+  constexpr int NCH = 16 * CI / 8;      // 16-B output chunks per 16-pixel group
+  constexpr int CPL = (NCH + 63) / 64;  // of which this lane stores CPL (c = lane + 64 q)
+  constexpr int XK = K0 > 0 ? K0 : 1;
   for (int g0 = (blockIdx.x * CM_WAVES + wave) * CM_UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * CM_UN) {
     bf16x8 a[CM_UN][KS];
+    bf16x8 pmv[CM_UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
+    float xk[CM_UN][CPL][XK];
 #pragma unroll
     for (int u = 0; u < CM_UN; ++u) {
       const int px = (g0 + u) * 16 + fr;
@@ -160,6 +192,30 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
       const int pp = pok ? px : 0;
       const int b = g.fHW.div(pp), rem = pp - b * (g.H * g.W);
       const int ih = g.fW.div(rem), iw = rem - ih * g.W;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        const int c = lane + 64 * q;
+        const int row = c / (CI / 8), col = (c - row * (CI / 8)) * 8;
+        const int p = (g0 + u) * 16 + row;
+        const bool okc = c < NCH && (g0 + u) < ngroups && p < M;
+        const int pc = okc ? p : 0;
+        pmv[u][q] = *(const bf16x8*)(ypp + (long)pc * CI + (okc ? col : 0));  // unconditional (ypp = yprev or dx)
+        if constexpr (K0 > 0) {
+          // im2col row of the input layer at this pixel (= the input layer's output pixel)
+          const int bb = g.fHW.div(pc), rr = pc - bb * (g.H * g.W);
+          const int oh = g.fW.div(rr), ow = rr - oh * g.W;
+#pragma unroll
+          for (int k = 0; k < K0; ++k) {
+            const int kh = k / gi.KW, kw = k - kh * gi.KW;  // Cin = 1
+            const int ih0 = oh * gi.sh - gi.ph + kh * gi.dh, iw0 = ow * gi.sw - gi.pw + kw * gi.dw;
+            const bool in = okc && ih0 >= 0 && ih0 < gi.H && iw0 >= 0 && iw0 < gi.W;
+            const long xi = in ? ((long)bb * gi.H + ih0) * gi.W + iw0 : 0;
+            const float xv = xscale != 0.f ? fmaf((float)((const uint8_t*)x0)[xi], xscale, xshift)
+                                           : bf2f(((const bf16_raw*)x0)[xi]);
+            xk[u][q][k] = in ? xv : 0.f;
+          }
+        }
+      }
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
         const int k0 = kk * 32 + 8 * fq;
@@ -198,16 +254,25 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
       __builtin_amdgcn_wave_barrier();
       const int base = (g0 + u) * 16;
 #pragma unroll
-      for (int c = lane; c < 16 * CI / 8; c += 64) {  // a lane always lands on the same 8 columns
+      for (int q = 0; q < CPL; ++q) {  // a lane always lands on the same 8 columns
+        const int c = lane + 64 * q;
         const int row = c / (CI / 8), col = (c - row * (CI / 8)) * 8;
-        if (base + row < M) {
+        if (c < NCH && base + row < M) {
           bf16x8 v = *(const bf16x8*)(sc + row * CI + col);
-          const long o = (long)(base + row) * CI + col;
-          const bf16x8 pm = *(const bf16x8*)(ypp + o);  // unconditional (ypp = yprev or dx)
-          if (yprev) mask8(v, pm, act_prev);
-          *(bf16x8*)(dx + o) = v;
+          if (yprev) mask8(v, pmv[u][q], act_prev);
+          if constexpr (K0 > 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) cacc[j] += bf2f((uint16_t)v[j]);
+            for (int j = 0; j < 8; ++j) {
+              const float d = bf2f((uint16_t)v[j]);
+              cacc[j] += d;
+#pragma unroll
+              for (int k = 0; k < K0; ++k) cw[j][k] = fmaf(d, xk[u][q][k], cw[j][k]);
+            }
+          } else {
+            *(bf16x8*)(dx + (long)(base + row) * CI + col) = v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cacc[j] += bf2f((uint16_t)v[j]);
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -223,9 +288,27 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
 #pragma unroll
       for (int j = 0; j < 8; ++j) atomicAdd(csum + lane * 8 + j, cacc[j]);  // LDS atomics, 4 waves
     }
+    if constexpr (K0 > 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < K0; ++k)
+          for (int off = CI / 8; off < 64; off <<= 1) cw[j][k] += __shfl_xor(cw[j][k], off, 64);
+      if (lane < CI / 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int k = 0; k < K0; ++k) atomicAdd(cwsum + (lane * 8 + j) * K0 + k, cw[j][k]);
+      }
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < CI; i += blockDim.x)
       if (csum[i] != 0.f) atomicAdd(colsum + i, csum[i]);
+    if constexpr (K0 > 0) {
+      // no-return f32 atomics: ~1 us for ~200 workgroups into these few rows (row 'Global float atomics')
+      for (int i = threadIdx.x; i < CI * K0; i += blockDim.x)
+        if (cwsum[i] != 0.f) atomicAdd(dw0 + i, cwsum[i]);
+    }
   }
 }
 
@@ -289,31 +372,71 @@ extern "C" int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* ge
   return (int)hipGetLastError();
 }
 
-extern "C" int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
-                                       int act_prev, float* colsum, const void* y, int yact, hipStream_t st) {
+static ConvGeom cm_geom(const int* geom) {
   ConvGeom g;
   g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
   g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
   g.dh = geom[13]; g.dw = geom[14];
   g.init_div();
+  return g;
+}
+
+// the dgrad of this conv (geom) can carry the wgrad of the input layer feeding it (geom0)
+bool hopsx_conv_dgrad_fused_wgrad_ok(const int* geom, const int* geom0) {
+  const int K0 = geom0[7] * geom0[8] * geom0[3];
+  return hopsx_conv_dgrad_mfma_ok(geom) && geom[3] <= 64 && geom0[3] == 1 && (K0 == 4 || K0 == 9) &&
+         geom0[0] == geom[0] && geom0[4] == geom[1] && geom0[5] == geom[2] && geom0[6] == geom[3] &&
+         geom[7] * geom[8] * geom[6] <= 256 && !hopsx_disabled("fused_wgrad0");
+}
+
+extern "C" int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                       int act_prev, float* colsum, const void* y, int yact, hipStream_t st) {
+  return hopsx_conv2d_dgrad_mfma_ex(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, nullptr, nullptr, 0.f, 0.f,
+                                    nullptr, st);
+}
+
+extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                          int act_prev, float* colsum, const void* y, int yact, const int* geom0,
+                                          const void* x0, float xscale, float xshift, float* dw0, hipStream_t st) {
+  const bool fused = geom0 != nullptr;
+  if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
+  ConvGeom g0 = fused ? cm_geom(geom0) : ConvGeom{};
+  const int K0 = fused ? geom0[7] * geom0[8] : 0;
+  ConvGeom g = cm_geom(geom);
   const int K = g.KH * g.KW * g.CO;
   const int KS = cm_ks((K + 31) / 32);
   const long M = (long)g.B * g.H * g.W;
   long blocks = cm_grid((M + 15) / 16);
   if (colsum && blocks > 256) blocks = 256;  // one colsum atomic per channel per workgroup
-  const size_t shm =
-      (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) + (size_t)g.C * sizeof(float);
-#define HOPSX_CMD(NF, KSV)                                                                                     \
-  hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy,       \
+  const size_t shm = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
+                     (size_t)g.C * (1 + K0) * sizeof(float);
+  const int wvec = (uintptr_t)w % 16 == 0;
+#define HOPSX_CMD(NF, KSV, K0V)                                                                                \
+  hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy, \
                      (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,              \
-                     (const bf16_raw*)y, yact, g, K)
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0)
 #define HOPSX_CMD_NF(NF)          \
   switch (KS) {                   \
-    case 2: HOPSX_CMD(NF, 2); break;  \
-    case 4: HOPSX_CMD(NF, 4); break;  \
-    case 8: HOPSX_CMD(NF, 8); break;  \
-    case 9: HOPSX_CMD(NF, 9); break;  \
-    default: HOPSX_CMD(NF, 16); break; \
+    case 2: HOPSX_CMD(NF, 2, 0); break;  \
+    case 4: HOPSX_CMD(NF, 4, 0); break;  \
+    case 8: HOPSX_CMD(NF, 8, 0); break;  \
+    case 9: HOPSX_CMD(NF, 9, 0); break;  \
+    default: HOPSX_CMD(NF, 16, 0); break; \
+  }
+#define HOPSX_CMD_FUSED(NF, K0V)  \
+  switch (KS) {                   \
+    case 2: HOPSX_CMD(NF, 2, K0V); break;  \
+    case 4: HOPSX_CMD(NF, 4, K0V); break;  \
+    default: HOPSX_CMD(NF, 8, K0V); break;  \
+  }
+  if (fused) {  // K <= 256: KS in {2, 4, 8}
+    if (g.C != 16 && g.C != 32 && g.C != 64) return -2;
+    if (K0 == 4) {
+      if (g.C == 16) { HOPSX_CMD_FUSED(1, 4); } else if (g.C == 32) { HOPSX_CMD_FUSED(2, 4); } else { HOPSX_CMD_FUSED(4, 4); }
+    } else {
+      if (g.C == 16) { HOPSX_CMD_FUSED(1, 9); } else if (g.C == 32) { HOPSX_CMD_FUSED(2, 9); } else { HOPSX_CMD_FUSED(4, 9); }
+    }
+    return (int)hipGetLastError();
   }
   switch (g.C / 16) {
     case 1: HOPSX_CMD_NF(1); break;
@@ -322,6 +445,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int*
     case 8: HOPSX_CMD_NF(8); break;
     default: return -2;
   }
+#undef HOPSX_CMD_FUSED
 #undef HOPSX_CMD_NF
 #undef HOPSX_CMD
   return (int)hipGetLastError();

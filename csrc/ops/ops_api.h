@@ -84,6 +84,12 @@ int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* o
                           hipStream_t st);
 int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                             int act_prev, float* colsum, const void* y, int yact, hipStream_t st);
+// dgrad with the input layer's weight gradient fused into the epilogue (geom0: the input layer,
+// x0 its raw input, uint8 when xscale != 0; dw0 its [CO0][K0] grad, colsum its bias grad; dx unused)
+bool hopsx_conv_dgrad_fused_wgrad_ok(const int* geom, const int* geom0);
+int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                               int act_prev, float* colsum, const void* y, int yact, const int* geom0,
+                               const void* x0, float xscale, float xshift, float* dw0, hipStream_t st);
 
 // ---- zero-fill kernel (elementwise.hip): graph-safe replacement for hipMemsetAsync ----
 int hopsx_zero(void* p, long bytes, hipStream_t st);

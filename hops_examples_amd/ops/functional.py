@@ -103,28 +103,72 @@ def _pad_same(k, d=1):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None):
+    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None):
         x = x.contiguous()
         wb = _arena.weight_bf16(w)
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
         y = K.conv2d_fwd(x, wb, g, bias=b, act=act, in_affine=in_affine)
         ctx.save_for_backward(x, y)
-        ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine = w, b, g, act, in_affine
+        ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
+        # an input layer whose gradient was fused into the next conv receives no dY: do not
+        # let autograd materialise (and this backward then reduce) a zero tensor
+        ctx.set_materialize_grads(False)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        if dy is None:
+            return (None,) * 9
         x, y = ctx.saved_tensors
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
         gb = _wgrad_buf(b) if b is not None else None
         ymask = y if act else None
         dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.prev is not None:
+            # x is the output of the network's input layer: its weight/bias gradients are
+            # produced by this dgrad launch directly, dX is never materialised and the input
+            # layer's own backward is never reached (returning None for x)
+            w0, b0, g0, act0, aff0, x0 = ctx.prev
+            gw0, gb0 = _arena.grad_target(w0), _arena.grad_target(b0)
+            K.conv2d_dgrad_fused_wgrad(dy, _arena.weight_bf16(w), g, x, act0, ymask, act, x0, g0, gw0, gb0,
+                                       in_affine=aff0)
+            hooks.grad_ready(w0)
+            hooks.grad_ready(b0)
+        elif ctx.needs_input_grad[0]:
             dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act)
         gw = _wgrad_buf(w)
         K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
-        return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None)
+        return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None,
+                None)
+
+
+def _fusable_input_layer(x, geom):
+    """(w0, b0, geom0, act0, in_affine0, x0) when x is the output of the network's input layer
+    and that layer's weight gradient can ride on this conv's dgrad (see conv_mfma.hip K0)."""
+    prev = getattr(x, "_hx_input_layer", None)
+    if prev is None or not torch.is_grad_enabled() or "fused_wgrad0" in _disabled():
+        return None
+    w0, b0, g0 = prev[0], prev[1], prev[2]
+    if b0 is None or not w0.requires_grad or _arena.grad_target(w0) is None or _arena.grad_target(b0) is None:
+        return None
+    return prev if K.conv_dgrad_fused_wgrad_ok(geom, g0) else None
+
+
+def _disabled() -> str:
+    import os
+
+    return os.environ.get("HOPSX_DISABLE", "")
+
+
+def _conv_apply(x, w, b, st, pd, dl, a, in_affine):
+    """Apply the conv Function; tag the output of an input layer (input needs no gradient) so
+    the next conv can fuse this layer's weight gradient into its dgrad."""
+    prev = _fusable_input_layer(x, K.conv_geom(x.shape, w.shape, st, pd, dl)) if x.requires_grad else None
+    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev)
+    if not x.requires_grad and w.requires_grad and x.shape[-1] == 1:
+        y._hx_input_layer = (w, b, K.conv_geom(x.shape, w.shape, st, pd, dl), a, in_affine, x)
+    return y
 
 
 def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None):
@@ -149,7 +193,7 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
         elif padding != "same" or (w.shape[1] % 2 == 1 and w.shape[2] % 2 == 1):
             g = K.conv_geom(x.shape, w.shape, st, pd, dl)
             if K.conv_u8_fusable(g):
-                return _Conv2dFn.apply(x, w, b, st, pd, dl, a, (float(sc), float(sh)))
+                return _conv_apply(x, w, b, st, pd, dl, a, (float(sc), float(sh)))
             x = K.u8_normalize(x.contiguous(), float(sc), float(sh))
         else:
             x = K.u8_normalize(x.contiguous(), float(sc), float(sh))
@@ -166,7 +210,7 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
         th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
         x = F.pad(to_compute(x), (0, 0, tw // 2, tw - tw // 2, th // 2, th - th // 2))
         pd = (0, 0)
-    return _Conv2dFn.apply(to_compute(x), w, b, st, pd, dl, a, None)
+    return _conv_apply(to_compute(x), w, b, st, pd, dl, a, None)
 
 
 # ==================================================================== pooling

@@ -175,6 +175,26 @@ def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=N
     return out
 
 
+def conv_dgrad_fused_wgrad_ok(geom, geom0) -> bool:
+    """conv(geom)'s dgrad can carry the weight gradient of the input layer conv(geom0) feeding it."""
+    return bool(_C.ext().conv2d_dgrad_fused_wgrad_ok(list(geom), list(geom0)))
+
+
+def conv2d_dgrad_fused_wgrad(dy, w, geom, yprev, act_prev, y, act, x0, geom0, dw0, db0, in_affine=None):
+    """Backward of conv(geom) when its input came from the network's input layer conv(geom0):
+    instead of dX (which only that layer's wgrad would read) the kernel accumulates
+    dw0 += (dX * act_prev'(yprev))^T . im2col(x0) and db0 += column sums, in one launch."""
+    _req(dy, BF16, "dy")
+    _req(yprev, BF16, "yprev")
+    _req(x0, torch.uint8 if in_affine else BF16, "x0")
+    _req(dw0, F32, "dw0")
+    _req(db0, F32, "db0")
+    sc, sh = (float(in_affine[0]), float(in_affine[1])) if in_affine else (0.0, 0.0)
+    check(_C.ext().conv2d_dgrad_fused_wgrad(ptr(dy), ptr(w), list(geom), ptr(yprev), act_id(act_prev), ptr(db0),
+                                            ptr(y), act_id(act), list(geom0), ptr(x0), sc, sh, ptr(dw0), stream()),
+          "conv2d_dgrad_fused_wgrad")
+
+
 def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0, in_affine=None):
     """dw += (dy * act'(y))^T . im2col(x); dbias += per-channel sums of the masked dy.
     in_affine=(scale, shift): x is the raw uint8 input (see conv_u8_fusable)."""

@@ -122,3 +122,71 @@ def test_conv_mfma_dgrad_masks_colsum(k, C, CO, H, pad):
     torch.testing.assert_close(dx.float(), ref, atol=3e-2 * ref.abs().max().item(), rtol=2e-2)
     torch.testing.assert_close(cs, ref.sum((0, 1, 2)), atol=3e-2 * ref.abs().sum((0, 1, 2)).max().item() + 1e-2,
                                rtol=3e-2)
+
+
+@pytest.mark.parametrize("k0,pad0,C,CO,k,u8", [(2, 0, 32, 64, 2, True), (2, 0, 32, 64, 2, False),
+                                               (3, 1, 16, 32, 2, True), (3, 1, 64, 32, 2, False),
+                                               (2, 0, 32, 16, 3, True)])
+def test_dgrad_fused_input_layer_wgrad(k0, pad0, C, CO, k, u8):
+    """conv(g) dgrad carrying the input layer conv(g0) weight/bias gradient (no dX written):
+    compared with an fp32 autograd reference of the two-layer chain."""
+    torch.manual_seed(4)
+    B, H = 3, 20
+    sc, sh = (1 / 255.0, -0.5) if u8 else (None, None)
+    if u8:
+        x0 = torch.randint(0, 256, (B, H, H, 1), dtype=torch.uint8, device=dev)
+        x0f = x0.float() * sc + sh
+    else:
+        x0 = torch.randn(B, H, H, 1, device=dev).to(bf)
+        x0f = x0.float()
+    w0 = (torch.randn(C, k0, k0, 1, device=dev) * 0.5).to(bf)
+    b0 = torch.randn(C, device=dev) * 0.1
+    g0 = K.conv_geom(x0.shape, w0.shape, (1, 1), (pad0, pad0), (1, 1))
+    y0 = K.conv2d_fwd(x0, w0, g0, bias=b0, act="relu", in_affine=(sc, sh) if u8 else None)
+    w = (torch.randn(CO, k, k, C, device=dev) * 0.1).to(bf)
+    g = K.conv_geom(y0.shape, w.shape, (1, 1), (0, 0), (1, 1))
+    assert K.conv_dgrad_fused_wgrad_ok(g, g0)
+    OH = g[4]
+    y = torch.relu(torch.randn(B, OH, OH, CO, device=dev)).to(bf)
+    dy = torch.randn(B, OH, OH, CO, device=dev).to(bf)
+    dw0 = torch.zeros(C, k0 * k0, device=dev)
+    db0 = torch.zeros(C, device=dev)
+    K.conv2d_dgrad_fused_wgrad(dy, w, g, y0, "relu", y, "relu", x0, g0, dw0, db0,
+                               in_affine=(sc, sh) if u8 else None)
+    # reference: dX1 = conv^T(dy * relu'(y)) masked by relu'(y0), then the input layer's wgrad
+    xr = y0.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2)).backward((dy.float() * (y.float() > 0)).permute(0, 3, 1, 2))
+    d1 = (xr.grad.permute(0, 2, 3, 1) * (y0.float() > 0)).to(bf).float()  # the kernel masks bf16 dX
+    wr = torch.zeros(C, 1, k0, k0, device=dev, requires_grad=True)
+    F.conv2d(x0f.permute(0, 3, 1, 2), wr, padding=pad0).backward(d1.permute(0, 3, 1, 2))
+    rw = wr.grad.permute(0, 2, 3, 1).reshape(C, -1)
+    torch.testing.assert_close(dw0, rw, atol=2e-2 * rw.abs().max().item(), rtol=2e-2)
+    torch.testing.assert_close(db0, d1.sum((0, 1, 2)), atol=2e-2 * d1.abs().sum((0, 1, 2)).max().item() + 1e-3,
+                               rtol=2e-2)
+
+
+def test_mirrored_cnn_fused_input_wgrad_matches_unfused(monkeypatch):
+    """MirroredMnistCNN's conv1 weight gradient comes out of conv2's dgrad launch; the gradients
+    must equal the unfused path (separate dX + small-K wgrad) up to bf16 rounding."""
+    from hops_examples_amd.models.mnist import MirroredMnistCNN
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    grads = []
+    for disable in ("", "fused_wgrad0"):
+        monkeypatch.setenv("HOPSX_DISABLE", disable)
+        HF.seed_device_rng(7, dev)  # same dropout mask in both runs
+        torch.manual_seed(0)
+        m = MirroredMnistCNN().to(dev)
+        m.pool.salt = 7919  # per-instance dropout salt: pin it
+        ParamArena.from_module(m, dev)
+        x = torch.randint(0, 256, (16, 28, 28, 1), dtype=torch.uint8, device=dev)
+        t = torch.randint(0, 10, (16,), device=dev)
+        out = m(x)
+        _, _, _, dl = HF.loss_and_grad(out, t, "sparse_ce")
+        out.backward(dl)
+        torch.cuda.synchronize()
+        assert m.conv1.weight._hx_grad.abs().sum().item() > 0
+        grads.append(m._hx_arena.grad.float().clone())
+    a, b = grads
+    torch.testing.assert_close(a, b, atol=2e-2 * b.abs().max().item(), rtol=2e-2)

@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 TAG=${1:-q}
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/${TAG}_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider -x --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
 echo "EXIT tests $?" >> gpurun_out/${TAG}_tests.log
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1 || { echo "bench failed rc=$?" >> gpurun_out/${TAG}_bench.log; exit 1; }
 timeout -k 10 300 python bench.py --batch-per-gpu 2048 --no-taxi --steps 100 >> gpurun_out/${TAG}_bench.log 2>&1 || exit 1
