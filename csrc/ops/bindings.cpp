@@ -47,6 +47,11 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                                       P<float>(colsum), P<void>(y), yact, g0.data(), P<void>(x0), xscale, xshift,
                                       P<float>(dw0), S(st));
   });
+  m.def("wgrad_debug_times", [](int n) {
+    std::vector<unsigned long long> v((size_t)n);
+    hopsx_wgrad_debug_times(v.data(), n);
+    return v;
+  });
   m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
                            float xscale, float xshift, u counter, u st) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,

@@ -367,6 +367,8 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
     return (int)hipGetLastError();
   }
   if (xscale != 0.f) return -3;
+  if (hopsx_conv_wgrad_mfma_ok(geom) && (uintptr_t)dy % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0)
+    return hopsx_conv2d_wgrad_mfma(dy, x, geom, dw, dbias, y, yact, st);
   if (direct_ok(g)) {
     const int KC = N * M;
     int R = 1024 / KC;

@@ -10,6 +10,9 @@
 //   * v_mfma_f32_16x16x32_bf16 over all Cout fragments, then a fused epilogue (bias + act
 //     for fwd; act'(yprev) mask + previous layer's bias gradient for dgrad) written through
 //     a per-wave LDS transpose so the stores leave as 16-B vectors.
+#include <algorithm>
+#include <cstdlib>
+
 #include "gemm_core.h"
 #include "ops_api.h"
 
@@ -312,6 +315,182 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
   }
 }
 
+
+// ---------------------------------------------------------------------------- wgrad
+// dW[co][k] += sum_px dY'[px][co] * im2col(X)[px][k] (dY' = dY * act'(y)), db[co] += sum_px dY'[px][co]
+// for short convs (CO <= 64, C % 8 == 0).  The generic split-K GEMM walks 4+ K-tiles per
+// workgroup with a workgroup barrier and a dependent global round trip each.  Here:
+//   * grid = (pixel groups, 16*NFKW-column blocks of K): a workgroup owns a CO x 16*NFKW
+//     output block and a contiguous run of 32-pixel chunks (the MFMA K), split over its 4 waves;
+//   * each wave stages its chunk (dY' and the 16-B im2col gathers of X) into a wave-private
+//     LDS image (no workgroup barrier in the loop) while the next chunk's loads are in flight,
+//     and reads both MFMA operands back transposed with ds_read_b64_tr_b16 (T10): the
+//     reduction runs over pixels, the rows of the NHWC images;
+//   * the waves meet once: lane-major float4 partials in LDS (conflict-free), summed, restaged
+//     row-major, and the workgroup leaves one coalesced no-return f32 atomic per output element.
+// (LDS float atomics were measured at ~200 cycles per ds_add_f32 here: not used.)
+constexpr int WG_PX = 32;  // pixels per wave chunk (= MFMA K)
+// per-workgroup phase timestamps (100 MHz wall clock), written only when HOPSX_PHASE_DBG is set:
+// tools/dbg_wgrad.py reads them back to split a launch into load / compute / reduce / atomics
+__device__ unsigned long long g_wgrad_dbg[2048 * 4];
+__device__ __forceinline__ void phase_mark(int on, int slot) {
+  if (on && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 2048) g_wgrad_dbg[blockIdx.x * 4 + slot] = wall_clock64();
+}
+
+template <int NFC, int NFKW>
+__global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
+                                                        const bf16_raw* __restrict__ y, int yact,
+                                                        float* __restrict__ dw, float* __restrict__ dbias, ConvGeom g,
+                                                        int K, int cpw, int dbg) {
+  phase_mark(dbg, 0);
+  constexpr int CO = NFC * 16, KB = NFKW * 16;
+  constexpr int DCH = WG_PX * CO / 8 / 64;  // 16-B dY chunks per lane per pixel chunk
+  constexpr int XCH = WG_PX * KB / 8 / 64;  // 16-B im2col chunks per lane per pixel chunk
+  static_assert(DCH >= 1 && XCH >= 1, "tile too small");
+  constexpr int NFR = NFC * NFKW;           // output fragments per wave
+  extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bf16_raw* sA = cm_smem + wave * WG_PX * (CO + KB);  // [px][CO]  rc-swizzled
+  bf16_raw* sB = sA + WG_PX * CO;                     // [px][KB]  rc-swizzled
+  const int kb0 = blockIdx.y * KB;
+  const int M = g.B * g.OH * g.OW;
+  const int nchunks = (M + WG_PX - 1) / WG_PX;
+  // this lane's fixed columns: dY chunk column dc (8 channels), im2col chunk column xc (8 ci of one tap)
+  const int dc = lane % (CO / 8);
+  const int xc = lane % (KB / 8);
+  const int kcol = kb0 + xc * 8;
+  const bool kin = kcol < K;
+  const int tap = kin ? g.fC.div(kcol) : 0, ci0 = kin ? kcol - tap * g.C : 0;
+  const int kh = g.fKW.div(tap), kw = tap - kh * g.KW;
+  const bool do_bias = dbias != nullptr && blockIdx.y == 0;
+  f32x4 acc[NFC][NFKW];
+#pragma unroll
+  for (int i = 0; i < NFC; ++i)
+#pragma unroll
+    for (int j = 0; j < NFKW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float cacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+
+  bf16x8 dv[DCH], xv[XCH];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < DCH; ++i) {
+      const int p = c * WG_PX + (lane + 64 * i) / (CO / 8);
+      const bool ok = p < M;
+      const long o = (long)(ok ? p : 0) * CO + dc * 8;
+      bf16x8 v = zero_unless(*(const bf16x8*)(dy + o), ok);
+      if (y) mask8(v, *(const bf16x8*)(y + o), yact);
+      dv[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int p = c * WG_PX + (lane + 64 * i) / (KB / 8);
+      const int pc = p < M ? p : 0;
+      const int b = g.fOHW.div(pc), rem = pc - b * (g.OH * g.OW);
+      const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
+      const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
+      const bool ok = kin && p < M && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const long o = ok ? (((long)b * g.H + ih) * g.W + iw) * g.C + ci0 : 0;
+      xv[i] = zero_unless(*(const bf16x8*)(x + o), ok);
+    }
+  };
+  // transposed fragment read (T10): lane 4q+p addresses row 8fq+q (+4), columns col0+4p..+3
+  auto frag = [&](const bf16_raw* sm, int col0, int ROWS) -> bf16x8 {
+    const int cpr = ROWS / 8;
+    const int col = col0 + 4 * tp;
+    const int k1 = 8 * fq + tq, k2 = k1 + 4;
+    const bf16_raw* p1 = sm + k1 * ROWS + 8 * ((col >> 3) ^ rc_swz(k1, cpr)) + (col & 7);
+    const bf16_raw* p2 = sm + k2 * ROWS + 8 * ((col >> 3) ^ rc_swz(k2, cpr)) + (col & 7);
+    bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_ptr)(p1));
+    bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_ptr)(p2));
+    return (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  };
+
+  const int cbeg = (blockIdx.x * 4 + wave) * cpw;
+  const int cend = min(nchunks, cbeg + cpw);
+  if (cbeg < cend) load(cbeg);
+  for (int c = cbeg; c < cend; ++c) {  // wave-uniform: EXEC stays full for the tr reads
+#pragma unroll
+    for (int i = 0; i < DCH; ++i) {
+      const int px = (lane + 64 * i) / (CO / 8);
+      *(bf16x8*)(sA + px * CO + 8 * (dc ^ rc_swz(px, CO / 8))) = dv[i];
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cacc[j] += bf2f((uint16_t)dv[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int px = (lane + 64 * i) / (KB / 8);
+      *(bf16x8*)(sB + px * KB + 8 * (xc ^ rc_swz(px, KB / 8))) = xv[i];
+    }
+    if (c + 1 < cend) load(c + 1);  // in flight behind this chunk's MFMAs
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    bf16x8 af[NFC], bfr[NFKW];
+#pragma unroll
+    for (int i = 0; i < NFC; ++i) af[i] = frag(sA, i * 16, CO);
+#pragma unroll
+    for (int j = 0; j < NFKW; ++j) bfr[j] = frag(sB, j * 16, KB);
+#pragma unroll
+    for (int i = 0; i < NFC; ++i)
+#pragma unroll
+      for (int j = 0; j < NFKW; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next chunk's writes
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- cross-wave reduction (the staging images are free after this barrier)
+  phase_mark(dbg, 1);
+  __syncthreads();
+  f32x4* red4 = (f32x4*)cm_smem;  // [wave][NFR][64] lane-major: conflict-free 16-B accesses
+#pragma unroll
+  for (int i = 0; i < NFC; ++i)
+#pragma unroll
+    for (int j = 0; j < NFKW; ++j) red4[(wave * NFR + i * NFKW + j) * 64 + lane] = acc[i][j];
+  float* bsum = (float*)(red4 + 4 * NFR * 64);  // [4][CO] per-wave bias partials
+  if (do_bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      for (int off = CO / 8; off < 64; off <<= 1) cacc[j] += __shfl_xor(cacc[j], off, 64);
+    if (lane < CO / 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bsum[wave * CO + lane * 8 + j] = cacc[j];
+    }
+  }
+  __syncthreads();
+  // sum the 4 waves' copies, restage row-major [CO][KB] behind them
+  float* rowm = (float*)(bsum + 4 * CO);
+  for (int e = threadIdx.x; e < NFR * 64; e += 256) {
+    const int f = e >> 6, l = e & 63;
+    f32x4 v = red4[f * 64 + l];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const f32x4 u = red4[(w * NFR + f) * 64 + l];
+      v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+    }
+    const int i = f / NFKW, j = f - i * NFKW;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rowm[(i * 16 + (l >> 4) * 4 + r) * KB + j * 16 + (l & 15)] = v[r];
+  }
+  __syncthreads();
+  phase_mark(dbg, 2);
+  for (int e = threadIdx.x; e < CO * KB; e += 256) {
+    const int co = e / KB, col = e - co * KB;
+    const float v = rowm[e];
+    if (kb0 + col < K && v != 0.f) atomicAdd(dw + (long)co * K + kb0 + col, v);
+  }
+  if (do_bias)
+    for (int e = threadIdx.x; e < CO; e += 256) {
+      const float v = bsum[e] + bsum[CO + e] + bsum[2 * CO + e] + bsum[3 * CO + e];
+      if (v != 0.f) atomicAdd(dbias + e, v);
+    }
+  if (dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    phase_mark(dbg, 3);
+  }
+}
+
 // supported K-step counts (K is zero-padded up to one of them)
 int cm_ks(int ks) { return ks <= 2 ? 2 : ks <= 4 ? 4 : ks <= 8 ? 8 : ks <= 9 ? 9 : 16; }
 
@@ -449,4 +628,50 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
 #undef HOPSX_CMD_NF
 #undef HOPSX_CMD
   return (int)hipGetLastError();
+}
+
+// short-conv weight gradient on MFMA: C % 8 == 0, CO in {16, 32, 64}, K = KH*KW*C <= 256
+bool hopsx_conv_wgrad_mfma_ok(const int* geom) {
+  const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * C;
+  return C % 8 == 0 && K <= 256 && (CO == 16 || CO == 32 || CO == 64) && !hopsx_disabled("wgrad_mfma");
+}
+
+extern "C" int hopsx_conv2d_wgrad_mfma(const void* dy, const void* x, const int* geom, float* dw, float* dbias,
+                                       const void* y, int yact, hipStream_t st) {
+  ConvGeom g = cm_geom(geom);
+  const int K = g.KH * g.KW * g.C;
+  const long M = (long)g.B * g.OH * g.OW;
+  const long nchunks = (M + WG_PX - 1) / WG_PX;
+  static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
+  static const int nfkw_env = getenv("HOPSX_WGRAD_NFKW") ? atoi(getenv("HOPSX_WGRAD_NFKW")) : 2;
+  const int NFKW = nfkw_env == 4 ? 4 : 2, KB = NFKW * 16;  // 32-column blocks: 8 KB of atomics per workgroup
+  const int colblk = (K + KB - 1) / KB;
+  // ~384 workgroups in all: each wave walks a run of cpw chunks with one chunk of prefetch
+  static const int cpw_env = getenv("HOPSX_WGRAD_CPW") ? atoi(getenv("HOPSX_WGRAD_CPW")) : 0;
+  const long want_groups = std::max(1L, 384L / colblk);
+  int cpw = cpw_env > 0 ? cpw_env : (int)std::max(1L, (nchunks + 4 * want_groups - 1) / (4 * want_groups));
+  const long groups = (nchunks + 4L * cpw - 1) / (4L * cpw);
+  dim3 grid((unsigned)groups, (unsigned)colblk);
+  const size_t stage = (size_t)4 * WG_PX * (g.CO + KB) * sizeof(bf16_raw);
+  const int NFR = (g.CO / 16) * NFKW;
+  const size_t redb = ((size_t)4 * NFR * 64 * 4 + 4 * g.CO + (size_t)g.CO * KB) * sizeof(float);
+  const size_t shm = std::max(stage, redb);
+#define HOPSX_CWM(NFC)                                                                                     \
+  if (NFKW == 4) hipLaunchKernelGGL((conv_wgrad_mfma_k<NFC, 4>), grid, dim3(256), shm, st, (const bf16_raw*)dy, \
+                     (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, K, cpw, dbg);                     \
+  else hipLaunchKernelGGL((conv_wgrad_mfma_k<NFC, 2>), grid, dim3(256), shm, st, (const bf16_raw*)dy,           \
+                     (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, K, cpw, dbg)
+  switch (g.CO) {
+    case 16: HOPSX_CWM(1); break;
+    case 32: HOPSX_CWM(2); break;
+    case 64: HOPSX_CWM(4); break;
+    default: return -2;
+  }
+#undef HOPSX_CWM
+  return (int)hipGetLastError();
+}
+
+extern "C" int hopsx_wgrad_debug_times(unsigned long long* host_out, int n) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wgrad_dbg), sizeof(unsigned long long) * (size_t)n, 0,
+                                  hipMemcpyDeviceToHost);
 }

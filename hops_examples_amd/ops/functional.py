@@ -11,6 +11,8 @@ test-suite and the ``experiment.launch`` CPU config (BASELINE.json config 1).
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -123,7 +125,10 @@ class _Conv2dFn(torch.autograd.Function):
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
         gb = _wgrad_buf(b) if b is not None else None
-        ymask = y if act else None
+        premasked = act == 1 and _take_premasked(dy)
+        ymask = y if (act and not premasked) else None
+        if premasked:
+            act = 0
         dx = None
         if ctx.prev is not None:
             # x is the output of the network's input layer: its weight/bias gradients are
@@ -166,6 +171,8 @@ def _conv_apply(x, w, b, st, pd, dl, a, in_affine):
     the next conv can fuse this layer's weight gradient into its dgrad."""
     prev = _fusable_input_layer(x, K.conv_geom(x.shape, w.shape, st, pd, dl)) if x.requires_grad else None
     y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev)
+    if a:
+        y._hx_act_out = a  # activation fused into this conv's epilogue (see max_pool2d premask)
     if not x.requires_grad and w.requires_grad and x.shape[-1] == 1:
         y._hx_input_layer = (w, b, K.conv_geom(x.shape, w.shape, st, pd, dl), a, in_affine, x)
     return y
@@ -214,22 +221,44 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
 
 
 # ==================================================================== pooling
+# data_ptrs of gradients that already carry the ReLU' mask of the tensor they are the gradient
+# of (applied by the max-pool backward at its argmax scatter): the producing conv's backward
+# then skips its own mask and never loads its activation output (half the dY traffic of its
+# dgrad/wgrad).  Written and consumed within one backward pass (also during graph capture).
+_PREMASKED: dict = {}  # data_ptr -> weakref of the pool's dX (a dead ref means the memory may be reused)
+
+
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p, drop_p, salt):
+    def forward(ctx, x, k, s, p, drop_p, salt, premask):
         x = x.contiguous()
         rng = rng_state(x.device) if drop_p > 0 else None
         y, am = K.maxpool2d_fwd(x, k, s, p, drop_p=drop_p, rng=rng, salt=salt)
-        ctx.save_for_backward(am)
-        ctx.cfg = (x.shape, k, s, p, drop_p, rng, salt)
+        if premask:
+            ctx.save_for_backward(am, x)
+        else:
+            ctx.save_for_backward(am)
+        ctx.cfg = (x.shape, k, s, p, drop_p, rng, salt, premask)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (am,) = ctx.saved_tensors
-        shape, k, s, p, drop_p, rng, salt = ctx.cfg
+        shape, k, s, p, drop_p, rng, salt, premask = ctx.cfg
         dy = dy.to(BF16).contiguous()
-        return K.maxpool2d_bwd(dy, am, shape, k, s, p, drop_p=drop_p, rng=rng, salt=salt), None, None, None, None, None
+        if premask:
+            am, x = ctx.saved_tensors
+            dx = K.maxpool2d_bwd(dy, am, shape, k, s, p, x=x, act="relu", drop_p=drop_p, rng=rng, salt=salt)
+            _PREMASKED[dx.data_ptr()] = weakref.ref(dx)
+        else:
+            (am,) = ctx.saved_tensors
+            dx = K.maxpool2d_bwd(dy, am, shape, k, s, p, drop_p=drop_p, rng=rng, salt=salt)
+        return dx, None, None, None, None, None, None
+
+
+def _take_premasked(dy) -> bool:
+    ref = _PREMASKED.pop(dy.data_ptr(), None)
+    src = ref() if ref is not None else None
+    return src is not None and src.shape == dy.shape
 
 
 def max_pool2d(x, kernel, stride=None, padding=0, dropout_p: float = 0.0, training: bool = True, salt: int = 0):
@@ -241,7 +270,11 @@ def max_pool2d(x, kernel, stride=None, padding=0, dropout_p: float = 0.0, traini
     if not x.is_cuda:
         y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous()
         return F.dropout(y, dp, True) if dp > 0 else y
-    return _MaxPoolFn.apply(to_compute(x), k, s, p, dp, salt)
+    # a ReLU conv output feeding the pool: apply ReLU' at the argmax scatter (idempotent, so it
+    # stays correct if the conv output has other consumers whose gradients get added)
+    premask = (getattr(x, "_hx_act_out", None) == 1 and x.requires_grad and x.dtype == BF16
+               and "premask" not in _disabled())
+    return _MaxPoolFn.apply(to_compute(x), k, s, p, dp, salt, premask)
 
 
 class _GapFn(torch.autograd.Function):

@@ -190,3 +190,53 @@ def test_mirrored_cnn_fused_input_wgrad_matches_unfused(monkeypatch):
         grads.append(m._hx_arena.grad.float().clone())
     a, b = grads
     torch.testing.assert_close(a, b, atol=2e-2 * b.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("k,C,CO,H,pad,stride", [(2, 32, 64, 27, 0, 1), (3, 16, 16, 16, 1, 1), (1, 64, 16, 7, 0, 1),
+                                                 (3, 8, 64, 11, 1, 1), (3, 16, 32, 16, 1, 2), (2, 32, 32, 5, 0, 1)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_conv_wgrad_mfma(k, C, CO, H, pad, stride, masked):
+    """Direct MFMA weight gradient (wave-private LDS images read back with ds_read_b64_tr_b16)."""
+    torch.manual_seed(5)
+    B = 3
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    g = K.conv_geom(x.shape, (CO, k, k, C), (stride, stride), (pad, pad), (1, 1))
+    OH, OW = g[4], g[5]
+    dy = torch.randn(B, OH, OW, CO, device=dev).to(bf)
+    y = torch.relu(torch.randn(B, OH, OW, CO, device=dev)).to(bf) if masked else None
+    dw = torch.zeros(CO, k * k * C, device=dev)
+    db = torch.zeros(CO, device=dev)
+    K.conv2d_wgrad(dy, x, g, dw, dbias=db, y=y, act="relu" if masked else 0)
+    d = dy.float() * ((y.float() > 0).float() if masked else 1.0)
+    wr = torch.zeros(CO, C, k, k, device=dev, requires_grad=True)
+    F.conv2d(x.float().permute(0, 3, 1, 2), wr, stride=stride, padding=pad).backward(d.permute(0, 3, 1, 2))
+    rw = wr.grad.permute(0, 2, 3, 1).reshape(CO, -1)
+    torch.testing.assert_close(dw, rw, atol=2e-2 * rw.abs().max().item(), rtol=1e-2)
+    rb = d.sum((0, 1, 2))
+    torch.testing.assert_close(db, rb, atol=2e-2 * rb.abs().max().item() + 1e-3, rtol=1e-2)
+
+
+def test_pool_premask_matches_conv_mask(monkeypatch):
+    """conv(ReLU) -> max-pool: the ReLU' mask moved into the pool backward gives the same
+    gradients as the conv applying it itself."""
+    from hops_examples_amd.models.mnist import MirroredMnistCNN
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    grads = []
+    for disable in ("", "premask"):
+        monkeypatch.setenv("HOPSX_DISABLE", disable)
+        HF.seed_device_rng(11, dev)
+        torch.manual_seed(0)
+        m = MirroredMnistCNN().to(dev)
+        m.pool.salt = 7919
+        ParamArena.from_module(m, dev)
+        x = torch.randint(0, 256, (16, 28, 28, 1), dtype=torch.uint8, device=dev)
+        t = torch.randint(0, 10, (16,), device=dev)
+        out = m(x)
+        _, _, _, dl = HF.loss_and_grad(out, t, "sparse_ce")
+        out.backward(dl)
+        torch.cuda.synchronize()
+        grads.append(m._hx_arena.grad.float().clone())
+    assert not HF._PREMASKED
+    torch.testing.assert_close(grads[0], grads[1], atol=2e-2 * grads[1].abs().max().item(), rtol=2e-2)

@@ -15,6 +15,7 @@ w2 = (torch.randn(64, 2, 2, 32, device=dev) * 0.1).to(bf)
 b1 = torch.zeros(32, device=dev); b2 = torch.zeros(64, device=dev)
 g1 = K.conv_geom(xn.shape, w1.shape, (1, 1), (0, 0), (1, 1))
 h1 = K.conv2d_fwd(xn, w1, g1, bias=b1, act=1)
+g1u = K.conv_geom(x0.shape, w1.shape, (1, 1), (0, 0), (1, 1))
 g2 = K.conv_geom(h1.shape, w2.shape, (1, 1), (0, 0), (1, 1))
 h2 = K.conv2d_fwd(h1, w2, g2, bias=b2, act=1)
 p, am = K.maxpool2d_fwd(h2, (2, 2), (2, 2), (0, 0))
@@ -39,6 +40,9 @@ ops = {
     "fc1_wgrad": lambda: K.linear_wgrad(df1, flat, dwf1, y=f1, act=1),
     "pool_bwd": lambda: K.maxpool2d_bwd(dyp, am, h2.shape, (2, 2), (2, 2), (0, 0)),
     "conv2_dgrad": lambda: K.conv2d_dgrad(dy2, w2, g2, yprev=h1, act_prev=1, y=h2, act=1),
+    "conv2_dgrad_cs": lambda: K.conv2d_dgrad(dy2, w2, g2, yprev=h1, act_prev=1, y=h2, act=1, colsum=db1),
+    "conv2_dgrad_fused": lambda: K.conv2d_dgrad_fused_wgrad(dy2, w2, g2, h1, 1, h2, 1, x0, g1u, dw1, db1,
+                                                            in_affine=(1 / 255, -0.5)),
     "conv2_wgrad": lambda: K.conv2d_wgrad(dy2, h1, g2, dw2, dbias=db2, y=h2, act=1),
     "conv1_wgrad": lambda: K.conv2d_wgrad(dh1, xn, g1, dw1, dbias=db1, y=h1, act=1),
 }
