@@ -20,6 +20,13 @@ using namespace hopsx;
 
 namespace {
 
+// per-workgroup phase timestamps (100 MHz wall clock), written only when HOPSX_PHASE_DBG is set:
+// tools/dbg_wgrad.py reads them back to split a launch into load / compute / reduce / atomics
+__device__ unsigned long long g_wgrad_dbg[2048 * 4];
+__device__ __forceinline__ void phase_mark(int on, int slot) {
+  if (on && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 2048) g_wgrad_dbg[blockIdx.x * 4 + slot] = wall_clock64();
+}
+
 constexpr int CM_WAVES = 4;
 constexpr int CM_UN = 2;  // pixel groups per wave per trip
 
@@ -127,47 +134,49 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
 // multiplies each masked dX row by the input layer's im2col row (K0 raw pixels, uint8 with the
 // fused affine or bf16) and accumulates dW0[ci][k] in registers; the previous layer's bias
 // gradient is the existing colsum.  Saves the dX write/re-read and a whole launch.
-template <int NF, int KS, int K0>
+template <int NF, int KS, int K0, int UN>
 __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ w,
                                                         bf16_raw* __restrict__ dx, const bf16_raw* __restrict__ yprev,
                                                         int act_prev, float* __restrict__ colsum,
                                                         const bf16_raw* __restrict__ y, int yact, ConvGeom g, int K,
                                                         int wvec, const void* __restrict__ x0, float xscale,
-                                                        float xshift, ConvGeom gi, float* __restrict__ dw0) {
+                                                        float xshift, ConvGeom gi, float* __restrict__ dw0, int dbg) {
+  phase_mark(dbg, 0);
   constexpr int CI = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
   constexpr int cpr = KS * 4;
   constexpr int RS = cm_rs(cpr);
-  bf16_raw* sw = cm_smem;                     // [CI][RS*8]: (ci, k=(kh,kw,co)) = W[co][kh][kw][ci]
-  bf16_raw* scratch = cm_smem + CI * RS * 8;  // [waves][16][CI]
+  // W image [KP = 32*KS rows k = (kh,kw,co)][CI] rc-swizzled: every 16-B chunk of W (8 ci of one
+  // (co,kh,kw) row) lands whole in image row k, so staging is one 16-B load + one ds_write_b128 per
+  // chunk; the MFMA B fragments (8 consecutive k at one ci) come back via ds_read_b64_tr_b16.
+  (void)RS;
+  bf16_raw* sw = cm_smem;                     // [KP][CI]
+  bf16_raw* scratch = cm_smem + CI * RS * 8;  // [waves][16][CI]   (CI*RS*8 >= KP*CI)
   float* csum = (float*)(scratch + CM_WAVES * 16 * CI);  // [CI]
-  // zero the K padding, then scatter W (read in its own order: coalesced) into the
-  // transposed image; the 2-B LDS writes are cheap next to strided global reads
-  for (int i = threadIdx.x; i < CI * (cpr * 8 - K); i += blockDim.x) {
-    const int ci = i / (cpr * 8 - K), kk = K + i - ci * (cpr * 8 - K);
-    sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = 0;
+  constexpr int CPR = CI / 8;  // 16-B chunks per image row
+  const int T = g.KH * g.KW;
+  for (int i = threadIdx.x; i < (cpr * 8 - K) * CPR; i += blockDim.x) {  // zero the K padding rows
+    const int kk = K + i / CPR, c8 = i % CPR;
+    *(bf16x8*)(sw + kk * CI + 8 * (c8 ^ rc_swz(kk, CPR))) = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   }
-  if (wvec) {  // 16-B loads of 8 consecutive ci (CI % 8 == 0, 16-B aligned W): 8x fewer global loads
-    for (int i = threadIdx.x; i < K * CI / 8; i += blockDim.x) {
-      const int r = i / (CI / 8), ci0 = (i - r * (CI / 8)) * 8;
-      const int co = r / (g.KH * g.KW), t = r - co * (g.KH * g.KW);
+  if (wvec) {
+    for (int i = threadIdx.x; i < K * CPR; i += blockDim.x) {
+      const int r = i / CPR, c8 = i - r * CPR;  // source row r = co*T + t
+      const int co = r / T, t = r - co * T;
       const int kk = t * g.CO + co;
-      const bf16x8 v = *(const bf16x8*)(w + (long)i * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sw[(ci0 + j) * RS * 8 + 8 * cm_swz(ci0 + j, kk >> 3, cpr) + (kk & 7)] = v[j];
+      *(bf16x8*)(sw + kk * CI + 8 * (c8 ^ rc_swz(kk, CPR))) = *(const bf16x8*)(w + (long)i * 8);
     }
   } else {
     for (int i = threadIdx.x; i < K * CI; i += blockDim.x) {
-      const int ci = i % CI, r = i / CI;               // r = co*KH*KW + t  (source order [co][kh][kw][ci])
-      const int co = r / (g.KH * g.KW), t = r - co * (g.KH * g.KW);
-      const int kk = t * g.CO + co;                     // k = (kh, kw, co)
-      sw[ci * RS * 8 + 8 * cm_swz(ci, kk >> 3, cpr) + (kk & 7)] = w[i];
+      const int ci = i % CI, r = i / CI;
+      const int co = r / T, t = r - co * T;
+      const int kk = t * g.CO + co;
+      sw[kk * CI + 8 * ((ci >> 3) ^ rc_swz(kk, CPR)) + (ci & 7)] = w[i];
     }
   }
-  for (int i = threadIdx.x; i < CI; i += blockDim.x) csum[i] = 0.f;
-  float* cwsum = csum + CI;  // [CI][K0] (K0 > 0)
-  for (int i = threadIdx.x; i < CI * K0; i += blockDim.x) cwsum[i] = 0.f;
+  float* cwsum = csum + CM_WAVES * CI;  // [wave][CI][K0] (K0 > 0); csum is [wave][CI]
   __syncthreads();
+  phase_mark(dbg, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int M = g.B * g.H * g.W;
@@ -184,12 +193,12 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
   constexpr int NCH = 16 * CI / 8;      // 16-B output chunks per 16-pixel group
   constexpr int CPL = (NCH + 63) / 64;  // of which this lane stores CPL (c = lane + 64 q)
   constexpr int XK = K0 > 0 ? K0 : 1;
-  for (int g0 = (blockIdx.x * CM_WAVES + wave) * CM_UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * CM_UN) {
-    bf16x8 a[CM_UN][KS];
-    bf16x8 pmv[CM_UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
-    float xk[CM_UN][CPL][XK];
+  for (int g0 = (blockIdx.x * CM_WAVES + wave) * UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * UN) {
+    bf16x8 a[UN][KS];
+    bf16x8 pmv[UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
+    float xk[UN][CPL][XK];
 #pragma unroll
-    for (int u = 0; u < CM_UN; ++u) {
+    for (int u = 0; u < UN; ++u) {
       const int px = (g0 + u) * 16 + fr;
       const bool pok = (g0 + u) < ngroups && px < M;
       const int pp = pok ? px : 0;
@@ -229,13 +238,12 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
         const bool ok = pok && k0 < K && oh >= 0 && oh < g.OH && ow >= 0 && ow < g.OW;
         const long o = ok ? (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co : 0;
         bf16x8 v = zero_unless(*(const bf16x8*)(dy + o), ok);
-        const bf16x8 ym = *(const bf16x8*)(yp + o);  // unconditional load (yp = y or dy)
-        if (y) mask8(v, ym, yact);
+        if (y) mask8(v, *(const bf16x8*)(yp + o), yact);  // y is uniform: no load when dY is pre-masked
         a[u][kk] = v;
       }
     }
 #pragma unroll
-    for (int u = 0; u < CM_UN; ++u) {
+    for (int u = 0; u < UN; ++u) {
       if (g0 + u >= ngroups) break;
       f32x4 acc[NF];
 #pragma unroll
@@ -244,8 +252,14 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf) {
-          const int ci = nf * 16 + fr;
-          const bf16x8 bfr = *(const bf16x8*)(sw + ci * RS * 8 + 8 * cm_swz(ci, kk * 4 + fq, cpr));
+          // transposed read (T10): lane 4q+p addresses rows k1 = 32kk+8fq+q (+4), ci = 16nf+4p..+3
+          const int col = nf * 16 + 4 * (lane & 3);
+          const int k1 = kk * 32 + 8 * fq + ((lane & 15) >> 2), k2 = k1 + 4;
+          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4_ptr)(sw + k1 * CI + 8 * ((col >> 3) ^ rc_swz(k1, CPR)) + (col & 7)));
+          const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4_ptr)(sw + k2 * CI + 8 * ((col >> 3) ^ rc_swz(k2, CPR)) + (col & 7)));
+          const bf16x8 bfr = (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
           acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][kk], bfr, acc[nf], 0, 0, 0);
         }
       }
@@ -281,15 +295,17 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
       __builtin_amdgcn_wave_barrier();
     }
   }
+  phase_mark(dbg, 2);
   if (colsum) {
     // lanes l, l + CI/8, l + 2*CI/8, ... own the same 8 columns
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int off = CI / 8; off < 64; off <<= 1) cacc[j] += __shfl_xor(cacc[j], off, 64);
+    // per-wave partial slots (LDS float atomics cost ~200 cycles each here), summed after one barrier
     if (lane < CI / 8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(csum + lane * 8 + j, cacc[j]);  // LDS atomics, 4 waves
+      for (int j = 0; j < 8; ++j) csum[wave * CI + lane * 8 + j] = cacc[j];
     }
     if constexpr (K0 > 0) {
 #pragma unroll
@@ -301,17 +317,25 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int k = 0; k < K0; ++k) atomicAdd(cwsum + (lane * 8 + j) * K0 + k, cw[j][k]);
+          for (int k = 0; k < K0; ++k) cwsum[wave * CI * K0 + (lane * 8 + j) * K0 + k] = cw[j][k];
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < CI; i += blockDim.x)
-      if (csum[i] != 0.f) atomicAdd(colsum + i, csum[i]);
+    for (int i = threadIdx.x; i < CI; i += blockDim.x) {
+      const float v = csum[i] + csum[CI + i] + csum[2 * CI + i] + csum[3 * CI + i];
+      if (v != 0.f) atomicAdd(colsum + i, v);
+    }
     if constexpr (K0 > 0) {
       // no-return f32 atomics: ~1 us for ~200 workgroups into these few rows (row 'Global float atomics')
-      for (int i = threadIdx.x; i < CI * K0; i += blockDim.x)
-        if (cwsum[i] != 0.f) atomicAdd(dw0 + i, cwsum[i]);
+      for (int i = threadIdx.x; i < CI * K0; i += blockDim.x) {
+        const float v = cwsum[i] + cwsum[CI * K0 + i] + cwsum[2 * CI * K0 + i] + cwsum[3 * CI * K0 + i];
+        if (v != 0.f) atomicAdd(dw0 + i, v);
+      }
     }
+  }
+  if (dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    phase_mark(dbg, 3);
   }
 }
 
@@ -330,12 +354,6 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
 //     row-major, and the workgroup leaves one coalesced no-return f32 atomic per output element.
 // (LDS float atomics were measured at ~200 cycles per ds_add_f32 here: not used.)
 constexpr int WG_PX = 32;  // pixels per wave chunk (= MFMA K)
-// per-workgroup phase timestamps (100 MHz wall clock), written only when HOPSX_PHASE_DBG is set:
-// tools/dbg_wgrad.py reads them back to split a launch into load / compute / reduce / atomics
-__device__ unsigned long long g_wgrad_dbg[2048 * 4];
-__device__ __forceinline__ void phase_mark(int on, int slot) {
-  if (on && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 2048) g_wgrad_dbg[blockIdx.x * 4 + slot] = wall_clock64();
-}
 
 template <int NFC, int NFKW>
 __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
@@ -585,15 +603,24 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   const int K = g.KH * g.KW * g.CO;
   const int KS = cm_ks((K + 31) / 32);
   const long M = (long)g.B * g.H * g.W;
-  long blocks = cm_grid((M + 15) / 16);
-  if (colsum && blocks > 256) blocks = 256;  // one colsum atomic per channel per workgroup
+  // two 16-pixel groups per wave per trip (HOPSX_DGRAD_UN=1: one)
+  static const int un_env = getenv("HOPSX_DGRAD_UN") ? atoi(getenv("HOPSX_DGRAD_UN")) : 0;
+  const long ngroups = (M + 15) / 16;
+  const int un = un_env == 1 ? 1 : 2;  // UN=1 measured slower at the MNIST shape (more colsum atomics)
+  long blocks = (ngroups + CM_WAVES * un - 1) / (CM_WAVES * un);
+  if (blocks > 1024) blocks = 1024;
+  if (colsum && blocks > 512) blocks = 512;  // one colsum atomic per channel per workgroup
   const size_t shm = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                     (size_t)g.C * (1 + K0) * sizeof(float);
+                     (size_t)CM_WAVES * g.C * (1 + K0) * sizeof(float);
   const int wvec = (uintptr_t)w % 16 == 0;
+  static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
 #define HOPSX_CMD(NF, KSV, K0V)                                                                                \
-  hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy, \
+  if (un == 1) hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 1>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy, \
                      (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,              \
-                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0)
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg);                  \
+  else hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 2>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy, \
+                     (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,              \
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg)
 #define HOPSX_CMD_NF(NF)          \
   switch (KS) {                   \
     case 2: HOPSX_CMD(NF, 2, 0); break;  \

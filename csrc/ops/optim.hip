@@ -92,25 +92,40 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
   constexpr int NS = nstate<KIND>();
   const long n4 = vec ? (n >> 2) : 0;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 w = ((float4*)p)[i];
-    float4 gr = ((float4*)g)[i];
-    if (zero_grad) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 a = NS >= 1 ? ((float4*)s1)[i] : make_float4(0, 0, 0, 0);
-    float4 b = NS >= 2 ? ((float4*)s2)[i] : make_float4(0, 0, 0, 0);
-    float4 c = NS >= 3 ? ((float4*)s3)[i] : make_float4(0, 0, 0, 0);
-    w.x = upd<KIND>(w.x, gr.x * h.gscale, a.x, b.x, c.x, h, bc1, bc2);
-    w.y = upd<KIND>(w.y, gr.y * h.gscale, a.y, b.y, c.y, h, bc1, bc2);
-    w.z = upd<KIND>(w.z, gr.z * h.gscale, a.z, b.z, c.z, h, bc1, bc2);
-    w.w = upd<KIND>(w.w, gr.w * h.gscale, a.w, b.w, c.w, h, bc1, bc2);
-    ((float4*)p)[i] = w;
-    if (NS >= 1) ((float4*)s1)[i] = a;
-    if (NS >= 2) ((float4*)s2)[i] = b;
-    if (NS >= 3) ((float4*)s3)[i] = c;
-    if (shadow) {
-      const uint32_t lo = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
-      const uint32_t hi = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
-      ((uint2*)shadow)[i] = make_uint2(lo, hi);
+  // UN float4 per thread per trip with every load issued before the first update: at the
+  // 512-workgroup cap a 1.4 M-parameter model is ONE trip (one memory round trip, not three)
+  constexpr int UN = 3;
+  for (long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x; i0 < n4; i0 += UN * stride) {
+    float4 w[UN], gr[UN], a[UN], b[UN], c[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const long i = i0 + u * stride;
+      const long ic = i < n4 ? i : 0;  // clamped, unconditional loads
+      w[u] = ((const float4*)p)[ic];
+      gr[u] = ((const float4*)g)[ic];
+      a[u] = NS >= 1 ? ((const float4*)s1)[ic] : make_float4(0, 0, 0, 0);
+      b[u] = NS >= 2 ? ((const float4*)s2)[ic] : make_float4(0, 0, 0, 0);
+      c[u] = NS >= 3 ? ((const float4*)s3)[ic] : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n4) break;
+      if (zero_grad) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 ww = w[u], aa = a[u], bb = b[u], cc = c[u];
+      ww.x = upd<KIND>(ww.x, gr[u].x * h.gscale, aa.x, bb.x, cc.x, h, bc1, bc2);
+      ww.y = upd<KIND>(ww.y, gr[u].y * h.gscale, aa.y, bb.y, cc.y, h, bc1, bc2);
+      ww.z = upd<KIND>(ww.z, gr[u].z * h.gscale, aa.z, bb.z, cc.z, h, bc1, bc2);
+      ww.w = upd<KIND>(ww.w, gr[u].w * h.gscale, aa.w, bb.w, cc.w, h, bc1, bc2);
+      ((float4*)p)[i] = ww;
+      if (NS >= 1) ((float4*)s1)[i] = aa;
+      if (NS >= 2) ((float4*)s2)[i] = bb;
+      if (NS >= 3) ((float4*)s3)[i] = cc;
+      if (shadow) {
+        const uint32_t lo = (uint32_t)f2bf(ww.x) | ((uint32_t)f2bf(ww.y) << 16);
+        const uint32_t hi = (uint32_t)f2bf(ww.z) | ((uint32_t)f2bf(ww.w) << 16);
+        ((uint2*)shadow)[i] = make_uint2(lo, hi);
+      }
     }
   }
   for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
