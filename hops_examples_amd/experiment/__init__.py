@@ -89,64 +89,74 @@ def launch(train_fn, args_dict: dict | None = None, name: str = "no-name", local
 
 
 # ------------------------------------------------------ distributed training
-def _distributed(train_fn, name, local_logdir, description, metric_key, num_workers, mode, timeout, extra_env=None):
+def _distributed(train_fn, name, local_logdir, description, metric_key, num_workers, mode, timeout, extra_env=None,
+                 heartbeat_timeout=None, max_restarts=0):
+    """One worker process per GPU; the first failing rank tears the job down (runtime.health).
+    ``max_restarts`` > 0 relaunches the whole gang after a failure with HOPSX_RESTART=<attempt>
+    in the environment; a train_fn that checkpoints into ``tensorboard.logdir()``
+    (hops_examples_amd.checkpoint) resumes from its latest checkpoint."""
     app_id = R.next_app_id()
     d = _exp_dir(app_id)
     d.mkdir(parents=True, exist_ok=True)
     ngpu = R.num_gpus()
     if num_workers is None:
         num_workers = max(1, ngpu)
-    port = R.free_port()
     t0 = time.time()
     R.write_meta(d, name=name, description=description, type=mode, app_id=app_id, start=t0, status="RUNNING",
                  num_workers=num_workers)
-    workers = []
-    for rank in range(num_workers):
-        env = {"RANK": rank, "LOCAL_RANK": rank if ngpu else 0, "WORLD_SIZE": num_workers,
-               "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port, "HOPSX_DP_MODE": mode}
-        if extra_env:
-            env.update(extra_env)
-        log = "chief_0_output.log" if rank == 0 else f"worker_{rank - 1}_output.log"
-        # every rank sees all GPUs and pins itself to cuda:LOCAL_RANK (RCCL needs peer visibility)
-        workers.append(R.spawn(train_fn, {}, d, log, env=env, gpu=None, local_logdir=local_logdir and rank == 0))
-    values, err = [], None
-    for w in workers:
+    attempt = 0
+    while True:
+        port = R.free_port()
+        workers = []
+        for rank in range(num_workers):
+            env = {"RANK": rank, "LOCAL_RANK": rank if ngpu else 0, "WORLD_SIZE": num_workers,
+                   "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port, "HOPSX_DP_MODE": mode,
+                   "HOPSX_RESTART": attempt}
+            if extra_env:
+                env.update(extra_env)
+            log = "chief_0_output.log" if rank == 0 else f"worker_{rank - 1}_output.log"
+            # every rank sees all GPUs and pins itself to cuda:LOCAL_RANK (RCCL needs peer visibility)
+            workers.append(R.spawn(train_fn, {}, d, log, env=env, gpu=None, local_logdir=local_logdir and rank == 0))
         try:
-            values.append(R.collect(w, timeout))
-        except Exception as e:  # first failure aborts the job
-            err = err or e
-            for o in workers:
-                if o.proc.poll() is None:
-                    o.proc.kill()
-    if err is not None:
-        R.write_meta(d, status="FAILED", end=time.time())
-        raise err
+            values = R.wait_all(workers, timeout=timeout, heartbeat_timeout=heartbeat_timeout)
+            break
+        except Exception as e:  # first failure aborts the gang (SURVEY §5.3)
+            if attempt >= max_restarts:
+                R.write_meta(d, status="FAILED", end=time.time(), attempts=attempt + 1, error=str(e)[:2000])
+                raise
+            attempt += 1
+            R.write_meta(d, status="RESTARTING", attempts=attempt, last_error=str(e)[:2000])
     res = R.finalize_result(values[0], d, "chief_0_output.log")
     if metric_key and isinstance(res, dict):
         R.write_meta(d, metric=res.get(metric_key))
-    R.write_meta(d, status="FINISHED", end=time.time(), duration_s=time.time() - t0, result=res)
+    R.write_meta(d, status="FINISHED", end=time.time(), duration_s=time.time() - t0, result=res,
+                 attempts=attempt + 1)
     return _uri(d), res
 
 
 def mirrored(train_fn, name: str = "no-name", local_logdir: bool = False, description: str | None = None,
              evaluator: bool = False, metric_key: str | None = None, num_workers: int | None = None,
-             timeout: float | None = None):
+             timeout: float | None = None, heartbeat_timeout: float | None = None, max_restarts: int = 0):
     """Synchronous data parallel training: one worker process per GPU of this node.
 
     Inside ``train_fn`` the process group is already initialised (RCCL); wrap the
     model in ``hops_examples_amd.parallel.DataParallel`` (bucketed all-reduce) —
     the counterpart of building the Keras model under ``strategy.scope()``.
+    ``heartbeat_timeout``: tear the job down when a rank stops making progress;
+    ``max_restarts``: relaunch after a failure (resume via hops_examples_amd.checkpoint).
     """
-    return _distributed(train_fn, name, local_logdir, description, metric_key, num_workers, "mirrored", timeout)
+    return _distributed(train_fn, name, local_logdir, description, metric_key, num_workers, "mirrored", timeout,
+                        heartbeat_timeout=heartbeat_timeout, max_restarts=max_restarts)
 
 
 def collective_allreduce(train_fn, name: str = "no-name", local_logdir: bool = False,
                          description: str | None = None, evaluator: bool = False, metric_key: str | None = None,
-                         num_workers: int | None = None, timeout: float | None = None):
+                         num_workers: int | None = None, timeout: float | None = None,
+                         heartbeat_timeout: float | None = None, max_restarts: int = 0):
     """Multi-worker collective all-reduce (TF CollectiveAllReduceStrategy / MultiWorkerMirrored).
     Same engine as :func:`mirrored`; multi-node rendezvous comes from MASTER_ADDR/PORT."""
     return _distributed(train_fn, name, local_logdir, description, metric_key, num_workers, "collective_allreduce",
-                        timeout)
+                        timeout, heartbeat_timeout=heartbeat_timeout, max_restarts=max_restarts)
 
 
 def parameter_server(train_fn, name: str = "no-name", local_logdir: bool = False, description: str | None = None,

@@ -135,6 +135,72 @@ def collect(w: Worker, timeout: float | None = None):
     return value
 
 
+def _tail(w: Worker, n: int = 3000) -> str:
+    try:
+        return w.log_path.read_text(errors="replace")[-n:]
+    except OSError:
+        return ""
+
+
+def wait_all(workers: list, timeout: float | None = None, heartbeat_timeout: float | None = None,
+             poll_s: float = 0.2) -> list:
+    """Wait for a gang of workers (one distributed job) and return their values in order.
+
+    Unlike collecting them one by one, the FIRST failing rank ends the job: the others are
+    killed at once (a rank blocked in a collective on a dead peer would otherwise wait for
+    the collective timeout) and the error names that rank with its log tail.  With
+    ``heartbeat_timeout`` a rank whose progress heartbeat (runtime.health.beat, written by
+    TrainStep every step) stops for that long is declared stalled and the job is torn down.
+    """
+    from ..runtime import health
+
+    t0 = time.time()
+    pending = set(range(len(workers)))
+    failure = None
+    while pending and failure is None:
+        for i in sorted(pending):
+            rc = workers[i].proc.poll()
+            if rc is None:
+                continue
+            pending.discard(i)
+            if rc != 0 or not workers[i].result_path.exists():
+                failure = (i, f"rank {i} exited with code {rc}")
+                break
+        if failure is not None or not pending:
+            break
+        now = time.time()
+        if timeout is not None and now - t0 > timeout:
+            failure = (min(pending), f"job timed out after {timeout}s")
+            break
+        if heartbeat_timeout:
+            for i in sorted(pending):
+                hb = health.last_beat(workers[i].run_dir, i)
+                if hb is not None and now - hb > heartbeat_timeout:
+                    failure = (i, f"rank {i} stalled: no progress heartbeat for {now - hb:.1f}s "
+                                  f"(> heartbeat_timeout={heartbeat_timeout}s)")
+                    break
+        time.sleep(poll_s)
+    if failure is not None:
+        for w in workers:
+            if w.proc.poll() is None:
+                w.proc.kill()
+        for w in workers:
+            try:
+                w.proc.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                pass
+            w.logf.close()
+        i, why = failure
+        w = workers[i]
+        detail = ""
+        if w.result_path.exists():
+            ok, value = cloudpickle.loads(w.result_path.read_bytes())
+            if not ok:
+                detail = f"\nuser function raised:\n{value}"
+        raise TrialError(f"{why}; first failure in {w.log_path}{detail}\nlog tail:\n{_tail(w)}")
+    return [collect(w) for w in workers]
+
+
 def run_inline(fn, kwargs: dict, run_dir: Path, log_name="output.log"):
     """In-process execution (``HOPSX_INLINE=1``): same directory/log contract, no child process."""
     import contextlib

@@ -21,6 +21,7 @@ import torch
 
 from ..ops import functional as HF
 from ..parallel import dist as hdist
+from . import health
 
 
 def _clone(x):
@@ -121,6 +122,7 @@ class TrainStep:
 
     def __call__(self, x, y):
         self._n += 1
+        health.beat(self._n)  # progress heartbeat for the launcher's watchdog (+ HOPSX_FAULT injection)
         if not self.use_graph or self._n <= self.warmup or (
                 self._sx is not None and (_shape(x) != _shape(self._sx) or y.shape != self._sy.shape)):
             return self.eager(x, y)  # warm-up, or a ragged (e.g. last) batch the graph was not captured for
