@@ -52,6 +52,10 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     hopsx_wgrad_debug_times(v.data(), n);
     return v;
   });
+  m.def("zero", [](u p, long bytes, u st) { return hopsx_zero(P<void>(p), bytes, S(st)); });
+  m.def("nonfinite", [](u x, long n, int is_bf16, u out, u st) {
+    return hopsx_nonfinite(P<void>(x), n, is_bf16, P<unsigned>(out), S(st));
+  });
   m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
                            float xscale, float xshift, u counter, u st) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,

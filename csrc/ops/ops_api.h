@@ -97,6 +97,8 @@ int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const int* geom, v
 
 // ---- zero-fill kernel (elementwise.hip): graph-safe replacement for hipMemsetAsync ----
 int hopsx_zero(void* p, long bytes, hipStream_t st);
+// NaN / Inf counts of an fp32 or bf16 tensor: out[0] += #NaN, out[1] += #Inf (elementwise.hip)
+int hopsx_nonfinite(const void* x, long n, int is_bf16, unsigned* out, hipStream_t st);
 
 // ---- embedding bag (embedding.hip) ----
 int hopsx_embedding_bag_fwd(const float* table, const long* idx, const long* offsets, int nbags, int dim,

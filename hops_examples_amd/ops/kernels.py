@@ -412,3 +412,22 @@ def gram(x, mean):
     g = torch.zeros(cols, cols, device=x.device, dtype=F32)
     check(_C.ext().gram(ptr(x), ptr(mean), rows, cols, ptr(g), stream()), "gram")
     return g
+
+
+# ------------------------------------------------------------- health checks
+def zero_(t):
+    """Graph-safe zero fill (a kernel node, not a hipMemsetAsync blit node)."""
+    check(_C.ext().zero(ptr(t), t.numel() * t.element_size(), stream()), "zero")
+    return t
+
+
+def nonfinite_counts(x, out=None):
+    """int32[2] = (#NaN, #Inf) of an fp32 / bf16 GPU tensor; one fused read pass, no host sync."""
+    if x.dtype not in (F32, BF16):
+        raise TypeError(f"nonfinite_counts: fp32 or bf16 expected, got {x.dtype}")
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty(2, device=x.device, dtype=torch.int32)
+    zero_(out)
+    check(_C.ext().nonfinite(ptr(x), x.numel(), int(x.dtype == BF16), ptr(out), stream()), "nonfinite")
+    return out

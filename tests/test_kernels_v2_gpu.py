@@ -240,3 +240,29 @@ def test_pool_premask_matches_conv_mask(monkeypatch):
         grads.append(m._hx_arena.grad.float().clone())
     assert not HF._PREMASKED
     torch.testing.assert_close(grads[0], grads[1], atol=2e-2 * grads[1].abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("dtype,n", [(torch.float32, 1), (torch.float32, 100003), (bf, 4097), (bf, 1 << 20)])
+def test_nonfinite_counts(dtype, n):
+    """hopsx_nonfinite (health pill) vs torch.isnan / isinf."""
+    torch.manual_seed(6)
+    x = torch.randn(n, device=dev).to(dtype)
+    idx = torch.randperm(n, device=dev)
+    x[idx[: n // 7]] = float("nan")
+    x[idx[n // 7: n // 7 + n // 11]] = float("inf")
+    x[idx[n // 7 + n // 11: n // 7 + n // 11 + n // 13]] = float("-inf")
+    c = K.nonfinite_counts(x).cpu()
+    assert int(c[0]) == int(torch.isnan(x.float()).sum()) and int(c[1]) == int(torch.isinf(x.float()).sum())
+
+
+def test_step_profiler_captures_hip_kernels(tmp_path):
+    """torch.profiler (roctracer) sees the hopsx kernels by name inside the step window."""
+    from hops_examples_amd import profiler
+
+    x = torch.randn(4096, device=dev)
+    with profiler.profile("1,2", logdir=str(tmp_path), run_name="g") as p:
+        for _ in range(3):
+            K.nonfinite_counts(x)
+            p.step()
+    names = [r["name"] for r in profiler.trace_kernel_summary(p.trace_path)]
+    assert any("nonfinite_k" in n for n in names), names[:10]
