@@ -35,6 +35,12 @@ from . import rules as R
 from . import statistics as ST
 
 
+def _camel_to_snake(name: str) -> str:
+    import re
+
+    return re.sub(r"(?<!^)(?=[A-Z])", "_", name).lower()
+
+
 class VersionWarning(Warning):
     pass
 
@@ -231,6 +237,11 @@ class Join:
 
 
 class Query:
+    def __getattr__(self, name):  # JVM-style camelCase (asOf, selectAll ...)
+        if name.startswith("_") or not any(c.isupper() for c in name):
+            raise AttributeError(name)
+        return object.__getattribute__(self, _camel_to_snake(name))
+
     def __init__(self, fg, features: list[Feature]):
         self._left_fg = fg
         self._left_features = features
@@ -347,7 +358,20 @@ class FeatureGroupBase:
         for f in self.__dict__.get("_features", []):
             if f.name == name:
                 return f
+        if any(c.isupper() for c in name):  # JVM-style camelCase method (builders.CamelCaseAPI)
+            sn = _camel_to_snake(name)
+            if sn != name:
+                try:
+                    return object.__getattribute__(self, sn)
+                except AttributeError:
+                    pass
         raise AttributeError(f"'{type(self).__name__}' has no feature or attribute {name!r}")
+
+    def getValidation(self, time, time_type="VALIDATION_TIME"):  # noqa: N802 (JVM API)
+        """``fg.getValidation(ts, ValidationTimeType.COMMIT_TIME)`` (feature_validation_scala.ipynb:741-765)."""
+        if str(time_type).upper() == "COMMIT_TIME":
+            return self.get_validations(commit_time=time)
+        return self.get_validations(validation_time=time)
 
     def __getitem__(self, name):
         return self.__getattr__(name)

@@ -91,6 +91,12 @@ class Rule:
         return cls(d["name"], d.get("level", "ERROR"), d.get("min"), d.get("max"), d.get("pattern"),
                    d.get("acceptedType"), d.get("legalValues"))
 
+    @staticmethod
+    def createRule(name):  # noqa: N802  (JVM: Rule.createRule(RuleName.HAS_MIN).min(0).level(..).build())
+        from .builders import RuleBuilder
+
+        return RuleBuilder(name)
+
     def __repr__(self):
         return (f"Rule{{name={self.name}, level={self.level}, min={self.min}, max={self.max}, "
                 f"pattern='{self.pattern}', acceptedType={self.accepted_type}, legalValues={self.legal_values}}}")

@@ -9,6 +9,8 @@ from pathlib import Path
 import numpy as np
 import pandas as pd
 
+from .builders import (CamelCaseAPI, ExpectationBuilder, FeatureGroupBuilder, OnDemandFeatureGroupBuilder,
+                       TrainingDatasetBuilder)
 from .. import config, hdfs
 from . import rules as R
 from .core import (Feature, FeatureGroup, FeatureStoreException, OnDemandFeatureGroup, Query, _hsfs_type,
@@ -171,7 +173,26 @@ def _check_schema(schema, value, path):
 
 
 # ===================================================================== FeatureStore
-class FeatureStore:
+class FeatureStore(CamelCaseAPI):
+    # ---- JVM builder API (featurestore/builders.py): fs.createFeatureGroup().name(..)...build()
+    def createFeatureGroup(self):  # noqa: N802
+        return FeatureGroupBuilder(self)
+
+    def createOnDemandFeatureGroup(self):  # noqa: N802
+        return OnDemandFeatureGroupBuilder(self)
+
+    def createTrainingDataset(self):  # noqa: N802
+        return TrainingDatasetBuilder(self)
+
+    def createExpectation(self):  # noqa: N802
+        return ExpectationBuilder(self)
+
+    def getName(self):  # noqa: N802
+        return self.name
+
+    def getOnlineStorageConnector(self):  # noqa: N802
+        return self.get_storage_connector(f"{self.name}_onlinefeaturestore")
+
     def __init__(self, name: str, project_root: Path):
         self.name = name
         self._root = project_root / "Featurestore" / name
@@ -393,7 +414,37 @@ class FeatureStore:
 
 
 # ======================================================================= Connection
-class Connection:
+class _ConnectionBuilder(CamelCaseAPI):
+    """``HopsworksConnection.builder.host(..).project(..).build()`` (ComputeFeatures.scala:91)."""
+
+    def __init__(self):
+        self._kw = {}
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        key = {"hostname": "host", "apiKeyValue": "api_key_value", "apiKeyFile": "api_key_file"}.get(name, name)
+
+        def setter(v):
+            self._kw[key] = v
+            return self
+
+        return setter
+
+    def build(self):
+        kw = {k: v for k, v in self._kw.items() if k in ("host", "port", "project", "engine", "region_name",
+                                                          "api_key_value", "api_key_file")}
+        return connection(**kw)
+
+
+class _BuilderDescriptor:
+    def __get__(self, obj, cls):
+        return _ConnectionBuilder()
+
+
+class Connection(CamelCaseAPI):
+    builder = _BuilderDescriptor()
+
     def __init__(self, host=None, port=443, project=None, engine=None, region_name=None,
                  secrets_store=None, hostname_verification=True, trust_store_path=None, cert_folder=None,
                  api_key_file=None, api_key_value=None):
@@ -404,6 +455,9 @@ class Connection:
                 if project != config.get().project_name else None
         self._connected = True
         print("Connected. Call `.close()` to terminate connection gracefully.")
+
+    def getFeatureStore(self, name: str | None = None) -> FeatureStore:  # noqa: N802
+        return self.get_feature_store(name)
 
     def get_feature_store(self, name: str | None = None) -> FeatureStore:
         name = name or f"{config.get().project_name}_featurestore"

@@ -21,6 +21,7 @@ from pathlib import Path
 import numpy as np
 import pandas as pd
 
+from .builders import CamelCaseAPI
 from .. import io as hio
 from . import statistics as ST
 
@@ -36,7 +37,7 @@ class TrainingDatasetFeature:
         return f"TrainingDatasetFeature({self.name!r}, {self.type!r})"
 
 
-class TrainingDataset:
+class TrainingDataset(CamelCaseAPI):
     ENTITY_TYPE = "trainingdatasets"
 
     def __init__(self, fs, name, version, description="", data_format="tfrecords", coalesce=False,
