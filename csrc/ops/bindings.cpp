@@ -113,18 +113,18 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_add_bf16(P<void>(a), P<void>(b), P<void>(o), n, act, S(st));
   });
   m.def("bn_fwd_train", [](u x, u y, u g, u b, u mean, u rstd, u rm, u rv, float mom, float eps, int M, int C, u res,
-                           int act, u st) {
+                           int act, u acc, u st) {
     return hopsx_bn_fwd_train(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(mean), P<float>(rstd),
-                              P<float>(rm), P<float>(rv), mom, eps, M, C, P<void>(res), act, S(st));
+                              P<float>(rm), P<float>(rv), mom, eps, M, C, P<void>(res), act, P<float>(acc), S(st));
   });
   m.def("bn_fwd_infer", [](u x, u y, u g, u b, u rm, u rv, float eps, int M, int C, u res, int act, u st) {
     return hopsx_bn_fwd_infer(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(rm), P<float>(rv), eps, M, C,
                               P<void>(res), act, S(st));
   });
   m.def("bn_bwd", [](u dy, u x, u y, u g, u mean, u rstd, u dx, u dg, u db, u ws, int M, int C, int act, u dres,
-                     u st) {
+                     u acc, u st) {
     return hopsx_bn_bwd(P<void>(dy), P<void>(x), P<void>(y), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
-                        P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), S(st));
+                        P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), P<float>(acc), S(st));
   });
   m.def("embedding_bag_fwd", [](u table, u idx, u offs, int nbags, int dim, long nidx, int bag_len, int mode, u out,
                                 int of32, long ldo, u st) {

@@ -1,6 +1,8 @@
 // BatchNorm over NHWC activations viewed as [M = B*H*W, C] (channel-fastest),
 // with the residual add and the activation fused into the apply pass
 // (ResNet: y = act(bn(x) + residual)) and into the backward.
+#include <initializer_list>
+
 #include "common.h"
 #include "ops_api.h"
 
@@ -111,6 +113,244 @@ __global__ void bn_grad_acc_k(const float* __restrict__ ws, float* __restrict__ 
   if (dgamma) dgamma[c] += ws[C + c];
 }
 
+// ---------------------------------------------------------------------------------------------
+// Vectorized path (C % 8 == 0, C/8 a power of two <= 256, 16-B aligned tensors): every lane moves
+// 8 channels (16 B) per access, a workgroup covers all C columns and 256/(C/8) rows per pass with
+// UNR rows' loads in flight, and per-channel partials go to one of NREP replica rows of a
+// zero-at-rest accumulator (NREP-fold less same-address atomic contention); the finalize
+// kernels fold the replicas, re-zero them and (fwd) update the running statistics, so no
+// memset launches remain.  The scalar kernels above serve odd channel counts.
+constexpr int BN_NREP = 8;
+constexpr int BN_UNR = 4;
+
+__device__ __forceinline__ void ld8f(const bf16_raw* p, float* v) {
+  const bf16x8 q = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f((uint16_t)q[j]);
+}
+__device__ __forceinline__ void st8f(bf16_raw* p, const float* v) {
+  bf16x8 q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = (short)f2bf(v[j]);
+  *(bf16x8*)p = q;
+}
+
+// MODE 0 (stats): acc[rep][0:C] += x, acc[rep][C:2C] += x^2
+// MODE 1 (bwd):   acc[rep][0:C] += dz, acc[rep][C:2C] += dz * xhat, dz = dy * act'(y)
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ x,
+                                                    const bf16_raw* __restrict__ y, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, float* __restrict__ acc, int M,
+                                                    int C, int rpb, int act) {
+  const int CG = C >> 3, RPI = 256 / CG;
+  const int cg = threadIdx.x % CG, rsub = threadIdx.x / CG;
+  const int c0 = cg * 8;
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  float s1[8], s2[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; mu[j] = 0.f; rs[j] = 0.f; }
+  if (MODE == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+  }
+  for (int r = r0 + rsub; r < r1; r += BN_UNR * RPI) {
+    float va[BN_UNR][8], vx[BN_UNR][8], vy[BN_UNR][8];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {  // all loads of the trip first
+      const int rr = r + u * RPI;
+      const long o = (long)(rr < r1 ? rr : r0) * C + c0;
+      ld8f(a + o, va[u]);
+      if (MODE == 1) {
+        ld8f(x + o, vx[u]);
+        if (act != ACT_NONE) ld8f(y + o, vy[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      if (r + u * RPI >= r1) break;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (MODE == 0) {
+          s1[j] += va[u][j];
+          s2[j] = fmaf(va[u][j], va[u][j], s2[j]);
+        } else {
+          float dz = va[u][j];
+          if (act != ACT_NONE) dz *= act_grad_from_out(vy[u][j], act);
+          s1[j] += dz;
+          s2[j] = fmaf(dz, (vx[u][j] - mu[j]) * rs[j], s2[j]);
+        }
+      }
+    }
+  }
+  __shared__ float red[256 * 16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x * 16 + j] = s1[j];
+    red[threadIdx.x * 16 + 8 + j] = s2[j];
+  }
+  __syncthreads();
+  float* dst = acc + (long)(blockIdx.x % BN_NREP) * 2 * C;
+  for (int e = threadIdx.x; e < 2 * C; e += 256) {  // e < C: sum1 of channel e, else sum2 of channel e - C
+    const int which = e >= C, c = e - which * C;
+    const int g = c >> 3, j = c & 7;
+    float t = 0.f;
+    for (int q = 0; q < RPI; ++q) t += red[(q * CG + g) * 16 + which * 8 + j];
+    if (t != 0.f) atomicAdd(dst + e, t);
+  }
+}
+
+// fwd finalize: fold replicas -> mean / rstd, running stats, re-zero the replicas
+__global__ void bn_fin_fwd_k(float* __restrict__ acc, float* __restrict__ mean, float* __restrict__ rstd,
+                             float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps, int M,
+                             int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int r = 0; r < BN_NREP; ++r) {
+    a += acc[(long)r * 2 * C + c];
+    b += acc[(long)r * 2 * C + C + c];
+    acc[(long)r * 2 * C + c] = 0.f;
+    acc[(long)r * 2 * C + C + c] = 0.f;
+  }
+  const float mu = a / M;
+  const float var = fmaxf(b / M - mu * mu, 0.f);
+  mean[c] = mu;
+  rstd[c] = rsqrtf(var + eps);
+  if (rmean) {
+    const float unb = M > 1 ? var * M / (M - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  }
+}
+
+// bwd finalize: fold replicas into ws[0:2C], accumulate dbeta / dgamma, re-zero the replicas
+__global__ void bn_fin_bwd_k(float* __restrict__ acc, float* __restrict__ ws, float* __restrict__ dgamma,
+                             float* __restrict__ dbeta, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int r = 0; r < BN_NREP; ++r) {
+    a += acc[(long)r * 2 * C + c];
+    b += acc[(long)r * 2 * C + C + c];
+    acc[(long)r * 2 * C + c] = 0.f;
+    acc[(long)r * 2 * C + C + c] = 0.f;
+  }
+  ws[c] = a;
+  ws[C + c] = b;
+  if (dbeta) dbeta[c] += a;
+  if (dgamma) dgamma[c] += b;
+}
+
+// y = act((x - mean) * rstd * gamma + beta + res)  (var_mode: rstd holds a variance -> inference)
+__global__ __launch_bounds__(256) void bn_apply8_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                   int var_mode, float eps, long nch, int C,
+                                                   const bf16_raw* __restrict__ res, int act) {
+  const int CG = C >> 3;
+  const long stride = (long)gridDim.x * blockDim.x;  // a multiple of CG: the channel group is per-thread
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(i0 % CG) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float rs = var_mode ? rsqrtf(rstd[c0 + j] + eps) : rstd[c0 + j];
+    sc[j] = rs * (gamma ? gamma[c0 + j] : 1.f);
+    sh[j] = (beta ? beta[c0 + j] : 0.f) - mean[c0 + j] * sc[j];
+  }
+  for (long i = i0; i < nch; i += 2 * stride) {
+    float v[2][8], rv[2][8];
+    const long i1 = i + stride < nch ? i + stride : i;
+    ld8f(x + i * 8, v[0]);
+    ld8f(x + i1 * 8, v[1]);
+    if (res) {
+      ld8f(res + i * 8, rv[0]);
+      ld8f(res + i1 * 8, rv[1]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = fmaf(v[u][j], sc[j], sh[j]);
+        if (res) t += rv[u][j];
+        v[u][j] = apply_act(t, act);
+      }
+    }
+    st8f(y + i * 8, v[0]);
+    if (i + stride < nch) st8f(y + i1 * 8, v[1]);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply8_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
+                                                       const bf16_raw* __restrict__ y, const float* __restrict__ gamma,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       const float* __restrict__ ws, bf16_raw* __restrict__ dx,
+                                                       bf16_raw* __restrict__ dres, long nch, int M, int C, int act) {
+  const int CG = C >> 3;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(i0 % CG) * 8;
+  const float invM = 1.f / M;
+  float k1[8], k2[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float g = gamma ? gamma[c0 + j] : 1.f;
+    rs[j] = rstd[c0 + j];
+    mu[j] = mean[c0 + j];
+    k1[j] = g * rs[j];                 // dx = k1 * (dz - mean(dz) - xhat * mean(dz*xhat))
+    k2[j] = ws[C + c0 + j] * invM;
+    mu[j] = mean[c0 + j];
+  }
+  float md[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) md[j] = ws[c0 + j] * invM;
+  for (long i = i0; i < nch; i += stride) {
+    float d[8], xv[8], yv[8];
+    ld8f(dy + i * 8, d);
+    ld8f(x + i * 8, xv);
+    if (act != ACT_NONE) {
+      ld8f(y + i * 8, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] *= act_grad_from_out(yv[j], act);
+    }
+    if (dres) st8f(dres + i * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xv[j] - mu[j]) * rs[j];
+      d[j] = k1[j] * (d[j] - md[j] - xh * k2[j]);
+    }
+    st8f(dx + i * 8, d);
+  }
+}
+
+static bool bn_vec_ok(int C, std::initializer_list<const void*> ptrs) {
+  if (C % 8 != 0 || C / 8 > 256 || (256 % (C / 8)) != 0 || hopsx_disabled("bn_vec")) return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16 != 0) return false;
+  return true;
+}
+
+static int colred_grid(int M, int C, int& rpb) {
+  const int RPI = 256 / (C / 8);
+  long g = (M + (long)RPI * 8 - 1) / ((long)RPI * 8);  // ~8 rows per thread
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  rpb = (int)((M + g - 1) / g);
+  return (int)((M + rpb - 1) / rpb);
+}
+
+static int apply_grid(long nch, int C) {
+  const int CG = C >> 3;
+  long g = (nch + 511) / 512;  // two chunks per thread per trip
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  // gridDim*256 must be a multiple of CG (per-thread channel group); CG divides 256
+  (void)CG;
+  return (int)g;
+}
+
 static void slab_grid(int M, int C, int& gx, int& gy, int& rpb) {
   gx = (C + 63) / 64;
   gy = (M + 255) / 256;
@@ -126,7 +366,20 @@ static int ew_grid(long n) {
 
 extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
                                   float* rstd_out, float* running_mean, float* running_var, float momentum,
-                                  float eps, int M, int C, const void* residual, int act, hipStream_t st) {
+                                  float eps, int M, int C, const void* residual, int act, float* acc,
+                                  hipStream_t st) {
+  const long n = (long)M * C;
+  if (acc && bn_vec_ok(C, {x, y, residual})) {  // acc: BN_NREP x 2C floats, zero at rest
+    int rpb;
+    const int g = colred_grid(M, C, rpb);
+    hipLaunchKernelGGL(bn_colred8_k<0>, dim3(g), dim3(256), 0, st, (const bf16_raw*)x, nullptr, nullptr, nullptr,
+                       nullptr, acc, M, C, rpb, 0);
+    hipLaunchKernelGGL(bn_fin_fwd_k, dim3((C + 255) / 256), dim3(256), 0, st, acc, mean_out, rstd_out, running_mean,
+                       running_var, momentum, eps, M, C);
+    hipLaunchKernelGGL(bn_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y,
+                       gamma, beta, mean_out, rstd_out, 0, eps, n / 8, C, (const bf16_raw*)residual, act);
+    return (int)hipGetLastError();
+  }
   hopsx_zero(mean_out, C * sizeof(float), st);
   hopsx_zero(rstd_out, C * sizeof(float), st);
   int gx, gy, rpb;
@@ -134,7 +387,6 @@ extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, co
   hipLaunchKernelGGL(bn_stats_k, dim3(gx, gy), dim3(256), 0, st, (const bf16_raw*)x, mean_out, rstd_out, M, C, rpb);
   hipLaunchKernelGGL(bn_finalize_k, dim3((C + 255) / 256), dim3(256), 0, st, mean_out, rstd_out, running_mean,
                      running_var, momentum, eps, M, C);
-  const long n = (long)M * C;
   hipLaunchKernelGGL(bn_apply_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, gamma, beta,
                      mean_out, rstd_out, 0, eps, n, C, (const bf16_raw*)residual, act);
   return (int)hipGetLastError();
@@ -144,6 +396,11 @@ extern "C" int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, co
                                   const float* running_mean, const float* running_var, float eps, int M, int C,
                                   const void* residual, int act, hipStream_t st) {
   const long n = (long)M * C;
+  if (bn_vec_ok(C, {x, y, residual})) {
+    hipLaunchKernelGGL(bn_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y,
+                       gamma, beta, running_mean, running_var, 1, eps, n / 8, C, (const bf16_raw*)residual, act);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_apply_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, gamma, beta,
                      running_mean, running_var, 1, eps, n, C, (const bf16_raw*)residual, act);
   return (int)hipGetLastError();
@@ -151,13 +408,24 @@ extern "C" int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, co
 
 extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                             const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C,
-                            int act, void* dresidual, hipStream_t st) {
+                            int act, void* dresidual, float* acc, hipStream_t st) {
+  const long n = (long)M * C;
+  if (acc && bn_vec_ok(C, {dy, x, y, dx, dresidual})) {  // acc: BN_NREP x 2C floats, zero at rest
+    int rpb;
+    const int g = colred_grid(M, C, rpb);
+    hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
+                       (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act);
+    hipLaunchKernelGGL(bn_fin_bwd_k, dim3((C + 255) / 256), dim3(256), 0, st, acc, ws, dgamma, dbeta, C);
+    hipLaunchKernelGGL(bn_bwd_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
+                       (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, ws, (bf16_raw*)dx,
+                       (bf16_raw*)dresidual, n / 8, M, C, act);
+    return (int)hipGetLastError();
+  }
   hopsx_zero(ws, 2 * C * sizeof(float), st);
   int gx, gy, rpb;
   slab_grid(M, C, gx, gy, rpb);
   hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(gx, gy), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
                      (const bf16_raw*)y, mean, rstd, ws, M, C, rpb, act);
-  const long n = (long)M * C;
   hipLaunchKernelGGL(bn_bwd_apply_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
                      (const bf16_raw*)y, gamma, mean, rstd, ws, (bf16_raw*)dx, (bf16_raw*)dresidual, n, M, C, act);
   hipLaunchKernelGGL(bn_grad_acc_k, dim3((C + 255) / 256), dim3(256), 0, st, ws, dgamma, dbeta, C);

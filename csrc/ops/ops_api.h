@@ -69,13 +69,13 @@ int hopsx_add_bf16(const void* a, const void* b, void* out, long n, int act, hip
 // ---- batch norm (norm.hip), NHWC, per-channel over M = B*H*W rows ----
 int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
                        float* rstd_out, float* running_mean, float* running_var, float momentum, float eps, int M,
-                       int C, const void* residual, int act, hipStream_t st);
+                       int C, const void* residual, int act, float* acc, hipStream_t st);
 int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, int M, int C, const void* residual, int act,
                        hipStream_t st);
 int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                  const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
-                 void* dresidual, hipStream_t st);
+                 void* dresidual, float* acc, hipStream_t st);
 
 // ---- direct MFMA convs for short reductions (conv_mfma.hip) ----
 bool hopsx_conv_fwd_mfma_ok(const int* geom);

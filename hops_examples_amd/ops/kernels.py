@@ -339,12 +339,31 @@ def add(a, b, act=0, out=None):
 
 
 # ---------------------------------------------------------------- batchnorm
+_BN_ACC: dict = {}
+BN_NREP = 8  # replica rows of the BN column-reduction accumulators (norm.hip BN_NREP)
+
+
+def bn_acc(device, C) -> torch.Tensor:
+    """Zero-at-rest [BN_NREP, 2C] fp32 accumulator for the vectorized BN reductions: the finalize
+    kernel that consumes it re-zeroes it, so one buffer per (device, C) serves every BN layer of that
+    width in stream order, with no memset launches.  Created outside graph capture (warm-up)."""
+    key = (str(device), int(C))
+    t = _BN_ACC.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("BN accumulator must be created before graph capture (run an eager step first)")
+        t = torch.zeros(BN_NREP * 2 * C, device=device, dtype=F32)
+        _BN_ACC[key] = t
+    return t
+
+
 def bn_fwd_train(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, residual=None, act=0, out=None):
     M, C = x2d.shape
     if out is None:
         out = torch.empty_like(x2d)
     check(_C.ext().bn_fwd_train(ptr(x2d), ptr(out), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), ptr(rmean),
-                                ptr(rvar), float(momentum), float(eps), M, C, ptr(residual), act_id(act), stream()),
+                                ptr(rvar), float(momentum), float(eps), M, C, ptr(residual), act_id(act),
+                                ptr(bn_acc(x2d.device, C)), stream()),
           "bn_fwd_train")
     return out
 
@@ -363,7 +382,8 @@ def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None
     if out is None:
         out = torch.empty_like(x)
     check(_C.ext().bn_bwd(ptr(dy), ptr(x), ptr(y), ptr(gamma), ptr(mean), ptr(rstd), ptr(out), ptr(dgamma),
-                          ptr(dbeta), ptr(ws), M, C, act_id(act), ptr(dresidual), stream()), "bn_bwd")
+                          ptr(dbeta), ptr(ws), M, C, act_id(act), ptr(dresidual), ptr(bn_acc(dy.device, C)),
+                          stream()), "bn_bwd")
     return out
 
 

@@ -241,9 +241,11 @@ def test_dropout_mask_reuse():
     assert not torch.equal(y2, y)
 
 
-def test_batchnorm():
+@pytest.mark.parametrize("M,C", [(4096, 96), (8192, 64), (3136, 2048), (1000, 16), (50001, 256)])
+def test_batchnorm(M, C):
+    """Vectorized (C/8 | 256) and scalar (C = 96) BN paths; run twice so the zero-at-rest
+    replica accumulators must have been re-zeroed by the first call's finalize kernels."""
     torch.manual_seed(7)
-    M, C = 4096, 96
     x = bf(torch.randn(M, C, device=dev) * 2 + 1)
     res = bf(torch.randn(M, C, device=dev))
     gamma = torch.rand(C, device=dev) + 0.5
@@ -252,6 +254,9 @@ def test_batchnorm():
     rstd = torch.empty(C, device=dev)
     rm = torch.zeros(C, device=dev)
     rv = torch.ones(C, device=dev)
+    y = K.bn_fwd_train(x, gamma, beta, mean, rstd, rm, rv, 0.1, 1e-5, residual=res, act="relu")
+    rm.zero_()
+    rv.fill_(1.0)
     y = K.bn_fwd_train(x, gamma, beta, mean, rstd, rm, rv, 0.1, 1e-5, residual=res, act="relu")
     xr = x.float().requires_grad_(True)
     gr = gamma.clone().requires_grad_(True)
@@ -268,6 +273,9 @@ def test_batchnorm():
     db = torch.zeros(C, device=dev)
     ws = torch.empty(2 * C, device=dev)
     dres = torch.empty_like(x)
+    dx = K.bn_bwd(dy, x, y, gamma, mean, rstd, dg, db, ws, act="relu", dresidual=dres)
+    dg.zero_()
+    db.zero_()
     dx = K.bn_bwd(dy, x, y, gamma, mean, rstd, dg, db, ws, act="relu", dresidual=dres)
     close(dx, gx, rtol=3e-2, atol=3e-2)
     close(dg, gg, rtol=3e-2, atol=3e-2)
