@@ -237,6 +237,166 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_k(const bf16_raw* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Vectorized general windows (overlapping / padded, e.g. the ResNet stem 3x3/2 pad 1), C % 8 == 0:
+// one thread per (pixel, 8 channels) with 16-B loads/stores and the 8 argmax bytes packed; the
+// backward gathers over the <= ceil(K/s)^2 windows covering each input pixel.  Replaces the
+// scalar kernels above, which moved 2 bytes per lane.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void maxpool_fwdv_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y,
+                                                      unsigned char* __restrict__ am, int B, int H, int W, int C,
+                                                      int OH, int OW, int KH, int KW, int sh, int sw, int ph, int pw,
+                                                      float p, const unsigned long long* __restrict__ rng,
+                                                      unsigned salt) {
+  const int G = C >> 3;
+  const long total = (long)B * OH * OW * G;
+  const uint64_t key = p > 0.f ? drop_key(rng, salt) : 0;
+  const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % G);
+    const long pix = t / G;
+    const int ow = (int)(pix % OW);
+    const long r = pix / OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int kh = 0; kh < KH; ++kh) {
+      const int ih = oh * sh - ph + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int iw = ow * sw - pw + kw;
+        if (iw < 0 || iw >= W) continue;
+        const bf16x8 v = *(const bf16x8*)(x + (((long)b * H + ih) * W + iw) * C + cg * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f((uint16_t)v[j]);
+          if (f > best[j]) { best[j] = f; bi[j] = kh * KW + kw; }
+        }
+      }
+    }
+    const long o = pix * C + cg * 8;
+    bf16x8 out;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = best[j];
+      if (p > 0.f) f = uniform01(key, o + j) >= p ? f * dscale : 0.f;
+      out[j] = (short)f2bf(f);
+      if (j < 4) lo |= (uint32_t)bi[j] << (8 * j);
+      else hi |= (uint32_t)bi[j] << (8 * (j - 4));
+    }
+    *(bf16x8*)(y + o) = out;
+    if (am) *(uint2*)(am + o) = make_uint2(lo, hi);
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwdv_k(const bf16_raw* __restrict__ dy, const unsigned char* __restrict__ am,
+                                                      const bf16_raw* __restrict__ x, bf16_raw* __restrict__ dx, int B,
+                                                      int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
+                                                      int sw, int ph, int pw, int act, float p,
+                                                      const unsigned long long* __restrict__ rng, unsigned salt) {
+  const int G = C >> 3;
+  const long total = (long)B * H * W * G;
+  const uint64_t key = p > 0.f ? drop_key(rng, salt) : 0;
+  const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % G);
+    const long pix = t / G;
+    const int iw = (int)(pix % W);
+    const long r = pix / W;
+    const int ih = (int)(r % H);
+    const int b = (int)(r / H);
+    const int oh_lo = max(0, (ih + ph - KH + sh) / sh), oh_hi = min(OH - 1, (ih + ph) / sh);
+    const int ow_lo = max(0, (iw + pw - KW + sw) / sw), ow_hi = min(OW - 1, (iw + pw) / sw);
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = ih - (oh * sh - ph);
+      if (kh < 0 || kh >= KH) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int kw = iw - (ow * sw - pw);
+        if (kw < 0 || kw >= KW) continue;
+        const long o = (((long)b * OH + oh) * OW + ow) * C + cg * 8;
+        const bf16x8 d = *(const bf16x8*)(dy + o);
+        const uint2 pk = *(const uint2*)(am + o);
+        const int want = kh * KW + kw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int a = ((j < 4 ? pk.x : pk.y) >> (8 * (j & 3))) & 0xff;
+          if (a == want) {
+            float f = bf2f((uint16_t)d[j]);
+            if (p > 0.f) f = uniform01(key, o + j) >= p ? f * dscale : 0.f;
+            g[j] += f;
+          }
+        }
+      }
+    }
+    const long i = pix * C + cg * 8;
+    if (act != ACT_NONE && x) {
+      const bf16x8 xv = *(const bf16x8*)(x + i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] *= act_grad_from_out(bf2f((uint16_t)xv[j]), act);
+    }
+    bf16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = (short)f2bf(g[j]);
+    *(bf16x8*)(dx + i) = out;
+  }
+}
+
+// global average pool over HW, 8 channels per thread (16-B loads), fp32 sums
+__global__ __launch_bounds__(256) void gap_fwdv_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y, int HW,
+                                                  int C) {
+  const int G = C >> 3;
+  const int b = blockIdx.y, cg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cg >= G) return;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16_raw* p = x + (long)b * HW * C + cg * 8;
+  int q = 0;
+  for (; q + 4 <= HW; q += 4) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(p + (long)(q + u) * C);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += bf2f((uint16_t)v[u][j]);
+  }
+  for (; q < HW; ++q) {
+    const bf16x8 v = *(const bf16x8*)(p + (long)q * C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += bf2f((uint16_t)v[j]);
+  }
+  bf16x8 out;
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (short)f2bf(s[j] * inv);
+  *(bf16x8*)(y + (long)b * C + cg * 8) = out;
+}
+
+__global__ __launch_bounds__(256) void gap_bwdv_k(const bf16_raw* __restrict__ dy, bf16_raw* __restrict__ dx, int B,
+                                                  int HW, int C) {
+  const int G = C >> 3;
+  const long total = (long)B * HW * G;
+  const float inv = 1.f / HW;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % G);
+    const long b = t / ((long)HW * G);
+    const bf16x8 d = *(const bf16x8*)(dy + b * C + cg * 8);
+    bf16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = (short)f2bf(bf2f((uint16_t)d[j]) * inv);
+    *(bf16x8*)(dx + (t / G) * C + cg * 8) = out;
+  }
+}
+
+static bool pool_vec(int C, const void* a, const void* b, const void* c, const void* d) {
+  return !hopsx_disabled("poolv") && C % 8 == 0 && (((uintptr_t)a | (uintptr_t)b | (uintptr_t)d) % 16 == 0) &&
+         ((uintptr_t)c % 8 == 0);
+}
+
 static bool pool_fast(int C, int KH, int KW, int sh, int sw, int ph, int pw, const void* a, const void* b,
                       const void* c, const void* d) {
   return !hopsx_disabled("pool8") && C % 8 == 0 && (256 % (C / 8) == 0) && sh == KH && sw == KW && ph == 0 &&
@@ -251,6 +411,12 @@ extern "C" int hopsx_maxpool2d_fwd(const void* x, void* y, unsigned char* argmax
     const long n8 = (long)B * OH * OW * (C / 8);
     hipLaunchKernelGGL(maxpool_fwd8_k, dim3(grid_for(n8)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, argmax,
                        B, H, W, C, OH, OW, KH, KW, p, rng, salt);
+    return (int)hipGetLastError();
+  }
+  if (KH * KW <= 255 && pool_vec(C, x, y, argmax, nullptr)) {
+    const long n8 = (long)B * OH * OW * (C / 8);
+    hipLaunchKernelGGL(maxpool_fwdv_k, dim3(grid_for(n8)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, argmax,
+                       B, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, p, rng, salt);
     return (int)hipGetLastError();
   }
   const long n = (long)B * OH * OW * C;
@@ -272,6 +438,12 @@ extern "C" int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, 
                        (bf16_raw*)dx, B, H, W, C, OH, OW, KH, KW, act, colsum, p, rng, salt);
     return (int)hipGetLastError();
   }
+  if (!colsum && KH * KW <= 255 && pool_vec(C, dy, dx, argmax, x)) {
+    const long n8 = (long)B * H * W * (C / 8);
+    hipLaunchKernelGGL(maxpool_bwdv_k, dim3(grid_for(n8)), dim3(256), 0, st, (const bf16_raw*)dy, argmax,
+                       (const bf16_raw*)x, (bf16_raw*)dx, B, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, act, p, rng, salt);
+    return (int)hipGetLastError();
+  }
   const long n = (long)B * H * W * C;
   hipLaunchKernelGGL(maxpool_bwd_k, dim3(grid_for(n, 256) > 1024 ? 1024 : grid_for(n, 256)), dim3(256), shm, st, (const bf16_raw*)dy, argmax,
                      (const bf16_raw*)x, (bf16_raw*)dx, B, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, act, colsum, p, rng, salt);
@@ -279,11 +451,21 @@ extern "C" int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, 
 }
 
 extern "C" int hopsx_avgpool_global_fwd(const void* x, void* y, int B, int HW, int C, hipStream_t st) {
+  if (pool_vec(C, x, y, nullptr, nullptr)) {
+    const int G = C / 8;
+    hipLaunchKernelGGL(gap_fwdv_k, dim3((G + 255) / 256, B), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, HW, C);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(gap_fwd_k, dim3(B), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y, B, HW, C);
   return (int)hipGetLastError();
 }
 
 extern "C" int hopsx_avgpool_global_bwd(const void* dy, void* dx, int B, int HW, int C, hipStream_t st) {
+  if (pool_vec(C, dy, dx, nullptr, nullptr)) {
+    const long n8 = (long)B * HW * (C / 8);
+    hipLaunchKernelGGL(gap_bwdv_k, dim3(grid_for(n8)), dim3(256), 0, st, (const bf16_raw*)dy, (bf16_raw*)dx, B, HW, C);
+    return (int)hipGetLastError();
+  }
   const long n = (long)B * HW * C;
   hipLaunchKernelGGL(gap_bwd_k, dim3(grid_for(n)), dim3(256), 0, st, (const bf16_raw*)dy, (bf16_raw*)dx, B, HW, C);
   return (int)hipGetLastError();

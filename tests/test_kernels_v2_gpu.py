@@ -266,3 +266,36 @@ def test_step_profiler_captures_hip_kernels(tmp_path):
             p.step()
     names = [r["name"] for r in profiler.trace_kernel_summary(p.trace_path)]
     assert any("nonfinite_k" in n for n in names), names[:10]
+
+
+@pytest.mark.parametrize("B,H,C,k,s,p", [(4, 112, 64, 3, 2, 1), (3, 15, 16, 3, 2, 1), (2, 9, 32, 2, 1, 0),
+                                         (2, 14, 8, 3, 3, 1)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_maxpool_vectorized_general(B, H, C, k, s, p, act):
+    """Overlapping / padded windows on the 16-B general kernels (ResNet stem 3x3/2 pad 1), bwd
+    without colsum, with the fused ReLU' of the pool input."""
+    torch.manual_seed(8)
+    x = torch.relu(torch.randn(B, H, H, C, device=dev)).to(bf) if act else torch.randn(B, H, H, C, device=dev).to(bf)
+    y, am = K.maxpool2d_fwd(x, (k, k), (s, s), (p, p))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    torch.testing.assert_close(y.float(), yr.permute(0, 2, 3, 1), rtol=0, atol=1e-6)
+    dy = torch.randn_like(y.float()).to(bf)
+    (gx,) = torch.autograd.grad(yr, (xr,), dy.float().permute(0, 3, 1, 2))
+    gx = gx.permute(0, 2, 3, 1)
+    if act:
+        gx = gx * (x.float() > 0)
+    dx = K.maxpool2d_bwd(dy, am, x.shape, (k, k), (s, s), (p, p), x=x if act else None, act="relu" if act else 0)
+    torch.testing.assert_close(dx.float(), gx, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,HW,C", [(64, 49, 2048), (3, 64, 16), (5, 1, 64)])
+def test_global_avg_pool_vectorized(B, HW, C):
+    torch.manual_seed(9)
+    x = torch.randn(B, HW, 1, C, device=dev).to(bf)
+    y = K.gap_fwd(x.view(B, HW, 1, C))
+    torch.testing.assert_close(y.float(), x.float().mean((1, 2)), rtol=1e-2, atol=1e-2)
+    dy = torch.randn(B, C, device=dev).to(bf)
+    dx = K.gap_bwd(dy, (B, HW, 1, C))
+    torch.testing.assert_close(dx.float(), (dy.float() / HW)[:, None, None, :].expand(B, HW, 1, C), rtol=1e-2,
+                               atol=1e-3)
