@@ -11,6 +11,7 @@ test-suite and the ``experiment.launch`` CPU config (BASELINE.json config 1).
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -103,9 +104,34 @@ def _pad_same(k, d=1):
     return tot // 2
 
 
+def _plain_gemm_conv(g, b, act, in_affine, prev) -> bool:
+    """A 1x1 / stride-1 / unpadded conv with no epilogue (bias, activation) and no fused input layer
+    is a plain GEMM over [B*H*W, C] x [C, CO]: its forward and dgrad go to the hipBLASLt library GEMM
+    (the plain-GEMM case the kernel library leaves to the vendor library; ResNet-50 B=64 +8 %), its
+    weight gradient (a K = B*H*W reduction) stays on the split-K MFMA kernel, which measured faster
+    than the library's fp32-out path there (HOPSX_BLASLT_WGRAD=1 to compare).  Everything with a
+    fused prologue or epilogue stays on the hand-written MFMA kernels."""
+    B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw = g[:13]
+    return (KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 and b is None and not act
+            and in_affine is None and prev is None and B * H * W >= 4096 and C % 8 == 0 and CO % 8 == 0
+            and "blaslt_1x1" not in _disabled())
+
+
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None):
+        g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
+        if x.dtype == BF16 and _plain_gemm_conv(g, b, act, in_affine, prev):
+            x = x.contiguous()
+            wb = _arena.weight_bf16(w)
+            C, CO = g[3], g[6]
+            y = torch.mm(x.view(-1, C), wb.view(CO, C).t()).view(g[0], g[4], g[5], CO)
+            ctx.save_for_backward(x, y)
+            ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
+            ctx.plain = True
+            ctx.set_materialize_grads(False)
+            return y
+        ctx.plain = False
         x = x.contiguous()
         wb = _arena.weight_bf16(w)
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
@@ -121,6 +147,22 @@ class _Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy):
         if dy is None:
             return (None,) * 9
+        if ctx.plain:  # 1x1 conv as library GEMMs: dX = dY W, dW += dY^T X (fp32 out, bf16 in)
+            x, _ = ctx.saved_tensors
+            w, g = ctx.w, ctx.g
+            C, CO = g[3], g[6]
+            dy2 = dy.to(BF16).contiguous().view(-1, CO)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = torch.mm(dy2, _arena.weight_bf16(w).view(CO, C)).view(x.shape)
+            gw = _wgrad_buf(w)
+            if os.environ.get("HOPSX_BLASLT_WGRAD", "0") != "1":
+                # the library's fp32-out tall-skinny reductions (K = B*H*W) measured slower than the
+                # split-K MFMA kernel at ResNet-50 shapes: weight gradient stays on the hopsx kernel
+                K.conv2d_wgrad(dy2.view(dy.shape), x, g, gw)
+            else:
+                gw.view(CO, C).add_(torch.mm(dy2.t(), x.view(-1, C), out_dtype=torch.float32))
+            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None)
         x, y = ctx.saved_tensors
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
