@@ -195,6 +195,14 @@ def conv2d_dgrad_fused_wgrad(dy, w, geom, yprev, act_prev, y, act, x0, geom0, dw
           "conv2d_dgrad_fused_wgrad")
 
 
+def conv_wgrad_uses_ticket(geom, in_affine=None) -> bool:
+    """True when conv2d_wgrad would take the small-K kernel, whose in-launch combine draws from the
+    shared per-device ticket counter (so it must not run concurrently with another such kernel)."""
+    K = geom[7] * geom[8] * geom[3]
+    return K in (4, 9, 16) and geom[6] % 8 == 0 and geom[6] <= 256 and \
+        "smallk_wgrad" not in os.environ.get("HOPSX_DISABLE", "")
+
+
 def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0, in_affine=None):
     """dw += (dy * act'(y))^T . im2col(x); dbias += per-channel sums of the masked dy.
     in_affine=(scale, shift): x is the raw uint8 input (see conv_u8_fusable)."""

@@ -89,6 +89,9 @@ class FusedOptimizer:
         raise NotImplementedError
 
     def step(self, closure=None):
+        from .ops.functional import join_side_streams
+
+        join_side_streams()  # weight gradients still running on the parallel branch
         loss = closure() if closure is not None else None
         self.lr = self.param_groups[0]["lr"]
         a = self.arena

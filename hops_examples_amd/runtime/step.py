@@ -70,6 +70,7 @@ class TrainStep:
         out = self.forward_fn(self.model, x)
         loss, correct, count, dl = HF.loss_and_grad(out, y, self.loss_kind)
         out.backward(dl)
+        HF.join_side_streams()  # gradients complete before all-reduce / optimizer
         return {"loss": loss, "correct": correct, "count": count}
 
     def _opt(self):
