@@ -89,7 +89,9 @@ def main():
     out = {}
 
     def run(i):
-        out["r"] = step(xs[i % nb], ys[i % nb])
+        # cycles through the resident epoch; in the replayed graph the optimizer kernel's tail
+        # copies the next batch into the step's input buffers (no copy launch per step)
+        out["r"] = step.step_resident(xs, ys)
 
     for i in range(a.warmup):
         run(i)
@@ -121,7 +123,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (uint8 28x28 images + labels in HBM), random-init weights",
+            "data": "synthetic (a 60k-image uint8 28x28 epoch + labels resident in HBM, next batch prefetched "
+                    "by the optimizer kernel), random-init weights",
             "config": {
                 "model": f"MNIST CNN (experiment.mirrored model, {nparams} params), Adadelta(1.0)",
                 "global_batch": B * world,

@@ -16,6 +16,23 @@ struct OptHP {
   float lr, gscale, wd, a, b, c, d, e;
 };
 
+// Fused input prefetch (HBM-resident datasets): after its update each workgroup copies a slice of
+// batch (cursor + 1) % nbatch of up to two resident tensors (images, labels) into the step's
+// static input buffers, and the last-arriving workgroup advances the cursor.  The optimizer is the
+// last kernel of a replayed training step, so nothing reads the inputs any more: the next batch
+// lands with no launch and no copy engine on the critical path.
+struct PrefetchJob {
+  const unsigned char* src;  // batch 0 of the resident tensor; batch i at src + i * bytes
+  unsigned char* dst;        // static input buffer
+  long bytes;                // per batch (multiple of 16, 16-B aligned buffers)
+};
+struct Prefetch {
+  PrefetchJob job[2];
+  long long* cursor;  // device: index of the batch currently in dst
+  int nbatch;
+  int njobs;
+};
+
 template <int KIND>
 __device__ __forceinline__ float upd(float w, float gr, float& s1, float& s2, float& s3, const OptHP& h, float bc1,
                                      float bc2) {
@@ -79,7 +96,8 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
                                                float* __restrict__ s2, float* __restrict__ s3,
                                                bf16_raw* __restrict__ shadow, long n, OptHP h,
                                                float* __restrict__ step_dev, unsigned* __restrict__ arrive,
-                                               unsigned long long* __restrict__ rng, int zero_grad, int vec) {
+                                               unsigned long long* __restrict__ rng, int zero_grad, int vec,
+                                               Prefetch pf) {
   // step_dev holds the number of COMPLETED steps; this step is t = step + 1.
   // Every workgroup reads it before its final barrier; the last workgroup to
   // finish bumps it (and the dropout RNG counter).
@@ -139,6 +157,14 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
     if (NS >= 3) s3[i] = c;
     if (shadow) shadow[i] = f2bf(w);
   }
+  if (pf.njobs) {
+    const long long next = (pf.cursor[0] + 1) % pf.nbatch;  // every workgroup reads before the last arrives
+    for (int j = 0; j < pf.njobs; ++j) {
+      const uint4* src = (const uint4*)(pf.job[j].src + next * pf.job[j].bytes);
+      uint4* dst = (uint4*)pf.job[j].dst;
+      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pf.job[j].bytes / 16; i += stride) dst[i] = src[i];
+    }
+  }
   if (arrive) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -146,6 +172,7 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
       if (prev == gridDim.x - 1) {
         if (step_dev) step_dev[0] = t;
         if (rng) rng[1] += 1ull;
+        if (pf.njobs) pf.cursor[0] = (pf.cursor[0] + 1) % pf.nbatch;
         atomicExch(arrive, 0u);
       }
     }
@@ -159,7 +186,20 @@ __global__ void bump_k(float* step_dev, unsigned long long* rng) {
 
 extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, float* s2, float* s3,
                                 void* shadow_bf16, long n, const float* hp, int nhp, float* step_dev,
-                                unsigned* arrive, unsigned long long* rng, int zero_grad, hipStream_t st) {
+                                unsigned* arrive, unsigned long long* rng, int zero_grad, const void* const* pf_src,
+                                void* const* pf_dst, const long* pf_bytes, int pf_njobs, long long* pf_cursor,
+                                int pf_nbatch, hipStream_t st) {
+  Prefetch pf{};
+  pf.njobs = 0;
+  if (pf_njobs > 0 && pf_cursor && pf_nbatch > 0 && arrive) {  // the cursor advance needs the arrival counter
+    for (int j = 0; j < pf_njobs && j < 2; ++j) {
+      if (((uintptr_t)pf_src[j] | (uintptr_t)pf_dst[j] | (uintptr_t)pf_bytes[j]) % 16 != 0) return -5;
+      pf.job[j] = PrefetchJob{(const unsigned char*)pf_src[j], (unsigned char*)pf_dst[j], pf_bytes[j]};
+    }
+    pf.njobs = pf_njobs < 2 ? pf_njobs : 2;
+    pf.cursor = pf_cursor;
+    pf.nbatch = pf_nbatch;
+  }
   OptHP h{0, 1, 0, 0, 0, 0, 0, 0};
   float* hv = &h.lr;
   for (int i = 0; i < nhp && i < 8; ++i) hv[i] = hp[i];
@@ -175,7 +215,7 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
 #define OPT_CASE(K)                                                                                                   \
   case K:                                                                                                             \
     hipLaunchKernelGGL(optim_k<K>, dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, arr, rng, \
-                       zero_grad, (int)aligned);                                                                      \
+                       zero_grad, (int)aligned, pf);                                                                  \
     break;
   switch (kind) {
     OPT_CASE(0) OPT_CASE(1) OPT_CASE(2) OPT_CASE(3) OPT_CASE(4) OPT_CASE(5) OPT_CASE(6)

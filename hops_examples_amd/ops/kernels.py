@@ -282,15 +282,31 @@ def loss_fwd_bwd(kind: int, logits, target, grad_scale, loss_sum, correct, dlogi
 
 
 # --------------------------------------------------------------- optimizers
-def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True, arrive=None, rng=None):
+def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True, arrive=None, rng=None,
+               prefetch=None):
     """One fused update over flat buffers.  ``step_dev`` (f32[1]) counts completed steps and,
     with ``arrive`` (int32[1], zero-initialised), is bumped in-kernel by the last workgroup,
-    together with the dropout RNG counter ``rng[1]`` when given."""
+    together with the dropout RNG counter ``rng[1]`` when given.
+    ``prefetch`` = (pairs, cursor): pairs of (resident [nbatch, ...] tensor, static input buffer);
+    the kernel copies batch (cursor+1) % nbatch into the buffers and advances the int64 cursor."""
     n = param.numel()
     if step_dev is not None and arrive is None:
         arrive = torch.zeros(1, device=param.device, dtype=torch.int32)
+    srcs, dsts, nbytes, cur, nb = [], [], [], 0, 0
+    if prefetch is not None:
+        pairs, cursor = prefetch
+        for src, dst in pairs:
+            per = dst.numel() * dst.element_size()
+            assert src.is_contiguous() and dst.is_contiguous() and src.numel() == src.shape[0] * dst.numel(), \
+                "prefetch: src must be [nbatch, *dst.shape] contiguous"
+            srcs.append(ptr(src))
+            dsts.append(ptr(dst))
+            nbytes.append(per)
+            nb = src.shape[0]
+        cur = ptr(cursor)
     check(_C.ext().optim_step(kind, ptr(param), ptr(grad), ptr(s1), ptr(s2), ptr(s3), ptr(shadow), n,
-                              [float(v) for v in hp], ptr(step_dev), ptr(arrive), ptr(rng), int(zero_grad), stream()),
+                              [float(v) for v in hp], ptr(step_dev), ptr(arrive), ptr(rng), int(zero_grad), srcs,
+                              dsts, nbytes, cur, nb, stream()),
           "optim")
 
 

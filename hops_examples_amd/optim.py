@@ -66,6 +66,7 @@ class FusedOptimizer:
         self.weight_decay = float(weight_decay)
         self.hp = hp
         self.grad_scale = 1.0
+        self.prefetch = None  # (pairs, cursor): fused next-batch copy of a resident dataset (TrainStep)
         dev = self.arena.device
         self.step_count = torch.zeros(1, device=dev, dtype=torch.float32)
         self._arrive = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -105,7 +106,7 @@ class FusedOptimizer:
             sl = self._sl
             K.optim_step(OPTIM[self.kind], a.master[sl], a.grad[sl], s[0], s[1], s[2],
                          a.shadow[sl] if a.shadow is not None else None, self._hp(), self.step_count,
-                         zero_grad=True, arrive=self._arrive, rng=self.rng)
+                         zero_grad=True, arrive=self._arrive, rng=self.rng, prefetch=self.prefetch)
         else:
             self.step_count += 1
             sl = self._sl

@@ -62,6 +62,11 @@ class TrainStep:
         self._g1 = self._g2 = None
         self._sx = self._sy = None
         self._out = None
+        self._rn = 0
+        self._resident = None
+        self._cursor = None
+        self._pf_opt = None
+        self._pf_pending = None
         if dp is not None:
             optimizer.grad_scale = dp.grad_scale()
 
@@ -94,6 +99,9 @@ class TrainStep:
     def _capture(self, x, y):
         self._sx = _clone(x)
         self._sy = y.clone()
+        if self._pf_pending is not None and not isinstance(self._sx, (tuple, list)):
+            xs, ys = self._pf_pending
+            self._pf_opt.prefetch = ([(xs, self._sx), (ys, self._sy)], self._cursor)
         world = hdist.world_size()
         overlap = None
         if self.dp is not None and hasattr(self.dp, "_on_ready"):
@@ -118,8 +126,43 @@ class TrainStep:
                 self._opt()
             self._g2 = g2
         self._out = out
+        if self._pf_opt is not None:
+            self._pf_opt.prefetch = None  # only the captured optimizer kernel carries the prefetch
         if overlap is not None:
             self.dp.overlap = overlap
+
+    def step_resident(self, xs, ys):
+        """One step on an HBM-resident dataset (xs [nbatch, B, ...], ys [nbatch, B]), cycling through
+        its batches.  Once the step is a replayed hipGraph, the NEXT batch is copied into the static
+        input buffers by the optimizer kernel's tail (fused prefetch, optim.hip) and a device cursor
+        advances in-kernel: no copy launch and no host work per step beyond the replay."""
+        nb = xs.shape[0]
+        if self._g1 is None or self._resident is None or self._resident[0] is not xs or self._resident[1] is not ys:
+            i = self._rn % nb
+            self._rn += 1
+            if self.use_graph and self._n == self.warmup and self._g1 is None:
+                self._arm_prefetch(xs, ys, i)
+            r = self(xs[i], ys[i])
+            if self._g1 is not None and self._resident is None:
+                self._resident = (xs, ys)  # the graph exists and its optimizer carries the prefetch
+            return r
+        self._n += 1
+        health.beat(self._n)
+        self._g1.replay()
+        if self._g2 is not None:
+            self.dp.allreduce_all()
+            self._g2.replay()
+            self._post()
+        return self._out
+
+    def _arm_prefetch(self, xs, ys, i):
+        opt = self.opt.opts[-1] if hasattr(self.opt, "opts") else self.opt
+        if not hasattr(opt, "prefetch") or xs.device.type != "cuda":
+            return
+        # the capture clones xs[i] / ys[i] into the static buffers; the cursor says which batch they hold
+        self._cursor = torch.full((1,), i, device=xs.device, dtype=torch.int64)
+        self._pf_opt = opt
+        self._pf_pending = (xs, ys)
 
     def __call__(self, x, y):
         self._n += 1

@@ -51,3 +51,31 @@ def test_graph_replays_are_reproducible(B):
             dev_max[i] = (a.grad - ref).abs().max()
     torch.cuda.synchronize()
     assert float(dev_max.max()) < 1e-3 * float(scale), float(dev_max.max())
+
+
+def test_resident_prefetch_walks_the_epoch():
+    """TrainStep.step_resident: after capture the optimizer kernel copies batch (cursor+1) into the
+    static inputs; the losses of a resident run match explicit per-batch copies step for step."""
+    from hops_examples_amd import optim
+    from hops_examples_amd.runtime.step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    nb, B = 5, 16
+    xs = torch.randint(0, 256, (nb, B, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (nb, B), device=dev)
+    losses = []
+    for resident in (True, False):
+        HF.seed_device_rng(5, dev)
+        torch.manual_seed(0)
+        m = MirroredMnistCNN().to(dev)
+        m.pool.salt = 7919
+        ParamArena.from_module(m, dev)
+        st = TrainStep(m, optim.Adadelta(m, lr=1.0), "sparse_ce")
+        ls = []
+        for i in range(12):
+            r = st.step_resident(xs, ys) if resident else st(xs[i % nb], ys[i % nb])
+            ls.append(float(r["loss"].reshape(-1)[0]))
+        losses.append(ls)
+        if resident:
+            assert int(st._cursor.item()) == 12 % nb
+    torch.testing.assert_close(torch.tensor(losses[0]), torch.tensor(losses[1]), rtol=1e-3, atol=1e-3)
