@@ -53,6 +53,12 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     hopsx_wgrad_debug_times(v.data(), n);
     return v;
   });
+  m.def("head_ce_ok", [](int C, int KD) { return hopsx_head_ce_ok(C, KD); });
+  m.def("head_ce", [](int kind, u logits, int lf32, u target, int B, int C, int KD, float gs, u h, u w, u dw, u db,
+                      u dh, u loss, u correct, u st) {
+    return hopsx_head_ce(kind, P<void>(logits), lf32, P<void>(target), B, C, KD, gs, P<void>(h), P<void>(w),
+                         P<float>(dw), P<float>(db), P<void>(dh), P<float>(loss), P<int>(correct), S(st));
+  });
   m.def("zero", [](u p, long bytes, u st) { return hopsx_zero(P<void>(p), bytes, S(st)); });
   m.def("nonfinite", [](u x, long n, int is_bf16, u out, u st) {
     return hopsx_nonfinite(P<void>(x), n, is_bf16, P<unsigned>(out), S(st));

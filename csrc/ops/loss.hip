@@ -242,3 +242,145 @@ extern "C" int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, 
                      loss_sum, correct, dlogits, dlogits_f32, per_thread);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Classifier head, fused: for logits = h . W^T + b (the last Dense layer, C <= 32 classes) one
+// launch computes the loss, the correct count and dlogits (kept in LDS, never written), then
+//   dW[n][k] += sum_r dl[r][n] h[r][k],  db[n] += sum_r dl[r][n],  dh[r][k] = sum_n dl[r][n] W[n][k]
+// i.e. the loss kernel, the head's dgrad GEMM and its wgrad GEMM (three latency-bound launches at
+// small batch) become one.  One workgroup per 64 rows; dW/db partials leave as f32 atomics.
+constexpr int HEAD_ROWS = 32;
+constexpr int HEAD_CMAX = 32;
+
+// LDS: h tile [HEAD_ROWS][KD] bf16 | W [C][KD] bf16 | dlogits [HEAD_ROWS][C] f32 (dynamic size)
+__global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restrict__ logits, int lf32,
+                                                 const void* __restrict__ target, int B, int C, int KD, float gs,
+                                                 const bf16_raw* __restrict__ h, const bf16_raw* __restrict__ w,
+                                                 float* __restrict__ dw, float* __restrict__ db,
+                                                 bf16_raw* __restrict__ dh, float* __restrict__ loss_sum,
+                                                 int* __restrict__ correct, int vec) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char head_smem[];
+  bf16_raw* sh = (bf16_raw*)head_smem;
+  bf16_raw* sw = sh + HEAD_ROWS * KD;
+  float* sdl = (float*)(sw + ((C * KD + 7) / 8) * 8);
+  __shared__ float sl[16];
+  __shared__ int sc[16];
+  const int r0 = blockIdx.x * HEAD_ROWS;
+  const int nr = min(HEAD_ROWS, B - r0);
+  // stage the h tile and W (one round trip of independent 16-B loads)
+  if (vec) {
+    const int hch = nr * KD / 8, wch = C * KD / 8;
+    for (int i = threadIdx.x; i < hch + wch; i += blockDim.x) {
+      if (i < hch) ((bf16x8*)sh)[i] = ((const bf16x8*)(h + (long)r0 * KD))[i];
+      else ((bf16x8*)sw)[i - hch] = ((const bf16x8*)w)[i - hch];
+    }
+  } else {
+    for (int i = threadIdx.x; i < nr * KD; i += blockDim.x) sh[i] = h[(long)r0 * KD + i];
+    for (int i = threadIdx.x; i < C * KD; i += blockDim.x) sw[i] = w[i];
+  }
+  float lacc = 0.f;
+  int cacc = 0;
+  if ((int)threadIdx.x < nr) {
+    const void* lg = lf32 ? (const void*)((const float*)logits + (long)r0 * C)
+                          : (const void*)((const bf16_raw*)logits + (long)r0 * C);
+    const void* tg = kind == 0 ? (const void*)((const long*)target + r0)
+                               : (const void*)((const float*)target + (long)r0 * C);
+    row_thread(kind, lg, lf32, tg, threadIdx.x, C, gs, sdl, 1, lacc, cacc);
+  }
+  lacc = wave_sum(lacc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cacc += __shfl_xor(cacc, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    sl[wave] = lacc;
+    sc[wave] = cacc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f;
+    int c = 0;
+    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
+      l += sl[q];
+      c += sc[q];
+    }
+    l *= gs;
+    if (gridDim.x == 1) {
+      if (loss_sum) *loss_sum = l;
+      if (correct) *correct = c;
+    } else {
+      if (loss_sum) atomicAdd(loss_sum, l);
+      if (correct) atomicAdd(correct, c);
+    }
+  }
+  // weight / bias gradient of the head, all operands in LDS; 8 rows' loads in flight per step
+  for (int e = threadIdx.x; e < C * KD; e += blockDim.x) {
+    const int n = e / KD, k = e - n * KD;
+    float s0 = 0.f, s1 = 0.f;
+    int r = 0;
+    for (; r + 8 <= nr; r += 8) {
+      float a[8], v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = sdl[(r + u) * C + n];
+        v[u] = bf2f(sh[(r + u) * KD + k]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 = fmaf(a[u], v[u], s0);
+        s1 = fmaf(a[u + 1], v[u + 1], s1);
+      }
+    }
+    for (; r < nr; ++r) s0 = fmaf(sdl[r * C + n], bf2f(sh[r * KD + k]), s0);
+    const float s = s0 + s1;
+    if (s != 0.f) atomicAdd(dw + e, s);
+  }
+  if (db)
+    for (int n = threadIdx.x; n < C; n += blockDim.x) {
+      float s = 0.f;
+      for (int r = 0; r < nr; ++r) s += sdl[r * C + n];
+      if (s != 0.f) atomicAdd(db + n, s);
+    }
+  // input gradient of the head (the previous layer applies its own act' mask)
+  for (int e = threadIdx.x; e < nr * KD; e += blockDim.x) {
+    const int r = e / KD, k = e - r * KD;
+    float s0 = 0.f, s1 = 0.f;
+    int n = 0;
+    for (; n + 8 <= C; n += 8) {
+      float a[8], v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = sdl[r * C + n + u];
+        v[u] = bf2f(sw[(n + u) * KD + k]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 = fmaf(a[u], v[u], s0);
+        s1 = fmaf(a[u + 1], v[u + 1], s1);
+      }
+    }
+    for (; n < C; ++n) s0 = fmaf(sdl[r * C + n], bf2f(sw[n * KD + k]), s0);
+    dh[(long)(r0 + r) * KD + k] = f2bf(s0 + s1);
+  }
+}
+
+static size_t head_lds_bytes(int C, int KD) {
+  return (size_t)HEAD_ROWS * KD * 2 + (size_t)((C * KD + 7) / 8) * 8 * 2 + (size_t)HEAD_ROWS * C * 4;
+}
+
+bool hopsx_head_ce_ok(int C, int KD) { return C >= 1 && C <= HEAD_CMAX && KD >= 1 && head_lds_bytes(C, KD) <= 65536; }
+
+extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
+                             float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh,
+                             float* loss_sum, int* correct, hipStream_t st) {
+  if (!hopsx_head_ce_ok(C, KD) || B < 1) return -2;
+  const int grid = (B + HEAD_ROWS - 1) / HEAD_ROWS;
+  if (grid > 1) {
+    if (loss_sum) hopsx_zero(loss_sum, sizeof(float), st);
+    if (correct) hopsx_zero(correct, sizeof(int), st);
+  }
+  const int vec = KD % 8 == 0 && ((uintptr_t)h % 16 == 0) && ((uintptr_t)w % 16 == 0);
+  hipLaunchKernelGGL(head_ce_k, dim3(grid), dim3(1024), head_lds_bytes(C, KD), st, kind, logits, logits_f32, target, B, C,
+                     KD, grad_scale, (const bf16_raw*)h, (const bf16_raw*)w, dw, db, (bf16_raw*)dh, loss_sum,
+                     correct, vec);
+  return (int)hipGetLastError();
+}

@@ -39,6 +39,11 @@ int hopsx_avgpool_global_bwd(const void* dy, void* dx, int B, int HW, int C, hip
 // ---- losses (loss.hip) ----
 // kind: 0 softmax cross-entropy (int labels), 1 softmax CE (dense/one-hot targets),
 //       2 sigmoid BCE from logits, 3 MSE, 4 BCE on probabilities
+// fused classifier head: loss + dlogits (in LDS) + head wgrad/bias grad + input gradient (loss.hip)
+bool hopsx_head_ce_ok(int C, int KD);
+int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
+                  float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh, float* loss_sum,
+                  int* correct, hipStream_t st);
 int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
                        float grad_scale, float* loss_sum, int* correct, void* dlogits, int dlogits_f32,
                        hipStream_t st);

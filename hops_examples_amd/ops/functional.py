@@ -163,7 +163,13 @@ def linear(x, w, b=None, act=None, out_f32=False):
     """y = act(x @ w.T + b); w is [out, in] (fp32 master; bf16 shadow used on GPU)."""
     if not x.is_cuda:
         return _cpu_act(F.linear(x.float(), w, b), act)
-    return _LinearFn.apply(to_compute(x), w, b, ACT[act] if not isinstance(act, int) else act, out_f32)
+    a = ACT[act] if not isinstance(act, int) else act
+    xc = to_compute(x)
+    y = _LinearFn.apply(xc, w, b, a, out_f32)
+    if (not a and x.dim() == 2 and w.shape[0] <= 32 and y.requires_grad and xc.dtype == BF16
+            and _arena.grad_target(w) is not None and (b is None or _arena.grad_target(b) is not None)):
+        y._hx_dense_head = (xc, w, b)  # logits layer: loss_and_grad can fuse its backward (head_ce)
+    return y
 
 
 # ===================================================================== Conv2d
@@ -619,6 +625,35 @@ def loss_and_grad(logits, target, kind: str = "sparse_ce"):
     dl = torch.empty(B, C, device=logits.device, dtype=logits.dtype)
     K.loss_fwd_bwd(k, logits.detach().contiguous(), target.contiguous(), 1.0 / cnt, loss_sum, correct, dl)
     return loss_sum, correct, (B if k in (0, 1) else cnt), dl
+
+
+def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
+    """Like :func:`loss_and_grad` but returns ``(loss, correct, count, root, grad)`` for
+    ``root.backward(grad)``.  When ``logits`` come from a linear logits layer (tagged by
+    :func:`linear`), ONE kernel computes the loss, that layer's weight and bias gradients and the
+    gradient w.r.t. its input ``h`` (loss.hip head_ce_k), and backward starts at ``h``: the loss
+    kernel and the head's two backward GEMMs collapse into one launch."""
+    head = getattr(logits, "_hx_dense_head", None)
+    k = LOSS[kind]
+    if (head is None or not logits.is_cuda or logits.dim() != 2 or "head_ce" in _disabled()
+            or not K.head_ce_ok(logits.shape[1], head[0].shape[1])):
+        loss_, correct, count, dl = loss_and_grad(logits, target, kind)
+        return loss_, correct, count, logits, dl
+    h, w, b = head
+    B, C = logits.shape
+    cnt = B * (C if k in (2, 3, 4) else 1)
+    if k in (2, 3, 4) and target.dim() == 1:
+        target = target.unsqueeze(1)
+    target = (target.long() if k == 0 else target.float()).contiguous()
+    loss_sum = torch.empty(1, device=logits.device)
+    correct = torch.empty(1, device=logits.device, dtype=torch.int32)
+    dh = K.head_ce(k, logits.detach().contiguous(), target, h.detach(), _arena.weight_bf16(w),
+                   _arena.grad_target(w), _arena.grad_target(b) if b is not None else None, 1.0 / cnt, loss_sum,
+                   correct)
+    hooks.grad_ready(w)
+    if b is not None:
+        hooks.grad_ready(b)
+    return loss_sum, correct, (B if k in (0, 1) else cnt), h, dh
 
 
 def loss(logits, target, kind: str = "sparse_ce", stats: dict | None = None):

@@ -475,3 +475,23 @@ def nonfinite_counts(x, out=None):
     zero_(out)
     check(_C.ext().nonfinite(ptr(x), x.numel(), int(x.dtype == BF16), ptr(out), stream()), "nonfinite")
     return out
+
+
+# --------------------------------------------------------- fused classifier head
+def head_ce_ok(C: int, KD: int) -> bool:
+    return bool(_C.ext().head_ce_ok(int(C), int(KD)))
+
+
+def head_ce(kind: int, logits, target, h, w, dw, db, grad_scale: float, loss_sum, correct):
+    """Loss + dlogits (never materialised) + dW += dl^T h + db += sum dl + returns dh = dl W, in one
+    launch (loss.hip head_ce_k).  logits [B, C<=32] fp32/bf16, h [B, KD] bf16, w [C, KD] bf16."""
+    B, C = logits.shape
+    KD = h.shape[1]
+    _req(h, BF16, "h")
+    _req(w, BF16, "w")
+    _req(dw, F32, "dw")
+    dh = torch.empty(B, KD, device=h.device, dtype=BF16)
+    check(_C.ext().head_ce(kind, ptr(logits), int(logits.dtype == F32), ptr(target), B, C, KD, float(grad_scale),
+                           ptr(h), ptr(w), ptr(dw), ptr(db), ptr(dh), ptr(loss_sum), ptr(correct), stream()),
+          "head_ce")
+    return dh

@@ -73,8 +73,8 @@ class TrainStep:
     # ------------------------------------------------------------- eager path
     def _fwd_bwd(self, x, y):
         out = self.forward_fn(self.model, x)
-        loss, correct, count, dl = HF.loss_and_grad(out, y, self.loss_kind)
-        out.backward(dl)
+        loss, correct, count, root, grad = HF.loss_and_grad_root(out, y, self.loss_kind)
+        root.backward(grad)
         HF.join_side_streams()  # gradients complete before all-reduce / optimizer
         return {"loss": loss, "correct": correct, "count": count}
 

@@ -320,3 +320,42 @@ def test_plain_1x1_conv_library_gemm_matches_kernel(monkeypatch):
         outs.append((y.float(), x.grad.float(), w.grad.float()))
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, atol=2e-2 * b.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("kind,C,B", [("sparse_ce", 10, 32), ("sparse_ce", 10, 200), ("ce", 10, 17),
+                                      ("bce_logits", 1, 40), ("mse", 3, 9)])
+def test_fused_classifier_head(monkeypatch, kind, C, B):
+    """loss_and_grad_root on a linear logits layer: one head_ce launch (loss, dW, db, dh) must give
+    the same loss and gradients as the loss kernel + the layer's backward GEMMs."""
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    torch.manual_seed(11)
+    h0 = torch.randn(B, 128, device=dev).to(bf)
+    if kind == "sparse_ce":
+        t = torch.randint(0, C, (B,), device=dev)
+    elif kind == "ce":
+        t = torch.nn.functional.one_hot(torch.randint(0, C, (B,), device=dev), C).float()
+    else:
+        t = torch.rand(B, C, device=dev).round() if kind == "bce_logits" else torch.randn(B, C, device=dev)
+    res = []
+    for disable in ("", "head_ce"):
+        monkeypatch.setenv("HOPSX_DISABLE", disable)
+        lin = torch.nn.Linear(128, C).to(dev)
+        with torch.no_grad():
+            torch.manual_seed(12)
+            lin.weight.copy_(torch.randn(C, 128, device=dev) * 0.1)
+            lin.bias.copy_(torch.randn(C, device=dev) * 0.1)
+        ParamArena.from_module(lin, dev)
+        h = h0.clone().requires_grad_(True)
+        out = HF.linear(h, lin.weight, lin.bias, out_f32=True)
+        loss, correct, count, root, grad = HF.loss_and_grad_root(out, t, kind)
+        assert (root is h) == (disable == "")
+        root.backward(grad)
+        torch.cuda.synchronize()
+        res.append((loss.clone(), correct.clone(), lin._hx_arena.grad.clone(), h.grad.float().clone()))
+    (l0, c0, g0, d0), (l1, c1, g1, d1) = res
+    torch.testing.assert_close(l0, l1, rtol=1e-4, atol=1e-5)
+    assert int(c0) == int(c1)
+    torch.testing.assert_close(g0, g1, rtol=2e-2, atol=2e-2 * g1.abs().max().item())
+    torch.testing.assert_close(d0, d1, rtol=2e-2, atol=2e-2 * d1.abs().max().item())
