@@ -296,7 +296,7 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
     sc[wave] = cacc;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && blockIdx.y == 0) {
     float l = 0.f;
     int c = 0;
     for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
@@ -312,9 +312,12 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
       if (correct) atomicAdd(correct, c);
     }
   }
-  // weight / bias gradient of the head, all operands in LDS; 8 rows' loads in flight per step
-  for (int e = threadIdx.x; e < C * KD; e += blockDim.x) {
-    const int n = e / KD, k = e - n * KD;
+  // weight / bias gradient of the head, all operands in LDS; 8 rows' loads in flight per step.
+  // blockIdx.y owns columns [k0, k0 + kw) of KD (the dl recompute per column block is ~free)
+  const int kw = (KD + gridDim.y - 1) / gridDim.y;
+  const int k0 = blockIdx.y * kw, kn = min(kw, KD - k0);
+  for (int e = threadIdx.x; e < C * kn; e += blockDim.x) {
+    const int n = e / kn, k = k0 + (e - n * kn);
     float s0 = 0.f, s1 = 0.f;
     int r = 0;
     for (; r + 8 <= nr; r += 8) {
@@ -332,17 +335,17 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
     }
     for (; r < nr; ++r) s0 = fmaf(sdl[r * C + n], bf2f(sh[r * KD + k]), s0);
     const float s = s0 + s1;
-    if (s != 0.f) atomicAdd(dw + e, s);
+    if (s != 0.f) atomicAdd(dw + (long)n * KD + k, s);
   }
-  if (db)
+  if (db && blockIdx.y == 0)
     for (int n = threadIdx.x; n < C; n += blockDim.x) {
       float s = 0.f;
       for (int r = 0; r < nr; ++r) s += sdl[r * C + n];
       if (s != 0.f) atomicAdd(db + n, s);
     }
   // input gradient of the head (the previous layer applies its own act' mask)
-  for (int e = threadIdx.x; e < nr * KD; e += blockDim.x) {
-    const int r = e / KD, k = e - r * KD;
+  for (int e = threadIdx.x; e < nr * kn; e += blockDim.x) {
+    const int r = e / kn, k = k0 + (e - r * kn);
     float s0 = 0.f, s1 = 0.f;
     int n = 0;
     for (; n + 8 <= C; n += 8) {
@@ -374,12 +377,16 @@ extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const
                              float* loss_sum, int* correct, hipStream_t st) {
   if (!hopsx_head_ce_ok(C, KD) || B < 1) return -2;
   const int grid = (B + HEAD_ROWS - 1) / HEAD_ROWS;
-  if (grid > 1) {
+  // column blocks of >= 32 columns so a small batch still spreads over several CUs
+  int gy = KD / 32;
+  if (gy > 8) gy = 8;
+  if (gy < 1) gy = 1;
+  if (grid > 1) {  // (one row block: the blockIdx.y == 0 workgroup overwrites the totals)
     if (loss_sum) hopsx_zero(loss_sum, sizeof(float), st);
     if (correct) hopsx_zero(correct, sizeof(int), st);
   }
   const int vec = KD % 8 == 0 && ((uintptr_t)h % 16 == 0) && ((uintptr_t)w % 16 == 0);
-  hipLaunchKernelGGL(head_ce_k, dim3(grid), dim3(1024), head_lds_bytes(C, KD), st, kind, logits, logits_f32, target, B, C,
+  hipLaunchKernelGGL(head_ce_k, dim3(grid, gy), dim3(1024), head_lds_bytes(C, KD), st, kind, logits, logits_f32, target, B, C,
                      KD, grad_scale, (const bf16_raw*)h, (const bf16_raw*)w, dw, db, (bf16_raw*)dh, loss_sum,
                      correct, vec);
   return (int)hipGetLastError();
