@@ -134,13 +134,44 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
 // multiplies each masked dX row by the input layer's im2col row (K0 raw pixels, uint8 with the
 // fused affine or bf16) and accumulates dW0[ci][k] in registers; the previous layer's bias
 // gradient is the existing colsum.  Saves the dX write/re-read and a whole launch.
+struct DgradArgs {
+  const bf16_raw* dy;
+  const bf16_raw* w;
+  bf16_raw* dx;
+  const bf16_raw* yprev;
+  int act_prev;
+  float* colsum;
+  const bf16_raw* y;
+  int yact;
+  ConvGeom g;
+  int K;
+  int wvec;
+  const void* x0;
+  float xscale, xshift;
+  ConvGeom gi;
+  float* dw0;
+  int dbg;
+};
+
+// bid / nblk: this workgroup's index and the number of workgroups doing dgrad work (a paired
+// launch, conv_bwd_pair_k, hands the remaining workgroups to the weight gradient)
 template <int NF, int KS, int K0, int UN>
-__global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ w,
-                                                        bf16_raw* __restrict__ dx, const bf16_raw* __restrict__ yprev,
-                                                        int act_prev, float* __restrict__ colsum,
-                                                        const bf16_raw* __restrict__ y, int yact, ConvGeom g, int K,
-                                                        int wvec, const void* __restrict__ x0, float xscale,
-                                                        float xshift, ConvGeom gi, float* __restrict__ dw0, int dbg) {
+__device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int nblk) {
+  const bf16_raw* __restrict__ dy = A.dy;
+  const bf16_raw* __restrict__ w = A.w;
+  bf16_raw* __restrict__ dx = A.dx;
+  const bf16_raw* __restrict__ yprev = A.yprev;
+  const int act_prev = A.act_prev;
+  float* __restrict__ colsum = A.colsum;
+  const bf16_raw* __restrict__ y = A.y;
+  const int yact = A.yact;
+  const ConvGeom& g = A.g;
+  const int K = A.K, wvec = A.wvec;
+  const void* __restrict__ x0 = A.x0;
+  const float xscale = A.xscale, xshift = A.xshift;
+  const ConvGeom& gi = A.gi;
+  float* __restrict__ dw0 = A.dw0;
+  const int dbg = A.dbg;
   phase_mark(dbg, 0);
   constexpr int CI = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
@@ -193,7 +224,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
   constexpr int NCH = 16 * CI / 8;      // 16-B output chunks per 16-pixel group
   constexpr int CPL = (NCH + 63) / 64;  // of which this lane stores CPL (c = lane + 64 q)
   constexpr int XK = K0 > 0 ? K0 : 1;
-  for (int g0 = (blockIdx.x * CM_WAVES + wave) * UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * UN) {
+  for (int g0 = (bid * CM_WAVES + wave) * UN; g0 < ngroups; g0 += nblk * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
     bf16x8 pmv[UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
     float xk[UN][CPL][XK];
@@ -340,6 +371,11 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
 }
 
 
+template <int NF, int KS, int K0, int UN>
+__global__ __launch_bounds__(256) void conv_dgrad_mfma_k(DgradArgs A) {
+  conv_dgrad_body<NF, KS, K0, UN>(A, blockIdx.x, gridDim.x);
+}
+
 // ---------------------------------------------------------------------------- wgrad
 // dW[co][k] += sum_px dY'[px][co] * im2col(X)[px][k] (dY' = dY * act'(y)), db[co] += sum_px dY'[px][co]
 // for short convs (CO <= 64, C % 8 == 0).  The generic split-K GEMM walks 4+ K-tiles per
@@ -355,11 +391,28 @@ __global__ __launch_bounds__(256) void conv_dgrad_mfma_k(const bf16_raw* __restr
 // (LDS float atomics were measured at ~200 cycles per ds_add_f32 here: not used.)
 constexpr int WG_PX = 32;  // pixels per wave chunk (= MFMA K)
 
+struct WgradArgs {
+  const bf16_raw* dy;
+  const bf16_raw* x;
+  const bf16_raw* y;
+  int yact;
+  float* dw;
+  float* dbias;
+  ConvGeom g;
+  int K, cpw, dbg;
+};
+
+// (bx, by): pixel-group and column-block coordinates of this workgroup
 template <int NFC, int NFKW>
-__global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
-                                                        const bf16_raw* __restrict__ y, int yact,
-                                                        float* __restrict__ dw, float* __restrict__ dbias, ConvGeom g,
-                                                        int K, int cpw, int dbg) {
+__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& A, int bx, int by) {
+  const bf16_raw* __restrict__ dy = A.dy;
+  const bf16_raw* __restrict__ x = A.x;
+  const bf16_raw* __restrict__ y = A.y;
+  const int yact = A.yact;
+  float* __restrict__ dw = A.dw;
+  float* __restrict__ dbias = A.dbias;
+  const ConvGeom& g = A.g;
+  const int K = A.K, cpw = A.cpw, dbg = A.dbg;
   phase_mark(dbg, 0);
   constexpr int CO = NFC * 16, KB = NFKW * 16;
   constexpr int DCH = WG_PX * CO / 8 / 64;  // 16-B dY chunks per lane per pixel chunk
@@ -370,7 +423,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restr
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   bf16_raw* sA = cm_smem + wave * WG_PX * (CO + KB);  // [px][CO]  rc-swizzled
   bf16_raw* sB = sA + WG_PX * CO;                     // [px][KB]  rc-swizzled
-  const int kb0 = blockIdx.y * KB;
+  const int kb0 = by * KB;
   const int M = g.B * g.OH * g.OW;
   const int nchunks = (M + WG_PX - 1) / WG_PX;
   // this lane's fixed columns: dY chunk column dc (8 channels), im2col chunk column xc (8 ci of one tap)
@@ -380,7 +433,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restr
   const bool kin = kcol < K;
   const int tap = kin ? g.fC.div(kcol) : 0, ci0 = kin ? kcol - tap * g.C : 0;
   const int kh = g.fKW.div(tap), kw = tap - kh * g.KW;
-  const bool do_bias = dbias != nullptr && blockIdx.y == 0;
+  const bool do_bias = dbias != nullptr && by == 0;
   f32x4 acc[NFC][NFKW];
 #pragma unroll
   for (int i = 0; i < NFC; ++i)
@@ -424,7 +477,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restr
     return (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
   };
 
-  const int cbeg = (blockIdx.x * 4 + wave) * cpw;
+  const int cbeg = (bx * 4 + wave) * cpw;
   const int cend = min(nchunks, cbeg + cpw);
   if (cbeg < cend) load(cbeg);
   for (int c = cbeg; c < cend; ++c) {  // wave-uniform: EXEC stays full for the tr reads
@@ -506,6 +559,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(const bf16_raw* __restr
   if (dbg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     phase_mark(dbg, 3);
+  }
+}
+
+template <int NFC, int NFKW>
+__global__ __launch_bounds__(256) void conv_wgrad_mfma_k(WgradArgs A) {
+  conv_wgrad_body<NFC, NFKW>(A, blockIdx.x, blockIdx.y);
+}
+
+// Horizontal fusion of one conv layer's backward: the input-gradient workgroups (first nA) and
+// the weight-gradient workgroups (the rest, nBx x nBy) share ONE launch.  The two GEMMs are
+// independent and each alone leaves most CUs idle at small batch; a second stream would run them
+// concurrently too, but a cross-queue dependency costs ~10 us per replayed graph, a launch ~1.5.
+template <int NF, int KS, int K0, int NFC>
+__global__ __launch_bounds__(256) void conv_bwd_pair_k(DgradArgs A, WgradArgs B, int nA, int nBx) {
+  if ((int)blockIdx.x < nA) {
+    conv_dgrad_body<NF, KS, K0, 2>(A, blockIdx.x, nA);
+  } else {
+    const int j = blockIdx.x - nA;
+    conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx);
   }
 }
 
@@ -614,13 +686,11 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
                      (size_t)CM_WAVES * g.C * (1 + K0) * sizeof(float);
   const int wvec = (uintptr_t)w % 16 == 0;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
+  const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg};
 #define HOPSX_CMD(NF, KSV, K0V)                                                                                \
-  if (un == 1) hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 1>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy, \
-                     (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,              \
-                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg);                  \
-  else hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 2>), dim3(blocks), dim3(256), shm, st, (const bf16_raw*)dy, \
-                     (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,              \
-                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg)
+  if (un == 1) hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 1>), dim3(blocks), dim3(256), shm, st, DA); \
+  else hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 2>), dim3(blocks), dim3(256), shm, st, DA)
 #define HOPSX_CMD_NF(NF)          \
   switch (KS) {                   \
     case 2: HOPSX_CMD(NF, 2, 0); break;  \
@@ -683,11 +753,10 @@ extern "C" int hopsx_conv2d_wgrad_mfma(const void* dy, const void* x, const int*
   const int NFR = (g.CO / 16) * NFKW;
   const size_t redb = ((size_t)4 * NFR * 64 * 4 + 4 * g.CO + (size_t)g.CO * KB) * sizeof(float);
   const size_t shm = std::max(stage, redb);
+  const WgradArgs WA{(const bf16_raw*)dy, (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, K, cpw, dbg};
 #define HOPSX_CWM(NFC)                                                                                     \
-  if (NFKW == 4) hipLaunchKernelGGL((conv_wgrad_mfma_k<NFC, 4>), grid, dim3(256), shm, st, (const bf16_raw*)dy, \
-                     (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, K, cpw, dbg);                     \
-  else hipLaunchKernelGGL((conv_wgrad_mfma_k<NFC, 2>), grid, dim3(256), shm, st, (const bf16_raw*)dy,           \
-                     (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, K, cpw, dbg)
+  if (NFKW == 4) hipLaunchKernelGGL((conv_wgrad_mfma_k<NFC, 4>), grid, dim3(256), shm, st, WA); \
+  else hipLaunchKernelGGL((conv_wgrad_mfma_k<NFC, 2>), grid, dim3(256), shm, st, WA)
   switch (g.CO) {
     case 16: HOPSX_CWM(1); break;
     case 32: HOPSX_CWM(2); break;
@@ -701,4 +770,62 @@ extern "C" int hopsx_conv2d_wgrad_mfma(const void* dy, const void* x, const int*
 extern "C" int hopsx_wgrad_debug_times(unsigned long long* host_out, int n) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wgrad_dbg), sizeof(unsigned long long) * (size_t)n, 0,
                                   hipMemcpyDeviceToHost);
+}
+
+// One launch for a conv layer's whole backward: dgrad (optionally carrying the input layer's
+// weight gradient, geom0 != null) + the layer's own weight gradient.  Same argument meaning as
+// hopsx_conv2d_dgrad_mfma_ex and hopsx_conv2d_wgrad_mfma; returns -2 for shapes outside the
+// instantiated set (the caller then issues the two launches).
+extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                     int act_prev, float* colsum, const void* y, int yact, const int* geom0,
+                                     const void* x0, float xscale, float xshift, float* dw0, const void* x,
+                                     float* dw, float* dbias, hipStream_t st) {
+  if (hopsx_disabled("bwd_pair") || !hopsx_conv_dgrad_mfma_ok(geom) || !hopsx_conv_wgrad_mfma_ok(geom)) return -2;
+  const bool fused = geom0 != nullptr;
+  if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
+  if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)yprev) % 16 != 0) return -2;
+  ConvGeom g = cm_geom(geom);
+  ConvGeom g0 = fused ? cm_geom(geom0) : ConvGeom{};
+  const int K0 = fused ? geom0[7] * geom0[8] : 0;
+  // ---- dgrad part
+  const int Kd = g.KH * g.KW * g.CO;
+  const int KS = cm_ks((Kd + 31) / 32);
+  const long Md = (long)g.B * g.H * g.W;
+  long nA = ((Md + 15) / 16 + CM_WAVES * 2 - 1) / (CM_WAVES * 2);
+  if (nA > 1024) nA = 1024;
+  if (colsum && nA > 512) nA = 512;
+  const size_t shmA = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
+                      (size_t)CM_WAVES * g.C * (1 + K0) * sizeof(float);
+  static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
+  const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
+                     (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg};
+  // ---- wgrad part (32-column blocks)
+  const int Kw = g.KH * g.KW * g.C;
+  const long nchunks = ((long)g.B * g.OH * g.OW + WG_PX - 1) / WG_PX;
+  constexpr int KB = 32;
+  const int colblk = (Kw + KB - 1) / KB;
+  const long want_groups = std::max(1L, 384L / colblk);
+  const int cpw = (int)std::max(1L, (nchunks + 4 * want_groups - 1) / (4 * want_groups));
+  const long nBx = (nchunks + 4L * cpw - 1) / (4L * cpw);
+  const size_t stage = (size_t)4 * WG_PX * (g.CO + KB) * sizeof(bf16_raw);
+  const size_t redb = ((size_t)4 * (g.CO / 16) * 2 * 64 * 4 + 4 * g.CO + (size_t)g.CO * KB) * sizeof(float);
+  const size_t shm = std::max(shmA, std::max(stage, redb));
+  const WgradArgs WA{(const bf16_raw*)dy, (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, Kw, cpw, dbg};
+  const long total = nA + nBx * colblk;
+  if (shm > 65536 || total > (1L << 20)) return -2;
+  const int NF = g.C / 16, NFC = g.CO / 16;
+#define HOPSX_PAIR(NFv, KSv, K0v, NFCv)                                                                      \
+  if (NF == NFv && KS == KSv && K0 == K0v && NFC == NFCv) {                                                  \
+    hipLaunchKernelGGL((conv_bwd_pair_k<NFv, KSv, K0v, NFCv>), dim3((unsigned)total), dim3(256), shm, st, DA, WA, \
+                       (int)nA, (int)nBx);                                                                     \
+    return (int)hipGetLastError();                                                                           \
+  }
+#define HOPSX_PAIR_K0(NFv, KSv, NFCv) HOPSX_PAIR(NFv, KSv, 0, NFCv) HOPSX_PAIR(NFv, KSv, 4, NFCv)
+#define HOPSX_PAIR_NFC(NFv, KSv) HOPSX_PAIR_K0(NFv, KSv, 1) HOPSX_PAIR_K0(NFv, KSv, 2) HOPSX_PAIR_K0(NFv, KSv, 4)
+  HOPSX_PAIR_NFC(1, 4) HOPSX_PAIR_NFC(1, 8) HOPSX_PAIR_NFC(2, 4) HOPSX_PAIR_NFC(2, 8) HOPSX_PAIR_NFC(4, 4)
+  HOPSX_PAIR_NFC(4, 8)
+#undef HOPSX_PAIR_NFC
+#undef HOPSX_PAIR_K0
+#undef HOPSX_PAIR
+  return -2;
 }

@@ -251,6 +251,21 @@ class _Conv2dFn(torch.autograd.Function):
             act = 0
         dx = None
         gw = _wgrad_buf(w)
+        wflop = 2.0 * dy.numel() * g[7] * g[8] * g[3]
+        if (wflop < _PAR_MIN_FLOP and (ctx.prev is not None or ctx.needs_input_grad[0])
+                and dy.dtype == BF16 and x.dtype == BF16 and "bwd_pair" not in _disabled()):
+            # small layer: dgrad and wgrad as ONE launch (horizontal fusion) instead of two
+            pprev = None
+            if ctx.prev is not None:
+                w0, b0, g0, act0, aff0, x0 = ctx.prev
+                pprev = (x0, g0, _arena.grad_target(w0), _arena.grad_target(b0), x, act0, aff0)
+            r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, dbias=gb, y=ymask, act=act, prev=pprev)
+            if r is not False:
+                if ctx.prev is not None:
+                    hooks.grad_ready(ctx.prev[0])
+                    hooks.grad_ready(ctx.prev[1])
+                return (r, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None,
+                        None, None)
         side_ok = not K.conv_wgrad_uses_ticket(g, ctx.in_affine)
         if side_ok:  # wgrad || dgrad on a parallel branch (its kernels keep no shared ticket/workspace)
             with _on_side(dy.device, dy, x, ymask, flop=2.0 * dy.numel() * g[7] * g[8] * g[3]):

@@ -359,3 +359,33 @@ def test_fused_classifier_head(monkeypatch, kind, C, B):
     assert int(c0) == int(c1)
     torch.testing.assert_close(g0, g1, rtol=2e-2, atol=2e-2 * g1.abs().max().item())
     torch.testing.assert_close(d0, d1, rtol=2e-2, atol=2e-2 * d1.abs().max().item())
+
+
+@pytest.mark.parametrize("model", ["mirrored", "cifar"])
+def test_paired_conv_backward_matches_separate_launches(monkeypatch, model):
+    """conv_bwd_pair_k (dgrad + wgrad workgroups in one launch) vs the two separate launches."""
+    from hops_examples_amd.models.mnist import MirroredMnistCNN
+    from hops_examples_amd.models.resnet import cifar_resnet
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    grads = []
+    for disable in ("", "bwd_pair"):
+        monkeypatch.setenv("HOPSX_DISABLE", disable)
+        HF.seed_device_rng(3, dev)
+        torch.manual_seed(0)
+        if model == "mirrored":
+            m = MirroredMnistCNN().to(dev)
+            m.pool.salt = 7919
+            x = torch.randint(0, 256, (32, 28, 28, 1), dtype=torch.uint8, device=dev)
+        else:
+            m = cifar_resnet(20).to(dev)
+            x = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, device=dev)
+        ParamArena.from_module(m, dev)
+        t = torch.randint(0, 10, (x.shape[0],), device=dev)
+        out = m(x)
+        _, _, _, root, g = HF.loss_and_grad_root(out, t, "sparse_ce")
+        root.backward(g)
+        torch.cuda.synchronize()
+        grads.append(m._hx_arena.grad.float().clone())
+    torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
