@@ -63,6 +63,11 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   m.def("nonfinite", [](u x, long n, int is_bf16, u out, u st) {
     return hopsx_nonfinite(P<void>(x), n, is_bf16, P<unsigned>(out), S(st));
   });
+  m.def("linear_bwd_pair", [](u dy, u w, u x, u dx, u yprev, int act_prev, u colsum, u ay, int aact, u dw, u db,
+                              int M, int N, int K, u st) {
+    return hopsx_linear_bwd_pair(P<void>(dy), P<void>(w), P<void>(x), P<void>(dx), P<void>(yprev), act_prev,
+                                 P<float>(colsum), P<void>(ay), aact, P<float>(dw), P<float>(db), M, N, K, S(st));
+  });
   m.def("conv2d_bwd_pair", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact,
                               std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u st) {
     return hopsx_conv2d_bwd_pair(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act,

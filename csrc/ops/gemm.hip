@@ -124,3 +124,58 @@ extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long
                                       st, arowsum);
   return dispatch_epi<false, true>(al, bl, M, N, K, epi, out, ldo, bias, alpha, beta, act, aux, ldaux, colsum, st, arowsum);
 }
+
+// ---------------------------------------------------------------------------
+// A Linear layer's whole backward in ONE launch (horizontal fusion): the first gxA*gyA
+// workgroups compute dX = (dY*act'(y)) . W (masked by the previous layer's act'), the rest
+// dW += (dY*act'(y))^T . X with the bias gradient as the staged operand's row sums.  At small
+// batch each GEMM alone is a latency-bound launch on a few hundred workgroups.
+template <int BMA, int BMB>
+__global__ __launch_bounds__(256) void linear_bwd_pair_k(DenseLoader aA, DenseLoader bA, EpiDActBF16 eA, int MA,
+                                                         int NA, int KA, int kpsA, int gxA, int gyA, DenseLoader aB,
+                                                         DenseLoader bB, EpiAtomicF32 eB, int MB, int NB, int KB,
+                                                         int kpsB, int gxB, int gyB, float* rowsumB) {
+  const int nA = gxA * gyA;
+  if ((int)blockIdx.x < nA) {
+    const int b = blockIdx.x;
+    mfma_gemm_body<BMA, BMA, 2, true, false>(aA, bA, eA, MA, NA, KA, kpsA, nullptr, b % gxA, gxA, b / gxA, gyA);
+  } else {
+    const int b = blockIdx.x - nA;
+    mfma_gemm_body<BMB, BMB, 2, false, false>(aB, bB, eB, MB, NB, KB, kpsB, rowsumB, b % gxB, gxB, b / gxB, gyB);
+  }
+}
+
+static int bm_of(int cfg) { return cfg == 0 ? 128 : (cfg == 1 ? 64 : 32); }
+
+// dy [M,N] (masked by act'(y) when ay), W [N,K], x [M,K]: dx [M,K] (masked by act'(yprev), colsum ->
+// previous layer's bias grad), dw [N,K] += , dbias [N] += .  -2: shape better served by two launches.
+extern "C" int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* x, void* dx, const void* yprev,
+                                     int act_prev, float* colsum, const void* ay, int aact, float* dw, float* dbias,
+                                     int M, int N, int K, hipStream_t st) {
+  if (hopsx_disabled("bwd_pair") || M <= 0 || N <= 0 || K <= 0) return -2;
+  // dgrad: [M x K] = dy[M x N] . W[N x K]
+  if (want_splitk(M, K, N)) return -2;  // the small-M split-K dgrad path keeps its own launch
+  GemmPlan pa = plan_gemm(M, K, N, false);
+  GemmPlan pb = plan_gemm(N, K, M, true);
+  const int bma = bm_of(pa.cfg), bmb = bm_of(pb.cfg);
+  const int gxA = ((M + bma - 1) / bma) * ((K + bma - 1) / bma), gyA = pa.split;
+  const int gxB = ((N + bmb - 1) / bmb) * ((K + bmb - 1) / bmb), gyB = pb.split;
+  const long total = (long)gxA * gyA + (long)gxB * gyB;
+  if (total > (1L << 20)) return -2;
+  DenseLoader aA{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
+  DenseLoader bA{(const bf16_raw*)w, K, is_vec_ok(w, K)};
+  EpiDActBF16 eA{(bf16_raw*)dx, K, (const bf16_raw*)yprev, K, act_prev, colsum};
+  DenseLoader aB{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
+  DenseLoader bB{(const bf16_raw*)x, K, is_vec_ok(x, K)};
+  EpiAtomicF32 eB{dw, K, 1.f, nullptr};
+#define HOPSX_LP(A_, B_)                                                                                          \
+  if (bma == A_ && bmb == B_) {                                                                                   \
+    hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_>), dim3((unsigned)total), dim3(256), 0, st, aA, bA, eA, M, K, N,  \
+                       pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);                            \
+    return (int)hipGetLastError();                                                                               \
+  }
+  HOPSX_LP(32, 32) HOPSX_LP(32, 64) HOPSX_LP(32, 128) HOPSX_LP(64, 32) HOPSX_LP(64, 64) HOPSX_LP(64, 128)
+  HOPSX_LP(128, 32) HOPSX_LP(128, 64) HOPSX_LP(128, 128)
+#undef HOPSX_LP
+  return -2;
+}

@@ -315,9 +315,11 @@ struct EpiDActBF16 {
 // ----------------------------------------------------------------------------
 // Main loop
 // ----------------------------------------------------------------------------
+// Body with explicit block coordinates (bx of gx tiles, by of gy K-splits) so several GEMMs can
+// share one launch (mfma_gemm_pair_k); mfma_gemm_kernel passes the builtins.
 template <int BM, int BN, int WAVES_M, bool A_KC, bool B_KC, class AL, class BL, class EP>
-__global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl, const EP ep, int M, int N,
-                                                       int K, int kps, float* rowsum_a) {
+__device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const EP& ep, int M, int N, int K, int kps,
+                                               float* rowsum_a, int bx, int gx, int by, int gy) {
   // rowsum_a (RC-A only): rowsum_a[m] += sum_k A[m][k] of the staged (masked) A
   // operand — in wgrad dW = dY^T X that is the bias gradient sum_b dY[b][m],
   // accumulated while the tiles pass through registers, by the tn == 0 blocks.
@@ -338,10 +340,10 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
 
   const int ntn = (N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_remap(bx, gx);
   const int tm = bid / ntn, tn = bid - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * kps;
+  const int kbeg = by * kps;
   const int kend = min(K, kbeg + kps);
   if (kbeg >= kend) return;
   const int nt = (kend - kbeg + BK - 1) / BK;
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned t = __hip_atomic_fetch_add(ep.fin.cnt + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = (t == gridDim.y - 1) ? 1 : 0;
+      flag[0] = (t == (unsigned)gy - 1) ? 1 : 0;
     }
     __syncthreads();
     if (flag[0] == 0) return;
@@ -591,6 +593,13 @@ __global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl
 // ----------------------------------------------------------------------------
 // Host-side config selection + launch
 // ----------------------------------------------------------------------------
+template <int BM, int BN, int WAVES_M, bool A_KC, bool B_KC, class AL, class BL, class EP>
+__global__ __launch_bounds__(256) void mfma_gemm_kernel(const AL al, const BL bl, const EP ep, int M, int N,
+                                                       int K, int kps, float* rowsum_a) {
+  mfma_gemm_body<BM, BN, WAVES_M, A_KC, B_KC, AL, BL, EP>(al, bl, ep, M, N, K, kps, rowsum_a, blockIdx.x, gridDim.x,
+                                                          blockIdx.y, gridDim.y);
+}
+
 struct GemmPlan {
   int cfg;    // 0: 128x128, 1: 64x64, 2: 32x32
   int split;  // split-K factor (only honoured for atomic epilogues)

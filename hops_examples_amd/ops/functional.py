@@ -152,7 +152,14 @@ class _LinearFn(torch.autograd.Function):
         ymask = y if (act and y.dtype == BF16) else None
         dx = None
         gw = _wgrad_buf(w)
-        with _on_side(dy2.device, dy2, x2, ymask, flop=2.0 * dy2.numel() * x2.shape[1]):  # wgrad || dgrad
+        wflop = 2.0 * dy2.numel() * x2.shape[1]
+        if ctx.needs_input_grad[0] and wflop < _PAR_MIN_FLOP and "bwd_pair" not in _disabled():
+            # small layer: dgrad and wgrad (+ bias grad) as ONE launch (horizontal fusion)
+            r = K.linear_bwd_pair(dy2, _arena.weight_bf16(w), x2, gw, y=ymask, act=act, dbias=gb)
+            if r is not False:
+                return (r.view(ctx.xshape), _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None,
+                        None)
+        with _on_side(dy2.device, dy2, x2, ymask, flop=wflop):  # wgrad || dgrad
             K.linear_wgrad(dy2, x2, gw, y=ymask, act=act, dbias=gb)
         if ctx.needs_input_grad[0]:
             dx = K.linear_dgrad(dy2, _arena.weight_bf16(w), y=ymask, act=act).view(ctx.xshape)

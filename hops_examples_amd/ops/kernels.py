@@ -105,6 +105,24 @@ def linear_wgrad(dy, x, dw, alpha=1.0, y=None, act=0, dbias=None):
     return dw
 
 
+def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None):
+    """dX and dW (+ dbias) of a Linear layer in ONE launch (gemm.hip linear_bwd_pair_k); returns
+    dX [M, K] bf16, or False when the shape goes to the separate launches (small-M split-K dgrad)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    _req(dy, BF16, "dy")
+    _req(x, BF16, "x")
+    _req(w, BF16, "w")
+    _req(dw, F32, "dw")
+    dx = torch.empty(M, K, device=dy.device, dtype=BF16)
+    rc = _C.ext().linear_bwd_pair(ptr(dy), ptr(w), ptr(x), ptr(dx), 0, 0, 0, ptr(y), act_id(act), ptr(dw),
+                                  ptr(dbias), M, N, K, stream())
+    if rc == -2:
+        return False
+    check(rc, "linear_bwd_pair")
+    return dx
+
+
 def colsum(x, out):
     """out[N] += sum_m x[M,N]."""
     _req(x, BF16, "x")
