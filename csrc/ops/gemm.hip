@@ -130,8 +130,8 @@ extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long
 // workgroups compute dX = (dY*act'(y)) . W (masked by the previous layer's act'), the rest
 // dW += (dY*act'(y))^T . X with the bias gradient as the staged operand's row sums.  At small
 // batch each GEMM alone is a latency-bound launch on a few hundred workgroups.
-template <int BMA, int BMB>
-__global__ __launch_bounds__(256) void linear_bwd_pair_k(DenseLoader aA, DenseLoader bA, EpiDActBF16 eA, int MA,
+template <int BMA, int BMB, class EPA>
+__global__ __launch_bounds__(256) void linear_bwd_pair_k(DenseLoader aA, DenseLoader bA, EPA eA, int MA,
                                                          int NA, int KA, int kpsA, int gxA, int gyA, DenseLoader aB,
                                                          DenseLoader bB, EpiAtomicF32 eB, int MB, int NB, int KB,
                                                          int kpsB, int gxB, int gyB, float* rowsumB) {
@@ -151,7 +151,9 @@ static int bm_of(int cfg) { return cfg == 0 ? 128 : (cfg == 1 ? 64 : 32); }
 // previous layer's bias grad), dw [N,K] += , dbias [N] += .  -2: shape better served by two launches.
 extern "C" int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* x, void* dx, const void* yprev,
                                      int act_prev, float* colsum, const void* ay, int aact, float* dw, float* dbias,
-                                     int M, int N, int K, hipStream_t st) {
+                                     int M, int N, int K, const int* pool, const unsigned char* pool_am,
+                                     const void* pool_x, const unsigned long long* pool_rng, unsigned pool_salt,
+                                     float pool_p, hipStream_t st) {
   if (hopsx_disabled("bwd_pair") || M <= 0 || N <= 0 || K <= 0) return -2;
   // dgrad: [M x K] = dy[M x N] . W[N x K]
   if (want_splitk(M, K, N)) return -2;  // the small-M split-K dgrad path keeps its own launch
@@ -165,13 +167,22 @@ extern "C" int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* 
   DenseLoader aA{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
   DenseLoader bA{(const bf16_raw*)w, K, is_vec_ok(w, K)};
   EpiDActBF16 eA{(bf16_raw*)dx, K, (const bf16_raw*)yprev, K, act_prev, colsum};
+  // pool = {C, PH, PW, KH, KW, act}: dx is the pool INPUT gradient (see EpiPoolScatterBF16)
+  EpiPoolScatterBF16 eP{(bf16_raw*)dx, pool_am, (const bf16_raw*)pool_x, pool ? pool[5] : 0, pool_rng, pool_salt,
+                        pool_p, K, pool ? pool[0] : 1, pool ? pool[2] : 1, pool ? pool[3] : 1, pool ? pool[4] : 1,
+                        pool ? pool[1] * pool[3] : 1, pool ? pool[2] * pool[4] : 1, nullptr};
+  if (pool && pool[0] * pool[1] * pool[2] != K) return -2;
   DenseLoader aB{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
   DenseLoader bB{(const bf16_raw*)x, K, is_vec_ok(x, K)};
   EpiAtomicF32 eB{dw, K, 1.f, nullptr};
 #define HOPSX_LP(A_, B_)                                                                                          \
   if (bma == A_ && bmb == B_) {                                                                                   \
-    hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_>), dim3((unsigned)total), dim3(256), 0, st, aA, bA, eA, M, K, N,  \
-                       pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);                            \
+    if (pool)                                                                                                     \
+      hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_, EpiPoolScatterBF16>), dim3((unsigned)total), dim3(256), 0, st, \
+                         aA, bA, eP, M, K, N, pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);      \
+    else                                                                                                          \
+      hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_, EpiDActBF16>), dim3((unsigned)total), dim3(256), 0, st, aA, bA, \
+                         eA, M, K, N, pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);             \
     return (int)hipGetLastError();                                                                               \
   }
   HOPSX_LP(32, 32) HOPSX_LP(32, 64) HOPSX_LP(32, 128) HOPSX_LP(64, 32) HOPSX_LP(64, 64) HOPSX_LP(64, 128)

@@ -296,6 +296,10 @@ template <class EP, class = void>
 struct has_ticket { static constexpr bool value = false; };
 template <class EP>
 struct has_ticket<EP, decltype((void)EP::kTicket)> { static constexpr bool value = EP::kTicket; };
+template <class EP, class = void>
+struct has_pre { static constexpr bool value = false; };
+template <class EP>
+struct has_pre<EP, decltype((void)EP::kPre)> { static constexpr bool value = EP::kPre; };
 
 // out = acc * act'(y[m,n])  (backprop through the activation whose OUTPUT is y)
 struct EpiDActBF16 {
@@ -308,6 +312,46 @@ struct EpiDActBF16 {
   __device__ __forceinline__ float operator()(int m, int n, float v) const {
     if (y) v *= act_grad_from_out(bf2f(y[(long)m * ldy + n]), act);
     out[(long)m * ldo + n] = f2bf(v);
+    return v;
+  }
+};
+
+// Linear dgrad whose input came from a non-overlapping max-pool (exact windows): the epilogue IS
+// the pool backward — each pooled-gradient element (row m, column n = (ph, pw, c)) is routed to
+// its argmax position of the pool input (dropout mask regenerated, ReLU' of the pool input
+// applied), the rest of the window gets zeros.  Removes the pool-backward launch and the dX
+// round trip between them.
+struct EpiPoolScatterBF16 {
+  static constexpr bool kPre = true;  // two-phase: all gathers issued before any dX store
+  bf16_raw* dx;                 // pool-input gradient [B][H][W][C]
+  const unsigned char* am;      // argmax bytes [B][PH][PW][C]
+  const bf16_raw* y;            // pooled output = this Linear's input [B][N] (ReLU' mask), or null
+  int act;
+  const unsigned long long* rng;
+  unsigned salt;
+  float p;                      // dropout probability of the pool (0: none)
+  int N, C, PW, KH, KW, H, W;
+  float* colsum;                // unused (kept for the epilogue interface)
+  // phase 1: argmax byte | ReLU'(pooled value) << 8.  The pooled value is positive iff the window
+  // max is (dropout only scales or zeroes it, and a zeroed element has no gradient anyway).
+  __device__ __forceinline__ unsigned pre(int m, int n) const {
+    const long o = (long)m * N + n;
+    unsigned keep = 1u;
+    if (y && act != ACT_NONE) {
+      const unsigned short r = y[o];
+      keep = (r & 0x8000u) == 0 && (r & 0x7fffu) != 0;
+    }
+    return (unsigned)am[o] | (keep << 8);
+  }
+  __device__ __forceinline__ float apply(int m, int n, float v, unsigned aux) const {
+    const long o = (long)m * N + n;
+    const int c = n % C, t = n / C;
+    const int pw = t % PW, ph = t / PW;
+    if (p > 0.f) v = uniform01(drop_key(rng, salt), (uint64_t)o) >= p ? v * (1.f / (1.f - p)) : 0.f;
+    const int a = aux & 0xff;
+    const float g = (aux >> 8) ? v : 0.f;
+    bf16_raw* base = dx + (((long)m * H + ph * KH) * W + pw * KW) * C + c;
+    for (int q = 0; q < KH * KW; ++q) base[((long)(q / KW) * W + q % KW) * C] = f2bf(q == a ? g : 0.f);
     return v;
   }
 };
@@ -511,15 +555,43 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
   float cs[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) cs[j] = 0.f;
+  if constexpr (has_pre<EP>::value) {
+    // gather-then-scatter epilogues: issue every gather first (the scatter stores may alias them
+    // as far as the compiler knows, which would serialise one load latency per element)
+    unsigned aux[FM][FN][4];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * WTN + j * 16 + fr;
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + fr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        if (m < M && n < N) cs[j] += ep(m, n, acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+          aux[i][j][r] = (m < M && n < N) ? ep.pre(m, n) : 0u;
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+          if (m < M && n < N) cs[j] += ep.apply(m, n, acc[i][j][r], aux[i][j][r]);
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+          if (m < M && n < N) cs[j] += ep(m, n, acc[i][j][r]);
+        }
       }
     }
   }

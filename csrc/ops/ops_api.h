@@ -15,9 +15,12 @@ int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b
                hipStream_t st);
 // xscale != 0: x is uint8 and is read as x * xscale + xshift (input-layer normalisation fused; direct kernel only)
 // a Linear layer's dgrad + wgrad (+ bias grad) in one launch; -2: unsupported shape (gemm.hip)
+// pool (optional) = {C, PH, PW, KH, KW, act}: x came from a non-overlapping max-pool and dx is the
+// POOL INPUT gradient, scattered by the dgrad epilogue (pool_am argmax, pool_x for ReL', dropout p)
 int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* x, void* dx, const void* yprev, int act_prev,
                           float* colsum, const void* ay, int aact, float* dw, float* dbias, int M, int N, int K,
-                          hipStream_t st);
+                          const int* pool, const unsigned char* pool_am, const void* pool_x,
+                          const unsigned long long* pool_rng, unsigned pool_salt, float pool_p, hipStream_t st);
 int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out, const float* bias, int act,
                      float* colsum, float xscale, float xshift, hipStream_t st);
 // y/yact: this conv's activation output -> fused act' mask on dY (prologue fusion)

@@ -9,6 +9,8 @@
 //     workgroup), so a captured step needs no extra bookkeeping launches.
 // Streams are moved as float4 (16 B/lane); the grid is capped at 2 workgroups
 // per CU so the single arrival counter sees only ~512 atomics.
+#include <cstdlib>
+
 #include "common.h"
 #include "ops_api.h"
 
@@ -207,7 +209,8 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
   const bool aligned = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)s3) % 16 == 0 &&
                        ((uintptr_t)shadow_bf16 % 8 == 0);
   long g = ((aligned ? n / 4 : n) + 255) / 256;
-  if (g > 512) g = 512;
+  static const int gcap = getenv("HOPSX_OPT_GRID") ? atoi(getenv("HOPSX_OPT_GRID")) : 512;
+  if (g > gcap) g = gcap;
   if (g < 1) g = 1;
   bf16_raw* sh = (bf16_raw*)shadow_bf16;
   // without an arrival counter the bookkeeping needs its own tiny launch

@@ -130,7 +130,8 @@ def to_compute(x: torch.Tensor) -> torch.Tensor:
 # ===================================================================== Linear
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, out_f32):
+    def forward(ctx, x, w, b, act, out_f32, pool=None):
+        ctx.pool = pool
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         wb = _arena.weight_bf16(w)
         y = K.linear_fwd(x2, wb, b, act=act, out_f32=out_f32)
@@ -154,16 +155,25 @@ class _LinearFn(torch.autograd.Function):
         gw = _wgrad_buf(w)
         wflop = 2.0 * dy2.numel() * x2.shape[1]
         if ctx.needs_input_grad[0] and wflop < _PAR_MIN_FLOP and "bwd_pair" not in _disabled():
-            # small layer: dgrad and wgrad (+ bias grad) as ONE launch (horizontal fusion)
-            r = K.linear_bwd_pair(dy2, _arena.weight_bf16(w), x2, gw, y=ymask, act=act, dbias=gb)
+            # small layer: dgrad and wgrad (+ bias grad) as ONE launch (horizontal fusion); when the
+            # input is a flattened max-pool output, the dgrad epilogue also does the pool backward
+            pool = ctx.pool if "pool_scatter" not in _disabled() else None
+            r = K.linear_bwd_pair(dy2, _arena.weight_bf16(w), x2, gw, y=ymask, act=act, dbias=gb, pool=pool)
             if r is not False:
-                return (r.view(ctx.xshape), _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None,
-                        None)
+                if pool is not None:
+                    # r is the pool-INPUT gradient: hand autograd an unfilled placeholder for this
+                    # layer's input and let the pool backward return r (registry keyed by address)
+                    ph = torch.empty(ctx.xshape, device=dy2.device, dtype=BF16)
+                    _PRESCATTERED[ph.data_ptr()] = (weakref.ref(ph), r, bool(pool[1]))
+                    dxr = ph
+                else:
+                    dxr = r.view(ctx.xshape)
+                return (dxr, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None)
         with _on_side(dy2.device, dy2, x2, ymask, flop=wflop):  # wgrad || dgrad
             K.linear_wgrad(dy2, x2, gw, y=ymask, act=act, dbias=gb)
         if ctx.needs_input_grad[0]:
             dx = K.linear_dgrad(dy2, _arena.weight_bf16(w), y=ymask, act=act).view(ctx.xshape)
-        return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None
+        return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None
 
 
 def linear(x, w, b=None, act=None, out_f32=False):
@@ -172,7 +182,9 @@ def linear(x, w, b=None, act=None, out_f32=False):
         return _cpu_act(F.linear(x.float(), w, b), act)
     a = ACT[act] if not isinstance(act, int) else act
     xc = to_compute(x)
-    y = _LinearFn.apply(xc, w, b, a, out_f32)
+    src = x if hasattr(x, "_hx_pool") else getattr(x, "_base", None)
+    pool = getattr(src, "_hx_pool", None) if src is not None and src.numel() == x.numel() else None
+    y = _LinearFn.apply(xc, w, b, a, out_f32, pool)
     if (not a and x.dim() == 2 and w.shape[0] <= 32 and y.requires_grad and xc.dtype == BF16
             and _arena.grad_target(w) is not None and (b is None or _arena.grad_target(b) is not None)):
         y._hx_dense_head = (xc, w, b)  # logits layer: loss_and_grad can fuse its backward (head_ce)
@@ -372,6 +384,7 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
 # of (applied by the max-pool backward at its argmax scatter): the producing conv's backward
 # then skips its own mask and never loads its activation output (half the dY traffic of its
 # dgrad/wgrad).  Written and consumed within one backward pass (also during graph capture).
+_PRESCATTERED: dict = {}  # placeholder data_ptr -> (weakref, pool-input gradient, premasked)
 _PREMASKED: dict = {}  # data_ptr -> weakref of the pool's dX (a dead ref means the memory may be reused)
 
 
@@ -386,11 +399,22 @@ class _MaxPoolFn(torch.autograd.Function):
         else:
             ctx.save_for_backward(am)
         ctx.cfg = (x.shape, k, s, p, drop_p, rng, salt, premask)
+        B, H, W, C = x.shape
+        if x.is_cuda and s == k and p == (0, 0) and H % k[0] == 0 and W % k[1] == 0 and k[0] * k[1] <= 255:
+            # a Linear consuming the (flattened) output can do this backward in its dgrad epilogue
+            y._hx_pool = (am, bool(premask), tuple(x.shape), k, "relu" if premask else 0,
+                          rng, salt, drop_p)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         shape, k, s, p, drop_p, rng, salt, premask = ctx.cfg
+        ent = _PRESCATTERED.pop(dy.data_ptr(), None)
+        if ent is not None and ent[0]() is not None and tuple(ent[1].shape) == tuple(shape):
+            dx = ent[1]  # already produced by the consuming Linear's dgrad epilogue
+            if ent[2]:
+                _PREMASKED[dx.data_ptr()] = weakref.ref(dx)
+            return dx, None, None, None, None, None, None
         dy = dy.to(BF16).contiguous()
         if premask:
             am, x = ctx.saved_tensors

@@ -105,18 +105,30 @@ def linear_wgrad(dy, x, dw, alpha=1.0, y=None, act=0, dbias=None):
     return dw
 
 
-def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None):
+def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None, pool=None):
     """dX and dW (+ dbias) of a Linear layer in ONE launch (gemm.hip linear_bwd_pair_k); returns
-    dX [M, K] bf16, or False when the shape goes to the separate launches (small-M split-K dgrad)."""
+    dX [M, K] bf16, or False when the shape goes to the separate launches (small-M split-K dgrad).
+    ``pool`` = (am, premask, in_shape, (KH, KW), act, rng, salt, p): the Linear's input is the
+    flattened output of a non-overlapping max-pool; the returned tensor is then the gradient of the
+    POOL INPUT (shape in_shape), scattered by the dgrad epilogue (the pool backward fused away).
+    ``premask``: also apply ReLU' of the pool input (read off the pooled value = this layer's input)."""
     M, N = dy.shape
     K = x.shape[1]
     _req(dy, BF16, "dy")
     _req(x, BF16, "x")
     _req(w, BF16, "w")
     _req(dw, F32, "dw")
-    dx = torch.empty(M, K, device=dy.device, dtype=BF16)
+    pl, pam, px, prng, psalt, pp = [], 0, 0, 0, 0, 0.0
+    if pool is not None:
+        am, xin, in_shape, (kh, kw), pact, rng, salt, p = pool
+        B, H, W, C = in_shape
+        pl = [C, H // kh, W // kw, kh, kw, act_id(pact) if xin else 0]
+        pam, px, prng, psalt, pp = ptr(am), (ptr(x) if xin else 0), ptr(rng), int(salt) & 0xFFFFFFFF, float(p)
+        dx = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+    else:
+        dx = torch.empty(M, K, device=dy.device, dtype=BF16)
     rc = _C.ext().linear_bwd_pair(ptr(dy), ptr(w), ptr(x), ptr(dx), 0, 0, 0, ptr(y), act_id(act), ptr(dw),
-                                  ptr(dbias), M, N, K, stream())
+                                  ptr(dbias), M, N, K, pl, pam, px, prng, psalt, pp, stream())
     if rc == -2:
         return False
     check(rc, "linear_bwd_pair")

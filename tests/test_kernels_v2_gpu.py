@@ -389,3 +389,38 @@ def test_paired_conv_backward_matches_separate_launches(monkeypatch, model):
         torch.cuda.synchronize()
         grads.append(m._hx_arena.grad.float().clone())
     torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
+
+
+@pytest.mark.parametrize("model", ["mirrored", "torch"])
+def test_pool_backward_fused_into_linear_dgrad(monkeypatch, model):
+    """Max-pool (+dropout, +ReLU' premask) -> flatten -> Linear: the pool backward done by the
+    Linear's dgrad epilogue (EpiPoolScatterBF16) equals the separate pool-backward launch."""
+    from hops_examples_amd.models import mnist
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    grads = []
+    for disable in ("", "pool_scatter"):
+        monkeypatch.setenv("HOPSX_DISABLE", disable)
+        calls = []
+        real = K.maxpool2d_bwd
+        monkeypatch.setattr(K, "maxpool2d_bwd", lambda *a, **kw: calls.append(1) or real(*a, **kw))
+        HF.seed_device_rng(5, dev)
+        torch.manual_seed(0)
+        m = (mnist.MirroredMnistCNN() if model == "mirrored" else mnist.TorchMnistNet()).to(dev)
+        for mod in m.modules():
+            if hasattr(mod, "salt"):
+                mod.salt = 7919
+        ParamArena.from_module(m, dev)
+        x = torch.randint(0, 256, (32, 28, 28, 1), dtype=torch.uint8, device=dev)
+        t = torch.randint(0, 10, (32,), device=dev)
+        out = m(x)
+        _, _, _, root, g = HF.loss_and_grad_root(out, t, "sparse_ce")
+        root.backward(g)
+        torch.cuda.synchronize()
+        grads.append(m._hx_arena.grad.float().clone())
+        if disable == "" and model == "mirrored":
+            assert not calls, "pool backward should have been fused into the Linear dgrad"
+        monkeypatch.setattr(K, "maxpool2d_bwd", real)
+    assert not HF._PRESCATTERED
+    torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
