@@ -39,6 +39,12 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
                               P<void>(y), yact, S(st));
   });
+  m.def("conv2d_fwd_pool_ok", [](std::vector<int> g, int act) { return hopsx_conv_fwd_pool_ok(g.data(), act); });
+  m.def("conv2d_fwd_pool", [](u x, u w, std::vector<int> g, u out, u am, u bias, int act, float p, u rng,
+                              unsigned salt, u st) {
+    return hopsx_conv2d_fwd_pool(P<void>(x), P<void>(w), g.data(), P<void>(out), P<void>(am), P<float>(bias), act, p,
+                                 P<unsigned long long>(rng), salt, S(st));
+  });
   m.def("conv2d_dgrad_fused_wgrad_ok", [](std::vector<int> g, std::vector<int> g0) {
     return hopsx_conv_dgrad_fused_wgrad_ok(g.data(), g0.data());
   });

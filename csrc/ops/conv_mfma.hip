@@ -43,10 +43,24 @@ __device__ __forceinline__ int cm_swz(int r, int c, int cpr) {
 }
 
 // ---------------------------------------------------------------------------- forward
-template <int NF, int KS>
+// POOL: a 2x2/stride-2 max-pool (+ dropout) fused into the epilogue.  The 16 A rows of a pixel
+// group are then 4 pooled outputs x their 4 window taps (row = 4*pooled + tap), so in the C
+// fragment each lane's 4 accumulator registers ARE one pooling window of one channel: max /
+// argmax in registers, only the pooled tensor (a quarter of the conv output) and the 1-byte
+// argmax are written.  With a ReLU the argmax of an all-zero window is stored as 0xFF, so every
+// pool backward (which routes the gradient to the tap equal to the argmax) applies ReLU' for
+// free and the full conv output is never needed again.
+struct PoolEpi {
+  unsigned char* am;
+  const unsigned long long* rng;
+  unsigned salt;
+  float p;
+};
+
+template <int NF, int KS, bool POOL = false>
 __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
                                                       const float* __restrict__ bias, bf16_raw* __restrict__ y,
-                                                      ConvGeom g, int act, int K) {
+                                                      ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{}) {
   constexpr int CO = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
   constexpr int cpr = KS * 4;  // 16-B chunks per weight row (K padded to 32*KS)
@@ -62,12 +76,14 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int M = g.B * g.OH * g.OW;
+  const int PH = g.OH >> 1, PW = g.OW >> 1;
+  const int M = POOL ? g.B * PH * PW * 4 : g.B * g.OH * g.OW;  // A rows (pooled: 4 taps per output)
   const int ngroups = (M + 15) / 16;
   bf16_raw* sc = scratch + wave * 16 * CO;
   float bv[NF];
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) bv[nf] = bias ? bias[nf * 16 + fr] : 0.f;
+  const uint64_t dkey = POOL && pe.p > 0.f ? drop_key(pe.rng, pe.salt) : 0;
   for (int g0 = (blockIdx.x * CM_WAVES + wave) * CM_UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * CM_UN) {
     bf16x8 a[CM_UN][KS];
 #pragma unroll
@@ -75,8 +91,19 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
       const int px = (g0 + u) * 16 + fr;
       const bool pok = (g0 + u) < ngroups && px < M;
       const int pp = pok ? px : 0;
-      const int b = g.fOHW.div(pp), rem = pp - b * (g.OH * g.OW);
-      const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
+      int b, oh, ow;
+      if constexpr (POOL) {
+        const int po = pp >> 2, tap = pp & 3;  // pooled output index, window tap
+        const int pr = po / PW, pw_ = po - pr * PW;
+        b = pr / PH;
+        oh = 2 * (pr - b * PH) + (tap >> 1);
+        ow = 2 * pw_ + (tap & 1);
+      } else {
+        b = g.fOHW.div(pp);
+        const int rem = pp - b * (g.OH * g.OW);
+        oh = g.fOW.div(rem);
+        ow = rem - oh * g.OW;
+      }
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
         const int k0 = kk * 32 + 8 * fq;
@@ -103,6 +130,42 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
           const bf16x8 bfr = *(const bf16x8*)(sw + co * RS * 8 + 8 * cm_swz(co, kk * 4 + fq, cpr));
           acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][kk], bfr, acc[nf], 0, 0, 0);
         }
+      }
+      if constexpr (POOL) {
+        // lane (fr, fq): channel nf*16+fr of pooled output 4*(g0+u)+fq; acc[nf][0..3] = its window
+        const int po = (g0 + u) * 4 + fq;
+        unsigned char* sa = (unsigned char*)(sc + 4 * CO);  // [4][CO] argmax bytes after [4][CO] bf16
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          float best = -INFINITY;
+          int bi = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // round to bf16 first: ties and the stored max follow the unfused conv -> pool chain
+            const float v = bf2f(f2bf(apply_act(acc[nf][r] + bv[nf], act)));
+            if (v > best) { best = v; bi = r; }
+          }
+          if (act == ACT_RELU && !(best > 0.f)) bi = 0xFF;  // ReLU'(window) == 0: no gradient
+          const int co = nf * 16 + fr;
+          if (pe.p > 0.f)
+            best = uniform01(dkey, (uint64_t)((long)po * CO + co)) >= pe.p ? best * (1.f / (1.f - pe.p)) : 0.f;
+          sc[fq * CO + co] = f2bf(best);
+          sa[fq * CO + co] = (unsigned char)bi;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int nout = g.B * PH * PW;
+        const int pbase = (g0 + u) * 4;
+        for (int c = lane; c < 4 * CO / 8; c += 64) {  // 4 pooled rows x CO, 16-B vectors
+          const int row = c / (CO / 8), col = (c - row * (CO / 8)) * 8;
+          if (pbase + row < nout) *(bf16x8*)(y + (long)(pbase + row) * CO + col) = *(const bf16x8*)(sc + row * CO + col);
+        }
+        for (int c = lane; c < 4 * CO / 8; c += 64) {  // argmax bytes, 8-B vectors
+          const int row = c / (CO / 8), col = (c - row * (CO / 8)) * 8;
+          if (pbase + row < nout) *(uint2*)(pe.am + (long)(pbase + row) * CO + col) = *(const uint2*)(sa + row * CO + col);
+        }
+        __builtin_amdgcn_wave_barrier();
+        continue;
       }
       // epilogue through the wave's LDS scratch: C map col = lane&15 (co), row = (lane>>4)*4 + r (pixel)
 #pragma unroll
@@ -599,6 +662,13 @@ bool hopsx_conv_fwd_mfma_ok(const int* geom) {
          !hopsx_disabled("conv_mfma");
 }
 
+// conv (act none / relu) -> 2x2 stride-2 max-pool (+ dropout p) in one launch (POOL epilogue):
+// needs the plain MFMA forward and an even output size
+bool hopsx_conv_fwd_pool_ok(const int* geom, int act) {
+  return hopsx_conv_fwd_mfma_ok(geom) && geom[4] % 2 == 0 && geom[5] % 2 == 0 && (act == ACT_NONE || act == ACT_RELU) &&
+         !hopsx_disabled("conv_pool");
+}
+
 // stride 1 only; K = KH*KW*CO <= 512, CO % 8 == 0, C in {16, 32, 64, 128}
 bool hopsx_conv_dgrad_mfma_ok(const int* geom) {
   const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * CO;
@@ -828,4 +898,42 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
 #undef HOPSX_PAIR_K0
 #undef HOPSX_PAIR
   return -2;
+}
+
+extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* out, void* am,
+                                     const float* bias, int act, float p, const unsigned long long* rng, unsigned salt,
+                                     hipStream_t st) {
+  if (!hopsx_conv_fwd_pool_ok(geom, act)) return -2;
+  ConvGeom g;
+  g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
+  g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
+  g.dh = geom[13]; g.dw = geom[14];
+  g.init_div();
+  const int K = g.KH * g.KW * g.C;
+  const int KS = cm_ks((K + 31) / 32);
+  const long rows = (long)g.B * (g.OH / 2) * (g.OW / 2) * 4;
+  const int grid = cm_grid((rows + 15) / 16);
+  const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw);
+  const PoolEpi pe{(unsigned char*)am, rng, salt, p};
+#define HOPSX_CMP(NF, KSV)                                                                                     \
+  hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,       \
+                     (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe)
+#define HOPSX_CMP_NF(NF)              \
+  switch (KS) {                       \
+    case 2: HOPSX_CMP(NF, 2); break;  \
+    case 4: HOPSX_CMP(NF, 4); break;  \
+    case 8: HOPSX_CMP(NF, 8); break;  \
+    case 9: HOPSX_CMP(NF, 9); break;  \
+    default: HOPSX_CMP(NF, 16); break; \
+  }
+  switch (g.CO / 16) {
+    case 1: HOPSX_CMP_NF(1); break;
+    case 2: HOPSX_CMP_NF(2); break;
+    case 4: HOPSX_CMP_NF(4); break;
+    case 8: HOPSX_CMP_NF(8); break;
+    default: return -2;
+  }
+#undef HOPSX_CMP_NF
+#undef HOPSX_CMP
+  return (int)hipGetLastError();
 }

@@ -697,7 +697,11 @@ inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu =
     const long target = 2L * num_cu;
     if (tiles < target) {
       long s = (target + tiles - 1) / tiles;
-      const long maxs = (K + 4 * GEMM_BK - 1) / (4 * GEMM_BK);  // >= 4 k-tiles per split
+      static const int minkt = [] {
+        const char* e = std::getenv("HOPSX_SPLIT_MINKT");
+        return e ? std::atoi(e) : 4;
+      }();
+      const long maxs = (K + minkt * GEMM_BK - 1) / (minkt * GEMM_BK);  // >= minkt k-tiles per split
       if (s > maxs) s = maxs;
       if (s < 1) s = 1;
       p.split = (int)s;

@@ -93,6 +93,9 @@ int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamm
 
 // ---- direct MFMA convs for short reductions (conv_mfma.hip) ----
 bool hopsx_conv_fwd_mfma_ok(const int* geom);
+bool hopsx_conv_fwd_pool_ok(const int* geom, int act);
+int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* out, void* am, const float* bias, int act,
+                          float p, const unsigned long long* rng, unsigned salt, hipStream_t st);
 bool hopsx_conv_dgrad_mfma_ok(const int* geom);
 int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* out, const float* bias, int act,
                           hipStream_t st);

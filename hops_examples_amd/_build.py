@@ -15,6 +15,7 @@ Usage: ``python -m hops_examples_amd._build [--force] [-j N]``
 from __future__ import annotations
 
 import argparse
+import hashlib
 import concurrent.futures as cf
 import os
 import subprocess
@@ -41,6 +42,33 @@ def _newer(target: Path, deps: list[Path]) -> bool:
         return True
     t = target.stat().st_mtime
     return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def _digest(cmd: list[str], deps: list[Path]) -> str:
+    """Content hash of the compile command and every input: an object is reused only when it was
+    built from exactly these bytes (mtimes alone miss a source edited while a build was running)."""
+    h = hashlib.sha1(" ".join(cmd).encode())
+    for d in deps:
+        if d.exists():
+            h.update(d.name.encode())
+            h.update(d.read_bytes())
+    return h.hexdigest()
+
+
+def _stale(o: Path, cmd: list[str], deps: list[Path]) -> tuple[bool, str]:
+    dg = _digest(cmd, deps)
+    stamp = o.with_suffix(o.suffix + ".sha1")
+    return (not o.exists() or not stamp.exists() or stamp.read_text().strip() != dg), dg
+
+
+def _check_undefined(lib: Path) -> None:
+    """A symbol of our own left undefined in the extension would only fail when first called (lazy
+    binding aborts the process): refuse such a link."""
+    r = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], stdout=subprocess.PIPE, text=True)
+    bad = [ln.split()[-1] for ln in r.stdout.splitlines() if ln.split() and ln.split()[-1].startswith("hopsx_")]
+    if bad:
+        lib.unlink()
+        raise RuntimeError(f"{lib.name}: undefined hopsx symbols {bad}")
 
 
 def _run(cmd: list[str]) -> None:
@@ -70,20 +98,28 @@ def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra
     jobs_list = []
     for s in srcs:
         o = objdir / (s.name + ".o")
-        if force or _newer(o, [s, *headers]):
-            if kind == "hip" or s.suffix == ".hip":
-                cmd = [HIPCC, *HIP_FLAGS, *_py_includes(), f"-I{srcdir}", "-c", str(s), "-o", str(o)]
-                if s.suffix == ".cpp":
-                    cmd.insert(1, "-x")
-                    cmd.insert(2, "hip")
-            else:
-                cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-march=x86-64-v2", "-msse4.2", "-pthread",
-                       *_py_includes(), f"-I{srcdir}", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
-                       "-c", str(s), "-o", str(o)]
-            jobs_list.append(cmd)
+        if kind == "hip" or s.suffix == ".hip":
+            cmd = [HIPCC, *HIP_FLAGS, *_py_includes(), f"-I{srcdir}", "-c", str(s), "-o", str(o)]
+            if s.suffix == ".cpp":
+                cmd.insert(1, "-x")
+                cmd.insert(2, "hip")
+        else:
+            cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-march=x86-64-v2", "-msse4.2", "-pthread",
+                   *_py_includes(), f"-I{srcdir}", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
+                   "-c", str(s), "-o", str(o)]
+        # the digest is taken BEFORE compiling: an edit during the compile leaves a mismatching stamp
+        stale, dg = _stale(o, cmd, [s, *headers])
+        if force or stale:
+            jobs_list.append((cmd, o, dg))
+
+    def _compile(job):
+        cmd, o, dg = job
+        _run(cmd)
+        o.with_suffix(o.suffix + ".sha1").write_text(dg)
+
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            list(ex.map(_run, jobs_list))
+            list(ex.map(_compile, jobs_list))
     objs = [str(objdir / (s.name + ".o")) for s in srcs]
     if force or jobs_list or _newer(out, [Path(o) for o in objs]):
         if kind == "hip":
@@ -91,6 +127,7 @@ def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra
         else:
             cmd = ["g++", "-shared", "-fPIC", "-pthread", *objs, "-o", str(out), *extra_link]
         _run(cmd)
+        _check_undefined(out)
     return out
 
 

@@ -64,9 +64,8 @@ class KerasMnistCNN(_ImageModel):
         self._set_input_affine()
 
     def forward(self, x):
-        x = self.conv2(self.conv1(self.prep(x)))
-        x = self.pool(x).reshape(x.shape[0], -1)
-        return self.fc2(self.drop2(self.fc1(x)))
+        x = hnn.conv_pool(self.conv2, self.pool, self.conv1(self.prep(x)))
+        return self.fc2(self.drop2(self.fc1(x.reshape(x.shape[0], -1))))
 
 
 class MirroredMnistCNN(_ImageModel):
@@ -82,8 +81,7 @@ class MirroredMnistCNN(_ImageModel):
         self._set_input_affine()
 
     def forward(self, x):
-        x = self.conv2(self.conv1(self.prep(x)))
-        x = self.pool(x)
+        x = hnn.conv_pool(self.conv2, self.pool, self.conv1(self.prep(x)))  # conv2 + pool + dropout: 1 launch
         return self.fc2(self.fc1(x.reshape(x.shape[0], -1)))
 
 
@@ -100,9 +98,8 @@ class FashionMnistCNN(_ImageModel):
         self._set_input_affine()
 
     def forward(self, x):
-        x = self.conv2(self.conv1(self.prep(x)))
-        x = self.pool(x).reshape(x.shape[0], -1)
-        return self.fc2(self.drop2(self.fc1(x)))
+        x = hnn.conv_pool(self.conv2, self.pool, self.conv1(self.prep(x)))
+        return self.fc2(self.drop2(self.fc1(x.reshape(x.shape[0], -1))))
 
 
 class TorchMnistNet(_ImageModel):

@@ -118,6 +118,16 @@ class MaxPool2d(nn.Module):
 MaxPooling2D = MaxPool2d
 
 
+def conv_pool(conv: Conv2d, pool: MaxPool2d, x):
+    """``pool(conv(x))`` as ONE fused launch when the pair qualifies (functional.conv2d_maxpool);
+    parameters and results are those of the two modules applied in sequence."""
+    if conv.in_affine is not None or x.dtype == torch.uint8:
+        return pool(conv(x))
+    return HF.conv2d_maxpool(x, conv.weight, conv.bias, act=conv.activation, pool_kernel=pool.k,
+                             pool_stride=pool.s, pool_padding=pool.p, dropout_p=pool.dropout,
+                             training=pool.training, salt=pool.salt, **conv.cfg)
+
+
 class GlobalAvgPool2d(nn.Module):
     def forward(self, x):
         return HF.global_avg_pool(x)

@@ -164,7 +164,7 @@ class _LinearFn(torch.autograd.Function):
                     # r is the pool-INPUT gradient: hand autograd an unfilled placeholder for this
                     # layer's input and let the pool backward return r (registry keyed by address)
                     ph = torch.empty(ctx.xshape, device=dy2.device, dtype=BF16)
-                    _PRESCATTERED[ph.data_ptr()] = (weakref.ref(ph), r, bool(pool[1]))
+                    _PRESCATTERED[ph.data_ptr()] = (weakref.ref(ph), r, bool(pool[8]))
                     dxr = ph
                 else:
                     dxr = r.view(ctx.xshape)
@@ -212,8 +212,23 @@ def _plain_gemm_conv(g, b, act, in_affine, prev) -> bool:
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None):
+    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None, pool=None):
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
+        ctx.pool = None
+        if pool is not None:
+            # conv + act + 2x2 max-pool (+ dropout) as one launch; only the pooled tensor and the
+            # argmax exist afterwards (ReLU' is encoded in the argmax, see conv2d_fwd_pool)
+            drop_p, salt = pool
+            x = x.contiguous()
+            rng = rng_state(x.device) if drop_p > 0 else None
+            y, am = K.conv2d_fwd_pool(x, _arena.weight_bf16(w), g, bias=b, act=act, drop_p=drop_p, rng=rng, salt=salt)
+            ctx.save_for_backward(x, am)
+            ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
+            ctx.plain = False
+            ctx.pool = (drop_p, rng, salt)
+            ctx.set_materialize_grads(False)
+            y._hx_pool = (am, False, (g[0], g[4], g[5], g[6]), (2, 2), 0, rng, salt, drop_p, True)
+            return y
         if x.dtype == BF16 and _plain_gemm_conv(g, b, act, in_affine, prev):
             x = x.contiguous()
             wb = _arena.weight_bf16(w)
@@ -239,7 +254,7 @@ class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return (None,) * 9
+            return (None,) * 10
         if ctx.plain:  # 1x1 conv as library GEMMs: dX = dY W, dW += dY^T X (fp32 out, bf16 in)
             x, _ = ctx.saved_tensors
             w, g = ctx.w, ctx.g
@@ -259,12 +274,25 @@ class _Conv2dFn(torch.autograd.Function):
                         K.conv2d_wgrad(dy2.view(dy.shape), x, g, gw)
             else:
                 gw.view(CO, C).add_(torch.mm(dy2.t(), x.view(-1, C), out_dtype=torch.float32))
-            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None)
-        x, y = ctx.saved_tensors
+            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None, None)
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
-        dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
+        if ctx.pool is not None:
+            x, am = ctx.saved_tensors
+            y = None
+            drop_p, rng, salt = ctx.pool
+            oshape = (g[0], g[4], g[5], g[6])
+            ent = _PRESCATTERED.pop(dy.data_ptr(), None)
+            if ent is not None and ent[0]() is not None and tuple(ent[1].shape) == oshape:
+                dy = ent[1]  # the consuming Linear's dgrad epilogue already did the pool backward
+            else:
+                dy = K.maxpool2d_bwd(dy.to(BF16).contiguous(), am, oshape, (2, 2), (2, 2), (0, 0), drop_p=drop_p,
+                                     rng=rng, salt=salt)
+            premasked = True  # ReLU' rode on the argmax
+        else:
+            x, y = ctx.saved_tensors
+            dy = dy.to(BF16).contiguous() if dy.dtype != BF16 else dy.contiguous()
+            premasked = act == 1 and _take_premasked(dy)
         gb = _wgrad_buf(b) if b is not None else None
-        premasked = act == 1 and _take_premasked(dy)
         ymask = y if (act and not premasked) else None
         if premasked:
             act = 0
@@ -284,7 +312,7 @@ class _Conv2dFn(torch.autograd.Function):
                     hooks.grad_ready(ctx.prev[0])
                     hooks.grad_ready(ctx.prev[1])
                 return (r, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None,
-                        None, None)
+                        None, None, None)
         side_ok = not K.conv_wgrad_uses_ticket(g, ctx.in_affine)
         if side_ok:  # wgrad || dgrad on a parallel branch (its kernels keep no shared ticket/workspace)
             with _on_side(dy.device, dy, x, ymask, flop=2.0 * dy.numel() * g[7] * g[8] * g[3]):
@@ -304,7 +332,31 @@ class _Conv2dFn(torch.autograd.Function):
         if not side_ok:
             K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
         return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None,
-                None)
+                None, None)
+
+
+def conv2d_maxpool(x, w, b=None, stride=1, padding=0, dilation=1, act=None, pool_kernel=2, pool_stride=None,
+                   pool_padding=0, dropout_p: float = 0.0, training: bool = True, salt: int = 0):
+    """max_pool2d(conv2d(x, ...), ...) with the pool (+ its fused dropout) folded into the conv's
+    epilogue when the pair qualifies (bf16 NHWC on the GPU, 2x2 stride-2 unpadded pool, even conv
+    output, ReLU or no activation): one launch, and neither the conv output nor a pool pass."""
+    pk = (pool_kernel, pool_kernel) if isinstance(pool_kernel, int) else tuple(pool_kernel)
+    ps = pk if pool_stride is None else ((pool_stride,) * 2 if isinstance(pool_stride, int) else tuple(pool_stride))
+    pp = (pool_padding,) * 2 if isinstance(pool_padding, int) else tuple(pool_padding)
+    a = ACT[act] if not isinstance(act, int) else act
+    if (x.is_cuda and x.dtype == BF16 and pk == (2, 2) and ps == (2, 2) and pp == (0, 0)
+            and padding != "valid" and "conv_pool" not in _disabled() and x.data_ptr() % 16 == 0
+            and not (padding == "same" and (w.shape[1] % 2 == 0 or w.shape[2] % 2 == 0))):
+        st = (stride, stride) if isinstance(stride, int) else tuple(stride)
+        dl = (dilation, dilation) if isinstance(dilation, int) else tuple(dilation)
+        if padding == "same":
+            pd = (_pad_same(w.shape[1], dl[0]), _pad_same(w.shape[2], dl[1]))
+        else:
+            pd = (padding, padding) if isinstance(padding, int) else tuple(padding)
+        if K.conv_fwd_pool_ok(K.conv_geom(x.shape, w.shape, st, pd, dl), a):
+            return _conv_apply(x, w, b, st, pd, dl, a, None, pool=(float(dropout_p) if training else 0.0, salt))
+    y = conv2d(x, w, b, stride, padding, dilation, act)
+    return max_pool2d(y, pool_kernel, pool_stride, pool_padding, dropout_p, training, salt)  # unfused
 
 
 def _fusable_input_layer(x, geom):
@@ -325,11 +377,13 @@ def _disabled() -> str:
     return os.environ.get("HOPSX_DISABLE", "")
 
 
-def _conv_apply(x, w, b, st, pd, dl, a, in_affine):
+def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None):
     """Apply the conv Function; tag the output of an input layer (input needs no gradient) so
     the next conv can fuse this layer's weight gradient into its dgrad."""
     prev = _fusable_input_layer(x, K.conv_geom(x.shape, w.shape, st, pd, dl)) if x.requires_grad else None
-    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev)
+    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev, pool)
+    if pool is not None:
+        return y
     if a:
         y._hx_act_out = a  # activation fused into this conv's epilogue (see max_pool2d premask)
     if not x.requires_grad and w.requires_grad and x.shape[-1] == 1:
@@ -403,7 +457,7 @@ class _MaxPoolFn(torch.autograd.Function):
         if x.is_cuda and s == k and p == (0, 0) and H % k[0] == 0 and W % k[1] == 0 and k[0] * k[1] <= 255:
             # a Linear consuming the (flattened) output can do this backward in its dgrad epilogue
             y._hx_pool = (am, bool(premask), tuple(x.shape), k, "relu" if premask else 0,
-                          rng, salt, drop_p)
+                          rng, salt, drop_p, bool(premask))
         return y
 
     @staticmethod

@@ -424,3 +424,61 @@ def test_pool_backward_fused_into_linear_dgrad(monkeypatch, model):
         monkeypatch.setattr(K, "maxpool2d_bwd", real)
     assert not HF._PRESCATTERED
     torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
+
+
+@pytest.mark.parametrize("C,CO,k,H,pad,act,p", [(32, 64, 2, 27, 0, "relu", 0.01), (32, 64, 3, 28, 1, "relu", 0.45),
+                                               (16, 32, 3, 14, 0, 0, 0.0), (64, 128, 2, 9, 0, "relu", 0.0)])
+def test_conv_fwd_pool_matches_conv_then_pool(C, CO, k, H, pad, act, p):
+    """POOL epilogue of conv_fwd_mfma_k == conv kernel followed by the max-pool(+dropout) kernel."""
+    from hops_examples_amd.ops import functional as HF
+
+    torch.manual_seed(1)
+    B = 5
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    w = (torch.randn(CO, k, k, C, device=dev) * 0.2).to(bf)
+    b = torch.randn(CO, device=dev) * 0.1
+    g = K.conv_geom(x.shape, w.shape, (1, 1), (pad, pad), (1, 1))
+    assert K.conv_fwd_pool_ok(g, act)
+    rng = HF.rng_state(dev)
+    yp, am = K.conv2d_fwd_pool(x, w, g, bias=b, act=act, drop_p=p, rng=rng, salt=4242)
+    yc = K.conv2d_fwd(x, w, g, bias=b, act=act)
+    yr, amr = K.maxpool2d_fwd(yc, (2, 2), (2, 2), (0, 0), drop_p=p, rng=rng, salt=4242)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(yp.float(), yr.float(), rtol=0, atol=0)
+    if act == "relu":
+        # the argmax carries ReLU': 0xFF exactly where the window max is 0
+        wmax = yc.float().view(B, g[4] // 2, 2, g[5] // 2, 2, CO).amax((2, 4))
+        assert torch.equal(am == 255, wmax <= 0)
+        live = am != 255
+        assert torch.equal(am[live], amr[live])
+    else:
+        assert torch.equal(am, amr)
+
+
+@pytest.mark.parametrize("model", ["mirrored", "fashion"])
+def test_conv_pool_model_grads_match_unfused(monkeypatch, model):
+    """Models running conv2 -> max-pool(+dropout) as one launch train like the unfused chain."""
+    from hops_examples_amd.models import mnist
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    res = []
+    for disable in ("", "conv_pool"):
+        monkeypatch.setenv("HOPSX_DISABLE", disable)
+        HF.seed_device_rng(9, dev)
+        torch.manual_seed(0)
+        m = (mnist.MirroredMnistCNN() if model == "mirrored" else mnist.FashionMnistCNN()).to(dev)
+        for mod in m.modules():
+            if hasattr(mod, "salt"):
+                mod.salt = 7919
+        ParamArena.from_module(m, dev)
+        x = torch.randint(0, 256, (32, 28, 28, 1), dtype=torch.uint8, device=dev)
+        t = torch.randint(0, 10, (32,), device=dev)
+        out = m(x)
+        _, _, _, root, g = HF.loss_and_grad_root(out, t, "sparse_ce")
+        root.backward(g)
+        torch.cuda.synchronize()
+        res.append((out.float().clone(), m._hx_arena.grad.float().clone()))
+    assert not HF._PRESCATTERED
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
+    torch.testing.assert_close(res[0][1], res[1][1], atol=3e-2 * res[1][1].abs().max().item(), rtol=3e-2)
