@@ -61,9 +61,10 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   });
   m.def("head_ce_ok", [](int C, int KD) { return hopsx_head_ce_ok(C, KD); });
   m.def("head_ce", [](int kind, u logits, int lf32, u target, int B, int C, int KD, float gs, u h, u w, u dw, u db,
-                      u dh, u loss, u correct, u st) {
+                      u dh, u loss, u correct, u bias, u lout, u st) {
     return hopsx_head_ce(kind, P<void>(logits), lf32, P<void>(target), B, C, KD, gs, P<void>(h), P<void>(w),
-                         P<float>(dw), P<float>(db), P<void>(dh), P<float>(loss), P<int>(correct), S(st));
+                         P<float>(dw), P<float>(db), P<void>(dh), P<float>(loss), P<int>(correct), P<float>(bias),
+                         P<void>(lout), S(st));
   });
   m.def("zero", [](u p, long bytes, u st) { return hopsx_zero(P<void>(p), bytes, S(st)); });
   m.def("nonfinite", [](u x, long n, int is_bf16, u out, u st) {

@@ -258,11 +258,13 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
                                                  const bf16_raw* __restrict__ h, const bf16_raw* __restrict__ w,
                                                  float* __restrict__ dw, float* __restrict__ db,
                                                  bf16_raw* __restrict__ dh, float* __restrict__ loss_sum,
-                                                 int* __restrict__ correct, int vec) {
+                                                 int* __restrict__ correct, int vec, const float* __restrict__ bias,
+                                                 void* __restrict__ lout) {
   extern __shared__ __attribute__((aligned(16))) unsigned char head_smem[];
   bf16_raw* sh = (bf16_raw*)head_smem;
   bf16_raw* sw = sh + HEAD_ROWS * KD;
   float* sdl = (float*)(sw + ((C * KD + 7) / 8) * 8);
+  float* slog = sdl + HEAD_ROWS * C;  // forward mode: the logits computed here
   __shared__ float sl[16];
   __shared__ int sc[16];
   const int r0 = blockIdx.x * HEAD_ROWS;
@@ -278,14 +280,43 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
     for (int i = threadIdx.x; i < nr * KD; i += blockDim.x) sh[i] = h[(long)r0 * KD + i];
     for (int i = threadIdx.x; i < C * KD; i += blockDim.x) sw[i] = w[i];
   }
+  if (lout) {
+    // forward mode: the head layer's own GEMM (logits = h W^T + b) runs here from the staged
+    // operands, so the layer needs no forward launch; block y == 0 stores the logits
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
+      const int r = e / C, n = e - r * C;
+      float s0 = 0.f, s1 = 0.f;
+      int k = 0;
+      if (vec)
+        for (; k + 8 <= KD; k += 8) {
+          const bf16x8 a = *(const bf16x8*)(sh + r * KD + k), b = *(const bf16x8*)(sw + n * KD + k);
+#pragma unroll
+          for (int u = 0; u < 8; u += 2) {
+            s0 = fmaf(bf2f(a[u]), bf2f(b[u]), s0);
+            s1 = fmaf(bf2f(a[u + 1]), bf2f(b[u + 1]), s1);
+          }
+        }
+      for (; k < KD; ++k) s0 = fmaf(bf2f(sh[r * KD + k]), bf2f(sw[n * KD + k]), s0);
+      float v = s0 + s1 + (bias ? bias[n] : 0.f);
+      if (!lf32) v = bf2f(f2bf(v));  // the loss sees exactly the stored logits
+      slog[e] = v;
+      if (blockIdx.y == 0) {
+        if (lf32) ((float*)lout)[(long)r0 * C + e] = v;
+        else ((bf16_raw*)lout)[(long)r0 * C + e] = f2bf(v);
+      }
+    }
+    __syncthreads();
+  }
   float lacc = 0.f;
   int cacc = 0;
   if ((int)threadIdx.x < nr) {
-    const void* lg = lf32 ? (const void*)((const float*)logits + (long)r0 * C)
-                          : (const void*)((const bf16_raw*)logits + (long)r0 * C);
+    const void* lg = lout ? (const void*)slog
+                          : lf32 ? (const void*)((const float*)logits + (long)r0 * C)
+                                 : (const void*)((const bf16_raw*)logits + (long)r0 * C);
     const void* tg = kind == 0 ? (const void*)((const long*)target + r0)
                                : (const void*)((const float*)target + (long)r0 * C);
-    row_thread(kind, lg, lf32, tg, threadIdx.x, C, gs, sdl, 1, lacc, cacc);
+    row_thread(kind, lg, lout ? 1 : lf32, tg, threadIdx.x, C, gs, sdl, 1, lacc, cacc);
   }
   lacc = wave_sum(lacc);
 #pragma unroll
@@ -367,14 +398,14 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
 }
 
 static size_t head_lds_bytes(int C, int KD) {
-  return (size_t)HEAD_ROWS * KD * 2 + (size_t)((C * KD + 7) / 8) * 8 * 2 + (size_t)HEAD_ROWS * C * 4;
+  return (size_t)HEAD_ROWS * KD * 2 + (size_t)((C * KD + 7) / 8) * 8 * 2 + (size_t)HEAD_ROWS * C * 4 * 2;
 }
 
 bool hopsx_head_ce_ok(int C, int KD) { return C >= 1 && C <= HEAD_CMAX && KD >= 1 && head_lds_bytes(C, KD) <= 65536; }
 
 extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
                              float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh,
-                             float* loss_sum, int* correct, hipStream_t st) {
+                             float* loss_sum, int* correct, const float* bias, void* logits_out, hipStream_t st) {
   if (!hopsx_head_ce_ok(C, KD) || B < 1) return -2;
   const int grid = (B + HEAD_ROWS - 1) / HEAD_ROWS;
   // column blocks of >= 32 columns so a small batch still spreads over several CUs
@@ -388,6 +419,6 @@ extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const
   const int vec = KD % 8 == 0 && ((uintptr_t)h % 16 == 0) && ((uintptr_t)w % 16 == 0);
   hipLaunchKernelGGL(head_ce_k, dim3(grid, gy), dim3(1024), head_lds_bytes(C, KD), st, kind, logits, logits_f32, target, B, C,
                      KD, grad_scale, (const bf16_raw*)h, (const bf16_raw*)w, dw, db, (bf16_raw*)dh, loss_sum,
-                     correct, vec);
+                     correct, vec, bias, logits_out);
   return (int)hipGetLastError();
 }

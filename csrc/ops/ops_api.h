@@ -50,7 +50,7 @@ int hopsx_avgpool_global_bwd(const void* dy, void* dx, int B, int HW, int C, hip
 bool hopsx_head_ce_ok(int C, int KD);
 int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
                   float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh, float* loss_sum,
-                  int* correct, hipStream_t st);
+                  int* correct, const float* bias, void* logits_out, hipStream_t st);
 int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
                        float grad_scale, float* loss_sum, int* correct, void* dlogits, int dlogits_f32,
                        hipStream_t st);

@@ -184,11 +184,26 @@ def linear(x, w, b=None, act=None, out_f32=False):
     xc = to_compute(x)
     src = x if hasattr(x, "_hx_pool") else getattr(x, "_base", None)
     pool = getattr(src, "_hx_pool", None) if src is not None and src.numel() == x.numel() else None
+    head = (not a and x.dim() == 2 and w.shape[0] <= 32 and xc.dtype == BF16 and torch.is_grad_enabled()
+            and w.requires_grad and _arena.grad_target(w) is not None
+            and (b is None or _arena.grad_target(b) is not None))
+    if head and HEAD["defer"] and "head_fwd" not in _disabled() and K.head_ce_ok(w.shape[0], x.shape[1]):
+        # deferred logits layer (TrainStep verified that these logits are the model's output and
+        # only feed the loss): no forward launch — the loss kernel computes and stores the logits
+        y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=F32 if out_f32 else BF16)
+        y._hx_dense_head = (xc, w, b, out_f32, True)
+        return y
     y = _LinearFn.apply(xc, w, b, a, out_f32, pool)
-    if (not a and x.dim() == 2 and w.shape[0] <= 32 and y.requires_grad and xc.dtype == BF16
-            and _arena.grad_target(w) is not None and (b is None or _arena.grad_target(b) is not None)):
-        y._hx_dense_head = (xc, w, b)  # logits layer: loss_and_grad can fuse its backward (head_ce)
+    if head and y.requires_grad:
+        y._hx_dense_head = (xc, w, b, out_f32, False)  # logits layer: loss_and_grad can fuse its backward
+        if HEAD["probe"] is not None:
+            HEAD["probe"].append(y)
     return y
+
+
+# logits-layer deferral (set by runtime.step.TrainStep): "probe" collects the head-candidate
+# outputs of one forward; "defer" lets linear() skip the head's forward launch (head_ce computes it)
+HEAD = {"probe": None, "defer": False}
 
 
 # ===================================================================== Conv2d
@@ -737,9 +752,13 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
     k = LOSS[kind]
     if (head is None or not logits.is_cuda or logits.dim() != 2 or "head_ce" in _disabled()
             or not K.head_ce_ok(logits.shape[1], head[0].shape[1])):
+        if head is not None and head[4]:  # deferred logits the fused kernel cannot take: compute them now
+            real = _LinearFn.apply(head[0], head[1], head[2], 0, head[3], None)
+            logits.copy_(real.detach())
+            logits = real
         loss_, correct, count, dl = loss_and_grad(logits, target, kind)
         return loss_, correct, count, logits, dl
-    h, w, b = head
+    h, w, b, _, deferred = head
     B, C = logits.shape
     cnt = B * (C if k in (2, 3, 4) else 1)
     if k in (2, 3, 4) and target.dim() == 1:
@@ -747,9 +766,10 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
     target = (target.long() if k == 0 else target.float()).contiguous()
     loss_sum = torch.empty(1, device=logits.device)
     correct = torch.empty(1, device=logits.device, dtype=torch.int32)
-    dh = K.head_ce(k, logits.detach().contiguous(), target, h.detach(), _arena.weight_bf16(w),
-                   _arena.grad_target(w), _arena.grad_target(b) if b is not None else None, 1.0 / cnt, loss_sum,
-                   correct)
+    dh = K.head_ce(k, logits if deferred else logits.detach().contiguous(), target, h.detach(),
+                   _arena.weight_bf16(w), _arena.grad_target(w), _arena.grad_target(b) if b is not None else None,
+                   1.0 / cnt, loss_sum, correct, bias=b.detach() if (deferred and b is not None) else None,
+                   forward=deferred)
     hooks.grad_ready(w)
     if b is not None:
         hooks.grad_ready(b)

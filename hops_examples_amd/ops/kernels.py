@@ -553,9 +553,12 @@ def head_ce_ok(C: int, KD: int) -> bool:
     return bool(_C.ext().head_ce_ok(int(C), int(KD)))
 
 
-def head_ce(kind: int, logits, target, h, w, dw, db, grad_scale: float, loss_sum, correct):
+def head_ce(kind: int, logits, target, h, w, dw, db, grad_scale: float, loss_sum, correct, bias=None,
+            forward: bool = False):
     """Loss + dlogits (never materialised) + dW += dl^T h + db += sum dl + returns dh = dl W, in one
-    launch (loss.hip head_ce_k).  logits [B, C<=32] fp32/bf16, h [B, KD] bf16, w [C, KD] bf16."""
+    launch (loss.hip head_ce_k).  logits [B, C<=32] fp32/bf16, h [B, KD] bf16, w [C, KD] bf16.
+    ``forward``: the layer's forward runs in the same launch — logits = h W^T + bias are computed
+    from the staged operands and WRITTEN into ``logits`` (which is only an output then)."""
     B, C = logits.shape
     KD = h.shape[1]
     _req(h, BF16, "h")
@@ -563,6 +566,7 @@ def head_ce(kind: int, logits, target, h, w, dw, db, grad_scale: float, loss_sum
     _req(dw, F32, "dw")
     dh = torch.empty(B, KD, device=h.device, dtype=BF16)
     check(_C.ext().head_ce(kind, ptr(logits), int(logits.dtype == F32), ptr(target), B, C, KD, float(grad_scale),
-                           ptr(h), ptr(w), ptr(dw), ptr(db), ptr(dh), ptr(loss_sum), ptr(correct), stream()),
+                           ptr(h), ptr(w), ptr(dw), ptr(db), ptr(dh), ptr(loss_sum), ptr(correct), ptr(bias),
+                           ptr(logits) if forward else 0, stream()),
           "head_ce")
     return dh

@@ -67,12 +67,35 @@ class TrainStep:
         self._cursor = None
         self._pf_opt = None
         self._pf_pending = None
+        self.defer_head = os.environ.get("HOPSX_DEFER_HEAD", "1") == "1"
+        self._head_defer = None
         if dp is not None:
             optimizer.grad_scale = dp.grad_scale()
 
     # ------------------------------------------------------------- eager path
+    def _forward(self, x):
+        """Model forward.  The first CUDA step probes whether the logits layer's output is exactly
+        the model output (nothing else reads it); from then on that layer's forward is deferred
+        into the fused loss kernel (functional.HEAD, loss.hip head_ce_k forward mode)."""
+        if self.device.type != "cuda" or not self.defer_head:
+            return self.forward_fn(self.model, x)
+        if self._head_defer is None:
+            HF.HEAD["probe"] = []
+            try:
+                out = self.forward_fn(self.model, x)
+                probe = HF.HEAD["probe"]
+            finally:
+                HF.HEAD["probe"] = None
+            self._head_defer = len(probe) == 1 and probe[0] is out
+            return out
+        HF.HEAD["defer"] = self._head_defer
+        try:
+            return self.forward_fn(self.model, x)
+        finally:
+            HF.HEAD["defer"] = False
+
     def _fwd_bwd(self, x, y):
-        out = self.forward_fn(self.model, x)
+        out = self._forward(x)
         loss, correct, count, root, grad = HF.loss_and_grad_root(out, y, self.loss_kind)
         root.backward(grad)
         HF.join_side_streams()  # gradients complete before all-reduce / optimizer

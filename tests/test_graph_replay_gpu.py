@@ -79,3 +79,35 @@ def test_resident_prefetch_walks_the_epoch():
         if resident:
             assert int(st._cursor.item()) == 12 % nb
     torch.testing.assert_close(torch.tensor(losses[0]), torch.tensor(losses[1]), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("model", ["mirrored", "keras"])
+def test_deferred_logits_layer_matches_eager_head(monkeypatch, model):
+    """TrainStep defers the logits layer's forward into the fused loss kernel (head_ce forward
+    mode) once it has probed that the logits only feed the loss: losses and trained weights match
+    the undeferred run (eager warm-up + graph replays)."""
+    from hops_examples_amd import optim
+    from hops_examples_amd.models import mnist
+    from hops_examples_amd.runtime.step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    B = 32
+    xs = torch.randint(0, 256, (8, B, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (8, B), device=dev)
+    runs = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("HOPSX_DEFER_HEAD", defer)
+        HF.seed_device_rng(5, dev)
+        torch.manual_seed(0)
+        m = (mnist.MirroredMnistCNN() if model == "mirrored" else mnist.KerasMnistCNN()).to(dev)
+        for mod in m.modules():
+            if hasattr(mod, "salt"):
+                mod.salt = 7919
+        ParamArena.from_module(m, dev)
+        st = TrainStep(m, optim.Adadelta(m, lr=1.0), "sparse_ce")
+        ls = [float(st(xs[i], ys[i])["loss"].reshape(-1)[0]) for i in range(8)]
+        assert bool(st._head_defer) is (defer == "1")
+        runs.append((ls, m._hx_arena.master.float().clone()))
+    torch.testing.assert_close(torch.tensor(runs[0][0]), torch.tensor(runs[1][0]), rtol=1e-3, atol=1e-3)
+    # logits rounded from a different fp32 summation order: bf16 ties flip on a few elements
+    torch.testing.assert_close(runs[0][1], runs[1][1], rtol=1e-2, atol=5e-3)
