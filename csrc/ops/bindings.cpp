@@ -39,6 +39,11 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
                               P<void>(y), yact, S(st));
   });
+  m.def("widedeep_step_lds", [](std::vector<long> iv) { return hopsx_widedeep_step_lds(iv.data(), (int)iv.size()); });
+  m.def("widedeep_step", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, u st) {
+    return hopsx_widedeep_step(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),
+                               S(st));
+  });
   m.def("conv2d_fwd_pool_ok", [](std::vector<int> g, int act) { return hopsx_conv_fwd_pool_ok(g.data(), act); });
   m.def("conv2d_fwd_pool", [](u x, u w, std::vector<int> g, u out, u am, u bias, int act, float p, u rng,
                               unsigned salt, u st) {

@@ -92,6 +92,11 @@ int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamm
                  void* dresidual, float* acc, hipStream_t st);
 
 // ---- direct MFMA convs for short reductions (conv_mfma.hip) ----
+// ---- whole wide&deep training step in one workgroup (widedeep_step.hip) ----
+long hopsx_widedeep_step_lds(const long* iv, int ni);
+int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
+                        hipStream_t st);
+
 bool hopsx_conv_fwd_mfma_ok(const int* geom);
 bool hopsx_conv_fwd_pool_ok(const int* geom, int act);
 int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* out, void* am, const float* bias, int act,

@@ -24,6 +24,7 @@ two optimizers are single fused kernels over two slices of ONE parameter arena
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -91,6 +92,112 @@ def make_optimizer(model: TaxiWideDeep, ftrl_lr: float = 0.2, adagrad_lr: float 
                        optim.Adagrad(model.deep, lr=adagrad_lr, initial_accumulator_value=0.1))
 
 
+class FusedWideDeepStep:
+    """The whole taxi training step as ONE kernel launch (csrc/ops/widedeep_step.hip): forward,
+    sigmoid cross-entropy, backward, FTRL (wide) + Adagrad (deep) updates, step counters and the
+    batch cursor of an HBM-resident epoch — one workgroup holding the model and the batch in LDS.
+
+    Same model, optimizers and results as ``TrainStep(model, make_optimizer(model), "bce_logits")``
+    (fp32 GEMMs instead of bf16).  Data-parallel (``dp``): the kernel stops at the gradients, which
+    are all-reduced and applied by the regular optimizer kernels.  ``ok()`` says whether the
+    model/batch fit one workgroup's LDS; otherwise use TrainStep."""
+
+    def __init__(self, model: TaxiWideDeep, optimizer, dp=None):
+        from ..runtime.arena import ParamArena  # noqa: F401 (the model must live in an arena)
+
+        self.model, self.opt, self.dp = model, optimizer, dp
+        self.arena = model.wide.weight._hx_arena
+        self.ftrl, self.ada = optimizer.opts
+        lins = [m for m in model.deep if isinstance(m, hnn.Linear)]
+        self.lins = lins
+        self.dims = [lins[0].weight.shape[1]] + [m.weight.shape[0] for m in lins]
+        self.acts_ok = (all(m.activation == "relu" for m in lins[:-1]) and lins[-1].activation is None
+                        and all(m.bias is not None for m in lins))
+        if dp is not None:
+            optimizer.grad_scale = dp.grad_scale()
+        self._graph = None
+        self._key = None
+        self._n = 0
+        dev = self.arena.device
+        self.loss = torch.zeros(1, device=dev)
+        self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.cursor = torch.zeros(1, device=dev, dtype=torch.int64)
+
+    def _ints(self, B: int, nbatch: int) -> list[int]:
+        L = len(self.lins)
+        return ([L, B, nbatch, N_WIDE, int(self.model.wide.weight._hx_off), int(self.dp is None), 2] + self.dims
+                + [int(m.weight._hx_off) for m in self.lins] + [int(m.bias._hx_off) for m in self.lins])
+
+    def ok(self, B: int) -> bool:
+        from ..ops import _C
+
+        dev = self.arena.device
+        return (dev.type == "cuda" and self.acts_ok and self.dims[-1] == 1
+                and _C.ext().widedeep_step_lds(self._ints(B, 1)) > 0)
+
+    def _floats(self) -> list[float]:
+        def pad8(v):
+            return [float(x) for x in v] + [0.0] * (8 - len(v))
+
+        self.ada.lr = self.ada.param_groups[0]["lr"]
+        self.ftrl.lr = self.ftrl.param_groups[0]["lr"]
+        return pad8(self.ada._hp()) + pad8(self.ftrl._hp())
+
+    def _launch(self, dense, cat, label, nbatch: int, cursor):
+        from ..ops import _C
+        from ..ops.functional import rng_state
+        from ..ops.kernels import check, stream
+
+        a = self.arena
+        ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
+        ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")), ptr(a.state("ftrl_s0")),
+                ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label), ptr(cursor), ptr(self.loss),
+                ptr(self.correct), ptr(self.ada.step_count), ptr(self.ftrl.step_count), ptr(rng_state(a.device))]
+        check(_C.ext().widedeep_step(ptrs, self._ints(dense.shape[-2], nbatch), self._floats(), stream()),
+              "widedeep_step")
+
+    def _finish(self):
+        if self.dp is not None:
+            self.dp.allreduce_all()
+            self.opt.step()
+            if hasattr(self.dp, "post_step"):
+                self.dp.post_step()
+
+    def __call__(self, x, y):
+        """One step on an explicit batch: x = (dense [B, 3], cat [B, 13] int64), y [B, 1]."""
+        from ..runtime import health
+
+        self._n += 1
+        health.beat(self._n)
+        dense, cat = x
+        self._launch(dense.float().contiguous(), cat.contiguous(), y.float().contiguous(), 1, None)
+        self._finish()
+        return {"loss": self.loss, "correct": self.correct, "count": dense.shape[0]}
+
+    def step_resident(self, xs, ys, graph: bool = True):
+        """One step on batch ``cursor`` of a resident epoch xs = (dense [nb, B, 3] fp32, cat [nb, B, 13]),
+        ys [nb, B, 1]; the kernel advances the cursor.  Single-GPU steps replay a captured graph."""
+        from ..runtime import health
+
+        self._n += 1
+        health.beat(self._n)
+        dense, cat = xs
+        key = (dense.data_ptr(), cat.data_ptr(), ys.data_ptr(), tuple(self._floats()))
+        if not graph or self.dp is not None or self.arena.device.type != "cuda":
+            self._launch(dense, cat, ys, dense.shape[0], self.cursor)
+            self._finish()
+        else:
+            if self._key != key:  # new data or hyper-parameters (e.g. an lr schedule): recapture
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._launch(dense, cat, ys, dense.shape[0], self.cursor)
+                self._graph, self._key = g, key
+                # capture does not execute: run this step through the graph
+            self._graph.replay()
+        return {"loss": self.loss, "correct": self.correct, "count": dense.shape[1]}
+
+
 def synth_taxi(n: int, seed: int = 0, device="cpu"):
     """Transformed-feature synthetic taxi trips with a learnable tip rule.
     Returns dense [n, 3] f32, cat [n, 13] int64 (global one-hot ids), label [n, 1] f32."""
@@ -123,17 +230,27 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
     ParamArena.from_module(model, dev)
     opt = make_optimizer(model)
     dp = DataParallel(model) if world > 1 else None
-    step = TrainStep(model, opt, "bce_logits", dp=dp, graph=graph, forward_fn=lambda m, x: m(*x))
     nb = max(8, -(-pool_examples // batch))
     dense, cat, label = synth_taxi(nb * batch, seed=7, device=dev)
-    dense = dense.to(torch.bfloat16).view(nb, batch, -1)
     cat = cat.view(nb, batch, -1)
     label = label.view(nb, batch, 1)
     out = {}
+    fused = FusedWideDeepStep(model, opt, dp=dp) if os.environ.get("HOPSX_TAXI_FUSED", "1") == "1" else None
+    if fused is not None and fused.ok(batch):
+        dense = dense.view(nb, batch, -1)
+        path = "fused"
 
-    def run(i):
-        j = i % nb
-        out["r"] = step((dense[j], cat[j]), label[j])
+        def run(i):
+            # one launch: the kernel reads batch `cursor` of the resident epoch and advances it
+            out["r"] = fused.step_resident((dense, cat), label, graph=graph)
+    else:
+        step = TrainStep(model, opt, "bce_logits", dp=dp, graph=graph, forward_fn=lambda m, x: m(*x))
+        dense = dense.to(torch.bfloat16).view(nb, batch, -1)
+        path = "layerwise"
+
+        def run(i):
+            j = i % nb
+            out["r"] = step((dense[j], cat[j]), label[j])
 
     for i in range(warmup):
         run(i)
@@ -141,4 +258,4 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
     loss = float(out["r"]["loss"].reshape(-1)[0])
     return {"steps_per_sec": round(steps / el, 1), "examples_per_sec": round(batch * world * steps / el, 1),
             "ms_per_step": round(el / steps * 1e3, 4), "batch_per_gpu": batch, "loss": round(loss, 4),
-            "params": sum(p.numel() for p in model.parameters()), "hidden_units": hidden_units()}
+            "params": sum(p.numel() for p in model.parameters()), "hidden_units": hidden_units(), "step": path}
