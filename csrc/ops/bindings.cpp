@@ -39,6 +39,9 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
                               P<void>(y), yact, S(st));
   });
+  m.def("widedeep_slots", [](std::vector<long> iv, u out, long n) {
+    return hopsx_widedeep_slots(iv.data(), (int)iv.size(), P<int>(out), n);
+  });
   m.def("widedeep_step_lds", [](std::vector<long> iv) { return hopsx_widedeep_step_lds(iv.data(), (int)iv.size()); });
   m.def("widedeep_step", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, u st) {
     return hopsx_widedeep_step(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),

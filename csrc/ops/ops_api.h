@@ -94,6 +94,7 @@ int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamm
 // ---- direct MFMA convs for short reductions (conv_mfma.hip) ----
 // ---- whole wide&deep training step in one workgroup (widedeep_step.hip) ----
 long hopsx_widedeep_step_lds(const long* iv, int ni);
+int hopsx_widedeep_slots(const long* iv, int ni, int* out, long n);
 int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
                         hipStream_t st);
 

@@ -31,7 +31,8 @@ namespace {
 constexpr int WD_MAXL = 8;      // linear layers (hidden + logits)
 constexpr int WD_THREADS = 1024;
 constexpr int WD_WAVES = WD_THREADS / 64;
-constexpr int WD_MAXT = 8;      // dX tiles a wave holds in registers across the in-place barrier
+constexpr int WD_MAXT = 4;      // dW / dX tiles a wave holds in registers across the in-place barrier
+constexpr int WD_PF = 16;       // deep parameters per thread prefetched into registers (span <= 16 K)
 constexpr int WD_LDS_MAX = 160 * 1024;
 
 struct WideDeepArgs {
@@ -59,31 +60,35 @@ struct WideDeepArgs {
   unsigned long long* rng;
   int rng_bumps;
   int apply_opt;
+  unsigned long long* dbg;  // phase timestamps (wall clock, 100 MHz), or null
+  const int* slot;          // [deep span]: LDS slot of each deep arena element (-1: padding), host-built
 };
 
 __host__ __device__ inline int pad16(int x) { return (x + 15) & ~15; }
+// padded width of an activation of d features: one extra constant-1 column (the bias rides in the
+// GEMMs as weight column d, and db falls out of the dW GEMM as its column d)
+__host__ __device__ inline int dpad(int d) { return pad16(d + 1); }
 
 struct Lay {
-  int act[WD_MAXL + 1];  // LDS float offset of A_l [Bp][pad16(d_l) + 1]
-  int w[WD_MAXL];        // W_l [pad16(out)][pad16(in) + 1]
-  int b[WD_MAXL];        // bias_l [pad16(out)]
+  int act[WD_MAXL + 1];  // LDS float offset of A_l [Bp][dpad(d_l) + 1] (column d_l = 1)
+  int w[WD_MAXL];        // [W_l | b_l] [dpad(out)][dpad(in) + 1]
   int wsum;              // wide sums [Bp]
   int red;               // loss / correct partials [2 * WD_WAVES]
   int total;
 };
 
-__host__ __device__ inline Lay wd_layout(const WideDeepArgs& a) {
+__host__ __device__ inline Lay wd_layout(const WideDeepArgs& a, int L) {
   Lay l;
   int o = 0;
-  for (int i = 0; i <= a.L; ++i) {
+#pragma unroll
+  for (int i = 0; i <= L; ++i) {
     l.act[i] = o;
-    o += a.Bp * (pad16(a.dims[i]) + 1);
+    o += a.Bp * (dpad(a.dims[i]) + 1);
   }
-  for (int i = 0; i < a.L; ++i) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
     l.w[i] = o;
-    o += pad16(a.dims[i + 1]) * (pad16(a.dims[i]) + 1);
-    l.b[i] = o;
-    o += pad16(a.dims[i + 1]);
+    o += dpad(a.dims[i + 1]) * (dpad(a.dims[i]) + 1);
   }
   l.wsum = o;
   o += a.Bp;
@@ -93,88 +98,112 @@ __host__ __device__ inline Lay wd_layout(const WideDeepArgs& a) {
   return l;
 }
 
+__device__ __forceinline__ void wd_mark(const WideDeepArgs& A, int slot) {
+  if (A.dbg && threadIdx.x == 0) A.dbg[slot] = wall_clock64();
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// NL (the layer count) is a template parameter so every per-layer loop unrolls and the layout /
+// dims / offsets stay in scalar registers (a runtime-indexed struct would live in scratch memory)
+template <int NL>
 __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
   extern __shared__ __attribute__((aligned(16))) float wd_lds[];
-  const Lay Ly = wd_layout(A);
+  constexpr int L = NL;
+  const Lay Ly = wd_layout(A, NL);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int B = A.B, Bp = A.Bp, L = A.L;
+  const int B = A.B, Bp = A.Bp;
   const long long bi = A.cursor ? A.cursor[0] : 0;
+  const long deep_lo = A.woff[0], deep_hi = A.boff[L - 1] + A.dims[L];
+  wd_mark(A, 0);
 
   // ---------------------------------------------------------------- stage
+  // Every global load of the step is issued here, independent of each other (one memory round
+  // trip): this thread's deep parameters + Adagrad state (kept in registers until the update),
+  // its wide (example, column) entry with that row's FTRL state, the batch.
+  float pw[WD_PF], ps[WD_PF];
+  int psl[WD_PF];
+#pragma unroll
+  for (int k = 0; k < WD_PF; ++k) {
+    const long x = deep_lo + tid + (long)k * WD_THREADS;
+    const long xc = x < deep_hi ? x : deep_lo;
+    pw[k] = A.master[xc];
+    ps[k] = A.apply_opt ? A.ada_s[xc] : 0.f;
+    psl[k] = x < deep_hi ? A.slot[xc - deep_lo] : -1;
+  }
+  const long long* cb = A.cat + bi * (long long)B * A.nwide;
+  const bool wide_t = tid < B * A.nwide;
+  const long wrow = A.wide_off + (wide_t ? cb[tid] : 0);
+  const float wv = A.master[wrow];
+  float wz = 0.f, wn = 0.f;
+  if (A.apply_opt) {
+    wz = A.ftrl_z[wrow];
+    wn = A.ftrl_n[wrow];
+  }
+  const float* yb = A.label + bi * (long long)B;
+  const float yv = tid < B ? yb[tid] : 0.f;
   {
-    const int d0 = A.dims[0], s0 = pad16(d0) + 1;
+    const int d0 = A.dims[0], s0 = dpad(d0) + 1;
     const float* xb = A.dense + bi * (long long)B * d0;
     for (int e = tid; e < Bp * s0; e += WD_THREADS) {
       const int b = e / s0, i = e - b * s0;
-      wd_lds[Ly.act[0] + e] = (b < B && i < d0) ? xb[(long)b * d0 + i] : 0.f;
+      wd_lds[Ly.act[0] + e] = b < B ? (i < d0 ? xb[(long)b * d0 + i] : (i == d0 ? 1.f : 0.f)) : 0.f;
     }
-    for (int l = 0; l < L; ++l) {
-      const int in = A.dims[l], out = A.dims[l + 1], sw = pad16(in) + 1, op = pad16(out);
-      const float* wg = A.master + A.woff[l];
-      for (int e = tid; e < op * sw; e += WD_THREADS) {
-        const int o = e / sw, i = e - o * sw;
-        wd_lds[Ly.w[l] + e] = (o < out && i < in) ? wg[(long)o * in + i] : 0.f;
-      }
-      for (int o = tid; o < op; o += WD_THREADS) wd_lds[Ly.b[l] + o] = o < out ? A.master[A.boff[l] + o] : 0.f;
-    }
-    const long long* cb = A.cat + bi * (long long)B * A.nwide;
-    for (int b = tid; b < Bp; b += WD_THREADS) {
-      float s = 0.f;
-      if (b < B)
-        for (int j = 0; j < A.nwide; ++j) s += A.master[A.wide_off + cb[(long)b * A.nwide + j]];
-      wd_lds[Ly.wsum + b] = s;
-    }
+    // zero the weight / bias images (their padding must read 0) and the wide sums
+    for (int e = Ly.w[0] + tid; e < Ly.wsum + Bp; e += WD_THREADS) wd_lds[e] = 0.f;
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < WD_PF; ++k)
+    if (psl[k] >= 0) wd_lds[psl[k]] = pw[k];
+  if (wide_t) atomicAdd(wd_lds + Ly.wsum + tid / A.nwide, wv);  // sum of the example's 13 rows
+  __syncthreads();
+  wd_mark(A, 1);
 
   // ---------------------------------------------------------------- forward
+#pragma unroll
   for (int l = 0; l < L; ++l) {
     const int in = A.dims[l], out = A.dims[l + 1];
-    const int sa = pad16(in) + 1, sz = pad16(out) + 1, sw = sa;
-    const int tm = Bp / 16, tn = pad16(out) / 16, ks = pad16(in) / 4;
+    const int sa = dpad(in) + 1, sz = dpad(out) + 1, sw = sa;
+    const int tm = Bp / 16, tn = dpad(out) / 16, ks = dpad(in) / 4;
     const float* Ap = wd_lds + Ly.act[l];
     const float* Wp = wd_lds + Ly.w[l];
-    const float* bp = wd_lds + Ly.b[l];
     float* Zp = wd_lds + Ly.act[l + 1];
     const bool relu = l + 1 < L;
     for (int t = wave; t < tm * tn; t += WD_WAVES) {
       const int m0 = (t / tn) * 16, n0 = (t % tn) * 16;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
       for (int k = 0; k < ks; ++k)
         acc = mfma4(Ap[(m0 + fr) * sa + 4 * k + fq], Wp[(n0 + fr) * sw + 4 * k + fq], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = m0 + 4 * fq + r, o = n0 + fr;
-        float v = acc[r] + bp[o];
+        float v = acc[r];  // bias included (constant-1 input column)
         if (relu) v = fmaxf(v, 0.f);
-        Zp[b * sz + o] = (b < B && o < out) ? v : 0.f;
+        Zp[b * sz + o] = b < B ? (o < out ? v : (o == out && relu ? 1.f : 0.f)) : 0.f;
       }
     }
     __syncthreads();
+    wd_mark(A, 2 + l);
   }
 
   // ---------------------------------------------------------------- loss (sigmoid CE on logits)
   {
     float* Zp = wd_lds + Ly.act[L];  // [Bp][17]; column 0 = deep logit
-    const int sz = pad16(A.dims[L]) + 1;
-    const long long* cb = A.cat + bi * (long long)B * A.nwide;
-    const float* yb = A.label + bi * (long long)B;
+    const int sz = dpad(A.dims[L]) + 1;
     float lsum = 0.f;
     int csum = 0;
-    for (int b = tid; b < B; b += WD_THREADS) {
+    if (tid < B) {
+      const int b = tid;
       const float z = Zp[b * sz] + wd_lds[Ly.wsum + b];
-      const float y = yb[b];
       const float p = 1.f / (1.f + __expf(-z));
-      lsum += fmaxf(z, 0.f) - z * y + __logf(1.f + __expf(-fabsf(z)));
-      csum += ((p > 0.5f) == (y > 0.5f));
-      const float g = (p - y) / (float)B;
-      Zp[b * sz] = g;  // G_L in place of the logits
-      for (int j = 0; j < A.nwide; ++j) atomicAdd(A.grad + A.wide_off + cb[(long)b * A.nwide + j], g);
+      lsum = fmaxf(z, 0.f) - z * yv + __logf(1.f + __expf(-fabsf(z)));
+      csum = ((p > 0.5f) == (yv > 0.5f));
+      Zp[b * sz] = (p - yv) / (float)B;  // G_L in place of the logits
     }
     lsum = wave_sum(lsum);
 #pragma unroll
@@ -184,6 +213,7 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       wd_lds[Ly.red + WD_WAVES + wave] = (float)csum;
     }
     __syncthreads();
+    if (wide_t) atomicAdd(A.grad + wrow, Zp[(tid / A.nwide) * sz]);  // wide gradient (summed per row)
     if (tid == 0) {
       float l = 0.f, c = 0.f;
       for (int w = 0; w < WD_WAVES; ++w) {
@@ -193,103 +223,98 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       if (A.loss) A.loss[0] = l / (float)B;
       if (A.correct) A.correct[0] = (int)c;
     }
+    wd_mark(A, 10);
   }
 
   // ---------------------------------------------------------------- backward
+  // Per layer: phase A computes dW (o x i tiles) and dX (b x i tiles) from LDS into registers and
+  // db into the (dead) bias image; phase B — after every reader of A_{l-1} and W_l is done — writes
+  // G_{l-1} = dX * relu'(A_{l-1}) over A_{l-1} and dW over W_l.
+#pragma unroll
   for (int l = L - 1; l >= 0; --l) {
     const int in = A.dims[l], out = A.dims[l + 1];
-    const int sg = pad16(out) + 1, sa = pad16(in) + 1, sw = sa;
-    const float* Gp = wd_lds + Ly.act[l + 1];  // G_l [Bp][sg] (already masked by relu')
-    float* Ap = wd_lds + Ly.act[l];            // A_{l-1} [Bp][sa]
-    const float* Wp = wd_lds + Ly.w[l];
-    const int tdw = (pad16(out) / 16) * (pad16(in) / 16);           // dW tiles (o x i)
-    const int tdx = l > 0 ? (Bp / 16) * (pad16(in) / 16) : 0;       // dX tiles (b x i)
-    const int tni = pad16(in) / 16;
-    for (int t = wave; t < tdw; t += WD_WAVES) {
-      // dW[o][i] = sum_b G[b][o] A[b][i]   (M = o, N = i, K = b), optimizer applied on the fragment
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int o0 = (t / tni) * 16, i0 = (t % tni) * 16;
-      for (int k = 0; k < Bp / 4; ++k)
-        acc = mfma4(Gp[(4 * k + fq) * sg + o0 + fr], Ap[(4 * k + fq) * sa + i0 + fr], acc);
+    const int sg = dpad(out) + 1, sa = dpad(in) + 1, sw = sa;
+    const float* Gp = wd_lds + Ly.act[l + 1];
+    float* Ap = wd_lds + Ly.act[l];
+    float* Wp = wd_lds + Ly.w[l];
+    const int tni = dpad(in) / 16;
+    const int tdw = (dpad(out) / 16) * tni;  // includes the bias column: db = dW[:, in]
+    const int tdx = l > 0 ? (Bp / 16) * tni : 0;
+    f32x4 hw[WD_MAXT], hx[WD_MAXT];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = o0 + 4 * fq + r, i = i0 + fr;
-        if (o < out && i < in) {
-          const long idx = A.woff[l] + (long)o * in + i;
-          if (A.apply_opt) {
-            float s1 = A.ada_s[idx], s2 = 0.f, s3 = 0.f;
-            const float w = upd<5>(A.master[idx], acc[r] * A.ada.gscale, s1, s2, s3, A.ada, 1.f, 1.f);
-            A.master[idx] = w;
-            A.ada_s[idx] = s1;
-            if (A.shadow) A.shadow[idx] = f2bf(w);
-          } else {
-            A.grad[idx] = acc[r];
-          }
+    for (int j = 0; j < WD_MAXT; ++j) {
+      const int t = wave + j * WD_WAVES;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (t < tdw) {  // dW[o][i] = sum_b G[b][o] A[b][i]
+        const int o0 = (t / tni) * 16, i0 = (t % tni) * 16;
+#pragma unroll 4
+        for (int k = 0; k < Bp / 4; ++k)
+          acc = mfma4(Gp[(4 * k + fq) * sg + o0 + fr], Ap[(4 * k + fq) * sa + i0 + fr], acc);
+      }
+      hw[j] = acc;
+      f32x4 acx = {0.f, 0.f, 0.f, 0.f};
+      if (t < tdx) {  // dX[b][i] = sum_o G[b][o] W[o][i]
+        const int b0 = (t / tni) * 16, i0 = (t % tni) * 16;
+#pragma unroll 4
+        for (int k = 0; k < dpad(out) / 4; ++k)
+          acx = mfma4(Gp[(b0 + fr) * sg + 4 * k + fq], Wp[(4 * k + fq) * sw + i0 + fr], acx);
+      }
+      hx[j] = acx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < WD_MAXT; ++j) {
+      const int t = wave + j * WD_WAVES;
+      if (t < tdw) {
+        const int o0 = (t / tni) * 16, i0 = (t % tni) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Wp[(o0 + 4 * fq + r) * sw + i0 + fr] = hw[j][r];
+      }
+      if (t < tdx) {
+        const int b0 = (t / tni) * 16, i0 = (t % tni) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* p = Ap + (b0 + 4 * fq + r) * sa + i0 + fr;
+          *p = *p > 0.f ? hx[j][r] : 0.f;  // relu' of the hidden activation (0 on padding)
         }
       }
     }
-    // dX[b][i] = sum_o G[b][o] W[o][i]   (M = b, N = i, K = o): held in registers (static indices)
-    // until every reader of A_{l-1} is done, then written over it as G_{l-1}
-    f32x4 hold[WD_MAXT];
-#pragma unroll
-    for (int j = 0; j < WD_MAXT; ++j) {
-      const int tt = wave + j * WD_WAVES;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (tt < tdx) {
-        const int b0 = (tt / tni) * 16, i0 = (tt % tni) * 16;
-        for (int k = 0; k < pad16(out) / 4; ++k)
-          acc = mfma4(Gp[(b0 + fr) * sg + 4 * k + fq], Wp[(4 * k + fq) * sw + i0 + fr], acc);
-      }
-      hold[j] = acc;
-    }
-    // bias gradient: db[o] = sum_b G[b][o]
-    for (int o = tid; o < out; o += WD_THREADS) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += Gp[b * sg + o];
-      const long idx = A.boff[l] + o;
-      if (A.apply_opt) {
-        float s1 = A.ada_s[idx], s2 = 0.f, s3 = 0.f;
-        const float w = upd<5>(A.master[idx], s * A.ada.gscale, s1, s2, s3, A.ada, 1.f, 1.f);
-        A.master[idx] = w;
-        A.ada_s[idx] = s1;
-        if (A.shadow) A.shadow[idx] = f2bf(w);
-      } else {
-        A.grad[idx] = s;
-      }
-    }
-    if (l == 0) break;
-    __syncthreads();  // every reader of A_{l-1} (dW) is done: overwrite it with G_{l-1}
-#pragma unroll
-    for (int j = 0; j < WD_MAXT; ++j) {
-      const int tt = wave + j * WD_WAVES;
-      if (tt >= tdx) break;
-      const int b0 = (tt / tni) * 16, i0 = (tt % tni) * 16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = b0 + 4 * fq + r, i = i0 + fr;
-        float* p = Ap + b * sa + i;
-        *p = *p > 0.f ? hold[j][r] : 0.f;  // relu' of the hidden activation (0 on padding)
-      }
-    }
     __syncthreads();
+    wd_mark(A, 11 + l);
   }
 
-  // ---------------------------------------------------------------- wide FTRL + bookkeeping
-  __syncthreads();
-  if (A.apply_opt) {
-    const long long* cb = A.cat + bi * (long long)B * A.nwide;
-    for (int e = tid; e < B * A.nwide; e += WD_THREADS) {
-      const long idx = A.wide_off + cb[e];
-      // the summed gradient of this row, claimed by exactly one thread (and left zero)
-      const float g = atomicExch(A.grad + idx, 0.f);
-      if (g != 0.f) {
-        float z = A.ftrl_z[idx], n = A.ftrl_n[idx], s3 = 0.f;
-        const float w = upd<6>(A.master[idx], g * A.ftrl.gscale, z, n, s3, A.ftrl, 1.f, 1.f);
-        A.master[idx] = w;
-        A.ftrl_z[idx] = z;
-        A.ftrl_n[idx] = n;
-        if (A.shadow) A.shadow[idx] = f2bf(w);
+  // ---------------------------------------------------------------- updates + bookkeeping
+  // (the LDS weight images now hold dW, the bias images db)
+#pragma unroll
+  for (int k = 0; k < WD_PF; ++k) {
+    const long x = deep_lo + tid + (long)k * WD_THREADS;
+    {
+      const int sl = psl[k];
+      if (sl >= 0) {
+        const float g = wd_lds[sl];
+        if (A.apply_opt) {
+          float s1 = ps[k], s2 = 0.f, s3 = 0.f;
+          const float w = upd<5>(pw[k], g * A.ada.gscale, s1, s2, s3, A.ada, 1.f, 1.f);
+          A.master[x] = w;
+          A.ada_s[x] = s1;
+          if (A.shadow) A.shadow[x] = f2bf(w);
+        } else {
+          A.grad[x] = g;
+        }
       }
+    }
+  }
+  if (A.apply_opt && wide_t) {
+    // the summed gradient of this row, claimed by exactly one thread (and left zero); its state
+    // was prefetched at the start (no other thread touches the row before the claim)
+    const float g = atomicExch(A.grad + wrow, 0.f);
+    if (g != 0.f) {
+      float z = wz, n = wn, s3 = 0.f;
+      const float w = upd<6>(wv, g * A.ftrl.gscale, z, n, s3, A.ftrl, 1.f, 1.f);
+      A.master[wrow] = w;
+      A.ftrl_z[wrow] = z;
+      A.ftrl_n[wrow] = n;
+      if (A.shadow) A.shadow[wrow] = f2bf(w);
     }
   }
   if (tid == 0) {
@@ -300,11 +325,14 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     }
     if (A.cursor) A.cursor[0] = (bi + 1) % A.nbatch;
   }
+  wd_mark(A, 19);
 }
 
 int wd_fill(WideDeepArgs& a, const uint64_t* p, int np, const long* iv, int ni, const float* fv, int nf) {
   // ptrs: master grad shadow ada_s ftrl_z ftrl_n dense cat label cursor loss correct step_ada step_ftrl rng
-  if (np != 15 || nf != 16) return -2;
+  if (np != 17 || nf != 16) return -2;
+  a.dbg = (unsigned long long*)p[15];
+  a.slot = (const int*)p[16];
   a.master = (float*)p[0];
   a.grad = (float*)p[1];
   a.shadow = (bf16_raw*)p[2];
@@ -348,14 +376,38 @@ int wd_fill(WideDeepArgs& a, const uint64_t* p, int np, const long* iv, int ni, 
 // layer has one output, and a wave's dX tiles fit its register budget.
 extern "C" long hopsx_widedeep_step_lds(const long* iv, int ni) {
   WideDeepArgs a{};
-  const uint64_t p[15] = {};
+  const uint64_t p[17] = {};
   const float f[16] = {};
-  if (wd_fill(a, p, 15, iv, ni, f, 16)) return -1;
-  if (a.dims[a.L] != 1) return -1;
-  for (int l = 1; l < a.L; ++l)
-    if ((a.Bp / 16) * (pad16(a.dims[l]) / 16) > WD_WAVES * WD_MAXT) return -1;
-  const long bytes = (long)wd_layout(a).total * 4;
+  if (wd_fill(a, p, 17, iv, ni, f, 16)) return -1;
+  if (a.dims[a.L] != 1 || (long)a.B * a.nwide > WD_THREADS || a.B > WD_THREADS) return -1;
+  if (a.boff[a.L - 1] + a.dims[a.L] - a.woff[0] > (long)WD_PF * WD_THREADS) return -1;
+  for (int l = 0; l < a.L; ++l) {
+    const int tn = dpad(a.dims[l]) / 16;
+    if ((a.Bp / 16) * tn > WD_WAVES * WD_MAXT || (dpad(a.dims[l + 1]) / 16) * tn > WD_WAVES * WD_MAXT) return -1;
+  }
+  const long bytes = (long)wd_layout(a, a.L).total * 4;
   return bytes <= WD_LDS_MAX ? bytes : -1;
+}
+
+// The slot table the kernel reads: LDS float offset of every deep arena element (weights
+// W_l[o][i] -> W image row o col i, biases -> bias image), -1 for the arena's alignment padding.
+extern "C" int hopsx_widedeep_slots(const long* iv, int ni, int* out, long n) {
+  WideDeepArgs a{};
+  const uint64_t p[17] = {};
+  const float f[16] = {};
+  if (wd_fill(a, p, 17, iv, ni, f, 16)) return -2;
+  const Lay Ly = wd_layout(a, a.L);
+  const long lo = a.woff[0];
+  if (a.boff[a.L - 1] + a.dims[a.L] - lo != n) return -2;
+  for (long x = 0; x < n; ++x) out[x] = -1;
+  for (int l = 0; l < a.L; ++l) {
+    const int in = a.dims[l], out_ = a.dims[l + 1];
+    for (int o = 0; o < out_; ++o) {
+      const int row = Ly.w[l] + o * (dpad(in) + 1);
+      for (int i = 0; i <= in; ++i) out[(i < in ? a.woff[l] + (long)o * in + i : a.boff[l] + o) - lo] = row + i;
+    }
+  }
+  return 0;
 }
 
 extern "C" int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
@@ -364,11 +416,20 @@ extern "C" int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv,
   if (wd_fill(a, ptrs, np, iv, ni, fv, nf)) return -2;
   const long bytes = hopsx_widedeep_step_lds(iv, ni);
   if (bytes < 0) return -2;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)widedeep_step_k, hipFuncAttributeMaxDynamicSharedMemorySize, WD_LDS_MAX);
-    attr = true;
+  static bool attr[WD_MAXL + 1] = {};
+#define HOPSX_WD(NLV)                                                                                           \
+  case NLV:                                                                                                     \
+    if (!attr[NLV]) {                                                                                           \
+      hipFuncSetAttribute((const void*)widedeep_step_k<NLV>, hipFuncAttributeMaxDynamicSharedMemorySize,        \
+                          WD_LDS_MAX);                                                                          \
+      attr[NLV] = true;                                                                                         \
+    }                                                                                                           \
+    hipLaunchKernelGGL(widedeep_step_k<NLV>, dim3(1), dim3(WD_THREADS), (size_t)bytes, st, a);                 \
+    break;
+  switch (a.L) {
+    HOPSX_WD(1) HOPSX_WD(2) HOPSX_WD(3) HOPSX_WD(4) HOPSX_WD(5) HOPSX_WD(6) HOPSX_WD(7) HOPSX_WD(8)
+    default: return -2;
   }
-  hipLaunchKernelGGL(widedeep_step_k, dim3(1), dim3(WD_THREADS), (size_t)bytes, st, a);
+#undef HOPSX_WD
   return (int)hipGetLastError();
 }

@@ -117,11 +117,15 @@ class FusedWideDeepStep:
             optimizer.grad_scale = dp.grad_scale()
         self._graph = None
         self._key = None
+        self._slot_cache = {}
         self._n = 0
         dev = self.arena.device
         self.loss = torch.zeros(1, device=dev)
         self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
         self.cursor = torch.zeros(1, device=dev, dtype=torch.int64)
+        # HOPSX_PHASE_DBG=1: the kernel stamps its phase boundaries here (tools/dbg_widedeep.py)
+        self.dbg = (torch.zeros(20, device=dev, dtype=torch.int64)
+                    if os.environ.get("HOPSX_PHASE_DBG") == "1" else None)
 
     def _ints(self, B: int, nbatch: int) -> list[int]:
         L = len(self.lins)
@@ -134,6 +138,21 @@ class FusedWideDeepStep:
         dev = self.arena.device
         return (dev.type == "cuda" and self.acts_ok and self.dims[-1] == 1
                 and _C.ext().widedeep_step_lds(self._ints(B, 1)) > 0)
+
+    def _slots(self, B: int):
+        """Host-built table: LDS slot of every deep arena element for batch size B (cached)."""
+        from ..ops import _C
+        from ..ops.kernels import check
+
+        t = self._slot_cache.get(B)
+        if t is None:
+            lo = int(self.lins[0].weight._hx_off)
+            hi = int(self.lins[-1].bias._hx_off) + self.dims[-1]
+            host = torch.empty(hi - lo, dtype=torch.int32)
+            check(_C.ext().widedeep_slots(self._ints(B, 1), host.data_ptr(), hi - lo), "widedeep_slots")
+            t = host.to(self.arena.device)
+            self._slot_cache[B] = t
+        return t
 
     def _floats(self) -> list[float]:
         def pad8(v):
@@ -152,7 +171,8 @@ class FusedWideDeepStep:
         ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
         ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")), ptr(a.state("ftrl_s0")),
                 ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label), ptr(cursor), ptr(self.loss),
-                ptr(self.correct), ptr(self.ada.step_count), ptr(self.ftrl.step_count), ptr(rng_state(a.device))]
+                ptr(self.correct), ptr(self.ada.step_count), ptr(self.ftrl.step_count), ptr(rng_state(a.device)),
+                ptr(self.dbg), ptr(self._slots(dense.shape[-2]))]
         check(_C.ext().widedeep_step(ptrs, self._ints(dense.shape[-2], nbatch), self._floats(), stream()),
               "widedeep_step")
 
@@ -188,6 +208,7 @@ class FusedWideDeepStep:
             self._finish()
         else:
             if self._key != key:  # new data or hyper-parameters (e.g. an lr schedule): recapture
+                self._slots(dense.shape[-2])  # host->device copy of the slot table must precede capture
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):

@@ -27,7 +27,7 @@ def _cpu_reference(model_state, dense, cat, label, steps):
     return losses, m._hx_arena.master.clone()
 
 
-@pytest.mark.parametrize("B,graph", [(40, True), (40, False), (64, True), (13, True)])
+@pytest.mark.parametrize("B,graph", [(40, True), (40, False), (48, True), (13, True)])
 def test_fused_widedeep_step_matches_fp32_reference(B, graph):
     torch.manual_seed(0)
     nb, steps = 4, 10
@@ -85,3 +85,12 @@ def test_fused_widedeep_step_dp_gradients_match_layerwise():
     got = torch.cat([fused[p._hx_off:p._hx_off + p.numel()].cpu()
                      for p in [m.wide.weight] + [q for q in m.deep.parameters()]])
     torch.testing.assert_close(got, ref, rtol=1e-3, atol=1e-6)
+
+
+def test_fused_widedeep_step_declines_batches_beyond_lds():
+    """B > 48 pads to 64 rows, whose activations + gradients no longer fit one workgroup's 160 KB LDS:
+    the fused step declines and bench_taxi / the trainer run the generic TrainStep path instead."""
+    g = WD.TaxiWideDeep().to(dev)
+    ParamArena.from_module(g, dev)
+    fs = WD.FusedWideDeepStep(g, WD.make_optimizer(g))
+    assert fs.ok(48) and not fs.ok(64)
