@@ -23,6 +23,7 @@ from . import kernels as K
 from ._C import ACT, LOSS
 
 BF16 = torch.bfloat16
+F32 = torch.float32
 
 
 def _cpu_act(y, act):
