@@ -36,8 +36,11 @@ def timed(fn, n, dev):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(n):
-        fn(i)
+    if hasattr(fn, "run_n"):
+        fn.run_n(n)  # n steps, replayed steps_per_execution at a time
+    else:
+        for i in range(n):
+            fn(i)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     hdist.barrier()

@@ -121,3 +121,44 @@ def test_deferred_logits_layer_matches_eager_head(monkeypatch, model):
         return
     # logits rounded from a different fp32 summation order: bf16 ties flip on a few elements
     torch.testing.assert_close(runs[0][1], runs[1][1], rtol=1e-2, atol=5e-3)
+
+
+def test_steps_per_execution_matches_single_step_replays():
+    """TrainStep.run_resident: U = steps_per_execution steps captured in one graph (each step's
+    optimizer prefetches the next batch) trains like U one-step replays: same device cursor, the
+    next batch staged in the static inputs, same loss, and a weight trajectory that differs from the
+    one-step replays no more than two one-step runs differ from each other (split-K fp32 atomics
+    + bf16 shadow rounding make repeated runs diverge by a few %; tools/dbg_spe.py measures it)."""
+    from hops_examples_amd import optim
+    from hops_examples_amd.runtime.step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    B, nb, n = 32, 6, 4 + 8 + 3  # eager warm-up + capture, one U-graph replay, a ragged tail
+    xs = torch.randint(0, 256, (nb, B, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (nb, B), device=dev)
+    runs = []
+    for multi in (True, False, False):
+        HF.seed_device_rng(11, dev)
+        torch.manual_seed(0)
+        m = MirroredMnistCNN().to(dev)
+        m.pool.salt = 7919
+        ParamArena.from_module(m, dev)
+        w0 = m._hx_arena.master.clone()
+        st = TrainStep(m, optim.SGD(m, lr=0.05), "sparse_ce", steps_per_execution=8)
+        if multi:
+            r = st.run_resident(xs, ys, n)
+            assert st._gU is not None
+        else:
+            for _ in range(n):
+                r = st.step_resident(xs, ys)
+        torch.cuda.synchronize()
+        assert int(st._cursor.item()) == n % nb
+        assert torch.equal(st._sx, xs[n % nb]) and torch.equal(st._sy, ys[n % nb])
+        runs.append((float(r["loss"].reshape(-1)[0]), m._hx_arena.master - w0))
+    assert abs(runs[0][0] - runs[1][0]) <= 2e-3 * abs(runs[1][0])
+
+    def rel(a, b):
+        return float((a - b).norm()) / float(b.norm())
+
+    noise = rel(runs[2][1], runs[1][1])
+    assert rel(runs[0][1], runs[1][1]) <= 3 * noise + 0.05, (rel(runs[0][1], runs[1][1]), noise)

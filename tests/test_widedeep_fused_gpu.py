@@ -94,3 +94,32 @@ def test_fused_widedeep_step_declines_batches_beyond_lds():
     ParamArena.from_module(g, dev)
     fs = WD.FusedWideDeepStep(g, WD.make_optimizer(g))
     assert fs.ok(48) and not fs.ok(64)
+
+
+def test_fused_widedeep_steps_per_execution_matches_single_launches():
+    """run_resident replays U fused-step launches per graph: cursor, loss and weights equal those of
+    U one-launch replays."""
+    B, nb, n = 40, 5, 1 + 3 * 8 + 2
+    dense, cat, label = WD.synth_taxi(nb * B, seed=9)
+    xs = (dense.view(nb, B, -1).to(dev), cat.view(nb, B, -1).to(dev))
+    ys = label.view(nb, B, 1).to(dev)
+    state = {k: v.clone() for k, v in WD.TaxiWideDeep().state_dict().items()}
+    runs = []
+    for multi in (True, False):
+        g = WD.TaxiWideDeep()
+        g.load_state_dict(state)
+        g = g.to(dev)
+        ParamArena.from_module(g, dev)
+        fs = WD.FusedWideDeepStep(g, WD.make_optimizer(g))
+        fs.steps_per_execution = 8
+        if multi:
+            r = fs.run_resident(xs, ys, n)
+            assert fs._graphU is not None
+        else:
+            for _ in range(n):
+                r = fs.step_resident(xs, ys)
+        torch.cuda.synchronize()
+        assert int(fs.cursor.item()) == n % nb
+        runs.append((float(r["loss"].reshape(-1)[0]), g._hx_arena.master.clone()))
+    assert runs[0][0] == pytest.approx(runs[1][0], rel=1e-5)
+    torch.testing.assert_close(runs[0][1], runs[1][1], rtol=1e-5, atol=1e-6)
