@@ -42,6 +42,28 @@ def test_jobs_lifecycle(project_root):
     assert [j["name"] for j in jobs.get_jobs()] == ["bad", "pi"]
 
 
+def test_flink_runner_lifecycle_runs_pipeline_as_job(project_root):
+    """hops.beam runner lifecycle (jobs-client/flink/jobs_flink_client.py:45-51): a pipeline is only
+    accepted by a RUNNING runner and executes as a tracked job."""
+    from hops_examples_amd import beam, jobs
+
+    app = _prog(project_root, "wordcount.py", """
+        import collections, sys
+        words = "the quick brown fox jumps over the lazy dog the end".split()
+        print(dict(collections.Counter(words).most_common(1)))
+    """)
+    cfg = beam.create_runner("flinkrunner", num_of_taskmanagers=2, num_task_slots=4)
+    assert cfg["state"] == "CREATED" and beam.get_runner_state("flinkrunner") == "CREATED"
+    with pytest.raises(RuntimeError):
+        beam.run_pipeline("flinkrunner", app)
+    beam.start_runner("flinkrunner")
+    ex = beam.run_pipeline("flinkrunner", app)
+    st = jobs.wait_for_execution("flinkrunner-pipeline", ex["id"], timeout=60)
+    assert st["finalStatus"] == "SUCCEEDED"
+    assert "{'the': 3}" in jobs.get_logs("flinkrunner-pipeline")
+    assert beam.stop_runner("flinkrunner")["state"] == "STOPPED"
+
+
 def test_dag_job_chain_and_failure_propagation(project_root):
     from hops_examples_amd import jobs
     from hops_examples_amd.orchestration import DAG, HopsworksJobSuccessSensor, HopsworksLaunchOperator
