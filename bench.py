@@ -142,7 +142,8 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "hipgraph": not a.no_graph,
-                "steps_per_execution": step.steps_per_execution if world == 1 else 1,
+                "steps_per_execution": step.steps_per_execution if step._gU is not None else 1,
+                "allreduce": ("oneshot-xgmi" if getattr(dp, "_oneshot", None) is not None else "rccl") if dp else None,
             },
             "final_loss": round(loss, 4),
             "chicago_taxi": taxi,

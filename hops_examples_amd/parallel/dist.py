@@ -33,7 +33,9 @@ def init(backend: str | None = None, timeout_s: float = 600.0) -> tuple[int, int
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # HOPSX_DIST_BACKEND=gloo rehearses the multi-rank GPU path with several ranks on one
+            # GPU (RCCL refuses two ranks per device); production is RCCL ("nccl")
+            backend = os.environ.get("HOPSX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {}
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())

@@ -20,12 +20,15 @@ Modes (the three strategies the reference names):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 from ..runtime import hooks
 from ..runtime.arena import ParamArena
 from . import dist as hdist
+from . import oneshot
 
 MB = 1 << 20
 
@@ -74,6 +77,11 @@ class DataParallel:
         self._handles: list = []
         self._launched = [False] * len(self.buckets)
         self.grad_dtype = grad_dtype
+        # one-shot xGMI all-reduce (parallel/oneshot.py) for buckets that fit its staging buffer
+        self._oneshot = None
+        if self.world > 1 and oneshot.enabled() and self.arena.grad.is_cuda:
+            self._oneshot = oneshot.OneShotAllReduce(cap_bytes=int(os.environ.get("HOPSX_ONESHOT_MB", "8")) * MB,
+                                                     device=self.arena.grad.device)
         if broadcast and self.world > 1:
             self.broadcast_params()
         if self.overlap:
@@ -89,7 +97,9 @@ class DataParallel:
             return
         s, e, _ = self._launched_bucket(bi)
         view = self.arena.grad[s:e]
-        if self.grad_dtype == torch.bfloat16:
+        if self._oneshot is not None and self._oneshot.fits(view):
+            self._oneshot(view)  # stream-ordered: later kernels see the reduced bucket
+        elif self.grad_dtype == torch.bfloat16:
             # compressed all-reduce: bf16 on the wire, fp32 master accumulate
             tmp = view.to(torch.bfloat16)
             h = dist.all_reduce(tmp, async_op=True)
@@ -129,10 +139,22 @@ class DataParallel:
         if self.world <= 1:
             return
         for s, e, _ in self.buckets:
-            dist.all_reduce(self.arena.grad[s:e])
+            view = self.arena.grad[s:e]
+            if self._oneshot is not None and self._oneshot.fits(view):
+                self._oneshot(view)
+            else:
+                dist.all_reduce(view)
+
+    def capturable(self) -> bool:
+        """Every bucket goes through the one-shot kernel (no RCCL call), so the whole step,
+        all-reduce included, can live in one hipGraph (runtime/step.py)."""
+        return self._oneshot is not None and all(self._oneshot.fits(self.arena.grad[s:e]) for s, e, _ in self.buckets)
 
     def grad_scale(self) -> float:
         return 1.0 / self.world
 
     def close(self) -> None:
         hooks.unsubscribe(self._on_ready)
+        if self._oneshot is not None:
+            self._oneshot.close()
+            self._oneshot = None

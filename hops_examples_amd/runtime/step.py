@@ -81,6 +81,8 @@ class TrainStep:
         self._pool = None
         if dp is not None:
             optimizer.grad_scale = dp.grad_scale()
+            if getattr(dp, "capturable", lambda: False)():
+                self.graph_collectives = True  # one-shot all-reduce kernels capture like any other
 
     # ------------------------------------------------------------- eager path
     def _forward(self, x):
