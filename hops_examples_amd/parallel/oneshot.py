@@ -1,4 +1,4 @@
-"""One-shot all-reduce for small messages over IPC-mapped peer buffers (``_hopsx_comm``).
+"""One-shot / two-shot all-reduce for small and mid-size messages over IPC-mapped peer buffers (``_hopsx_comm``).
 
 SURVEY §5.8 item 3 / §2.4: a ring all-reduce needs 2(N-1) latency-bound hops, but MI355X wires
 every GPU to its 7 peers directly over xGMI, so below ~1 MB one hop is cheaper: each rank stages
@@ -52,8 +52,11 @@ class OneShotAllReduce:
         self.device = device or hdist.device()
         self.cap = (int(cap_bytes) // 4 + 3) & ~3
         self.blocks = max(1, min(int(blocks), C.MAX_BLOCKS))
-        self._buf, hb = C.alloc(2 * self.cap * 4, False)
-        self._flag, hf = C.alloc(C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
+        self._buf, hb = C.alloc(4 * self.cap * 4, False)
+        self._flag, hf = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
+        # two-shot (reduce-scatter + all-gather) above this size when N > 2: 2(N-1)/N * n of xGMI
+        # reads per GPU instead of (N-1) * n
+        self.two_shot_min = int(os.environ.get("HOPSX_TWOSHOT_MIN_KB", "256")) * 1024 // 4
         self._opened: list[int] = []
         if self.world > 1:
             objs = [None] * self.world
@@ -76,7 +79,10 @@ class OneShotAllReduce:
         return (t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= self.cap
                 and t.data_ptr() % 16 == 0)
 
-    def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def mode(self, n: int) -> str:
+        return "two_shot" if self.world > 2 and n >= self.two_shot_min else "one_shot"
+
+    def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None, mode: str | None = None) -> torch.Tensor:
         """In place by default; identical (rank-ordered) sums on every rank."""
         if not self.fits(t):
             raise ValueError("tensor must be contiguous fp32, 16-B aligned and within the staging capacity")
@@ -85,7 +91,8 @@ class OneShotAllReduce:
             raise ValueError("bad output tensor")
         st = torch.cuda.current_stream(self.device).cuda_stream
         ext().allreduce_f32(t.data_ptr(), out.data_ptr(), t.numel(), self.cap, self.rank, self.world,
-                            self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(), self.blocks, st)
+                            self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(), self.blocks, st,
+                            (mode or self.mode(t.numel())) == "two_shot")
         return out
 
     def check(self) -> None:

@@ -34,19 +34,21 @@ def main():
     dev = hdist.device()
     ar = OneShotAllReduce(cap_bytes=8 << 20, device=dev)
     res = {"world": world, "checks": 0}
+    modes = ("one_shot", "two_shot")
     for it, n in enumerate([1, 3, 4, 5, 257, 1000, 18866, 65536 + 7, 1394282, ar.cap]):
-        xs, ref = inputs(n, world, it, dev)
-        x = xs[rank].clone()
-        ar(x)
-        torch.cuda.synchronize()
-        ar.check()
-        assert torch.equal(x, ref), (rank, n, (x - ref).abs().max().item())
-        res["checks"] += 1
+        for mode in modes:  # interleaved modes share the epoch/parity staging layout
+            xs, ref = inputs(n, world, it, dev)
+            x = xs[rank].clone()
+            ar(x, mode=mode)
+            torch.cuda.synchronize()
+            ar.check()
+            assert torch.equal(x, ref), (rank, n, mode, (x - ref).abs().max().item())
+            res["checks"] += 1
     # out-of-place + repeated calls of the same size (double-buffer reuse)
     for it in range(20):
         xs, ref = inputs(4099, world, 100 + it, dev)
         out = torch.empty_like(ref)
-        ar(xs[rank], out)
+        ar(xs[rank], out, mode=modes[it % 2])
         torch.cuda.synchronize()
         assert torch.equal(out, ref), (rank, it)
         res["checks"] += 1
@@ -68,16 +70,17 @@ def main():
     ar.check()
     # timing (kernel + launch, back-to-back on one stream)
     for label, n in (("taxi_grads_75KB", 18866), ("mnist_grads_5.58MB", 1394282), ("metrics_16B", 4)):
-        t = torch.randn(n, device=dev)
-        for _ in range(20):
-            ar(t)
-        hdist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(200):
-            ar(t)
-        torch.cuda.synchronize()
-        res[f"us_per_call_{label}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+        for mode in modes:
+            t = torch.randn(n, device=dev)
+            for _ in range(20):
+                ar(t, mode=mode)
+            hdist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(200):
+                ar(t, mode=mode)
+            torch.cuda.synchronize()
+            res[f"us_per_call_{label}_{mode}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
     ar.check()
     ar.close()
     if rank == 0:
