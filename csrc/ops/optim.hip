@@ -156,7 +156,10 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
   const bool aligned = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)s3) % 16 == 0 &&
                        ((uintptr_t)shadow_bf16 % 8 == 0);
   long g = ((aligned ? n / 4 : n) + 255) / 256;
-  static const int gcap = getenv("HOPSX_OPT_GRID") ? atoi(getenv("HOPSX_OPT_GRID")) : 512;
+  // grid cap: 256 workgroups (one per CU) measured best for the 1.4 M-parameter flagship
+  // (0.0894 -> 0.0878 ms/step; 128: 0.0899, 512: 0.0894, 1024: 0.0946); larger arenas keep 512
+  static const int genv = getenv("HOPSX_OPT_GRID") ? atoi(getenv("HOPSX_OPT_GRID")) : 0;
+  const int gcap = genv > 0 ? genv : (n <= (8L << 20) ? 256 : 512);
   if (g > gcap) g = gcap;
   if (g < 1) g = 1;
   bf16_raw* sh = (bf16_raw*)shadow_bf16;

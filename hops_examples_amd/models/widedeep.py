@@ -28,6 +28,8 @@ import os
 
 import numpy as np
 import torch
+
+from ..runtime.capture import graph as _capture_graph
 from torch import nn
 
 from .. import nn as hnn
@@ -214,7 +216,7 @@ class FusedWideDeepStep:
                 self._slots(dense.shape[-2])  # host->device copy of the slot table must precede capture
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with _capture_graph(g):
                     self._launch(dense, cat, ys, dense.shape[0], self.cursor)
                 self._graph, self._key = g, key
                 # capture does not execute: run this step through the graph
@@ -232,7 +234,7 @@ class FusedWideDeepStep:
             self._slots(dense.shape[-2])
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _capture_graph(g):
                 for _ in range(U):
                     self._launch(dense, cat, ys, dense.shape[0], self.cursor)
             self._graphU, self._keyU = g, key

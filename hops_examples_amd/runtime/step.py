@@ -25,6 +25,8 @@ import os
 
 import torch
 
+from .capture import graph as _capture_graph
+
 from ..ops import functional as HF
 from ..parallel import dist as hdist
 from . import health
@@ -146,7 +148,7 @@ class TrainStep:
             hooks.unsubscribe(self.dp._on_ready)
         pool = self._pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=pool):
+        with _capture_graph(g1, pool=pool):
             out = self._fwd_bwd(self._sx, self._sy)
             if world == 1 or self.dp is None or self.graph_collectives:
                 if self.dp is not None:
@@ -157,7 +159,7 @@ class TrainStep:
         self._g1 = g1
         if world > 1 and self.dp is not None and not self.graph_collectives:
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=pool):
+            with _capture_graph(g2, pool=pool):
                 self._opt()
             self._g2 = g2
         self._out = out
@@ -202,7 +204,7 @@ class TrainStep:
         self._pf_opt.prefetch = ([(xs, self._sx), (ys, self._sy)], self._cursor)
         try:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._pool):
+            with _capture_graph(g, pool=self._pool):
                 for _ in range(self.steps_per_execution):
                     out = self._fwd_bwd(self._sx, self._sy)
                     if self.dp is not None:
