@@ -40,13 +40,19 @@ constexpr int nstate() {
   return KIND == 0 ? 1 : (KIND == 4 ? 3 : (KIND == 5 ? 1 : 2));
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ inline void st_nt(float* dst, long i, const float4& v) {
+  const f4v x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(dst) + i);
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __restrict__ g, float* __restrict__ s1,
                                                float* __restrict__ s2, float* __restrict__ s3,
                                                bf16_raw* __restrict__ shadow, long n, OptHP h,
                                                float* __restrict__ step_dev, unsigned* __restrict__ arrive,
                                                unsigned long long* __restrict__ rng, int zero_grad, int vec,
-                                               Prefetch pf) {
+                                               Prefetch pf, int nt) {
   // step_dev holds the number of COMPLETED steps; this step is t = step + 1.
   // Every workgroup reads it before its final barrier; the last workgroup to
   // finish bumps it (and the dropout RNG counter).
@@ -84,10 +90,19 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
       ww.y = upd<KIND>(ww.y, gr[u].y * h.gscale, aa.y, bb.y, cc.y, h, bc1, bc2);
       ww.z = upd<KIND>(ww.z, gr[u].z * h.gscale, aa.z, bb.z, cc.z, h, bc1, bc2);
       ww.w = upd<KIND>(ww.w, gr[u].w * h.gscale, aa.w, bb.w, cc.w, h, bc1, bc2);
-      ((float4*)p)[i] = ww;
-      if (NS >= 1) ((float4*)s1)[i] = aa;
-      if (NS >= 2) ((float4*)s2)[i] = bb;
-      if (NS >= 3) ((float4*)s3)[i] = cc;
+      if (nt) {
+        // master and optimizer state are next read by this kernel one step later: stream them
+        // past L2 so the shadow, the zeroed grad and the activations keep it
+        st_nt(p, i, ww);
+        if (NS >= 1) st_nt(s1, i, aa);
+        if (NS >= 2) st_nt(s2, i, bb);
+        if (NS >= 3) st_nt(s3, i, cc);
+      } else {
+        ((float4*)p)[i] = ww;
+        if (NS >= 1) ((float4*)s1)[i] = aa;
+        if (NS >= 2) ((float4*)s2)[i] = bb;
+        if (NS >= 3) ((float4*)s3)[i] = cc;
+      }
       if (shadow) {
         const uint32_t lo = (uint32_t)f2bf(ww.x) | ((uint32_t)f2bf(ww.y) << 16);
         const uint32_t hi = (uint32_t)f2bf(ww.z) | ((uint32_t)f2bf(ww.w) << 16);
@@ -160,6 +175,7 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
   // (0.0894 -> 0.0878 ms/step; 128: 0.0899, 512: 0.0894, 1024: 0.0946); larger arenas keep 512
   static const int genv = getenv("HOPSX_OPT_GRID") ? atoi(getenv("HOPSX_OPT_GRID")) : 0;
   const int gcap = genv > 0 ? genv : (n <= (8L << 20) ? 256 : 512);
+  static const int nt = getenv("HOPSX_OPT_NT") ? atoi(getenv("HOPSX_OPT_NT")) : 0;
   if (g > gcap) g = gcap;
   if (g < 1) g = 1;
   bf16_raw* sh = (bf16_raw*)shadow_bf16;
@@ -168,7 +184,7 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
 #define OPT_CASE(K)                                                                                                   \
   case K:                                                                                                             \
     hipLaunchKernelGGL(optim_k<K>, dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, arr, rng, \
-                       zero_grad, (int)aligned, pf);                                                                  \
+                       zero_grad, (int)aligned, pf, nt);                                                              \
     break;
   switch (kind) {
     OPT_CASE(0) OPT_CASE(1) OPT_CASE(2) OPT_CASE(3) OPT_CASE(4) OPT_CASE(5) OPT_CASE(6)
