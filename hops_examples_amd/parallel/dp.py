@@ -142,6 +142,11 @@ class DataParallel:
             view = self.arena.grad[s:e]
             if self._oneshot is not None and self._oneshot.fits(view):
                 self._oneshot(view)
+            elif self.grad_dtype == torch.bfloat16:
+                # bf16 on the wire (half the ring bytes), fp32 arena kept as the accumulator
+                tmp = view.to(torch.bfloat16)
+                dist.all_reduce(tmp)
+                view.copy_(tmp)
             else:
                 dist.all_reduce(view)
 

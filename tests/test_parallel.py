@@ -103,3 +103,36 @@ def test_bucket_plan():
     assert b[-1][0] == 0 and b[0][1] == big.numel
     assert all(s < e for s, e, _ in b) and all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
     assert 2 <= len(b) <= 4
+
+
+def _bf16_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from hops_examples_amd.parallel import dist as hdist
+    from hops_examples_amd.parallel.dp import DataParallel
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    hdist.init(backend="gloo")
+    m = _model()
+    ParamArena.from_module(m)
+    dp = DataParallel(m, grad_dtype=torch.bfloat16)
+    dp.arena.grad.fill_(0.5 + rank)
+    dp.allreduce_all()  # the between-graph-segments path, bf16 on the wire
+    q.put((rank, dp.arena.grad.clone()))
+    hdist.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_bf16_wire_allreduce_all():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_bf16_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for g in res.values():
+        assert g.dtype == torch.float32 and torch.equal(g, torch.full_like(g, 2.0))
