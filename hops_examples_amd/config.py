@@ -11,6 +11,17 @@ Environment:
   HOPSX_USER           project user (default ``$USER``)
   HOPSX_GPUS_PER_WORKER, HOPSX_NUM_PS, HOPSX_BUCKET_MB, HOPSX_DTYPE (bf16|fp32),
   HOPSX_GRAPH (1 = capture steady-state train steps into hipGraphs)
+
+Performance / communication knobs read where they act:
+  HOPSX_STEPS_PER_EXEC  steps per hipGraph replay (runtime/step.py, default 8)
+  HOPSX_DIST_BACKEND    process-group backend override, e.g. ``gloo`` to run several ranks on
+                        one GPU (parallel/dist.py; default ``nccl`` = RCCL on GPU)
+  HOPSX_ONESHOT_AR      1 = gradient buckets on the P2P one-/two-shot all-reduce kernels
+                        (parallel/oneshot.py); HOPSX_ONESHOT_MB staging size (default 8),
+                        HOPSX_TWOSHOT_MIN_KB two-shot threshold for N > 2 (default 256)
+  HOPSX_GRAPH_COLLECTIVES  1 = capture the RCCL all-reduce inside the step graph
+  HOPSX_OPT_GRID        optimizer grid cap (default 256 workgroups up to 8 M params, else 512)
+  HOPSX_OPT_NT          1 = nontemporal master/state stores in the optimizer kernel
 """
 from __future__ import annotations
 
