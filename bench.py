@@ -11,9 +11,15 @@ Model   : the MirroredStrategy MNIST CNN of the reference
 Data    : synthetic uint8 28x28 images + labels resident in HBM (no dataset download possible).
 Scaling : weak — per-GPU batch fixed (reference: 32 x num_replicas_in_sync, :128-131).
 Step    : full training step inside the timed region — forward, fused loss, backward,
-          RCCL gradient all-reduce (world > 1), fused Adadelta update.  hipGraph replay; on one
-          GPU 8 consecutive steps per graph (Keras steps_per_execution: every step still trains on
-          its own batch, the optimizer kernel prefetches the next one).
+          gradient exchange (world > 1), fused Adadelta update.  hipGraph replay, 8 consecutive
+          steps per graph (Keras steps_per_execution: every step still trains on its own batch,
+          the last kernel of each step prefetches the next one).
+World>1 : one process per GPU.  On one node the gradient exchange is the P2P xGMI path
+          (parallel/oneshot.py): ONE kernel per step reduce-scatters the gradient over the
+          peers' IPC-mapped buffers, runs Adadelta on this rank's 1/N slice and all-gathers the
+          new weights, inside the step's hipGraph.  If any rank fails the P2P self-test, every
+          rank uses RCCL all-reduce instead; config.allreduce says which path ran.  After the
+          timed region the fp32 weights are checked bit-identical across ranks.
 
 Also measures the Chicago-taxi wide&deep trainer (steps/sec) unless --no-taxi.
 
@@ -109,6 +115,11 @@ def main():
     loss = float(out["r"]["loss"].item())
     ms = el / a.steps * 1e3
     ips = B * world * a.steps / el
+    replicas = None
+    dp_path = dp.path if dp is not None else None
+    if dp is not None:
+        replicas = dp.verify_replicas()  # outside the timed region
+        dp.close()  # collective; raises if a P2P collective failed during the run
 
     taxi = None
     if not a.no_taxi:
@@ -143,8 +154,9 @@ def main():
                 "parallelism": f"dp{world}",
                 "hipgraph": not a.no_graph,
                 "steps_per_execution": step.steps_per_execution if step._gU is not None else 1,
-                "allreduce": ("oneshot-xgmi" if getattr(dp, "_oneshot", None) is not None else "rccl") if dp else None,
+                "allreduce": dp_path,
             },
+            "replicas_identical": None if replicas is None else replicas["identical"],
             "final_loss": round(loss, 4),
             "chicago_taxi": taxi,
         }

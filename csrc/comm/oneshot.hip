@@ -1,20 +1,32 @@
-// _hopsx_comm: one-shot all-reduce over IPC-mapped peer buffers (xGMI point-to-point).
+// _hopsx_comm: collectives over IPC-mapped peer buffers (xGMI point-to-point), gfx950.
 //
-// for buffers below ~1 MB on one node a ring all-reduce is latency bound
-// (2(N-1) hops).  MI355X links every GPU to its 7 peers directly, so each rank instead
-//   1. copies its chunk into its own IPC-shared staging buffer,
-//   2. raises a per-(source rank, workgroup) flag in every peer's uncached signal page,
-//   3. waits for the same flag from every peer, then
-//   4. reads the chunk from all N staging buffers (N-1 of them over xGMI) and sums them in rank
-//      order, so every rank produces bit-identical results.
-// One launch, one hop.  Staging is double-buffered by epoch parity; a rank cannot be two epochs
-// ahead of a reader (it needs that reader's flag of the epoch in between), so reuse is safe.
-// The epoch is a per-workgroup counter in device memory (not a kernel argument), so the launch
-// can be captured in a hipGraph and replayed.  Every spin is bounded by the wall clock: a peer
-// that never arrives sets *err and the wave exits, so the grid always drains.
+// for small and mid-size messages on one node a ring all-reduce is latency
+// bound (2(N-1) hops).  MI355X links every GPU to its 7 peers directly, so instead
+//   * one-shot: each rank copies its data into its own IPC-shared staging buffer, raises a
+//     per-(source rank, workgroup) flag in every peer's uncached signal page, waits for every
+//     peer's flag, then reads all N staging buffers (N-1 of them over xGMI) and sums them in
+//     rank order, so every rank produces bit-identical results.  One launch, one hop.
+//   * two-shot: rank r reduces slice r (reduce-scatter), then gathers the other owners' reduced
+//     slices: 2(N-1)/N of the bytes per GPU instead of (N-1).
+//   * dp_step (the data-parallel training step's tail, one launch): stage + zero the gradient,
+//     reduce slice r, apply the optimizer to slice r only, publish the new fp32 weights of slice r,
+//     gather every other slice's new weights (fp32 master + bf16 shadow).  Same xGMI bytes as a
+//     two-shot all-reduce, but the optimizer touches 1/N of the parameters and there is no
+//     separate optimizer launch.  Every replica ends with the owners' bit-identical weights.
+// Staging is double-buffered by epoch parity; a rank cannot be two epochs ahead of a reader (it
+// needs that reader's flag of the epoch in between), so reuse is safe.  The epoch is a
+// per-workgroup counter in device memory (not a kernel argument), so the launches can be captured
+// in a hipGraph and replayed.
+//
+// Failure handling: every spin is bounded by the wall clock (`spin` ticks of the 100 MHz
+// counter).  A workgroup whose peer never arrives sets *err and returns WITHOUT reducing or
+// writing its output (it would read an older epoch's staging) and without advancing its epoch.
+// *err is sticky: every later launch on this rank sees it at entry and does nothing, so peers
+// time out too and every rank reports the failure (the host polls err and raises) — no rank
+// silently trains on stale sums.
 //
 // Reference parity: the reference's all-reduces are TF-internal NCCL calls under
-// MirroredStrategy; this replaces the small-message ones.
+// MirroredStrategy; these replace them on one node.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -25,6 +37,8 @@
 #include <string>
 #include <vector>
 
+#include "../ops/optim_core.h"  // upd<KIND>, OptHP, Prefetch: one definition with optim.hip
+
 namespace py = pybind11;
 using u = uintptr_t;
 
@@ -33,11 +47,16 @@ namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 128;  // <= one workgroup per CU: every block of every rank is resident
 constexpr int kThreads = 256;
-constexpr unsigned long long kSpinTicks = 400000000ull;  // ~4 s at the 100 MHz wall clock
 
 struct Peers {
   float* buf[kMaxRanks];        // staging buffers, [parity][input | reduced] = 4 * cap floats each
   unsigned* flag[kMaxRanks];    // signal pages, [3 rows][kMaxRanks][kMaxBlocks] uint32 each
+};
+
+struct Sync {
+  unsigned* epochs;  // int32[kMaxBlocks] device counters (zeroed once)
+  int* err;          // sticky device error flag: 1 + the rank that never arrived
+  long long spin;    // wall-clock ticks (100 MHz) a workgroup waits for a peer
 };
 
 #define HIP_OK(x)                                                                  \
@@ -46,35 +65,33 @@ struct Peers {
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
 
-__global__ __launch_bounds__(kThreads) void oneshot_ar_k(const float* __restrict__ in, float* out, long n,
-                                                         long cap, int rank, int world, Peers peers,
-                                                         unsigned* epochs, int* err) {
-  const int b = blockIdx.x, G = gridDim.x, t = threadIdx.x;
-  const unsigned e = epochs[b] + 1;
-  const long off = (long)(e & 1u) * 2 * cap;  // same parity layout as two-shot (modes may mix)
-  // 16-B aligned chunk per workgroup
-  long per = (n + G - 1) / G;
-  per = (per + 3) & ~3L;
-  const long lo = (long)b * per, hi = lo + per < n ? lo + per : n;
+// workgroup-uniform: has an earlier launch on this rank failed?
+__device__ inline bool poisoned(const int* err) {
+  __shared__ int s_err;
+  if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return s_err != 0;
+}
 
-  float* mine = peers.buf[rank] + off;
-  for (long i = lo + 4L * t; i < hi; i += 4L * kThreads) {
-    if (i + 3 < hi) {
-      *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(in + i);
-    } else {
-      for (long j = i; j < hi; ++j) mine[j] = in[j];
-    }
-  }
+// Raise flag row `row` for this workgroup in every peer's page, then wait for every peer's.
+// Returns false (workgroup-uniform) when a peer did not arrive within the spin bound.
+__device__ inline bool flag_round(const Peers& peers, int rank, int world, int row, int b, unsigned e,
+                                  const Sync& sy) {
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
   // every wave publishes its own stores system-wide before the flags go out
   __threadfence_system();
   __syncthreads();
+  const int t = threadIdx.x;
   if (t < world) {
-    __hip_atomic_store(peers.flag[t] + rank * kMaxBlocks + b, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned* f = peers.flag[rank] + t * kMaxBlocks + b;
+    const int slot = (row * kMaxRanks + rank) * kMaxBlocks + b;
+    __hip_atomic_store(peers.flag[t] + slot, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* f = peers.flag[rank] + (row * kMaxRanks + t) * kMaxBlocks + b;
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      if (wall_clock64() - t0 > kSpinTicks) {
-        atomicExch(err, 1 + t);
+      if ((long long)(wall_clock64() - t0) > sy.spin) {
+        atomicExch(sy.err, 1 + t);
+        bad = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -82,27 +99,10 @@ __global__ __launch_bounds__(kThreads) void oneshot_ar_k(const float* __restrict
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system-scope acquire for every wave before the peer reads
-
-  for (long i = lo + 4L * t; i < hi; i += 4L * kThreads) {
-    if (i + 3 < hi) {
-      float4 s = *reinterpret_cast<const float4*>(peers.buf[0] + off + i);
-      for (int p = 1; p < world; ++p) {
-        const float4 v = *reinterpret_cast<const float4*>(peers.buf[p] + off + i);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      *reinterpret_cast<float4*>(out + i) = s;
-    } else {
-      for (long j = i; j < hi; ++j) {
-        float s = peers.buf[0][off + j];
-        for (int p = 1; p < world; ++p) s += peers.buf[p][off + j];
-        out[j] = s;
-      }
-    }
-  }
-  if (t == 0) epochs[b] = e;
+  return bad == 0;
 }
 
-// copy / reduce helpers over [lo, hi) with 16-B lanes and a scalar tail
+// copy over [lo, hi) with 16-B lanes and a scalar tail
 __device__ inline void copy_range(float* dst, const float* src, long lo, long hi) {
   for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
     if (i + 3 < hi) {
@@ -113,83 +113,228 @@ __device__ inline void copy_range(float* dst, const float* src, long lo, long hi
   }
 }
 
-// raise flag row `row` for this workgroup in every peer's page, then wait for every peer's
-__device__ inline void flag_round(const Peers& peers, int rank, int world, int row, int b, unsigned e, int* err) {
-  __threadfence_system();
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < world) {
-    const int slot = (row * kMaxRanks + rank) * kMaxBlocks + b;
-    __hip_atomic_store(peers.flag[t] + slot, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned* f = peers.flag[rank] + (row * kMaxRanks + t) * kMaxBlocks + b;
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      if (wall_clock64() - t0 > kSpinTicks) {
-        atomicExch(err, 1 + t);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
+// s = sum over ranks 0..world-1 (in rank order) of buf[p][off + i .. i+3]
+__device__ inline float4 sum4(const Peers& peers, int world, long off) {
+  float4 s = *reinterpret_cast<const float4*>(peers.buf[0] + off);
+  for (int p = 1; p < world; ++p) {
+    const float4 v = *reinterpret_cast<const float4*>(peers.buf[p] + off);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
-  __syncthreads();
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return s;
+}
+__device__ inline float sum1(const Peers& peers, int world, long off) {
+  float s = peers.buf[0][off];
+  for (int p = 1; p < world; ++p) s += peers.buf[p][off];
+  return s;
 }
 
-// Two-shot (reduce-scatter + all-gather over P2P) for mid-size messages: rank r owns slice r and
-// reduces it (reading (N-1)/N of the data from peers), then every rank gathers the other owners'
-// reduced slices.  Per-GPU xGMI traffic 2(N-1)/N * n instead of (N-1) * n for one-shot.
-// Staging per rank: [parity][input | reduced] of cap floats each; flag rows 1 and 2.
-__global__ __launch_bounds__(kThreads) void twoshot_ar_k(const float* __restrict__ in, float* out, long n,
-                                                         long cap, int rank, int world, Peers peers,
-                                                         unsigned* epochs, int* err) {
-  const int b = blockIdx.x, G = gridDim.x;
-  const unsigned e = epochs[b] + 1;
-  const long base = (long)(e & 1u) * 2 * cap;
-  long L = (n + world - 1) / world;
-  L = (L + 3) & ~3L;
-  long per = (L + G - 1) / G;
-  per = (per + 3) & ~3L;
-  auto sub = [&](int slice, long& lo, long& hi) {
+// Slice geometry shared by two-shot and dp_step: slice s = [s*L, (s+1)*L) (L a multiple of 4),
+// workgroup b owns [s*L + b*per, ...) of every slice, clipped to the slice and to n.
+struct Slices {
+  long L, per, n;
+  __device__ Slices(long n_, int world, int G) : n(n_) {
+    L = (n + world - 1) / world;
+    L = (L + 3) & ~3L;
+    per = (L + G - 1) / G;
+    per = (per + 3) & ~3L;
+  }
+  __device__ void sub(int slice, int b, long& lo, long& hi) const {
     lo = (long)slice * L + (long)b * per;
     hi = lo + per;
     const long send = (long)slice * L + L;
     if (hi > send) hi = send;
     if (hi > n) hi = n;
     if (lo > hi) lo = hi;
-  };
+  }
+};
+
+__global__ __launch_bounds__(kThreads) void oneshot_ar_k(const float* __restrict__ in, float* out, long n,
+                                                         long cap, int rank, int world, Peers peers, Sync sy) {
+  if (poisoned(sy.err)) return;
+  const int b = blockIdx.x, G = gridDim.x;
+  const unsigned e = sy.epochs[b] + 1;
+  const long off = (long)(e & 1u) * 2 * cap;  // same parity layout as two-shot (modes may mix)
+  // 16-B aligned chunk per workgroup
+  long per = (n + G - 1) / G;
+  per = (per + 3) & ~3L;
+  const long lo = (long)b * per, hi = lo + per < n ? lo + per : n;
+
+  copy_range(peers.buf[rank] + off, in, lo, hi);
+  if (!flag_round(peers, rank, world, 0, b, e, sy)) return;  // never reduce another epoch's data
+
+  for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+    if (i + 3 < hi) {
+      *reinterpret_cast<float4*>(out + i) = sum4(peers, world, off + i);
+    } else {
+      for (long j = i; j < hi; ++j) out[j] = sum1(peers, world, off + j);
+    }
+  }
+  if (threadIdx.x == 0) sy.epochs[b] = e;
+}
+
+// Two-shot (reduce-scatter + all-gather over P2P) for mid-size messages: rank r owns slice r and
+// reduces it (reading (N-1)/N of the data from peers), then every rank gathers the other owners'
+// reduced slices.  Staging per rank: [parity][input | reduced] of cap floats each; flag rows 1, 2.
+__global__ __launch_bounds__(kThreads) void twoshot_ar_k(const float* __restrict__ in, float* out, long n,
+                                                         long cap, int rank, int world, Peers peers, Sync sy) {
+  if (poisoned(sy.err)) return;
+  const int b = blockIdx.x;
+  const unsigned e = sy.epochs[b] + 1;
+  const long base = (long)(e & 1u) * 2 * cap;
+  const Slices S(n, world, gridDim.x);
   long lo, hi;
   for (int sl = 0; sl < world; ++sl) {
-    sub(sl, lo, hi);
+    S.sub(sl, b, lo, hi);
     copy_range(peers.buf[rank] + base, in, lo, hi);
   }
-  flag_round(peers, rank, world, 1, b, e, err);
-  sub(rank, lo, hi);
+  if (!flag_round(peers, rank, world, 1, b, e, sy)) return;
+  S.sub(rank, b, lo, hi);
   float* red = peers.buf[rank] + base + cap;
   for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
     if (i + 3 < hi) {
-      float4 s = *reinterpret_cast<const float4*>(peers.buf[0] + base + i);
-      for (int p = 1; p < world; ++p) {
-        const float4 v = *reinterpret_cast<const float4*>(peers.buf[p] + base + i);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
+      const float4 s = sum4(peers, world, base + i);
       *reinterpret_cast<float4*>(red + i) = s;
       *reinterpret_cast<float4*>(out + i) = s;
     } else {
       for (long j = i; j < hi; ++j) {
-        float s = peers.buf[0][base + j];
-        for (int p = 1; p < world; ++p) s += peers.buf[p][base + j];
+        const float s = sum1(peers, world, base + j);
         red[j] = s;
         out[j] = s;
       }
     }
   }
-  flag_round(peers, rank, world, 2, b, e, err);
+  if (!flag_round(peers, rank, world, 2, b, e, sy)) return;
   for (int k = 1; k < world; ++k) {
     const int p = (rank + k) % world;  // stagger so the N-1 peers are read over different links at once
-    sub(p, lo, hi);
+    S.sub(p, b, lo, hi);
     copy_range(out, peers.buf[p] + base + cap, lo, hi);
   }
-  if (threadIdx.x == 0) epochs[b] = e;
+  if (threadIdx.x == 0) sy.epochs[b] = e;
+}
+
+// ------------------------------------------------------------------ fused data-parallel step
+struct DpArgs {
+  float* master;      // fp32 [n] parameters (every replica ends with identical values)
+  float* grad;        // fp32 [n] local gradient; staged and zeroed here
+  float* s1;          // optimizer state (full-size buffers; only this rank's slice is kept current)
+  float* s2;
+  float* s3;
+  bf16_raw* shadow;   // bf16 [n] compute copy, refreshed for every slice
+  long n;
+  OptHP h;            // by value; overridden by hp_dev when given
+  const float* hp_dev;
+  float* step_dev;    // completed-step counter (bias correction)
+  unsigned* arrive;   // arrival counter of the bookkeeping (zero at rest)
+  unsigned long long* rng;
+  Prefetch pf;
+};
+
+template <int KIND>
+__device__ inline void owner_update(const DpArgs& a, const Peers& peers, int world, long base, float* red, long i,
+                                    const OptHP& h, float bc1, float bc2) {
+  constexpr int NS = nstate<KIND>();
+  const float4 g = sum4(peers, world, base + i);
+  float4 w = *reinterpret_cast<const float4*>(a.master + i);
+  float4 x = NS >= 1 ? *reinterpret_cast<const float4*>(a.s1 + i) : make_float4(0, 0, 0, 0);
+  float4 y = NS >= 2 ? *reinterpret_cast<const float4*>(a.s2 + i) : make_float4(0, 0, 0, 0);
+  float4 z = NS >= 3 ? *reinterpret_cast<const float4*>(a.s3 + i) : make_float4(0, 0, 0, 0);
+  w.x = upd<KIND>(w.x, g.x * h.gscale, x.x, y.x, z.x, h, bc1, bc2);
+  w.y = upd<KIND>(w.y, g.y * h.gscale, x.y, y.y, z.y, h, bc1, bc2);
+  w.z = upd<KIND>(w.z, g.z * h.gscale, x.z, y.z, z.z, h, bc1, bc2);
+  w.w = upd<KIND>(w.w, g.w * h.gscale, x.w, y.w, z.w, h, bc1, bc2);
+  *reinterpret_cast<float4*>(a.master + i) = w;
+  if (NS >= 1) *reinterpret_cast<float4*>(a.s1 + i) = x;
+  if (NS >= 2) *reinterpret_cast<float4*>(a.s2 + i) = y;
+  if (NS >= 3) *reinterpret_cast<float4*>(a.s3 + i) = z;
+  *reinterpret_cast<float4*>(red + i) = w;
+  const uint32_t lo = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
+  const uint32_t hi = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
+  *reinterpret_cast<uint2*>(a.shadow + i) = make_uint2(lo, hi);
+}
+
+template <int KIND>
+__device__ inline void owner_update1(const DpArgs& a, const Peers& peers, int world, long base, float* red, long j,
+                                     const OptHP& h, float bc1, float bc2) {
+  constexpr int NS = nstate<KIND>();
+  const float g = sum1(peers, world, base + j);
+  float x = NS >= 1 ? a.s1[j] : 0.f, y = NS >= 2 ? a.s2[j] : 0.f, z = NS >= 3 ? a.s3[j] : 0.f;
+  const float w = upd<KIND>(a.master[j], g * h.gscale, x, y, z, h, bc1, bc2);
+  a.master[j] = w;
+  if (NS >= 1) a.s1[j] = x;
+  if (NS >= 2) a.s2[j] = y;
+  if (NS >= 3) a.s3[j] = z;
+  red[j] = w;
+  a.shadow[j] = f2bf(w);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int rank, int world, Peers peers, Sync sy) {
+  if (poisoned(sy.err)) return;
+  const int b = blockIdx.x;
+  const unsigned e = sy.epochs[b] + 1;
+  const long base = (long)(e & 1u) * 2 * cap;
+  const Slices S(a.n, world, gridDim.x);
+  const OptHP h = load_hp(a.h, a.hp_dev);
+  const float t = (a.step_dev ? a.step_dev[0] : 0.f) + 1.f;  // read by every workgroup before the last bumps it
+  float bc1, bc2;
+  bias_corr<KIND>(h, t, bc1, bc2);
+  float* mine = peers.buf[rank] + base;
+  long lo, hi;
+
+  // phase 0: stage this workgroup's share of every slice and zero the local gradient for the next
+  // step's atomic accumulation; the next batch's prefetch overlaps the wait for the peers
+  for (int sl = 0; sl < world; ++sl) {
+    S.sub(sl, b, lo, hi);
+    for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+      if (i + 3 < hi) {
+        *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(a.grad + i);
+        *reinterpret_cast<float4*>(a.grad + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        for (long j = i; j < hi; ++j) {
+          mine[j] = a.grad[j];
+          a.grad[j] = 0.f;
+        }
+      }
+    }
+  }
+  prefetch_copy(a.pf);
+  if (!flag_round(peers, rank, world, 1, b, e, sy)) return;
+
+  // phase 1: reduce + update this rank's slice; publish the new weights
+  float* red = mine + cap;
+  S.sub(rank, b, lo, hi);
+  for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+    if (i + 3 < hi) {
+      owner_update<KIND>(a, peers, world, base, red, i, h, bc1, bc2);
+    } else {
+      for (long j = i; j < hi; ++j) owner_update1<KIND>(a, peers, world, base, red, j, h, bc1, bc2);
+    }
+  }
+  if (!flag_round(peers, rank, world, 2, b, e, sy)) return;
+
+  // phase 2: every other owner's new weights -> fp32 master + bf16 shadow
+  for (int k = 1; k < world; ++k) {
+    const int p = (rank + k) % world;
+    const float* src = peers.buf[p] + base + cap;
+    S.sub(p, b, lo, hi);
+    for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+      if (i + 3 < hi) {
+        const float4 w = *reinterpret_cast<const float4*>(src + i);
+        *reinterpret_cast<float4*>(a.master + i) = w;
+        const uint32_t l2 = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
+        const uint32_t h2 = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
+        *reinterpret_cast<uint2*>(a.shadow + i) = make_uint2(l2, h2);
+      } else {
+        for (long j = i; j < hi; ++j) {
+          const float w = src[j];
+          a.master[j] = w;
+          a.shadow[j] = f2bf(w);
+        }
+      }
+    }
+  }
+  if (threadIdx.x == 0) sy.epochs[b] = e;
+  step_bookkeeping(a.arrive, a.step_dev, t, a.rng, a.pf);
 }
 
 py::bytes handle_of(u ptr) {
@@ -198,14 +343,31 @@ py::bytes handle_of(u ptr) {
   return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 
+Peers make_peers(int rank, int world, const std::vector<u>& bufs, const std::vector<u>& flags) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("bad rank/world");
+  if ((int)bufs.size() != world || (int)flags.size() != world) throw std::runtime_error("need one ptr per rank");
+  Peers pr{};
+  for (int i = 0; i < world; ++i) {
+    if ((bufs[i] | flags[i]) & 15u) throw std::runtime_error("staging / flag pages must be 16-B aligned");
+    pr.buf[i] = reinterpret_cast<float*>(bufs[i]);
+    pr.flag[i] = reinterpret_cast<unsigned*>(flags[i]);
+  }
+  return pr;
+}
+
+long long spin_ticks(double seconds) {
+  if (!(seconds > 0)) throw std::runtime_error("timeout must be > 0");
+  return (long long)(seconds * 1e8);  // s_memrealtime runs at 100 MHz
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hopsx_comm, m) {
-  m.doc() = "hopsx one-shot xGMI all-reduce over IPC-mapped peer buffers (gfx950)";
+  m.doc() = "hopsx P2P collectives over IPC-mapped peer buffers (xGMI, gfx950)";
   m.attr("MAX_RANKS") = kMaxRanks;
   m.attr("MAX_BLOCKS") = kMaxBlocks;
   m.attr("THREADS") = kThreads;
-  m.attr("FLAG_ROWS") = 3;  // row 0: one-shot, rows 1-2: the two rounds of two-shot
+  m.attr("FLAG_ROWS") = 3;  // row 0: one-shot, rows 1-2: the two rounds of two-shot / dp_step
 
   // staging memory (coarse-grained) or an uncached signal page; zeroed; returns (ptr, ipc handle)
   m.def("alloc", [](long bytes, bool uncached) {
@@ -233,23 +395,75 @@ PYBIND11_MODULE(_hopsx_comm, m) {
   m.def("handle_size", []() { return (int)sizeof(hipIpcMemHandle_t); });
 
   // out = sum over ranks of in (fp32, n elements, n <= cap); blocks <= MAX_BLOCKS, identical on all
-  // ranks; epochs: int32[MAX_BLOCKS] device counters (zeroed once); err: int32 device flag
+  // ranks; epochs: int32[MAX_BLOCKS] device counters (zeroed once); err: int32 sticky device flag;
+  // timeout: seconds a workgroup waits for a peer before it gives up (sets err, writes nothing)
   // two_shot: reduce-scatter + all-gather variant (staging must hold 4 * cap floats)
   m.def("allreduce_f32", [](u in, u out, long n, long cap, int rank, int world, std::vector<u> bufs,
-                            std::vector<u> flags, u epochs, u err, int blocks, u stream, bool two_shot) {
-    if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("bad rank/world");
-    if ((int)bufs.size() != world || (int)flags.size() != world) throw std::runtime_error("need one ptr per rank");
+                            std::vector<u> flags, u epochs, u err, int blocks, u stream, bool two_shot,
+                            double timeout) {
+    const Peers pr = make_peers(rank, world, bufs, flags);
     if (n < 0 || n > cap) throw std::runtime_error("n exceeds the staging capacity");
     if (blocks < 1 || blocks > kMaxBlocks) throw std::runtime_error("blocks out of range");
     if ((in | out) & 15u) throw std::runtime_error("in/out must be 16-B aligned");
-    Peers pr{};
-    for (int i = 0; i < world; ++i) {
-      pr.buf[i] = reinterpret_cast<float*>(bufs[i]);
-      pr.flag[i] = reinterpret_cast<unsigned*>(flags[i]);
+    const Sync sy{reinterpret_cast<unsigned*>(epochs), reinterpret_cast<int*>(err), spin_ticks(timeout)};
+    hipLaunchKernelGGL(two_shot ? twoshot_ar_k : oneshot_ar_k, dim3(blocks), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float*>(in),
+                       reinterpret_cast<float*>(out), n, cap, rank, world, pr, sy);
+    HIP_OK(hipGetLastError());
+  });
+
+  // Fused data-parallel step tail: reduce-scatter(grad) -> optimizer on this rank's slice ->
+  // all-gather(new fp32 weights) + bf16 shadow refresh + grad zeroing + step bookkeeping, one launch.
+  // kind: 0 SGD, 1 Adam, 2 AdamW, 3 Adadelta, 4 RMSprop, 5 Adagrad, 6 FTRL (optim_core.h)
+  m.def("dp_step", [](int kind, u master, u grad, u s1, u s2, u s3, u shadow, long n, std::vector<float> hp,
+                      u hp_dev, u step_dev, u arrive, u rng, std::vector<u> pf_src, std::vector<u> pf_dst,
+                      std::vector<long> pf_bytes, u pf_cursor, int pf_nbatch, long cap, int rank, int world,
+                      std::vector<u> bufs, std::vector<u> flags, u epochs, u err, int blocks, u stream,
+                      double timeout) {
+    const Peers pr = make_peers(rank, world, bufs, flags);
+    if (n < 0 || n > cap) throw std::runtime_error("arena exceeds the staging capacity");
+    if (blocks < 1 || blocks > kMaxBlocks) throw std::runtime_error("blocks out of range");
+    if (!master || !grad || !shadow) throw std::runtime_error("dp_step needs master, grad and shadow");
+    if ((master | grad | s1 | s2 | s3) & 15u || shadow & 7u) throw std::runtime_error("buffers must be 16-B aligned");
+    DpArgs a{};
+    a.master = reinterpret_cast<float*>(master);
+    a.grad = reinterpret_cast<float*>(grad);
+    a.s1 = reinterpret_cast<float*>(s1);
+    a.s2 = reinterpret_cast<float*>(s2);
+    a.s3 = reinterpret_cast<float*>(s3);
+    a.shadow = reinterpret_cast<bf16_raw*>(shadow);
+    a.n = n;
+    a.h = OptHP{0, 1, 0, 0, 0, 0, 0, 0};
+    float* hv = &a.h.lr;
+    for (size_t i = 0; i < hp.size() && i < 8; ++i) hv[i] = hp[i];
+    a.hp_dev = reinterpret_cast<const float*>(hp_dev);
+    a.step_dev = reinterpret_cast<float*>(step_dev);
+    a.arrive = reinterpret_cast<unsigned*>(arrive);
+    a.rng = reinterpret_cast<unsigned long long*>(rng);
+    a.pf = Prefetch{};
+    const size_t nj = std::min<size_t>(2, std::min(pf_src.size(), std::min(pf_dst.size(), pf_bytes.size())));
+    if (nj > 0 && pf_cursor && pf_nbatch > 0 && arrive) {
+      for (size_t j = 0; j < nj; ++j) {
+        if ((pf_src[j] | pf_dst[j] | (u)pf_bytes[j]) % 16 != 0) throw std::runtime_error("prefetch not 16-B aligned");
+        a.pf.job[j] = PrefetchJob{reinterpret_cast<const unsigned char*>(pf_src[j]),
+                                  reinterpret_cast<unsigned char*>(pf_dst[j]), pf_bytes[j]};
+      }
+      a.pf.njobs = (int)nj;
+      a.pf.cursor = reinterpret_cast<long long*>(pf_cursor);
+      a.pf.nbatch = pf_nbatch;
     }
-    hipLaunchKernelGGL(two_shot ? twoshot_ar_k : oneshot_ar_k, dim3(blocks), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                       reinterpret_cast<const float*>(in), reinterpret_cast<float*>(out), n, cap, rank, world, pr,
-                       reinterpret_cast<unsigned*>(epochs), reinterpret_cast<int*>(err));
+    if ((step_dev || rng || a.pf.njobs) && !arrive) throw std::runtime_error("bookkeeping needs the arrival counter");
+    const Sync sy{reinterpret_cast<unsigned*>(epochs), reinterpret_cast<int*>(err), spin_ticks(timeout)};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define DP_CASE(K)                                                                                      \
+  case K:                                                                                               \
+    hipLaunchKernelGGL(dp_step_k<K>, dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy); \
+    break;
+    switch (kind) {
+      DP_CASE(0) DP_CASE(1) DP_CASE(2) DP_CASE(3) DP_CASE(4) DP_CASE(5) DP_CASE(6)
+      default: throw std::runtime_error("unknown optimizer kind");
+    }
+#undef DP_CASE
     HIP_OK(hipGetLastError());
   });
 }

@@ -120,7 +120,7 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   });
   m.def("optim_step", [](int kind, u p, u g, u s1, u s2, u s3, u shadow, long n, std::vector<float> hp, u step,
                          u arrive, u rng, int zero_grad, std::vector<u> pf_src, std::vector<u> pf_dst,
-                         std::vector<long> pf_bytes, u pf_cursor, int pf_nbatch, u st) {
+                         std::vector<long> pf_bytes, u pf_cursor, int pf_nbatch, u hp_dev, u st) {
     const void* srcs[2] = {nullptr, nullptr};
     void* dsts[2] = {nullptr, nullptr};
     long bytes[2] = {0, 0};
@@ -133,7 +133,7 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_optim_step(kind, P<float>(p), P<float>(g), P<float>(s1), P<float>(s2), P<float>(s3),
                             P<void>(shadow), n, hp.data(), (int)hp.size(), P<float>(step), P<unsigned>(arrive),
                             P<unsigned long long>(rng), zero_grad, srcs, dsts, bytes, nj, P<long long>(pf_cursor),
-                            pf_nbatch, S(st));
+                            pf_nbatch, P<float>(hp_dev), S(st));
   });
   m.def("dropout_fwd", [](u x, u y, long n, float p, u rng, unsigned salt, u st) {
     return hopsx_dropout_fwd(P<void>(x), P<void>(y), n, p, P<unsigned long long>(rng), salt, S(st));

@@ -58,10 +58,11 @@ int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void*
 // ---- optimizers (optim.hip) ----
 // kind: 0 SGD(momentum/nesterov), 1 Adam, 2 AdamW, 3 Adadelta, 4 RMSprop, 5 Adagrad, 6 FTRL
 // pf_*: optional fused prefetch of the next batch of up to two HBM-resident tensors (see optim.hip)
+// hp_dev: optional device copy of the 8 hyper-parameters (read at run time; overrides hp)
 int hopsx_optim_step(int kind, float* param, float* grad, float* s1, float* s2, float* s3, void* shadow_bf16,
                      long n, const float* hp, int nhp, float* step_dev, unsigned* arrive, unsigned long long* rng,
                      int zero_grad, const void* const* pf_src, void* const* pf_dst, const long* pf_bytes,
-                     int pf_njobs, long long* pf_cursor, int pf_nbatch, hipStream_t st);
+                     int pf_njobs, long long* pf_cursor, int pf_nbatch, const float* hp_dev, hipStream_t st);
 
 // ---- dropout / RNG (elementwise.hip) ----
 int hopsx_dropout_fwd(const void* x, void* y, long n, float p, const unsigned long long* rng, unsigned salt,

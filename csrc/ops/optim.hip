@@ -17,29 +17,6 @@
 
 
 
-// Fused input prefetch (HBM-resident datasets): after its update each workgroup copies a slice of
-// batch (cursor + 1) % nbatch of up to two resident tensors (images, labels) into the step's
-// static input buffers, and the last-arriving workgroup advances the cursor.  The optimizer is the
-// last kernel of a replayed training step, so nothing reads the inputs any more: the next batch
-// lands with no launch and no copy engine on the critical path.
-struct PrefetchJob {
-  const unsigned char* src;  // batch 0 of the resident tensor; batch i at src + i * bytes
-  unsigned char* dst;        // static input buffer
-  long bytes;                // per batch (multiple of 16, 16-B aligned buffers)
-};
-struct Prefetch {
-  PrefetchJob job[2];
-  long long* cursor;  // device: index of the batch currently in dst
-  int nbatch;
-  int njobs;
-};
-
-
-template <int KIND>
-constexpr int nstate() {
-  return KIND == 0 ? 1 : (KIND == 4 ? 3 : (KIND == 5 ? 1 : 2));
-}
-
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ inline void st_nt(float* dst, long i, const float4& v) {
   const f4v x = {v.x, v.y, v.z, v.w};
@@ -52,16 +29,14 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
                                                bf16_raw* __restrict__ shadow, long n, OptHP h,
                                                float* __restrict__ step_dev, unsigned* __restrict__ arrive,
                                                unsigned long long* __restrict__ rng, int zero_grad, int vec,
-                                               Prefetch pf, int nt) {
+                                               Prefetch pf, int nt, const float* __restrict__ hp_dev) {
   // step_dev holds the number of COMPLETED steps; this step is t = step + 1.
   // Every workgroup reads it before its final barrier; the last workgroup to
   // finish bumps it (and the dropout RNG counter).
   const float t = (step_dev ? step_dev[0] : 0.f) + 1.f;
-  float bc1 = 1.f, bc2 = 1.f;
-  if (KIND == 1 || KIND == 2) {
-    bc1 = 1.f - __powf(h.a, t);
-    bc2 = 1.f - __powf(h.b, t);
-  }
+  h = load_hp(h, hp_dev);
+  float bc1, bc2;
+  bias_corr<KIND>(h, t, bc1, bc2);
   constexpr int NS = nstate<KIND>();
   const long n4 = vec ? (n >> 2) : 0;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -121,26 +96,8 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
     if (NS >= 3) s3[i] = c;
     if (shadow) shadow[i] = f2bf(w);
   }
-  if (pf.njobs) {
-    const long long next = (pf.cursor[0] + 1) % pf.nbatch;  // every workgroup reads before the last arrives
-    for (int j = 0; j < pf.njobs; ++j) {
-      const uint4* src = (const uint4*)(pf.job[j].src + next * pf.job[j].bytes);
-      uint4* dst = (uint4*)pf.job[j].dst;
-      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pf.job[j].bytes / 16; i += stride) dst[i] = src[i];
-    }
-  }
-  if (arrive) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned prev = atomicAdd(arrive, 1u);
-      if (prev == gridDim.x - 1) {
-        if (step_dev) step_dev[0] = t;
-        if (rng) rng[1] += 1ull;
-        if (pf.njobs) pf.cursor[0] = (pf.cursor[0] + 1) % pf.nbatch;
-        atomicExch(arrive, 0u);
-      }
-    }
-  }
+  prefetch_copy(pf);
+  step_bookkeeping(arrive, step_dev, t, rng, pf);
 }
 
 __global__ void bump_k(float* step_dev, unsigned long long* rng) {
@@ -152,7 +109,7 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
                                 void* shadow_bf16, long n, const float* hp, int nhp, float* step_dev,
                                 unsigned* arrive, unsigned long long* rng, int zero_grad, const void* const* pf_src,
                                 void* const* pf_dst, const long* pf_bytes, int pf_njobs, long long* pf_cursor,
-                                int pf_nbatch, hipStream_t st) {
+                                int pf_nbatch, const float* hp_dev, hipStream_t st) {
   Prefetch pf{};
   pf.njobs = 0;
   if (pf_njobs > 0 && pf_cursor && pf_nbatch > 0 && arrive) {  // the cursor advance needs the arrival counter
@@ -184,7 +141,7 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
 #define OPT_CASE(K)                                                                                                   \
   case K:                                                                                                             \
     hipLaunchKernelGGL(optim_k<K>, dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, arr, rng, \
-                       zero_grad, (int)aligned, pf, nt);                                                              \
+                       zero_grad, (int)aligned, pf, nt, hp_dev);                                                              \
     break;
   switch (kind) {
     OPT_CASE(0) OPT_CASE(1) OPT_CASE(2) OPT_CASE(3) OPT_CASE(4) OPT_CASE(5) OPT_CASE(6)

@@ -88,13 +88,15 @@ HIP_FLAGS = [
 ]
 
 
-def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra_link: list[str]) -> Path:
-    """kind: 'hip' compiles every source with hipcc for gfx950, 'cpp' with g++."""
+def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra_link: list[str],
+               extra_headers: list[Path] | None = None) -> Path:
+    """kind: 'hip' compiles every source with hipcc for gfx950, 'cpp' with g++.  ``extra_headers``:
+    headers outside ``srcdir`` the sources include (part of the rebuild digest)."""
     out = PKG / f"{name}{EXT}"
     objdir = BUILD / name
     objdir.mkdir(parents=True, exist_ok=True)
     srcs = sorted([*srcdir.glob("*.hip"), *srcdir.glob("*.cpp")])
-    headers = sorted(srcdir.glob("*.h"))
+    headers = sorted(srcdir.glob("*.h")) + list(extra_headers or [])
     jobs_list = []
     for s in srcs:
         o = objdir / (s.name + ".o")
@@ -139,7 +141,9 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         outs.append(_build_lib("_hopsx_io", ROOT / "csrc" / "io", "cpp", force, jobs,
                                []))
     if (ROOT / "csrc" / "comm").exists() and any((ROOT / "csrc" / "comm").glob("*.hip")):
-        outs.append(_build_lib("_hopsx_comm", ROOT / "csrc" / "comm", "hip", force, jobs, []))
+        # the fused data-parallel step shares the optimizer update rules with csrc/ops
+        outs.append(_build_lib("_hopsx_comm", ROOT / "csrc" / "comm", "hip", force, jobs, [],
+                               [ROOT / "csrc" / "ops" / "optim_core.h", ROOT / "csrc" / "ops" / "common.h"]))
     if verbose:
         for o in outs:
             print(f"[hopsx build] {o.relative_to(ROOT)} ({o.stat().st_size // 1024} KiB)")

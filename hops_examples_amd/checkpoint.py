@@ -39,6 +39,17 @@ def _rng_tensor(device):
     return rng_state(device)
 
 
+def gather_sharded(model) -> None:
+    """Collective (every rank): a sharded data-parallel engine keeps parts of the fp32 master and
+    of the optimizer moments current only on their owner rank (ShardedPS on GPU all-gathers only
+    the bf16 shadow; the fused P2P step keeps moments owner-only).  Reassemble them so the
+    checkpoint written by rank 0 holds every shard's real values, not its stale local copy."""
+    arena = _arena(model)
+    eng = getattr(arena, "_hx_engine", None) if arena is not None else None
+    if eng is not None and hasattr(eng, "gather_state"):
+        eng.gather_state()
+
+
 def state(model, optimizer=None, step: int = 0, **extra) -> dict:
     """Collect a CPU-resident checkpoint dict (no file I/O)."""
     sd: dict = {"step": int(step), "extra": extra}
@@ -103,6 +114,7 @@ def save(directory, model, optimizer=None, step: int = 0, keep: int = 3, **extra
     d = Path(directory)
     path = d / f"ckpt-{int(step)}.pt"
     out = None
+    gather_sharded(model)  # collective: owner-only shards (parameter server / fused P2P step) -> rank 0
     sd = state(model, optimizer, step, **extra) if hdist.rank() == 0 else None
     if hdist.rank() == 0:
         d.mkdir(parents=True, exist_ok=True)

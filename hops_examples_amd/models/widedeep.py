@@ -208,35 +208,50 @@ class FusedWideDeepStep:
         health.beat(self._n)
         dense, cat = xs
         key = (dense.data_ptr(), cat.data_ptr(), ys.data_ptr(), tuple(self._floats()))
-        if not graph or self.dp is not None or self.arena.device.type != "cuda":
+        if not graph or not self._graphable():
             self._launch(dense, cat, ys, dense.shape[0], self.cursor)
             self._finish()
         else:
             if self._key != key:  # new data or hyper-parameters (e.g. an lr schedule): recapture
                 self._slots(dense.shape[-2])  # host->device copy of the slot table must precede capture
+                self._sync_hp()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with _capture_graph(g):
                     self._launch(dense, cat, ys, dense.shape[0], self.cursor)
+                    self._finish()  # multi-rank: the P2P all-reduce + optimizers are graph nodes too
                 self._graph, self._key = g, key
                 # capture does not execute: run this step through the graph
             self._graph.replay()
+            if self.dp is not None:
+                self.dp.poll()
         return {"loss": self.loss, "correct": self.correct, "count": dense.shape[1]}
+
+    def _graphable(self) -> bool:
+        """One GPU, or a data-parallel engine whose collectives are graph-capturable (P2P kernels)."""
+        return self.arena.device.type == "cuda" and (
+            self.dp is None or getattr(self.dp, "capturable", lambda: False)())
+
+    def _sync_hp(self):
+        if self.dp is not None and hasattr(self.opt, "sync_hp"):
+            self.opt.sync_hp()
 
     def prepare_resident(self, xs, ys) -> None:
         """Capture (not run) the U-step graph for this resident epoch, so it is built before a timed loop."""
         dense, cat = xs
         U = self.steps_per_execution
-        if U <= 1 or self.dp is not None or self.arena.device.type != "cuda" or self._graph is None:
+        if U <= 1 or not self._graphable() or self._graph is None:
             return
         key = (dense.data_ptr(), cat.data_ptr(), ys.data_ptr(), tuple(self._floats()), U)
         if self._keyU != key:
             self._slots(dense.shape[-2])
+            self._sync_hp()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with _capture_graph(g):
                 for _ in range(U):
                     self._launch(dense, cat, ys, dense.shape[0], self.cursor)
+                    self._finish()
             self._graphU, self._keyU = g, key
 
     def run_resident(self, xs, ys, n: int, graph: bool = True):
@@ -249,8 +264,7 @@ class FusedWideDeepStep:
         dense, cat = xs
         r = None
         while n > 0:
-            if (n < U or U <= 1 or not graph or self.dp is not None or self.arena.device.type != "cuda"
-                    or self._graph is None):
+            if n < U or U <= 1 or not graph or not self._graphable() or self._graph is None:
                 r = self.step_resident(xs, ys, graph=graph)
                 n -= 1
                 continue
@@ -259,6 +273,8 @@ class FusedWideDeepStep:
                 self._n += 1
                 health.beat(self._n)
             self._graphU.replay()
+            if self.dp is not None:
+                self.dp.poll()
             n -= U
             r = {"loss": self.loss, "correct": self.correct, "count": dense.shape[1]}
         return r

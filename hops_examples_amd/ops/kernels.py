@@ -354,12 +354,14 @@ def loss_fwd_bwd(kind: int, logits, target, grad_scale, loss_sum, correct, dlogi
 
 # --------------------------------------------------------------- optimizers
 def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True, arrive=None, rng=None,
-               prefetch=None):
+               prefetch=None, hp_dev=None):
     """One fused update over flat buffers.  ``step_dev`` (f32[1]) counts completed steps and,
     with ``arrive`` (int32[1], zero-initialised), is bumped in-kernel by the last workgroup,
     together with the dropout RNG counter ``rng[1]`` when given.
     ``prefetch`` = (pairs, cursor): pairs of (resident [nbatch, ...] tensor, static input buffer);
-    the kernel copies batch (cursor+1) % nbatch into the buffers and advances the int64 cursor."""
+    the kernel copies batch (cursor+1) % nbatch into the buffers and advances the int64 cursor.
+    ``hp_dev`` (f32[8] on the device): the kernel reads the hyper-parameters from it at run time
+    instead of ``hp`` (so a replayed hipGraph sees learning-rate changes)."""
     n = param.numel()
     if step_dev is not None and arrive is None:
         arrive = torch.zeros(1, device=param.device, dtype=torch.int32)
@@ -377,7 +379,7 @@ def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_gr
         cur = ptr(cursor)
     check(_C.ext().optim_step(kind, ptr(param), ptr(grad), ptr(s1), ptr(s2), ptr(s3), ptr(shadow), n,
                               [float(v) for v in hp], ptr(step_dev), ptr(arrive), ptr(rng), int(zero_grad), srcs,
-                              dsts, nbytes, cur, nb, stream()),
+                              dsts, nbytes, cur, nb, ptr(hp_dev), stream()),
           "optim")
 
 

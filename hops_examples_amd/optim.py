@@ -78,6 +78,10 @@ class FusedOptimizer:
             self.rng = rng_state(dev)
         self._states = [self.arena.state(f"{self.kind}_s{i}")[self._sl] for i in range(self.nstate)]
         self.param_groups = [{"params": self.arena.params, "lr": self.lr}]
+        # device copy of the hyper-parameter vector: the kernel reads it at run time, so a step
+        # replayed from a hipGraph sees lr / grad_scale changes made after the capture (sync_hp)
+        self._hp_dev = torch.zeros(8, device=dev, dtype=torch.float32) if dev.type == "cuda" else None
+        self._hp_up = None
 
     def restrict(self, sl: slice) -> "FusedOptimizer":
         """Own only ``sl`` of the arena (sharded parameter-server mode: each rank updates its shard)."""
@@ -88,6 +92,17 @@ class FusedOptimizer:
     # hyper-parameter vector in the kernel's layout: lr, gscale, wd, a..e
     def _hp(self) -> list[float]:
         raise NotImplementedError
+
+    def sync_hp(self) -> None:
+        """Upload the hyper-parameters if they changed since the last upload (stream-ordered; never
+        during a hipGraph capture — TrainStep calls this before every replay)."""
+        if self._hp_dev is None:
+            return
+        self.lr = self.param_groups[0]["lr"]
+        hp = [float(v) for v in self._hp()]
+        if hp != self._hp_up and not torch.cuda.is_current_stream_capturing():
+            self._hp_dev.copy_(torch.tensor((hp + [0.0] * 8)[:8], dtype=torch.float32))
+            self._hp_up = hp
 
     def step(self, closure=None):
         from .ops.functional import join_side_streams
@@ -104,9 +119,11 @@ class FusedOptimizer:
             from .ops import kernels as K
 
             sl = self._sl
+            self.sync_hp()
             K.optim_step(OPTIM[self.kind], a.master[sl], a.grad[sl], s[0], s[1], s[2],
                          a.shadow[sl] if a.shadow is not None else None, self._hp(), self.step_count,
-                         zero_grad=True, arrive=self._arrive, rng=self.rng, prefetch=self.prefetch)
+                         zero_grad=True, arrive=self._arrive, rng=self.rng, prefetch=self.prefetch,
+                         hp_dev=self._hp_dev)
         else:
             self.step_count += 1
             sl = self._sl
@@ -285,6 +302,10 @@ class Chain:
     def grad_scale(self, v):
         for o in self.opts:
             o.grad_scale = v
+
+    def sync_hp(self) -> None:
+        for o in self.opts:
+            o.sync_hp()
 
     def restrict(self, sl: slice) -> "Chain":
         for o in self.opts:

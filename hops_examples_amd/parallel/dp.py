@@ -13,6 +13,14 @@ link (~153 GB/s x 7 links per GPU); below ~10 MB the per-collective latency
 dominates, so models under ~10 M params (every reference CNN) get ONE bucket
 and ResNet50-class models 4-8 buckets of >= 16 MB.
 
+On one node the engine prefers the P2P path (parallel/oneshot.py, ``HOPSX_P2P=auto``): the
+peers' IPC-mapped staging buffers are read directly over the 7 xGMI links, and when the
+optimizer is one fused optimizer over the whole arena the ENTIRE step tail — gradient
+reduce-scatter, the optimizer on this rank's 1/N slice, all-gather of the new weights — is one
+kernel (``fused_update``) that lives inside the step's hipGraph (so multi-rank steps also replay
+``steps_per_execution`` at a time).  Setup is collective and fail-safe: unless every rank maps
+its peers and passes the self-test, everyone stays on RCCL.
+
 Modes (the three strategies the reference names):
   * ``mirrored`` / ``collective_allreduce`` — synchronous all-reduce (this class);
   * ``parameter_server`` — see parallel/ps.py (reduce-scatter to shard owners +
@@ -61,7 +69,8 @@ def plan_buckets(arena: ParamArena, bucket_mb: float, first_bucket_mb: float | N
 
 class DataParallel:
     def __init__(self, model_or_arena, bucket_mb: float = 25.0, overlap: bool = True, broadcast: bool = True,
-                 grad_dtype: torch.dtype = torch.float32):
+                 grad_dtype: torch.dtype = torch.float32, p2p: bool | None = None):
+        """``p2p``: None follows ``HOPSX_P2P`` (auto), False forces RCCL / the process group."""
         if isinstance(model_or_arena, ParamArena):
             self.arena = model_or_arena
         else:
@@ -77,15 +86,87 @@ class DataParallel:
         self._handles: list = []
         self._launched = [False] * len(self.buckets)
         self.grad_dtype = grad_dtype
-        # one-shot xGMI all-reduce (parallel/oneshot.py) for buckets that fit its staging buffer
+        # P2P xGMI collectives (parallel/oneshot.py): staging sized for the whole arena, so every
+        # bucket (and the fused step tail) fits
         self._oneshot = None
-        if self.world > 1 and oneshot.enabled() and self.arena.grad.is_cuda:
-            self._oneshot = oneshot.OneShotAllReduce(cap_bytes=int(os.environ.get("HOPSX_ONESHOT_MB", "8")) * MB,
-                                                     device=self.arena.grad.device)
+        if self.world > 1 and (oneshot.enabled() if p2p is None else p2p) and self.arena.grad.is_cuda:
+            self._oneshot = oneshot.P2PComm.create(cap_bytes=self.arena.numel * 4, device=self.arena.grad.device)
+        self._fused_opt = None
+        self._polls = 0
+        self.poll_every = int(os.environ.get("HOPSX_P2P_POLL_EVERY", "64"))
         if broadcast and self.world > 1:
             self.broadcast_params()
+        self.arena._hx_engine = self  # checkpoint.save gathers the owner-only optimizer slices
         if self.overlap:
             hooks.subscribe(self._on_ready)
+
+    # -------------------------------------------------------------- fused P2P step tail
+    def bind_optimizer(self, opt) -> None:
+        """Called by TrainStep: use the fused reduce-scatter / sharded update / all-gather kernel when
+        the P2P path is up and ``opt`` is ONE fused optimizer over the whole arena."""
+        from ..optim import FusedOptimizer
+
+        ok = (self._oneshot is not None and os.environ.get("HOPSX_P2P_FUSED", "1") == "1"
+              and isinstance(opt, FusedOptimizer) and opt.arena is self.arena
+              and opt._sl == slice(0, self.arena.numel) and self.arena.shadow is not None)
+        self._fused_opt = opt if ok else None
+        if ok and self.overlap:
+            hooks.unsubscribe(self._on_ready)  # no per-bucket all-reduce: the step tail does it all
+            self.overlap = False
+
+    def fuses_optimizer(self, opt) -> bool:
+        return self._fused_opt is not None and opt is self._fused_opt
+
+    def fused_update(self, opt) -> None:
+        self._oneshot.dp_step(opt)
+
+    def owner_slices(self) -> list[slice] | None:
+        """Per-rank slices whose optimizer state only the owner keeps current (fused mode), else None."""
+        if self._fused_opt is None:
+            return None
+        n, w = self.arena.numel, self.world
+        L = ((n + w - 1) // w + 3) & ~3
+        return [slice(min(n, r * L), min(n, (r + 1) * L)) for r in range(w)]
+
+    def gather_state(self) -> None:
+        """Collective: make every rank's optimizer-state buffers complete (each slice from its owner);
+        checkpoint.save calls this on every rank before rank 0 serialises."""
+        sl = self.owner_slices()
+        if sl is None:
+            return
+        for t in self.arena.states.values():
+            _gather_slices(t, sl, self._oneshot.rank)
+
+    # -------------------------------------------------------------- health
+    def poll(self) -> None:
+        """Every ``poll_every`` calls: asynchronous check of the P2P error flag (raises when a peer
+        never arrived; the kernels skipped that reduction instead of summing stale buffers)."""
+        if self._oneshot is None:
+            return
+        self._polls += 1
+        if self._polls % max(1, self.poll_every) == 0:
+            self._oneshot.poll()
+
+    def verify_replicas(self) -> dict:
+        """Collective consistency check: the fp32 master arena must be bit-identical on every rank
+        (after the same steps).  Returns {'identical': bool, 'max_abs_diff': float}."""
+        m = self.arena.master
+        ref = m.clone()
+        hdist.broadcast_(ref, 0)
+        d = float((m - ref).abs().max().item()) if m.numel() else 0.0
+        d = hdist.all_reduce_scalar(d, "max")
+        return {"identical": d == 0.0, "max_abs_diff": d}
+
+    @property
+    def path(self) -> str:
+        if self.world <= 1:
+            return "none"
+        if self._fused_opt is not None:
+            return "p2p-xgmi-fused-step"
+        if self._oneshot is not None:
+            return "p2p-xgmi-allreduce"
+        be = "rccl" if dist.get_backend() == "nccl" else dist.get_backend()
+        return be + ("-bf16" if self.grad_dtype == torch.bfloat16 else "")
 
     def broadcast_params(self) -> None:
         hdist.broadcast_(self.arena.master, 0)
@@ -159,7 +240,25 @@ class DataParallel:
         return 1.0 / self.world
 
     def close(self) -> None:
+        """Collective.  Raises if a P2P collective failed since the last poll."""
         hooks.unsubscribe(self._on_ready)
         if self._oneshot is not None:
-            self._oneshot.close()
-            self._oneshot = None
+            try:
+                self._oneshot.check()
+            finally:
+                self._oneshot.close()
+                self._oneshot = None
+
+
+def _gather_slices(t: torch.Tensor, slices: list[slice], rank: int) -> None:
+    """All-gather variable-size owner slices of a flat tensor in place (any backend)."""
+    if not hdist.is_dist():
+        return
+    sizes = [s.stop - s.start for s in slices]
+    mx = max(sizes)
+    buf = torch.zeros(mx, dtype=t.dtype, device=t.device)
+    buf[:sizes[rank]].copy_(t[slices[rank]])
+    parts = [torch.empty_like(buf) for _ in slices]
+    dist.all_gather(parts, buf)
+    for s, n, p in zip(slices, sizes, parts):
+        t[s].copy_(p[:n])

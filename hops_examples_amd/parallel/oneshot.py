@@ -1,14 +1,23 @@
-"""One-shot / two-shot all-reduce for small and mid-size messages over IPC-mapped peer buffers (``_hopsx_comm``).
+"""P2P collectives over IPC-mapped peer buffers (``_hopsx_comm``, csrc/comm/oneshot.hip).
 
 SURVEY §5.8 item 3 / §2.4: a ring all-reduce needs 2(N-1) latency-bound hops, but MI355X wires
-every GPU to its 7 peers directly over xGMI, so below ~1 MB one hop is cheaper: each rank stages
-its data in an IPC-shared buffer, flags every peer, and sums all N staging buffers itself
-(csrc/comm/oneshot.hip).  Small models (the taxi wide&deep net's 75 KB of gradients, metric
-scalars C7) and small buckets use it; larger buckets stay on RCCL rings.
+every GPU to its 7 peers directly over xGMI.  Each rank stages its data in an IPC-shared buffer,
+flags every peer, and reads the peers' buffers itself:
 
-Setup exchanges ``hipIpcMemHandle`` bytes through the default process group (any backend), so
-it works for RCCL and gloo groups alike.  The launch is hipGraph-capturable (device-resident
-epochs).  A peer that never arrives sets an error flag instead of hanging; ``check()`` raises.
+* one-shot all-reduce (small messages): every rank sums all N staging buffers;
+* two-shot all-reduce (mid-size): reduce-scatter + all-gather, 2(N-1)/N of the bytes;
+* ``dp_step``: the data-parallel step tail in ONE launch — reduce-scatter of the gradient, the
+  fused optimizer on this rank's slice only, all-gather of the new fp32 weights (+ bf16 shadow),
+  grad zeroing, step/RNG bookkeeping and the next-batch prefetch.  Every replica ends with the
+  owners' bit-identical weights; optimizer moments are kept current only on the slice owner
+  (``gather_states`` reassembles them for checkpoints).
+
+Setup exchanges ``hipIpcMemHandle`` bytes through the default process group (any backend), so it
+works for RCCL and gloo groups alike, then runs a self-test (a known all-reduce checked on every
+rank).  ``P2PComm.create`` returns None when any rank fails to map a peer or the self-test
+disagrees — the caller then stays on RCCL.  Launches are hipGraph-capturable (device-resident
+epochs).  A peer that never arrives makes the kernels set a sticky error flag and write nothing;
+``poll()`` (cheap, asynchronous) and ``check()`` (synchronous) raise on it.
 
 Reference parity: the implicit TF collectives of MirroredStrategy.
 """
@@ -36,45 +45,86 @@ def ext():
     return _ext
 
 
+def mode() -> str:
+    """``HOPSX_P2P``: ``auto`` (default: used when every rank shares one node and the self-test
+    passes), ``1`` (required: setup failures raise), ``0`` (RCCL only).  ``HOPSX_ONESHOT_AR`` is the
+    round-1 spelling of the same switch."""
+    m = os.environ.get("HOPSX_P2P")
+    if m is None:
+        legacy = os.environ.get("HOPSX_ONESHOT_AR")
+        m = {"1": "1", "0": "0"}.get(legacy or "", "auto")
+    return m if m in ("auto", "1", "0") else "auto"
+
+
 def enabled() -> bool:
-    """Opt-in via HOPSX_ONESHOT_AR=1 (RCCL rings remain the default for every bucket)."""
-    return os.environ.get("HOPSX_ONESHOT_AR", "0") == "1"
+    return mode() != "0"
+
+
+def _timeout() -> float:
+    return float(os.environ.get("HOPSX_P2P_TIMEOUT_S", "60"))
+
+
+def _default_blocks(world: int) -> int:
+    """One workgroup per CU at most (the flag protocol needs every block resident).  Ranks that share
+    one GPU (multi-rank rehearsal on a one-GPU box) split its 256 CUs."""
+    env = os.environ.get("HOPSX_P2P_BLOCKS")
+    if env:
+        return int(env)
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 1
+    if ndev < world:  # several ranks per device
+        return max(8, min(64, 256 // (2 * world)))
+    return 128
 
 
 class OneShotAllReduce:
-    """Sum-all-reduce of fp32 device tensors of up to ``cap_bytes`` across the default group."""
+    """Sum-all-reduce (and the fused DP step) of fp32 device tensors of up to ``cap_bytes`` across the
+    default group.  The constructor raises on any setup failure (see ``P2PComm.create`` for the
+    collective, fail-safe variant)."""
 
-    def __init__(self, cap_bytes: int = 8 << 20, blocks: int = 64, device=None):
+    def __init__(self, cap_bytes: int = 8 << 20, blocks: int | None = None, device=None, timeout: float | None = None):
         C = ext()
         self.rank, self.world = hdist.rank(), hdist.world_size()
         if self.world > C.MAX_RANKS:
-            raise ValueError(f"one-shot all-reduce supports <= {C.MAX_RANKS} ranks (one node)")
+            raise ValueError(f"P2P collectives support <= {C.MAX_RANKS} ranks (one node)")
         self.device = device or hdist.device()
         self.cap = (int(cap_bytes) // 4 + 3) & ~3
-        self.blocks = max(1, min(int(blocks), C.MAX_BLOCKS))
+        self.blocks = max(1, min(int(blocks or _default_blocks(self.world)), C.MAX_BLOCKS))
+        self.timeout = float(timeout or _timeout())
+        self._buf = self._flag = None
+        self._opened: list[int] = []
         self._buf, hb = C.alloc(4 * self.cap * 4, False)
         self._flag, hf = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
         # two-shot (reduce-scatter + all-gather) above this size when N > 2: 2(N-1)/N * n of xGMI
         # reads per GPU instead of (N-1) * n
         self.two_shot_min = int(os.environ.get("HOPSX_TWOSHOT_MIN_KB", "256")) * 1024 // 4
-        self._opened: list[int] = []
         if self.world > 1:
             objs = [None] * self.world
             dist.all_gather_object(objs, (self.rank, bytes(hb), bytes(hf)))
-            bufs, flags = [0] * self.world, [0] * self.world
-            for r, b, f in objs:
-                if r == self.rank:
-                    bufs[r], flags[r] = self._buf, self._flag
-                else:
-                    bufs[r], flags[r] = C.open(b), C.open(f)
-                    self._opened += [bufs[r], flags[r]]
+            self._map(objs)
         else:
-            bufs, flags = [self._buf], [self._flag]
-        self.bufs, self.flags = bufs, flags
+            self.bufs, self.flags = [self._buf], [self._flag]
         self.epochs = torch.zeros(C.MAX_BLOCKS, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory() if self.device.type == "cuda" else None
+        self._err_event = None
         hdist.barrier()
 
+    def _map(self, objs) -> None:
+        C = ext()
+        bufs, flags = [0] * self.world, [0] * self.world
+        for r, b, f in objs:
+            if r == self.rank:
+                bufs[r], flags[r] = self._buf, self._flag
+            else:
+                if b is None or f is None:
+                    raise RuntimeError(f"rank {r} has no P2P staging buffer")
+                bufs[r] = C.open(b)
+                self._opened.append(bufs[r])
+                flags[r] = C.open(f)
+                self._opened.append(flags[r])
+        self.bufs, self.flags = bufs, flags
+
+    # ------------------------------------------------------------ collectives
     def fits(self, t: torch.Tensor) -> bool:
         return (t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= self.cap
                 and t.data_ptr() % 16 == 0)
@@ -92,24 +142,177 @@ class OneShotAllReduce:
         st = torch.cuda.current_stream(self.device).cuda_stream
         ext().allreduce_f32(t.data_ptr(), out.data_ptr(), t.numel(), self.cap, self.rank, self.world,
                             self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(), self.blocks, st,
-                            (mode or self.mode(t.numel())) == "two_shot")
+                            (mode or self.mode(t.numel())) == "two_shot", self.timeout)
         return out
 
+    def dp_step(self, opt) -> None:
+        """Reduce-scatter the arena gradient, run ``opt``'s update on this rank's slice, all-gather the
+        new weights; one launch (see the module docstring).  ``opt`` must own the whole arena."""
+        from ..ops._C import OPTIM
+
+        a = opt.arena
+        if a.numel > self.cap:
+            raise ValueError(f"arena of {a.numel} elements exceeds the P2P staging capacity {self.cap}")
+        opt.sync_hp()
+        st = [t.data_ptr() for t in opt._states] + [0] * (3 - len(opt._states))
+        srcs, dsts, nbytes, cur, nb = [], [], [], 0, 0
+        if opt.prefetch is not None:
+            pairs, cursor = opt.prefetch
+            for src, dst in pairs:
+                srcs.append(src.data_ptr())
+                dsts.append(dst.data_ptr())
+                nbytes.append(dst.numel() * dst.element_size())
+                nb = src.shape[0]
+            cur = cursor.data_ptr()
+        ext().dp_step(OPTIM[opt.kind], a.master.data_ptr(), a.grad.data_ptr(), st[0], st[1], st[2],
+                      a.shadow.data_ptr(), a.numel, [float(v) for v in opt._hp()], opt._hp_dev.data_ptr(),
+                      opt.step_count.data_ptr(), opt._arrive.data_ptr(),
+                      opt.rng.data_ptr() if opt.rng is not None else 0, srcs, dsts, nbytes, cur, nb, self.cap,
+                      self.rank, self.world, self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(),
+                      self.blocks, torch.cuda.current_stream(self.device).cuda_stream, self.timeout)
+
+    # ------------------------------------------------------------ failure detection
     def check(self) -> None:
         """Raise if a peer failed to arrive within the spin bound (synchronises the device)."""
         e = int(self.err.item())
         if e:
-            raise RuntimeError(f"one-shot all-reduce: rank {e - 1} never raised its flag (peer lost?)")
+            raise RuntimeError(f"P2P collective: rank {e - 1} never raised its flag within {self.timeout:g} s "
+                               "(peer lost or stalled); the reduction was skipped, not applied")
+
+    def poll(self) -> None:
+        """Asynchronous check: read the result of the previous poll's device->host copy (if it has
+        landed) and enqueue a new one.  Costs one 4-byte copy on the stream; raises like check()."""
+        if self._err_host is None:
+            return self.check()
+        ev = self._err_event
+        if ev is not None and ev.query():
+            e = int(self._err_host[0])
+            if e:
+                raise RuntimeError(f"P2P collective: rank {e - 1} never raised its flag within {self.timeout:g} s "
+                                   "(peer lost or stalled); the reduction was skipped, not applied")
+            ev = None
+        if ev is None:
+            self._err_host.copy_(self.err, non_blocking=True)
+            self._err_event = torch.cuda.Event()
+            self._err_event.record(torch.cuda.current_stream(self.device))
 
     def close(self) -> None:
+        """Collective: every rank must call it (no peer may still read our staging buffer)."""
         if self._buf is None:
             return
         torch.cuda.synchronize(self.device)
-        hdist.barrier()  # no peer may still read our staging buffer
+        hdist.barrier()
+        self._release()
+
+    def _release(self) -> None:
+        """Local teardown (the caller has synchronised the ranks)."""
         C = ext()
         for p in self._opened:
             C.close(p)
-        C.free(self._buf)
-        C.free(self._flag)
+        if self._buf is not None:
+            C.free(self._buf)
+        if self._flag is not None:
+            C.free(self._flag)
         self._buf = self._flag = None
         self._opened = []
+
+
+def _agree(ok: bool) -> bool:
+    """Every rank's verdict, combined (min) over the default group."""
+    if hdist.world_size() <= 1:
+        return ok
+    return hdist.all_reduce_scalar(1.0 if ok else 0.0, "min") > 0.5
+
+
+def self_test(comm: OneShotAllReduce) -> bool:
+    """A known all-reduce in both modes, checked exactly on this rank (integer-valued floats: every
+    summation order gives the same result)."""
+    dev = comm.device
+    n = min(comm.cap, 4096 * comm.world + 12)
+    idx = torch.arange(n, device=dev, dtype=torch.float32)
+    want = sum(((idx % 97) + r + 1) for r in range(comm.world))
+    for mode in ("one_shot", "two_shot"):
+        x = (idx % 97) + comm.rank + 1
+        comm(x, mode=mode)
+        torch.cuda.synchronize(dev)
+        if int(comm.err.item()) != 0 or not torch.equal(x, want):
+            return False
+    return True
+
+
+class P2PComm:
+    @staticmethod
+    def create(cap_bytes: int, device=None, required: bool | None = None) -> OneShotAllReduce | None:
+        """Collective, fail-safe setup: every rank allocates, exchanges handles, maps its peers and runs
+        the self-test; unless ALL ranks succeed everyone gets None (or RuntimeError if required)."""
+        required = mode() == "1" if required is None else required
+        world = hdist.world_size()
+        if world <= 1 or world > ext().MAX_RANKS:
+            if required and world > 1:
+                raise RuntimeError(f"P2P collectives need 2..{ext().MAX_RANKS} ranks on one node")
+            return None
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if lw != world:  # ranks on other nodes are not IPC-reachable
+            if required:
+                raise RuntimeError("P2P collectives need every rank on one node")
+            return None
+        comm = _create_local(cap_bytes, device)  # never raises after joining the handle exchange
+        why = repr(comm._setup_err) if comm._setup_err is not None else ""
+        ok = _agree(comm._setup_err is None)
+        if ok:
+            try:
+                ok = self_test(comm)
+            except Exception as e:  # noqa: BLE001 - every failure falls back to RCCL
+                ok, why = False, repr(e)
+            ok = _agree(ok)
+        if not ok:
+            # every rank reaches this point: drain, meet, then tear down locally
+            try:
+                torch.cuda.synchronize(comm.device)
+            except Exception:  # noqa: BLE001
+                pass
+            hdist.barrier()
+            try:
+                comm._release()
+            except Exception:  # noqa: BLE001
+                pass
+            if required:
+                raise RuntimeError(f"P2P collectives unavailable on rank {hdist.rank()}: {why or 'self-test failed'}")
+            return None
+        return comm
+
+
+def _create_local(cap_bytes: int, device) -> OneShotAllReduce:
+    """OneShotAllReduce whose setup tolerates a failing rank: it sends None handles, every rank still
+    joins the exchange, and the failure is recorded in ``_setup_err`` instead of raised."""
+    C = ext()
+    comm = OneShotAllReduce.__new__(OneShotAllReduce)
+    comm.rank, comm.world = hdist.rank(), hdist.world_size()
+    comm.device = device or hdist.device()
+    comm.cap = (int(cap_bytes) // 4 + 3) & ~3
+    comm.blocks = max(1, min(_default_blocks(comm.world), C.MAX_BLOCKS))
+    comm.timeout = _timeout()
+    comm.two_shot_min = int(os.environ.get("HOPSX_TWOSHOT_MIN_KB", "256")) * 1024 // 4
+    comm._buf = comm._flag = None
+    comm._opened = []
+    err = None
+    hb = hf = None
+    try:
+        comm._buf, hb = C.alloc(4 * comm.cap * 4, False)
+        comm._flag, hf = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
+        hb, hf = bytes(hb), bytes(hf)
+    except Exception as e:  # noqa: BLE001
+        err, hb, hf = e, None, None
+    objs = [None] * comm.world
+    dist.all_gather_object(objs, (comm.rank, hb, hf))
+    comm._setup_err = err
+    if err is None:
+        try:
+            comm._map(objs)
+            comm.epochs = torch.zeros(C.MAX_BLOCKS, dtype=torch.int32, device=comm.device)
+            comm.err = torch.zeros(1, dtype=torch.int32, device=comm.device)
+            comm._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            comm._err_event = None
+        except Exception as e:  # noqa: BLE001
+            comm._setup_err = e
+    return comm

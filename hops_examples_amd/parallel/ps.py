@@ -45,6 +45,7 @@ class ShardedPS:
         if self.world > 1:
             hdist.broadcast_(self.arena.master, 0)
             self.arena.refresh_shadow()
+        self.arena._hx_engine = self  # checkpoint.save gathers the owner-only shards
         if optimizer is not None:
             self.attach(optimizer)
 
@@ -98,6 +99,16 @@ class ShardedPS:
         if self.world > 1:
             self._gather(self.arena.master)
         return self.arena.master
+
+    def gather_state(self) -> None:
+        """Collective: on GPU only the bf16 shadow is all-gathered per step, so the fp32 master and
+        every optimizer moment are current only on each shard's owner; reassemble them on every
+        rank (checkpoint.save calls this before rank 0 serialises)."""
+        if self.world <= 1:
+            return
+        self._gather(self.arena.master)
+        for t in self.arena.states.values():
+            self._gather(t)
 
     def close(self):
         pass

@@ -8,10 +8,17 @@ MI355X the small reference models are launch-bound (a 32-image MNIST step is
 host call per step instead of ~30 kernel launches plus autograd bookkeeping.
 
 world_size == 1 : one graph  = fwd + bwd + optimizer + rng
-world_size  > 1 : graph A    = fwd + bwd            (RCCL all-reduce of the flat
-                  grad buckets runs between the graphs, on RCCL's stream)
-                  graph B    = optimizer + rng
-                  HOPSX_GRAPH_COLLECTIVES=1 captures the all-reduce too (one graph).
+world_size  > 1 : P2P path (parallel/oneshot.py, one node): one graph = fwd + bwd + the fused
+                  reduce-scatter / sharded-update / all-gather kernel (or P2P all-reduce +
+                  optimizer), replayed steps_per_execution at a time like one GPU;
+                  RCCL path: graph A = fwd + bwd (the RCCL all-reduce of the flat grad
+                  buckets runs between the graphs, on RCCL's stream), graph B = optimizer + rng;
+                  HOPSX_GRAPH_COLLECTIVES=1 captures the RCCL collectives too (one graph).
+
+Every path — eager, one-step graph, multi-step graph — runs the same step tail (``_tail``):
+gradient exchange, optimizer, the engine's post-step (sharded PS all-gather).  Hyper-parameters
+live on the device (optim.FusedOptimizer.sync_hp before every replay), so lr changes after a
+capture take effect on replay.
 
 ``run_resident(xs, ys, n)`` (single GPU, HBM-resident epoch) also captures ``steps_per_execution``
 consecutive steps into ONE graph — Keras' ``compile(steps_per_execution=...)``.  Every step is
@@ -83,8 +90,10 @@ class TrainStep:
         self._pool = None
         if dp is not None:
             optimizer.grad_scale = dp.grad_scale()
+            if hasattr(dp, "bind_optimizer"):
+                dp.bind_optimizer(optimizer)  # fused P2P step tail when the engine supports it
             if getattr(dp, "capturable", lambda: False)():
-                self.graph_collectives = True  # one-shot all-reduce kernels capture like any other
+                self.graph_collectives = True  # P2P kernels capture like any other
 
     # ------------------------------------------------------------- eager path
     def _forward(self, x):
@@ -124,12 +133,33 @@ class TrainStep:
         if self.dp is not None and hasattr(self.dp, "post_step"):
             self.dp.post_step()  # sharded PS: all-gather the updated weights
 
-    def eager(self, x, y):
-        r = self._fwd_bwd(x, y)
+    def _fused(self) -> bool:
+        return self.dp is not None and getattr(self.dp, "fuses_optimizer", lambda o: False)(self.opt)
+
+    def _tail(self, eager: bool = False):
+        """Gradient exchange + optimizer + post-step: the one step tail every path runs."""
+        if self._fused():
+            self.dp.fused_update(self.opt)  # reduce-scatter + sharded update + all-gather, one kernel
+            return
         if self.dp is not None:
-            self.dp.finish()
+            if eager:
+                self.dp.finish()  # completes the bucket all-reduces overlapped with backward
+            else:
+                self.dp.allreduce_all()
         self._opt()
         self._post()
+
+    def _sync_hp(self):
+        if hasattr(self.opt, "sync_hp"):
+            self.opt.sync_hp()
+
+    def _after_replay(self):
+        if self.dp is not None and hasattr(self.dp, "poll"):
+            self.dp.poll()  # P2P failure flag, checked asynchronously every poll_every steps
+
+    def eager(self, x, y):
+        r = self._fwd_bwd(x, y)
+        self._tail(eager=True)
         return r
 
     # ------------------------------------------------------------- graph path
@@ -148,16 +178,14 @@ class TrainStep:
             hooks.unsubscribe(self.dp._on_ready)
         pool = self._pool = torch.cuda.graph_pool_handle()
         g1 = torch.cuda.CUDAGraph()
+        one_graph = world == 1 or self.dp is None or self.graph_collectives
+        self._sync_hp()
         with _capture_graph(g1, pool=pool):
             out = self._fwd_bwd(self._sx, self._sy)
-            if world == 1 or self.dp is None or self.graph_collectives:
-                if self.dp is not None:
-                    self.dp.allreduce_all()
-                self._opt()
-                if self.graph_collectives:
-                    self._post()
+            if one_graph:
+                self._tail()
         self._g1 = g1
-        if world > 1 and self.dp is not None and not self.graph_collectives:
+        if not one_graph:
             g2 = torch.cuda.CUDAGraph()
             with _capture_graph(g2, pool=pool):
                 self._opt()
@@ -185,12 +213,17 @@ class TrainStep:
             return r
         self._n += 1
         health.beat(self._n)
+        self._replay()
+        return self._out
+
+    def _replay(self):
+        self._sync_hp()
         self._g1.replay()
         if self._g2 is not None:
             self.dp.allreduce_all()
             self._g2.replay()
             self._post()
-        return self._out
+        self._after_replay()
 
     def _multi_ok(self, xs, ys) -> bool:
         return (self.steps_per_execution > 1 and self._g2 is None and self._g1 is not None
@@ -202,14 +235,13 @@ class TrainStep:
         one-step graph; each captured optimizer kernel prefetches the batch the next step reads)."""
         torch.cuda.synchronize()
         self._pf_opt.prefetch = ([(xs, self._sx), (ys, self._sy)], self._cursor)
+        self._sync_hp()
         try:
             g = torch.cuda.CUDAGraph()
             with _capture_graph(g, pool=self._pool):
                 for _ in range(self.steps_per_execution):
                     out = self._fwd_bwd(self._sx, self._sy)
-                    if self.dp is not None:
-                        self.dp.allreduce_all()
-                    self._opt()
+                    self._tail()  # the same tail as the one-step graph (incl. the PS post-step)
         finally:
             self._pf_opt.prefetch = None
         torch.cuda.synchronize()
@@ -234,7 +266,9 @@ class TrainStep:
             for _ in range(self.steps_per_execution):
                 self._n += 1
                 health.beat(self._n)
+            self._sync_hp()
             self._gU.replay()
+            self._after_replay()
             n -= self.steps_per_execution
             r = self._outU
         return r
@@ -261,9 +295,5 @@ class TrainStep:
         if not _same_storage(x, self._sx):
             _copy_into(self._sx, x)
             self._sy.copy_(y, non_blocking=True)
-        self._g1.replay()
-        if self._g2 is not None:
-            self.dp.allreduce_all()
-            self._g2.replay()
-            self._post()
+        self._replay()
         return self._out

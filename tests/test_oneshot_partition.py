@@ -42,3 +42,24 @@ def test_partition_tiles_exactly_once(n, world, G):
         for i in range(lo, hi):
             cover[i] += 1
     assert all(c == 1 for c in cover)
+
+
+@pytest.mark.parametrize("n,world", list(itertools.product([64, 1000, 18880, 1394304], [2, 3, 4, 8])))
+def test_dp_owner_slices_match_kernel_geometry(n, world):
+    """DataParallel.owner_slices (checkpoint gather of owner-only optimizer moments) must be exactly
+    the union of the kernel's per-workgroup ranges of each slice."""
+    from hops_examples_amd.parallel.dp import DataParallel
+
+    class _A:
+        numel = n
+
+    dp = DataParallel.__new__(DataParallel)
+    dp.arena, dp.world, dp._fused_opt = _A(), world, object()
+    sl = dp.owner_slices()
+    rng = twoshot_ranges(n, world, 64)
+    for r in range(world):
+        idx = set()
+        for b in range(64):
+            lo, hi = rng[(b, r)]
+            idx.update(range(lo, hi))
+        assert idx == set(range(sl[r].start, sl[r].stop)), r
