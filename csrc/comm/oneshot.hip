@@ -224,7 +224,7 @@ struct DpArgs {
   OptHP h;            // by value; overridden by hp_dev when given
   const float* hp_dev;
   float* step_dev;    // completed-step counter (bias correction)
-  unsigned* arrive;   // arrival counter of the bookkeeping (zero at rest)
+  unsigned* arrive;   // arrival counter of the bookkeeping (kArriveWords, zero at rest)
   unsigned long long* rng;
   Prefetch pf;
 };

@@ -80,11 +80,11 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   });
   m.def("linear_bwd_pair", [](u dy, u w, u x, u dx, u yprev, int act_prev, u colsum, u ay, int aact, u dw, u db,
                               int M, int N, int K, std::vector<int> pool, u pam, u px, u prng, unsigned psalt,
-                              float pp, u st) {
+                              float pp, int dw_store, u st) {
     return hopsx_linear_bwd_pair(P<void>(dy), P<void>(w), P<void>(x), P<void>(dx), P<void>(yprev), act_prev,
                                  P<float>(colsum), P<void>(ay), aact, P<float>(dw), P<float>(db), M, N, K,
                                  pool.empty() ? nullptr : pool.data(), P<unsigned char>(pam), P<void>(px),
-                                 P<unsigned long long>(prng), psalt, pp, S(st));
+                                 P<unsigned long long>(prng), psalt, pp, dw_store, S(st));
   });
   m.def("conv2d_bwd_pair", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact,
                               std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u st) {

@@ -130,10 +130,10 @@ extern "C" int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long
 // workgroups compute dX = (dY*act'(y)) . W (masked by the previous layer's act'), the rest
 // dW += (dY*act'(y))^T . X with the bias gradient as the staged operand's row sums.  At small
 // batch each GEMM alone is a latency-bound launch on a few hundred workgroups.
-template <int BMA, int BMB, class EPA>
+template <int BMA, int BMB, class EPA, class EPB>
 __global__ __launch_bounds__(256) void linear_bwd_pair_k(DenseLoader aA, DenseLoader bA, EPA eA, int MA,
                                                          int NA, int KA, int kpsA, int gxA, int gyA, DenseLoader aB,
-                                                         DenseLoader bB, EpiAtomicF32 eB, int MB, int NB, int KB,
+                                                         DenseLoader bB, EPB eB, int MB, int NB, int KB,
                                                          int kpsB, int gxB, int gyB, float* rowsumB) {
   const int nA = gxA * gyA;
   if ((int)blockIdx.x < nA) {
@@ -153,7 +153,7 @@ extern "C" int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* 
                                      int act_prev, float* colsum, const void* ay, int aact, float* dw, float* dbias,
                                      int M, int N, int K, const int* pool, const unsigned char* pool_am,
                                      const void* pool_x, const unsigned long long* pool_rng, unsigned pool_salt,
-                                     float pool_p, hipStream_t st) {
+                                     float pool_p, int dw_store, hipStream_t st) {
   if (hopsx_disabled("bwd_pair") || M <= 0 || N <= 0 || K <= 0) return -2;
   // dgrad: [M x K] = dy[M x N] . W[N x K]
   if (want_splitk(M, K, N)) return -2;  // the small-M split-K dgrad path keeps its own launch
@@ -175,18 +175,28 @@ extern "C" int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* 
   DenseLoader aB{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
   DenseLoader bB{(const bf16_raw*)x, K, is_vec_ok(x, K)};
   EpiAtomicF32 eB{dw, K, 1.f, nullptr};
-#define HOPSX_LP(A_, B_)                                                                                          \
-  if (bma == A_ && bmb == B_) {                                                                                   \
-    if (pool)                                                                                                     \
-      hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_, EpiPoolScatterBF16>), dim3((unsigned)total), dim3(256), 0, st, \
-                         aA, bA, eP, M, K, N, pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);      \
-    else                                                                                                          \
-      hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_, EpiDActBF16>), dim3((unsigned)total), dim3(256), 0, st, aA, bA, \
-                         eA, M, K, N, pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);             \
-    return (int)hipGetLastError();                                                                               \
+  // the only contribution to a zeroed dW and no K split: plain stores (see ops_api.h)
+  const bool store = dw_store && gyB == 1 && !hopsx_disabled("dw_store");
+  EpiStoreF32 eS{dw, K, nullptr, 1.f, 0.f, 0, nullptr};
+#define HOPSX_LP2(A_, B_, EPA_, ea_)                                                                               \
+  if (store)                                                                                                       \
+    hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_, EPA_, EpiStoreF32>), dim3((unsigned)total), dim3(256), 0, st, aA, \
+                       bA, ea_, M, K, N, pa.kps, gxA, gyA, aB, bB, eS, N, K, M, pb.kps, gxB, gyB, dbias);           \
+  else                                                                                                             \
+    hipLaunchKernelGGL((linear_bwd_pair_k<A_, B_, EPA_, EpiAtomicF32>), dim3((unsigned)total), dim3(256), 0, st,    \
+                       aA, bA, ea_, M, K, N, pa.kps, gxA, gyA, aB, bB, eB, N, K, M, pb.kps, gxB, gyB, dbias);
+#define HOPSX_LP(A_, B_)                                   \
+  if (bma == A_ && bmb == B_) {                            \
+    if (pool) {                                            \
+      HOPSX_LP2(A_, B_, EpiPoolScatterBF16, eP)            \
+    } else {                                               \
+      HOPSX_LP2(A_, B_, EpiDActBF16, eA)                   \
+    }                                                      \
+    return (int)hipGetLastError();                         \
   }
   HOPSX_LP(32, 32) HOPSX_LP(32, 64) HOPSX_LP(32, 128) HOPSX_LP(64, 32) HOPSX_LP(64, 64) HOPSX_LP(64, 128)
   HOPSX_LP(128, 32) HOPSX_LP(128, 64) HOPSX_LP(128, 128)
 #undef HOPSX_LP
+#undef HOPSX_LP2
   return -2;
 }

@@ -17,10 +17,13 @@ int hopsx_gemm(const void* A, long lda, int a_kc, const void* B, long ldb, int b
 // a Linear layer's dgrad + wgrad (+ bias grad) in one launch; -2: unsupported shape (gemm.hip)
 // pool (optional) = {C, PH, PW, KH, KW, act}: x came from a non-overlapping max-pool and dx is the
 // POOL INPUT gradient, scattered by the dgrad epilogue (pool_am argmax, pool_x for ReL', dropout p)
+// dw_store: dW is this step's only contribution to a zeroed gradient -> plain stores instead of
+// float atomics when K is not split (atomics run at the memory side at ~1.3 TB/s, stores ~6 TB/s)
 int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* x, void* dx, const void* yprev, int act_prev,
                           float* colsum, const void* ay, int aact, float* dw, float* dbias, int M, int N, int K,
                           const int* pool, const unsigned char* pool_am, const void* pool_x,
-                          const unsigned long long* pool_rng, unsigned pool_salt, float pool_p, hipStream_t st);
+                          const unsigned long long* pool_rng, unsigned pool_salt, float pool_p, int dw_store,
+                          hipStream_t st);
 int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out, const float* bias, int act,
                      float* colsum, float xscale, float xshift, hipStream_t st);
 // y/yact: this conv's activation output -> fused act' mask on dY (prologue fusion)

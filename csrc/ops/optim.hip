@@ -23,7 +23,7 @@ __device__ inline void st_nt(float* dst, long i, const float4& v) {
   __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(dst) + i);
 }
 
-template <int KIND>
+template <int KIND, int UN>
 __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __restrict__ g, float* __restrict__ s1,
                                                float* __restrict__ s2, float* __restrict__ s3,
                                                bf16_raw* __restrict__ shadow, long n, OptHP h,
@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
   constexpr int NS = nstate<KIND>();
   const long n4 = vec ? (n >> 2) : 0;
   const long stride = (long)gridDim.x * blockDim.x;
-  // UN float4 per thread per trip with every load issued before the first update: at the
-  // 512-workgroup cap a 1.4 M-parameter model is ONE trip (one memory round trip, not three)
-  constexpr int UN = 3;
+  // UN float4 per thread per trip with every load issued before the first update: the launcher
+  // picks UN so that a small arena (the 1.4 M-parameter flagship at 256 workgroups) is ONE trip —
+  // one memory round trip instead of two dependent ones
   for (long i0 = blockIdx.x * (long)blockDim.x + threadIdx.x; i0 < n4; i0 += UN * stride) {
     float4 w[UN], gr[UN], a[UN], b[UN], c[UN];
 #pragma unroll
@@ -128,20 +128,30 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
   const bool aligned = ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)s3) % 16 == 0 &&
                        ((uintptr_t)shadow_bf16 % 8 == 0);
   long g = ((aligned ? n / 4 : n) + 255) / 256;
-  // grid cap: 256 workgroups (one per CU) measured best for the 1.4 M-parameter flagship
-  // (0.0894 -> 0.0878 ms/step; 128: 0.0899, 512: 0.0894, 1024: 0.0946); larger arenas keep 512
+  // grid cap 512 (two workgroups per CU).  With the per-XCD sharded arrival counter the flagship
+  // step measured 256: 0.0875, 384: 0.0859, 512: 0.0848, 768: 0.0849, 1024: 0.0850 ms
+  // (profiles/r2s2_optim_grid_sweep.txt); with one arrival word 256 had been best (the fan-in
+  // grew with the grid)
   static const int genv = getenv("HOPSX_OPT_GRID") ? atoi(getenv("HOPSX_OPT_GRID")) : 0;
-  const int gcap = genv > 0 ? genv : (n <= (8L << 20) ? 256 : 512);
+  const int gcap = genv > 0 ? genv : 512;
   static const int nt = getenv("HOPSX_OPT_NT") ? atoi(getenv("HOPSX_OPT_NT")) : 0;
   if (g > gcap) g = gcap;
   if (g < 1) g = 1;
+  // 6 float4 per thread when that covers the whole arena in one trip, else 3 (VGPR budget)
+  static const int unenv = getenv("HOPSX_OPT_UN") ? atoi(getenv("HOPSX_OPT_UN")) : 0;
+  const long n4 = aligned ? n / 4 : 0;
+  const int un = unenv == 3 || unenv == 6 ? unenv : (n4 > 3L * g * 256 && n4 <= 6L * g * 256 ? 6 : 3);
   bf16_raw* sh = (bf16_raw*)shadow_bf16;
   // without an arrival counter the bookkeeping needs its own tiny launch
   unsigned* arr = (step_dev || rng) ? arrive : nullptr;
-#define OPT_CASE(K)                                                                                                   \
-  case K:                                                                                                             \
-    hipLaunchKernelGGL(optim_k<K>, dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, arr, rng, \
-                       zero_grad, (int)aligned, pf, nt, hp_dev);                                                              \
+#define OPT_CASE(K)                                                                                             \
+  case K:                                                                                                       \
+    if (un == 6)                                                                                                \
+      hipLaunchKernelGGL((optim_k<K, 6>), dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, \
+                         arr, rng, zero_grad, (int)aligned, pf, nt, hp_dev);                                     \
+    else                                                                                                        \
+      hipLaunchKernelGGL((optim_k<K, 3>), dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, \
+                         arr, rng, zero_grad, (int)aligned, pf, nt, hp_dev);                                     \
     break;
   switch (kind) {
     OPT_CASE(0) OPT_CASE(1) OPT_CASE(2) OPT_CASE(3) OPT_CASE(4) OPT_CASE(5) OPT_CASE(6)

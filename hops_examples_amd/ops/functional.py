@@ -129,10 +129,26 @@ def to_compute(x: torch.Tensor) -> torch.Tensor:
 
 
 # ===================================================================== Linear
+# Single-contribution weight gradients (set by runtime.step.TrainStep around one step's forward +
+# backward, whose gradients start zeroed): "uses" counts the forward uses of each weight, and a
+# Linear whose weight was used once STORES its dW instead of adding it with float atomics.
+STEP = {"overwrite": False, "uses": {}}
+
+
+def _note_use(w) -> None:
+    if STEP["overwrite"]:
+        STEP["uses"][id(w)] = STEP["uses"].get(id(w), 0) + 1
+
+
+def _sole_use(w) -> bool:
+    return STEP["overwrite"] and STEP["uses"].get(id(w), 0) == 1
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act, out_f32, pool=None):
         ctx.pool = pool
+        _note_use(w)
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         wb = _arena.weight_bf16(w)
         y = K.linear_fwd(x2, wb, b, act=act, out_f32=out_f32)
@@ -159,7 +175,8 @@ class _LinearFn(torch.autograd.Function):
             # small layer: dgrad and wgrad (+ bias grad) as ONE launch (horizontal fusion); when the
             # input is a flattened max-pool output, the dgrad epilogue also does the pool backward
             pool = ctx.pool if "pool_scatter" not in _disabled() else None
-            r = K.linear_bwd_pair(dy2, _arena.weight_bf16(w), x2, gw, y=ymask, act=act, dbias=gb, pool=pool)
+            r = K.linear_bwd_pair(dy2, _arena.weight_bf16(w), x2, gw, y=ymask, act=act, dbias=gb, pool=pool,
+                                  dw_store=_sole_use(w) and gw is _arena.grad_target(w))
             if r is not False:
                 if pool is not None:
                     # r is the pool-INPUT gradient: hand autograd an unfilled placeholder for this

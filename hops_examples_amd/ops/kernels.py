@@ -105,13 +105,14 @@ def linear_wgrad(dy, x, dw, alpha=1.0, y=None, act=0, dbias=None):
     return dw
 
 
-def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None, pool=None):
+def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None, pool=None, dw_store=False):
     """dX and dW (+ dbias) of a Linear layer in ONE launch (gemm.hip linear_bwd_pair_k); returns
     dX [M, K] bf16, or False when the shape goes to the separate launches (small-M split-K dgrad).
     ``pool`` = (am, premask, in_shape, (KH, KW), act, rng, salt, p): the Linear's input is the
     flattened output of a non-overlapping max-pool; the returned tensor is then the gradient of the
     POOL INPUT (shape in_shape), scattered by the dgrad epilogue (the pool backward fused away).
-    ``premask``: also apply ReLU' of the pool input (read off the pooled value = this layer's input)."""
+    ``premask``: also apply ReLU' of the pool input (read off the pooled value = this layer's input).
+    ``dw_store``: dW is the only contribution to a zeroed buffer — stored, not atomically added."""
     M, N = dy.shape
     K = x.shape[1]
     _req(dy, BF16, "dy")
@@ -128,7 +129,7 @@ def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None, pool=None):
     else:
         dx = torch.empty(M, K, device=dy.device, dtype=BF16)
     rc = _C.ext().linear_bwd_pair(ptr(dy), ptr(w), ptr(x), ptr(dx), 0, 0, 0, ptr(y), act_id(act), ptr(dw),
-                                  ptr(dbias), M, N, K, pl, pam, px, prng, psalt, pp, stream())
+                                  ptr(dbias), M, N, K, pl, pam, px, prng, psalt, pp, int(bool(dw_store)), stream())
     if rc == -2:
         return False
     check(rc, "linear_bwd_pair")
@@ -356,7 +357,7 @@ def loss_fwd_bwd(kind: int, logits, target, grad_scale, loss_sum, correct, dlogi
 def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_grad=True, arrive=None, rng=None,
                prefetch=None, hp_dev=None):
     """One fused update over flat buffers.  ``step_dev`` (f32[1]) counts completed steps and,
-    with ``arrive`` (int32[1], zero-initialised), is bumped in-kernel by the last workgroup,
+    with ``arrive`` (int32[288], zero-initialised), is bumped in-kernel by the last workgroup,
     together with the dropout RNG counter ``rng[1]`` when given.
     ``prefetch`` = (pairs, cursor): pairs of (resident [nbatch, ...] tensor, static input buffer);
     the kernel copies batch (cursor+1) % nbatch into the buffers and advances the int64 cursor.
@@ -364,7 +365,7 @@ def optim_step(kind: int, param, grad, s1, s2, s3, shadow, hp, step_dev, zero_gr
     instead of ``hp`` (so a replayed hipGraph sees learning-rate changes)."""
     n = param.numel()
     if step_dev is not None and arrive is None:
-        arrive = torch.zeros(1, device=param.device, dtype=torch.int32)
+        arrive = torch.zeros(9 * 32, device=param.device, dtype=torch.int32)  # optim_core.h kArriveWords
     srcs, dsts, nbytes, cur, nb = [], [], [], 0, 0
     if prefetch is not None:
         pairs, cursor = prefetch

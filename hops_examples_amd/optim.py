@@ -17,6 +17,8 @@ import torch
 from .ops._C import OPTIM
 from .runtime.arena import ALIGN, ParamArena
 
+ARRIVE_WORDS = 9 * 32  # csrc/ops/optim_core.h kArriveWords
+
 
 def _arena_of(obj) -> ParamArena:
     if isinstance(obj, ParamArena):
@@ -69,7 +71,8 @@ class FusedOptimizer:
         self.prefetch = None  # (pairs, cursor): fused next-batch copy of a resident dataset (TrainStep)
         dev = self.arena.device
         self.step_count = torch.zeros(1, device=dev, dtype=torch.float32)
-        self._arrive = torch.zeros(1, device=dev, dtype=torch.int32)
+        # arrival counter of the in-kernel step bookkeeping: 8 per-XCD shards + top word (optim_core.h)
+        self._arrive = torch.zeros(ARRIVE_WORDS, device=dev, dtype=torch.int32)
         # device RNG state advanced by the optimizer kernel's last workgroup (dropout masks)
         self.rng = None
         if dev.type == "cuda":

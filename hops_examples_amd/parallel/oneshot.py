@@ -224,19 +224,22 @@ def _agree(ok: bool) -> bool:
     return hdist.all_reduce_scalar(1.0 if ok else 0.0, "min") > 0.5
 
 
-def self_test(comm: OneShotAllReduce) -> bool:
-    """A known all-reduce in both modes, checked exactly on this rank (integer-valued floats: every
-    summation order gives the same result)."""
+def self_test(comm: OneShotAllReduce, rounds: int = 3) -> bool:
+    """Known all-reduces in both modes, checked exactly on this rank (integer-valued floats: every
+    summation order gives the same result).  Several rounds with changing values, so both staging
+    parities are written, read, and REUSED — a peer that saw a stale cached copy of an earlier
+    epoch (a missing write-back or invalidate over xGMI) fails the test."""
     dev = comm.device
     n = min(comm.cap, 4096 * comm.world + 12)
     idx = torch.arange(n, device=dev, dtype=torch.float32)
-    want = sum(((idx % 97) + r + 1) for r in range(comm.world))
-    for mode in ("one_shot", "two_shot"):
-        x = (idx % 97) + comm.rank + 1
-        comm(x, mode=mode)
-        torch.cuda.synchronize(dev)
-        if int(comm.err.item()) != 0 or not torch.equal(x, want):
-            return False
+    for it in range(rounds):
+        want = sum(((idx * (it + 1)) % 97) + r + 1 for r in range(comm.world))
+        for mode in ("one_shot", "two_shot"):
+            x = ((idx * (it + 1)) % 97) + comm.rank + 1
+            comm(x, mode=mode)
+            torch.cuda.synchronize(dev)
+            if int(comm.err.item()) != 0 or not torch.equal(x, want):
+                return False
     return True
 
 

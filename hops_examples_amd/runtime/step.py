@@ -118,9 +118,17 @@ class TrainStep:
             HF.HEAD["defer"] = False
 
     def _fwd_bwd(self, x, y):
-        out = self._forward(x)
-        loss, correct, count, root, grad = HF.loss_and_grad_root(out, y, self.loss_kind)
-        root.backward(grad)
+        # every step starts from zeroed gradients (the optimizer / fused DP step zeroes them): a weight
+        # used once in this forward may STORE its gradient instead of adding it (functional.STEP)
+        HF.STEP["overwrite"] = self.device.type == "cuda" and os.environ.get("HOPSX_DW_STORE", "1") == "1"
+        HF.STEP["uses"] = {}
+        try:
+            out = self._forward(x)
+            loss, correct, count, root, grad = HF.loss_and_grad_root(out, y, self.loss_kind)
+            root.backward(grad)
+        finally:
+            HF.STEP["overwrite"] = False
+            HF.STEP["uses"] = {}
         HF.join_side_streams()  # gradients complete before all-reduce / optimizer
         return {"loss": loss, "correct": correct, "count": count}
 
