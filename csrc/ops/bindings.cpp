@@ -11,6 +11,7 @@
 #include "ops_api.h"
 
 namespace py = pybind11;
+extern "C" void hopsx_mlp_head_debug(void* p);  // loss.hip: phase stamps (tools/dbg_mlp_head.py)
 using u = uintptr_t;
 
 template <class T>
@@ -73,6 +74,13 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_head_ce(kind, P<void>(logits), lf32, P<void>(target), B, C, KD, gs, P<void>(h), P<void>(w),
                          P<float>(dw), P<float>(db), P<void>(dh), P<float>(loss), P<int>(correct), P<float>(bias),
                          P<void>(lout), S(st));
+  });
+  m.def("mlp_head_debug", [](u p) { hopsx_mlp_head_debug(P<void>(p)); });
+  m.def("mlp_head", [](u x, u w1, u b1, int act1, u y, u ws, u arrive, int B, int K, int N1, int kind, u target,
+                       int C, float gs, u w2, u b2, u dw2, u db2, u dh, u loss, u correct, u lout, int lf32, u st) {
+    return hopsx_mlp_head(P<void>(x), P<void>(w1), P<float>(b1), act1, P<void>(y), P<float>(ws), P<unsigned>(arrive),
+                          B, K, N1, kind, P<void>(target), C, gs, P<void>(w2), P<float>(b2), P<float>(dw2),
+                          P<float>(db2), P<void>(dh), P<float>(loss), P<int>(correct), P<void>(lout), lf32, S(st));
   });
   m.def("zero", [](u p, long bytes, u st) { return hopsx_zero(P<void>(p), bytes, S(st)); });
   m.def("nonfinite", [](u x, long n, int is_bf16, u out, u st) {

@@ -54,6 +54,12 @@ bool hopsx_head_ce_ok(int C, int KD);
 int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
                   float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh, float* loss_sum,
                   int* correct, const float* bias, void* logits_out, hipStream_t st);
+// fused last hidden Dense + head (loss.hip mlp_head_k): y = act(x W1^T + b1) stored, then head_ce from
+// LDS; ws fp32 [B][N1] and arrive (kArriveWords) persistent, zero at rest.  -2: shape not supported
+int hopsx_mlp_head(const void* x, const void* w1, const float* b1, int act1, void* y, float* ws, unsigned* arrive,
+                   int B, int K, int N1, int kind, const void* target, int C, float grad_scale, const void* w2,
+                   const float* b2, float* dw2, float* db2, void* dh, float* loss_sum, int* correct,
+                   void* logits_out, int logits_f32, hipStream_t st);
 int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
                        float grad_scale, float* loss_sum, int* correct, void* dlogits, int dlogits_f32,
                        hipStream_t st);

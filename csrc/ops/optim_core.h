@@ -47,30 +47,16 @@ __device__ inline void prefetch_copy(const Prefetch& pf) {
 
 // The last workgroup to arrive bumps the completed-step counter (bias correction), the dropout
 // RNG counter and the prefetch cursor, so a captured step needs no bookkeeping launches.
-// Arrival counter: kArriveWords uint32, zero at rest — 8 shards (one per XCD under round-robin
-// dispatch, blockIdx % 8) on their own 128-B lines, then the top word at index 0.  256 arrivals
-// on ONE word serialise at ~12 ns each (a ~3 us fan-in, MI355X_MICROARCH "fanin"; measured 2.8 us
-// of the flagship's optimizer launch); sharded, each word sees grid/8 arrivals and the top 8.
-constexpr int kArriveWords = 9 * 32;
+// Arrival counter: kArriveWords uint32 (common.h grid_arrive_last: per-XCD shards, zero at rest);
+// with one arrival word the fan-in cost 2.8 us of the flagship's optimizer launch, sharded 1.2.
 __device__ inline void step_bookkeeping(unsigned* arrive, float* step_dev, float t, unsigned long long* rng,
                                         const Prefetch& pf) {
   if (!arrive) return;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned G = gridDim.x;
-    const unsigned shard = blockIdx.x & 7u;
-    const unsigned members = (G - shard + 7u) / 8u;  // blocks b < G with b % 8 == shard
-    unsigned* sw = arrive + 32u * (shard + 1u);
-    if (atomicAdd(sw, 1u) == members - 1u) {
-      atomicExch(sw, 0u);
-      const unsigned shards = G < 8u ? G : 8u;
-      if (atomicAdd(arrive, 1u) == shards - 1u) {
-        if (step_dev) step_dev[0] = t;
-        if (rng) rng[1] += 1ull;
-        if (pf.njobs) pf.cursor[0] = (pf.cursor[0] + 1) % pf.nbatch;
-        atomicExch(arrive, 0u);
-      }
-    }
+  if (threadIdx.x == 0 && grid_arrive_last(arrive)) {
+    if (step_dev) step_dev[0] = t;
+    if (rng) rng[1] += 1ull;
+    if (pf.njobs) pf.cursor[0] = (pf.cursor[0] + 1) % pf.nbatch;
   }
 }
 

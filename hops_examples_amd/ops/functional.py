@@ -151,7 +151,12 @@ class _LinearFn(torch.autograd.Function):
         _note_use(w)
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         wb = _arena.weight_bf16(w)
-        y = K.linear_fwd(x2, wb, b, act=act, out_f32=out_f32)
+        if PREHEAD["arm"]:
+            # deferred: the fused loss kernel (mlp_head) fills y before anything reads it
+            y = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=BF16)
+            PREHEAD["last"] = (x2, wb, b, act, y)
+        else:
+            y = K.linear_fwd(x2, wb, b, act=act, out_f32=out_f32)
         ctx.save_for_backward(x2, y)
         ctx.w, ctx.b, ctx.act, ctx.xshape = w, b, act, x.shape
         return y.view(*x.shape[:-1], y.shape[-1])
@@ -211,17 +216,46 @@ def linear(x, w, b=None, act=None, out_f32=False):
         y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=F32 if out_f32 else BF16)
         y._hx_dense_head = (xc, w, b, out_f32, True)
         return y
-    y = _LinearFn.apply(xc, w, b, a, out_f32, pool)
+    if PREHEAD["pending"] and xc.data_ptr() in PREHEAD["pending"]:
+        flush_pending()  # a deferred pre-head output read by anything but the deferred head
+    pre = (HEAD["defer"] and PREHEAD["w"] is w and not head and a in (0, 1) and xc.dim() == 2 and xc.dtype == BF16
+           and xc.shape[0] <= 32 and not out_f32 and torch.is_grad_enabled() and "prehead" not in _disabled())
+    PREHEAD["arm"] = pre
+    try:
+        y = _LinearFn.apply(xc, w, b, a, out_f32, pool)
+    finally:
+        PREHEAD["arm"] = False
+    if pre:
+        PREHEAD["pending"][y.data_ptr()] = PREHEAD.pop("last")
     if head and y.requires_grad:
         y._hx_dense_head = (xc, w, b, out_f32, False)  # logits layer: loss_and_grad can fuse its backward
         if HEAD["probe"] is not None:
             HEAD["probe"].append(y)
+            last = HEAD.get("last_lin")
+            # the layer right before the logits layer: a Linear whose output is exactly the head's input
+            HEAD["prehead_w"] = last[0] if last is not None and last[1] is x else None
+    elif HEAD["probe"] is not None:
+        HEAD["last_lin"] = (w, y) if (a in (0, 1) and y.dim() == 2 and not out_f32) else None
     return y
 
 
 # logits-layer deferral (set by runtime.step.TrainStep): "probe" collects the head-candidate
 # outputs of one forward; "defer" lets linear() skip the head's forward launch (head_ce computes it)
 HEAD = {"probe": None, "defer": False}
+
+# Pre-head deferral (also TrainStep): the Linear layer whose output feeds ONLY the deferred logits
+# layer (found by the probe: weight ``w``) launches nothing in its forward either; the loss call
+# runs it together with the head as ONE kernel (loss.hip mlp_head_k).  ``pending`` maps the
+# placeholder output's address to its forward operands until then; anything else that reads a
+# placeholder first gets it computed (flush_pending).
+PREHEAD = {"w": None, "arm": False, "pending": {}}
+
+
+def flush_pending() -> None:
+    """Compute every deferred pre-head output now (the unfused path)."""
+    while PREHEAD["pending"]:
+        _, (x2, wb, b, act, y) = PREHEAD["pending"].popitem()
+        K.linear_fwd(x2, wb, b, act=act, out=y)
 
 
 # ===================================================================== Conv2d
@@ -768,8 +802,12 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
     kernel and the head's two backward GEMMs collapse into one launch."""
     head = getattr(logits, "_hx_dense_head", None)
     k = LOSS[kind]
+    pend = PREHEAD["pending"].pop(head[0].data_ptr(), None) if (head is not None and head[4]) else None
+    flush_pending()  # deferred outputs other than the head's input
     if (head is None or not logits.is_cuda or logits.dim() != 2 or "head_ce" in _disabled()
             or not K.head_ce_ok(logits.shape[1], head[0].shape[1])):
+        if pend is not None:
+            K.linear_fwd(pend[0], pend[1], pend[2], act=pend[3], out=pend[4])
         if head is not None and head[4]:  # deferred logits the fused kernel cannot take: compute them now
             real = _LinearFn.apply(head[0], head[1], head[2], 0, head[3], None)
             logits.copy_(real.detach())
@@ -784,6 +822,18 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
     target = (target.long() if k == 0 else target.float()).contiguous()
     loss_sum = torch.empty(1, device=logits.device)
     correct = torch.empty(1, device=logits.device, dtype=torch.int32)
+    if pend is not None:
+        # the pre-head Dense layer + this head + the loss: one launch (loss.hip mlp_head_k)
+        x2, wb, b1, act1, y = pend
+        dh = K.mlp_head(x2, wb, b1.detach() if b1 is not None else None, act1, y, k, logits, target,
+                        _arena.weight_bf16(w), b.detach() if b is not None else None, _arena.grad_target(w),
+                        _arena.grad_target(b) if b is not None else None, 1.0 / cnt, loss_sum, correct)
+        if dh is not False:
+            hooks.grad_ready(w)
+            if b is not None:
+                hooks.grad_ready(b)
+            return loss_sum, correct, (B if k in (0, 1) else cnt), h, dh
+        K.linear_fwd(x2, wb, b1, act=act1, out=y)  # shape the fused kernel does not take
     dh = K.head_ce(k, logits if deferred else logits.detach().contiguous(), target, h.detach(),
                    _arena.weight_bf16(w), _arena.grad_target(w), _arena.grad_target(b) if b is not None else None,
                    1.0 / cnt, loss_sum, correct, bias=b.detach() if (deferred and b is not None) else None,

@@ -552,6 +552,43 @@ def nonfinite_counts(x, out=None):
 
 
 # --------------------------------------------------------- fused classifier head
+_MLP_WS: dict = {}
+
+
+def _mlp_ws(device, n: int):
+    """Persistent zero-at-rest workspace + arrival counter of the fused Dense->head kernel (one per
+    device; every launch leaves them zeroed, so graph replays reuse them)."""
+    cur = _MLP_WS.get(device)
+    if cur is None or cur[0].numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("mlp_head workspace must exist before graph capture (run an eager step first)")
+        cur = (torch.zeros(max(n, 4096), device=device, dtype=F32), torch.zeros(9 * 32, device=device, dtype=torch.int32))
+        _MLP_WS[device] = cur
+    return cur
+
+
+def mlp_head(x, w1, b1, act1, y, kind: int, logits, target, w2, b2, dw2, db2, grad_scale: float, loss_sum, correct):
+    """Last hidden Dense layer + classifier head in ONE launch (loss.hip mlp_head_k): fills ``y`` =
+    act(x W1^T + b1) (bf16 [B, N1]) and ``logits``, and does what head_ce does (loss, dW2/db2
+    accumulation); returns dh [B, N1] bf16, or False when the shape is not supported."""
+    B, K = x.shape
+    N1 = w1.shape[0]
+    C = w2.shape[0]
+    _req(x, BF16, "x")
+    _req(w1, BF16, "w1")
+    _req(w2, BF16, "w2")
+    _req(y, BF16, "y")
+    ws, arrive = _mlp_ws(x.device, B * N1)
+    dh = torch.empty(B, N1, device=x.device, dtype=BF16)
+    rc = _C.ext().mlp_head(ptr(x), ptr(w1), ptr(b1), act_id(act1), ptr(y), ptr(ws), ptr(arrive), B, K, N1, int(kind),
+                           ptr(target), C, float(grad_scale), ptr(w2), ptr(b2), ptr(dw2), ptr(db2), ptr(dh),
+                           ptr(loss_sum), ptr(correct), ptr(logits), int(logits.dtype == F32), stream())
+    if rc == -2:
+        return False
+    check(rc, "mlp_head")
+    return dh
+
+
 def head_ce_ok(C: int, KD: int) -> bool:
     return bool(_C.ext().head_ce_ok(int(C), int(KD)))
 

@@ -84,6 +84,7 @@ class TrainStep:
         self._pf_pending = None
         self.defer_head = os.environ.get("HOPSX_DEFER_HEAD", "1") == "1"
         self._head_defer = None
+        self._prehead_w = None
         self.steps_per_execution = max(1, int(os.environ.get("HOPSX_STEPS_PER_EXEC", steps_per_execution)))
         self._gU = None
         self._outU = None
@@ -104,18 +105,26 @@ class TrainStep:
             return self.forward_fn(self.model, x)
         if self._head_defer is None:
             HF.HEAD["probe"] = []
+            HF.HEAD["last_lin"] = HF.HEAD["prehead_w"] = None
             try:
                 out = self.forward_fn(self.model, x)
                 probe = HF.HEAD["probe"]
+                prehead = HF.HEAD["prehead_w"]
             finally:
                 HF.HEAD["probe"] = None
+                HF.HEAD["last_lin"] = HF.HEAD["prehead_w"] = None
             self._head_defer = len(probe) == 1 and probe[0] is out
+            # the Dense layer feeding the logits layer runs inside the loss kernel too (mlp_head)
+            self._prehead_w = prehead if (self._head_defer and os.environ.get("HOPSX_DEFER_PREHEAD", "1") == "1") \
+                else None
             return out
         HF.HEAD["defer"] = self._head_defer
+        HF.PREHEAD["w"] = self._prehead_w
         try:
             return self.forward_fn(self.model, x)
         finally:
             HF.HEAD["defer"] = False
+            HF.PREHEAD["w"] = None
 
     def _fwd_bwd(self, x, y):
         # every step starts from zeroed gradients (the optimizer / fused DP step zeroes them): a weight
