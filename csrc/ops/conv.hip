@@ -340,7 +340,9 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
 static bool smallk_ok(const ConvGeom& g, const void* dy, const void* y, const float* ws, long ws_elems,
                       const unsigned* counter) {
   const int K = g.KH * g.KW * g.C;
-  return (K == 4 || K == 9 || K == 16) && g.CO % 8 == 0 && g.CO <= 256 && ((uintptr_t)dy % 16 == 0) &&
+  // input layers only (C < 8: the MNIST uint8 inputs): a 1x1 conv with K = C = 16 is a plain
+  // short reduction that the MFMA wgrad does faster (CIFAR ResNet-20 77.4k -> 82.0k img/s)
+  return (K == 4 || K == 9 || K == 16) && g.C < 8 && g.CO % 8 == 0 && g.CO <= 256 && ((uintptr_t)dy % 16 == 0) &&
          ((uintptr_t)y % 16 == 0) && counter && ws && ws_elems >= 128L * g.CO * (K + 1) &&
          !hopsx_disabled("smallk_wgrad");
 }
@@ -369,7 +371,10 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
   if (xscale != 0.f) return -3;
   if (hopsx_conv_wgrad_mfma_ok(geom) && (uintptr_t)dy % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0)
     return hopsx_conv2d_wgrad_mfma(dy, x, geom, dw, dbias, y, yact, st);
-  if (direct_ok(g)) {
+  // the direct kernel re-loads dY and X per (k, co) thread: cheap for small pixel counts and the
+  // only path for uint8 inputs; past 16k pixels the implicit-GEMM MFMA path wins (the CIFAR
+  // ResNet stem, 131k pixels: 89 us direct)
+  if (direct_ok(g) && (xscale != 0.f || K <= 16384) && !hopsx_disabled("direct_wgrad")) {
     const int KC = N * M;
     int R = 1024 / KC;
     if (R > 8) R = 8;

@@ -137,11 +137,27 @@ __device__ __forceinline__ void st8f(bf16_raw* p, const float* v) {
 
 // MODE 0 (stats): acc[rep][0:C] += x, acc[rep][C:2C] += x^2
 // MODE 1 (bwd):   acc[rep][0:C] += dz, acc[rep][C:2C] += dz * xhat, dz = dy * act'(y)
+// The launch also FINISHES the statistics (no separate finalize launch): the last workgroup to
+// arrive (per-XCD sharded counter after the BN_NREP x 2C replicas, common.h grid_arrive_last)
+// folds the replicas with atomic exchanges (read + re-zero at the memory side, where the float
+// atomics landed) and writes mean / rstd + running statistics (MODE 0) or the two bwd sums + the
+// dgamma / dbeta accumulation (MODE 1).
+struct BnFin {
+  float* mean_out;  // MODE 0
+  float* rstd_out;
+  float* rmean;
+  float* rvar;
+  float momentum, eps;
+  float* ws;  // MODE 1: [sum dz | sum dz*xhat]
+  float* dgamma;
+  float* dbeta;
+};
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ x,
                                                     const bf16_raw* __restrict__ y, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, float* __restrict__ acc, int M,
-                                                    int C, int rpb, int act) {
+                                                    int C, int rpb, int act, BnFin fin) {
   const int CG = C >> 3, RPI = 256 / CG;
   const int cg = threadIdx.x % CG, rsub = threadIdx.x / CG;
   const int c0 = cg * 8;
@@ -197,50 +213,40 @@ __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__
     for (int q = 0; q < RPI; ++q) t += red[(q * CG + g) * 16 + which * 8 + j];
     if (t != 0.f) atomicAdd(dst + e, t);
   }
-}
-
-// fwd finalize: fold replicas -> mean / rstd, running stats, re-zero the replicas
-__global__ void bn_fin_fwd_k(float* __restrict__ acc, float* __restrict__ mean, float* __restrict__ rstd,
-                             float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps, int M,
-                             int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f, q = 0.f;
 #pragma unroll
-  for (int r = 0; r < BN_NREP; ++r) {
-    a += acc[(long)r * 2 * C + c];
-    b += acc[(long)r * 2 * C + C + c];
-    acc[(long)r * 2 * C + c] = 0.f;
-    acc[(long)r * 2 * C + C + c] = 0.f;
+    for (int r = 0; r < BN_NREP; ++r) {
+      s += atomicExch(acc + (long)r * 2 * C + c, 0.f);
+      q += atomicExch(acc + (long)r * 2 * C + C + c, 0.f);
+    }
+    if (MODE == 0) {
+      const float mu = s / M;
+      const float var = fmaxf(q / M - mu * mu, 0.f);
+      fin.mean_out[c] = mu;
+      fin.rstd_out[c] = rsqrtf(var + fin.eps);
+      if (fin.rmean) {
+        const float unb = M > 1 ? var * M / (M - 1) : var;
+        fin.rmean[c] = (1.f - fin.momentum) * fin.rmean[c] + fin.momentum * mu;
+        fin.rvar[c] = (1.f - fin.momentum) * fin.rvar[c] + fin.momentum * unb;
+      }
+    } else {
+      fin.ws[c] = s;
+      fin.ws[C + c] = q;
+      if (fin.dbeta) fin.dbeta[c] += s;
+      if (fin.dgamma) fin.dgamma[c] += q;
+    }
   }
-  const float mu = a / M;
-  const float var = fmaxf(b / M - mu * mu, 0.f);
-  mean[c] = mu;
-  rstd[c] = rsqrtf(var + eps);
-  if (rmean) {
-    const float unb = M > 1 ? var * M / (M - 1) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
-  }
-}
-
-// bwd finalize: fold replicas into ws[0:2C], accumulate dbeta / dgamma, re-zero the replicas
-__global__ void bn_fin_bwd_k(float* __restrict__ acc, float* __restrict__ ws, float* __restrict__ dgamma,
-                             float* __restrict__ dbeta, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
-#pragma unroll
-  for (int r = 0; r < BN_NREP; ++r) {
-    a += acc[(long)r * 2 * C + c];
-    b += acc[(long)r * 2 * C + C + c];
-    acc[(long)r * 2 * C + c] = 0.f;
-    acc[(long)r * 2 * C + C + c] = 0.f;
-  }
-  ws[c] = a;
-  ws[C + c] = b;
-  if (dbeta) dbeta[c] += a;
-  if (dgamma) dgamma[c] += b;
 }
 
 // y = act((x - mean) * rstd * gamma + beta + res)  (var_mode: rstd holds a variance -> inference)
@@ -369,13 +375,12 @@ extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, co
                                   float eps, int M, int C, const void* residual, int act, float* acc,
                                   hipStream_t st) {
   const long n = (long)M * C;
-  if (acc && bn_vec_ok(C, {x, y, residual})) {  // acc: BN_NREP x 2C floats, zero at rest
+  if (acc && bn_vec_ok(C, {x, y, residual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
     const int g = colred_grid(M, C, rpb);
+    const BnFin fin{mean_out, rstd_out, running_mean, running_var, momentum, eps, nullptr, nullptr, nullptr};
     hipLaunchKernelGGL(bn_colred8_k<0>, dim3(g), dim3(256), 0, st, (const bf16_raw*)x, nullptr, nullptr, nullptr,
-                       nullptr, acc, M, C, rpb, 0);
-    hipLaunchKernelGGL(bn_fin_fwd_k, dim3((C + 255) / 256), dim3(256), 0, st, acc, mean_out, rstd_out, running_mean,
-                       running_var, momentum, eps, M, C);
+                       nullptr, acc, M, C, rpb, 0, fin);
     hipLaunchKernelGGL(bn_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y,
                        gamma, beta, mean_out, rstd_out, 0, eps, n / 8, C, (const bf16_raw*)residual, act);
     return (int)hipGetLastError();
@@ -410,12 +415,12 @@ extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const 
                             const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C,
                             int act, void* dresidual, float* acc, hipStream_t st) {
   const long n = (long)M * C;
-  if (acc && bn_vec_ok(C, {dy, x, y, dx, dresidual})) {  // acc: BN_NREP x 2C floats, zero at rest
+  if (acc && bn_vec_ok(C, {dy, x, y, dx, dresidual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
     const int g = colred_grid(M, C, rpb);
+    const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta};
     hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
-                       (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act);
-    hipLaunchKernelGGL(bn_fin_bwd_k, dim3((C + 255) / 256), dim3(256), 0, st, acc, ws, dgamma, dbeta, C);
+                       (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act, fin);
     hipLaunchKernelGGL(bn_bwd_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
                        (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, ws, (bf16_raw*)dx,
                        (bf16_raw*)dresidual, n / 8, M, C, act);

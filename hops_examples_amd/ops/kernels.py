@@ -442,15 +442,17 @@ BN_NREP = 8  # replica rows of the BN column-reduction accumulators (norm.hip BN
 
 
 def bn_acc(device, C) -> torch.Tensor:
-    """Zero-at-rest [BN_NREP, 2C] fp32 accumulator for the vectorized BN reductions: the finalize
-    kernel that consumes it re-zeroes it, so one buffer per (device, C) serves every BN layer of that
-    width in stream order, with no memset launches.  Created outside graph capture (warm-up)."""
+    """Zero-at-rest [BN_NREP, 2C] fp32 accumulator (+ arrival counter) for the vectorized BN
+    reductions: the reduction's last workgroup finalizes and re-zeroes it, so one buffer per
+    (device, C) serves every BN layer of that width in stream order, with no memset or finalize
+    launches.  Created outside graph capture (warm-up)."""
     key = (str(device), int(C))
     t = _BN_ACC.get(key)
     if t is None:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("BN accumulator must be created before graph capture (run an eager step first)")
-        t = torch.zeros(BN_NREP * 2 * C, device=device, dtype=F32)
+        # + the 9 x 32 arrival words of the in-launch finalize (common.h grid_arrive_last)
+        t = torch.zeros(BN_NREP * 2 * C + 9 * 32, device=device, dtype=F32)
         _BN_ACC[key] = t
     return t
 
