@@ -18,7 +18,6 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <stdexcept>
@@ -27,49 +26,15 @@
 #include <unordered_map>
 #include <vector>
 
-#if defined(__SSE4_2__)
-#include <nmmintrin.h>
-#endif
+#include "io_core.h"  // the parsers (bounds-checked, no Python types; fuzzed under ASan)
 
 namespace py = pybind11;
-
-// ------------------------------------------------------------------ crc32c
-static uint32_t crc_table[256];
-static bool crc_init = false;
-static void init_crc() {
-  if (crc_init) return;
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
-    crc_table[i] = c;
-  }
-  crc_init = true;
-}
-
-uint32_t crc32c(const uint8_t* p, size_t n) {
-  uint32_t c = 0xFFFFFFFFu;
-#if defined(__SSE4_2__)
-  uint64_t c64 = c;
-  while (n >= 8) {
-    uint64_t v;
-    memcpy(&v, p, 8);
-    c64 = _mm_crc32_u64(c64, v);
-    p += 8;
-    n -= 8;
-  }
-  c = (uint32_t)c64;
-  while (n--) c = _mm_crc32_u8(c, *p++);
-#else
-  init_crc();
-  while (n--) c = crc_table[(c ^ *p++) & 0xFF] ^ (c >> 8);
-#endif
-  return c ^ 0xFFFFFFFFu;
-}
-
-static inline uint32_t masked_crc(const uint8_t* p, size_t n) {
-  const uint32_t c = crc32c(p, n);
-  return ((c >> 15) | (c << 17)) + 0xa282ead8u;
-}
+using hopsx_io::crc32c;
+using hopsx_io::FeatVal;
+using hopsx_io::masked_crc;
+using hopsx_io::parse_example;
+using hopsx_io::put_len;
+using hopsx_io::put_varint;
 
 // ---------------------------------------------------------------- TFRecord
 class TFRecordWriter {
@@ -85,15 +50,8 @@ class TFRecordWriter {
   }
   void write_raw(const uint8_t* d, size_t n) {
     if (!f_) throw std::runtime_error("writer closed");
-    uint64_t len = n;
-    uint8_t hdr[12];
-    memcpy(hdr, &len, 8);
-    const uint32_t lc = masked_crc(hdr, 8);
-    memcpy(hdr + 8, &lc, 4);
-    fwrite(hdr, 1, 12, f_);
-    fwrite(d, 1, n, f_);
-    const uint32_t dc = masked_crc(d, n);
-    fwrite(&dc, 1, 4, f_);
+    const std::string fr = hopsx_io::frame_record(d, n);
+    if (fwrite(fr.data(), 1, fr.size(), f_) != fr.size()) throw std::runtime_error("TFRecord write failed");
   }
   void flush() {
     if (f_) fflush(f_);
@@ -115,69 +73,12 @@ static std::string read_file(const std::string& path) {
   return std::string((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
 }
 
-static std::vector<std::pair<size_t, size_t>> index_records(const std::string& buf, bool verify) {
-  std::vector<std::pair<size_t, size_t>> out;
-  size_t pos = 0;
-  const uint8_t* b = (const uint8_t*)buf.data();
-  while (pos + 12 <= buf.size()) {
-    uint64_t len;
-    memcpy(&len, b + pos, 8);
-    if (verify) {
-      uint32_t lc;
-      memcpy(&lc, b + pos + 8, 4);
-      if (lc != masked_crc(b + pos, 8)) throw std::runtime_error("TFRecord length crc mismatch");
-    }
-    if (pos + 12 + len + 4 > buf.size()) throw std::runtime_error("truncated TFRecord");
-    if (verify) {
-      uint32_t dc;
-      memcpy(&dc, b + pos + 12 + len, 4);
-      if (dc != masked_crc(b + pos + 12, len)) throw std::runtime_error("TFRecord data crc mismatch");
-    }
-    out.emplace_back(pos + 12, len);
-    pos += 12 + len + 4;
-  }
-  return out;
-}
-
 static py::list read_tfrecords(const std::string& path, bool verify) {
   std::string buf = read_file(path);
-  auto idx = index_records(buf, verify);
+  auto idx = hopsx_io::index_records((const uint8_t*)buf.data(), buf.size(), verify);
   py::list l;
   for (auto& r : idx) l.append(py::bytes(buf.data() + r.first, r.second));
   return l;
-}
-
-// ------------------------------------------------------- protobuf helpers
-static inline void put_varint(std::string& o, uint64_t v) {
-  while (v >= 0x80) {
-    o.push_back((char)(v | 0x80));
-    v >>= 7;
-  }
-  o.push_back((char)v);
-}
-static inline void put_key(std::string& o, int field, int wire) { put_varint(o, ((uint64_t)field << 3) | wire); }
-static inline void put_len(std::string& o, int field, const std::string& s) {
-  put_key(o, field, 2);
-  put_varint(o, s.size());
-  o += s;
-}
-static inline uint64_t get_varint(const uint8_t*& p, const uint8_t* end) {
-  uint64_t v = 0;
-  int sh = 0;
-  while (p < end) {
-    const uint8_t b = *p++;
-    v |= (uint64_t)(b & 0x7f) << sh;
-    if (!(b & 0x80)) return v;
-    sh += 7;
-  }
-  throw std::runtime_error("truncated varint");
-}
-static inline void skip_field(const uint8_t*& p, const uint8_t* end, int wire) {
-  if (wire == 0) get_varint(p, end);
-  else if (wire == 1) p += 8;
-  else if (wire == 2) p += get_varint(p, end);
-  else if (wire == 5) p += 4;
-  else throw std::runtime_error("unsupported wire type");
 }
 
 // tf.train.Example: Example{1: Features{1: map<string, Feature>}}; Feature oneof
@@ -217,97 +118,6 @@ static py::bytes encode_example(py::dict feats) {
   std::string ex;
   put_len(ex, 1, features);
   return py::bytes(ex);
-}
-
-struct FeatVal {
-  int kind = -1;  // 0 bytes, 1 float, 2 int64
-  std::vector<float> f;
-  std::vector<int64_t> i;
-  std::vector<std::string> b;
-};
-
-static void parse_list(const uint8_t* p, const uint8_t* end, int kind, FeatVal& fv) {
-  fv.kind = kind;
-  while (p < end) {
-    const uint64_t key = get_varint(p, end);
-    const int field = (int)(key >> 3), wire = (int)(key & 7);
-    if (field != 1) {
-      skip_field(p, end, wire);
-      continue;
-    }
-    if (kind == 0) {
-      const uint64_t n = get_varint(p, end);
-      fv.b.emplace_back((const char*)p, n);
-      p += n;
-    } else if (kind == 1) {
-      if (wire == 2) {
-        const uint64_t n = get_varint(p, end);
-        const size_t cnt = n / 4;
-        const size_t off = fv.f.size();
-        fv.f.resize(off + cnt);
-        memcpy(fv.f.data() + off, p, cnt * 4);
-        p += n;
-      } else {
-        float v;
-        memcpy(&v, p, 4);
-        p += 4;
-        fv.f.push_back(v);
-      }
-    } else {
-      if (wire == 2) {
-        const uint64_t n = get_varint(p, end);
-        const uint8_t* e = p + n;
-        while (p < e) fv.i.push_back((int64_t)get_varint(p, e));
-      } else {
-        fv.i.push_back((int64_t)get_varint(p, end));
-      }
-    }
-  }
-}
-
-static std::unordered_map<std::string, FeatVal> parse_example(const uint8_t* p, const uint8_t* end) {
-  std::unordered_map<std::string, FeatVal> out;
-  while (p < end) {
-    const uint64_t key = get_varint(p, end);
-    if ((key >> 3) != 1) {
-      skip_field(p, end, key & 7);
-      continue;
-    }
-    const uint64_t flen = get_varint(p, end);
-    const uint8_t* fe = p + flen;
-    while (p < fe) {  // Features: repeated map entries (field 1)
-      const uint64_t k2 = get_varint(p, fe);
-      const uint64_t elen = get_varint(p, fe);
-      const uint8_t* ee = p + elen;
-      if ((k2 >> 3) != 1) {
-        p = ee;
-        continue;
-      }
-      std::string name;
-      FeatVal fv;
-      while (p < ee) {
-        const uint64_t k3 = get_varint(p, ee);
-        const uint64_t l3 = get_varint(p, ee);
-        if ((k3 >> 3) == 1) {
-          name.assign((const char*)p, l3);
-          p += l3;
-        } else if ((k3 >> 3) == 2) {
-          const uint8_t* fe2 = p + l3;
-          while (p < fe2) {  // Feature oneof
-            const uint64_t k4 = get_varint(p, fe2);
-            const uint64_t l4 = get_varint(p, fe2);
-            const int which = (int)(k4 >> 3);
-            parse_list(p, p + l4, which == 1 ? 0 : (which == 2 ? 1 : 2), fv);
-            p += l4;
-          }
-        } else {
-          p += l3;
-        }
-      }
-      out.emplace(std::move(name), std::move(fv));
-    }
-  }
-  return out;
 }
 
 static py::dict decode_example(py::bytes rec) {
@@ -403,68 +213,11 @@ static py::dict decode_examples_columnar(py::list records, py::list schema, int 
 
 // ---------------------------------------------------------------- CSV
 static py::tuple parse_csv_numeric(const std::string& path, char delim, bool header) {
-  std::string buf = read_file(path);
-  std::vector<std::string> names;
-  size_t pos = 0;
-  auto next_line = [&](size_t& s, size_t& e) -> bool {
-    if (pos >= buf.size()) return false;
-    s = pos;
-    e = buf.find('\n', pos);
-    if (e == std::string::npos) e = buf.size();
-    pos = e + 1;
-    if (e > s && buf[e - 1] == '\r') --e;
-    return true;
-  };
-  size_t s, e;
-  if (header && next_line(s, e)) {
-    std::string cur;
-    bool q = false;
-    for (size_t i = s; i < e; ++i) {
-      const char c = buf[i];
-      if (c == '"') q = !q;
-      else if (c == delim && !q) {
-        names.push_back(cur);
-        cur.clear();
-      } else cur.push_back(c);
-    }
-    names.push_back(cur);
-  }
-  std::vector<float> vals;
-  size_t ncols = names.size(), nrows = 0;
-  std::string field;
-  while (next_line(s, e)) {
-    if (e == s) continue;
-    size_t col = 0;
-    size_t fs = s;
-    bool q = false;
-    for (size_t i = s; i <= e; ++i) {
-      const bool end = (i == e);
-      if (!end && buf[i] == '"') q = !q;
-      if (end || (buf[i] == delim && !q)) {
-        field.assign(buf.data() + fs, i - fs);
-        if (field.size() >= 2 && field.front() == '"' && field.back() == '"') field = field.substr(1, field.size() - 2);
-        char* ep = nullptr;
-        float v = NAN;
-        if (!field.empty()) {
-          v = strtof(field.c_str(), &ep);
-          while (ep && *ep == ' ') ++ep;
-          if (!ep || *ep != '\0') v = NAN;
-        }
-        vals.push_back(v);
-        ++col;
-        fs = i + 1;
-      }
-    }
-    if (ncols == 0) ncols = col;
-    if (col < ncols)
-      for (; col < ncols; ++col) vals.push_back(NAN);
-    else if (col > ncols)
-      vals.resize(vals.size() - (col - ncols));
-    ++nrows;
-  }
-  py::array_t<float> a({(ssize_t)nrows, (ssize_t)ncols});
-  if (!vals.empty()) memcpy(a.mutable_data(), vals.data(), vals.size() * 4);
-  return py::make_tuple(names, a);
+  const std::string buf = read_file(path);
+  hopsx_io::CsvTable t = hopsx_io::parse_csv_numeric(buf.data(), buf.size(), delim, header);
+  py::array_t<float> a({(ssize_t)t.nrows, (ssize_t)t.ncols});
+  if (!t.vals.empty()) memcpy(a.mutable_data(), t.vals.data(), t.vals.size() * 4);
+  return py::make_tuple(t.names, a);
 }
 
 // ------------------------------------------------------- batch assembly
