@@ -19,6 +19,7 @@ import shutil
 from pathlib import Path
 
 import numpy as np
+import torch
 import pandas as pd
 
 from .builders import CamelCaseAPI
@@ -227,9 +228,42 @@ class TrainingDataset(CamelCaseAPI):
                    drop_last: bool = True, device=None, feature_names=None, shard=None):
         from ..io.loader import DeviceLoader
 
+        if self._parquet_parts(split) and (device is None or torch.device(device).type == "cuda") \
+                and torch.cuda.is_available():
+            x, y = self.to_device(target_name, split, feature_names=feature_names, device=device, shard=shard)
+            return DeviceLoader.from_tensors(x, y, batch_size, shuffle=shuffle, drop_last=drop_last, seed=self.seed)
         x, y = _xy(self.read(split), target_name, feature_names)
         return DeviceLoader(x, y, batch_size, shuffle=shuffle, drop_last=drop_last, device=device, shard=shard,
                             seed=self.seed)
+
+    def _parquet_parts(self, split):
+        files = self._files(split)
+        return files if files and all(p.suffix == ".parquet" for p in files) else None
+
+    def to_device(self, target_name: str, split: str | None = None, feature_names=None, device=None, shard=None):
+        """(features fp32 [n, k], target fp32 [n]) resident in HBM.  Parquet parts stream through
+        io.parquet.ParquetDeviceReader (Arrow decode -> pinned staging -> side-stream H2D -> fp32
+        conversion on the GPU); other formats go through ``read()``.  ``shard=(n, i)``: every n-th
+        row group of every part (petastorm-style sharding)."""
+        from ..io.parquet import ParquetDeviceReader
+
+        targets = [target_name] if isinstance(target_name, str) else list(target_name)
+        names = [f.name for f in self._schema]
+        feats = feature_names or [c for c in names if c not in targets]
+        parts = self._parquet_parts(split)
+        if parts is None:
+            x, y = _xy(self.read(split), target_name, feature_names)
+            dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            return torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+        readers = [ParquetDeviceReader(p, feats + targets, device=device, shard=shard) for p in parts]
+        n = sum(r.rows for r in readers)
+        out = torch.empty(n, len(feats) + len(targets), dtype=torch.float32, device=readers[0].device)
+        r0 = 0
+        for r in readers:
+            r.read(out[r0:r0 + r.rows])
+            r0 += r.rows
+        y = out[:, len(feats):]
+        return out[:, :len(feats)].contiguous(), (y[:, 0].contiguous() if len(targets) == 1 else y.contiguous())
 
     # --------------------------------------------------------------- online serving
     def init_prepared_statement(self, batch: bool | None = None, external: bool | None = None):

@@ -59,6 +59,20 @@ class DeviceLoader:
                                                              dtype=torch.from_numpy(self.y[:1]).dtype).pin_memory()
                 self._slots.append([hx, hy, None])
 
+    @classmethod
+    def from_tensors(cls, x: torch.Tensor, y: torch.Tensor | None, batch_size: int, shuffle: bool = True,
+                     drop_last: bool = True, seed: int | None = None) -> "DeviceLoader":
+        """A resident loader over tensors already in HBM (e.g. io.parquet.ParquetDeviceReader output)."""
+        self = cls.__new__(cls)
+        self.x, self.y = x, y
+        self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
+        self.device = x.device
+        self.rng = np.random.default_rng(seed)
+        self.depth = 0
+        self.resident = True
+        self._x_dev, self._y_dev = x, y
+        return self
+
     def __len__(self):
         n = len(self.x)
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)

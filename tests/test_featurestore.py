@@ -182,3 +182,21 @@ def test_append_features_default_value(fs):
     assert "CASE WHEN `fg0`.`appended_feature` IS NULL THEN 10.0 ELSE `fg0`.`appended_feature` END " \
            "`appended_feature`" in fg.select_all().to_string()
     assert (fg.read().appended_feature == 10.0).all()
+
+
+def test_training_dataset_to_device_parquet(fs):
+    """Parquet training datasets stream to the device through io.parquet (CPU device here; the GPU
+    box runs the pinned side-stream path in test_parquet_reader.py); same values as read()."""
+    import torch
+
+    s = fs.create_feature_group("sales_fg", 1, primary_key=["store", "dept", "date"])
+    s.save(_sales(300))
+    td = fs.create_training_dataset("sales_dev", version=1, data_format="parquet",
+                                    splits={"train": 0.8, "test": 0.2}, seed=3, label=["weekly_sales"])
+    td.save(s.select_all())
+    x, y = td.to_device("weekly_sales", split="train", device="cpu")
+    df = td.read("train")
+    feats = [c for c in df.columns if c != "weekly_sales"]
+    np.testing.assert_allclose(x.numpy(), df[feats].to_numpy(np.float32))
+    np.testing.assert_allclose(y.numpy(), df["weekly_sales"].to_numpy(np.float32))
+    assert x.dtype == torch.float32 and x.shape == (len(df), len(feats))
