@@ -110,7 +110,7 @@ def main():
     run.run_n = run_n
     for i in range(a.warmup):
         run(i)
-    step.prepare_resident(xs, ys)  # capture the steps_per_execution graph outside the timed region
+    step.prepare_resident(xs, ys, n=a.steps)  # capture the steps_per_execution (+ remainder) graphs untimed
     el = timed(run, a.steps, dev)
     loss = float(out["r"]["loss"].item())
     ms = el / a.steps * 1e3

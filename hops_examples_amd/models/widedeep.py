@@ -121,6 +121,7 @@ class FusedWideDeepStep:
         self._key = None
         self._graphU = None
         self._keyU = None
+        self._graphR: dict = {}  # remainder graphs (Keras steps_per_execution tail): U -> graph
         self.steps_per_execution = max(1, int(os.environ.get("HOPSX_STEPS_PER_EXEC", "8")))
         self._slot_cache = {}
         self._n = 0
@@ -236,23 +237,31 @@ class FusedWideDeepStep:
         if self.dp is not None and hasattr(self.opt, "sync_hp"):
             self.opt.sync_hp()
 
-    def prepare_resident(self, xs, ys) -> None:
-        """Capture (not run) the U-step graph for this resident epoch, so it is built before a timed loop."""
+    def _capture_u(self, dense, cat, ys, U: int):
+        self._slots(dense.shape[-2])
+        self._sync_hp()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with _capture_graph(g):
+            for _ in range(U):
+                self._launch(dense, cat, ys, dense.shape[0], self.cursor)
+                self._finish()
+        return g
+
+    def prepare_resident(self, xs, ys, n: int | None = None) -> None:
+        """Capture (not run) the U-step graph for this resident epoch, so it is built before a timed
+        loop; with ``n`` also the graph of the remainder n % U (Keras steps_per_execution tail)."""
         dense, cat = xs
         U = self.steps_per_execution
         if U <= 1 or not self._graphable() or self._graph is None:
             return
         key = (dense.data_ptr(), cat.data_ptr(), ys.data_ptr(), tuple(self._floats()), U)
         if self._keyU != key:
-            self._slots(dense.shape[-2])
-            self._sync_hp()
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with _capture_graph(g):
-                for _ in range(U):
-                    self._launch(dense, cat, ys, dense.shape[0], self.cursor)
-                    self._finish()
-            self._graphU, self._keyU = g, key
+            self._graphU, self._keyU = self._capture_u(dense, cat, ys, U), key
+            self._graphR = {}
+        rem = (n or 0) % U
+        if rem > 1 and rem not in self._graphR:
+            self._graphR[rem] = self._capture_u(dense, cat, ys, rem)
 
     def run_resident(self, xs, ys, n: int, graph: bool = True):
         """``n`` consecutive resident steps; single-GPU graph steps are replayed ``steps_per_execution``
@@ -264,7 +273,21 @@ class FusedWideDeepStep:
         dense, cat = xs
         r = None
         while n > 0:
-            if n < U or U <= 1 or not graph or not self._graphable() or self._graph is None:
+            usable = U > 1 and graph and self._graphable() and self._graph is not None
+            if usable and n < U and n in self._graphR:
+                self.prepare_resident(xs, ys)  # (re-keys on new data / hyper-parameters)
+                g = self._graphR.get(n)
+                if g is not None:
+                    for _ in range(n):
+                        self._n += 1
+                        health.beat(self._n)
+                    g.replay()
+                    if self.dp is not None:
+                        self.dp.poll()
+                    n = 0
+                    r = {"loss": self.loss, "correct": self.correct, "count": dense.shape[1]}
+                    continue
+            if n < U or not usable:
                 r = self.step_resident(xs, ys, graph=graph)
                 n -= 1
                 continue
@@ -330,7 +353,7 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
             out["r"] = fused.run_resident((dense, cat), label, n, graph=graph)
 
         run.run_n = run_n
-        run.prepare = lambda: fused.prepare_resident((dense, cat), label)
+        run.prepare = lambda: fused.prepare_resident((dense, cat), label, n=steps)
     else:
         step = TrainStep(model, opt, "bce_logits", dp=dp, graph=graph, forward_fn=lambda m, x: m(*x))
         dense = dense.to(torch.bfloat16).view(nb, batch, -1)

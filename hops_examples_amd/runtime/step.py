@@ -88,6 +88,7 @@ class TrainStep:
         self.steps_per_execution = max(1, int(os.environ.get("HOPSX_STEPS_PER_EXEC", steps_per_execution)))
         self._gU = None
         self._outU = None
+        self._gR: dict = {}  # remainder graphs: U -> (graph, outputs)
         self._pool = None
         if dp is not None:
             optimizer.grad_scale = dp.grad_scale()
@@ -247,45 +248,72 @@ class TrainStep:
                 and self._resident is not None and self._resident[0] is xs and self._resident[1] is ys
                 and self._pf_opt is not None and self._cursor is not None)
 
-    def _capture_multi(self, xs, ys):
-        """U = steps_per_execution resident steps in one graph (same pool and static buffers as the
-        one-step graph; each captured optimizer kernel prefetches the batch the next step reads)."""
+    def _capture_multi(self, xs, ys, U: int | None = None):
+        """U (default steps_per_execution) resident steps in one graph (same pool and static buffers
+        as the one-step graph; each captured optimizer kernel prefetches the batch the next step
+        reads).  Returns (graph, last step's outputs)."""
+        U = U or self.steps_per_execution
         torch.cuda.synchronize()
         self._pf_opt.prefetch = ([(xs, self._sx), (ys, self._sy)], self._cursor)
         self._sync_hp()
         try:
             g = torch.cuda.CUDAGraph()
             with _capture_graph(g, pool=self._pool):
-                for _ in range(self.steps_per_execution):
+                for _ in range(U):
                     out = self._fwd_bwd(self._sx, self._sy)
                     self._tail()  # the same tail as the one-step graph (incl. the PS post-step)
         finally:
             self._pf_opt.prefetch = None
         torch.cuda.synchronize()
-        self._gU, self._outU = g, out
+        if U == self.steps_per_execution:
+            self._gU, self._outU = g, out
+        return g, out
 
-    def prepare_resident(self, xs, ys) -> None:
-        """Capture (not run) the steps_per_execution graph once the one-step graph exists."""
+    def prepare_resident(self, xs, ys, n: int | None = None) -> None:
+        """Capture (not run) the steps_per_execution graph once the one-step graph exists, and, when
+        the caller says how many steps follow (``n``), a graph for the remainder n % steps_per_execution
+        — what Keras does with an epoch that is not a multiple of steps_per_execution (a 20-step run
+        at 8 per execution replays 8 + 8 + 4 instead of 8 + 8 + 1 + 1 + 1 + 1)."""
         if self._gU is None and self._multi_ok(xs, ys):
             self._capture_multi(xs, ys)
+        if n is not None and self._multi_ok(xs, ys):
+            rem = n % self.steps_per_execution
+            if rem > 1 and rem not in self._gR:
+                self._gR[rem] = self._capture_multi(xs, ys, rem)
+
+    def _replay_multi(self, g, U: int):
+        for _ in range(U):
+            self._n += 1
+            health.beat(self._n)
+        self._sync_hp()
+        g.replay()
+        self._after_replay()
 
     def run_resident(self, xs, ys, n: int):
         """``n`` consecutive steps on the resident epoch (see step_resident); returns the last
-        step's outputs.  Single-GPU graph steps run ``steps_per_execution`` at a time."""
+        step's outputs.  Single-GPU and P2P data-parallel graph steps run ``steps_per_execution`` at
+        a time (a prepared remainder graph takes the tail)."""
         r = None
+        rem = n % self.steps_per_execution
+        if n > self.steps_per_execution and rem in self._gR and self._multi_ok(xs, ys):
+            # the short remainder graph first: its launch is cheaper, so the GPU starts sooner and the
+            # full graphs are issued while it runs
+            g, r = self._gR[rem]
+            self._replay_multi(g, rem)
+            n -= rem
         while n > 0:
+            if n in self._gR and n < self.steps_per_execution and self._multi_ok(xs, ys):
+                g, r = self._gR[n]
+                self._replay_multi(g, n)
+                n = 0
+                continue
             if n < self.steps_per_execution or not self._multi_ok(xs, ys):
                 r = self.step_resident(xs, ys)
                 n -= 1
                 continue
             if self._gU is None:
                 self._capture_multi(xs, ys)
-            for _ in range(self.steps_per_execution):
-                self._n += 1
-                health.beat(self._n)
-            self._sync_hp()
-            self._gU.replay()
-            self._after_replay()
+            self._replay_multi(self._gU, self.steps_per_execution)
             n -= self.steps_per_execution
             r = self._outU
         return r
