@@ -43,6 +43,22 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// DPP row rotation (lane l of a 16-lane row reads lane (l + R) % 16 of the same row): plain VALU,
+// no LDS round trip, unlike __shfl_xor (ds_bpermute)
+template <int R>
+__device__ __forceinline__ float dpp_ror(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + R, 0xF, 0xF, false));
+}
+// sum of the lanes of v congruent to this lane mod CW (CW a power of two <= 16) within its 16-lane row
+template <int CW>
+__device__ __forceinline__ float row_fold(float v) {
+  if constexpr (CW <= 1) v += dpp_ror<1>(v);
+  if constexpr (CW <= 2) v += dpp_ror<2>(v);
+  if constexpr (CW <= 4) v += dpp_ror<4>(v);
+  if constexpr (CW <= 8) v += dpp_ror<8>(v);
+  return v;
+}
+
 // Grid-wide "am I the last workgroup?" for a launch whose workgroups each arrive once (thread 0
 // calls it after the workgroup's writes are complete and released).  The counter is 9 x 32 uint32,
 // zero at rest: 8 shards on their own 128-B lines (blockIdx % 8 = the XCD under round-robin
@@ -72,14 +88,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
-// Counter-based RNG (splitmix-style hash): stateless, so dropout masks are
-// regenerated in the backward pass from (seed, offset, index) instead of stored.
+// Counter-based RNG: stateless, so dropout masks are regenerated in the backward pass from
+// (seed, offset, index) instead of stored.  Two rounds of a 32-bit xorshift-multiply finalizer
+// (4 v_mul_lo_u32) with the 64-bit key folded in between: a splitmix64 finalizer costs ~16
+// quarter-rate 32-bit multiplies per draw, which made the RNG the bulk of the conv+pool+dropout
+// epilogue.  The first round is a bijection of the index, the second mixes in the other key half.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= (z >> 31);
-  return (uint32_t)(z >> 8);
+  const uint32_t ka = (uint32_t)seed ^ (uint32_t)(idx >> 32) * 0x9E3779B9u;
+  const uint32_t kb = (uint32_t)(seed >> 32);
+  return mix32(mix32((uint32_t)idx ^ ka) + kb);
 }
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
   return (hash_u32(seed, idx) & 0xFFFFFF) * (1.0f / 16777216.0f);

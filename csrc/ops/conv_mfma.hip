@@ -29,6 +29,7 @@ __device__ __forceinline__ void phase_mark(int on, int slot) {
 
 constexpr int CM_WAVES = 4;
 constexpr int CM_UN = 2;  // pixel groups per wave per trip
+constexpr int CM_RSLOTS = CM_WAVES * 4;  // dgrad column-sum partials: one per (wave, 16-lane row)
 
 // LDS row stride (in 16-B chunks) of a weight image with cpr chunks per row: rows of >= 16
 // chunks are padded to a multiple of 16 so the XOR swizzle below never leaves its row
@@ -55,9 +56,10 @@ struct PoolEpi {
   const unsigned long long* rng;
   unsigned salt;
   float p;
+  int dbg;  // HOPSX_PHASE_DBG: per-workgroup phase stamps (tools/dbg_convfwd.py)
 };
 
-template <int NF, int KS, bool POOL = false>
+template <int NF, int KS, bool POOL = false, int UN = CM_UN>
 __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
                                                       const float* __restrict__ bias, bf16_raw* __restrict__ y,
                                                       ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{}) {
@@ -67,13 +69,29 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
   constexpr int RS = cm_rs(cpr);  // row stride in chunks: the XOR swizzle stays inside the row
   bf16_raw* sw = cm_smem;                                 // [CO][RS*8]
   bf16_raw* scratch = cm_smem + CO * RS * 8;              // [waves][16][CO]
-  for (int i = threadIdx.x; i < CO * cpr; i += blockDim.x) {
-    const int co = i / cpr, c = i - co * cpr;
-    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (8 * c < K) v = *(const bf16x8*)(w + (long)co * K + 8 * c);  // K % 8 == 0 (Cin % 8 == 0)
-    *(bf16x8*)(sw + co * RS * 8 + 8 * cm_swz(co, c, cpr)) = v;
+  phase_mark(pe.dbg, 0);
+  {
+    // every staging load leaves before the first LDS write: one memory round trip, not one per
+    // chunk (a load + ds_write loop waits for each load in turn)
+    constexpr int NCHK = CO * cpr, NPT = (NCHK + 255) / 256;
+    bf16x8 wv[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int co = i / cpr, c = i - co * cpr;
+      const bool ok = i < NCHK && 8 * c < K;  // K % 8 == 0 (Cin % 8 == 0)
+      wv[j] = *(const bf16x8*)(w + (ok ? (long)co * K + 8 * c : 0));
+      wv[j] = zero_unless(wv[j], ok);
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int co = i / cpr, c = i - co * cpr;
+      if (i < NCHK) *(bf16x8*)(sw + co * RS * 8 + 8 * cm_swz(co, c, cpr)) = wv[j];
+    }
   }
   __syncthreads();
+  phase_mark(pe.dbg, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int PH = g.OH >> 1, PW = g.OW >> 1;
@@ -84,10 +102,10 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) bv[nf] = bias ? bias[nf * 16 + fr] : 0.f;
   const uint64_t dkey = POOL && pe.p > 0.f ? drop_key(pe.rng, pe.salt) : 0;
-  for (int g0 = (blockIdx.x * CM_WAVES + wave) * CM_UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * CM_UN) {
-    bf16x8 a[CM_UN][KS];
+  for (int g0 = (blockIdx.x * CM_WAVES + wave) * UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * UN) {
+    bf16x8 a[UN][KS];
 #pragma unroll
-    for (int u = 0; u < CM_UN; ++u) {
+    for (int u = 0; u < UN; ++u) {
       const int px = (g0 + u) * 16 + fr;
       const bool pok = (g0 + u) < ngroups && px < M;
       const int pp = pok ? px : 0;
@@ -117,7 +135,7 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
       }
     }
 #pragma unroll
-    for (int u = 0; u < CM_UN; ++u) {
+    for (int u = 0; u < UN; ++u) {
       if (g0 + u >= ngroups) break;
       f32x4 acc[NF];
 #pragma unroll
@@ -131,6 +149,7 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
           acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][kk], bfr, acc[nf], 0, 0, 0);
         }
       }
+      if (u == 0) phase_mark(pe.dbg, 2);
       if constexpr (POOL) {
         // lane (fr, fq): channel nf*16+fr of pooled output 4*(g0+u)+fq; acc[nf][0..3] = its window
         const int po = (g0 + u) * 4 + fq;
@@ -183,6 +202,10 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
       }
       __builtin_amdgcn_wave_barrier();
     }
+  }
+  if (pe.dbg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    phase_mark(pe.dbg, 3);
   }
 }
 
@@ -254,11 +277,27 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     *(bf16x8*)(sw + kk * CI + 8 * (c8 ^ rc_swz(kk, CPR))) = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   }
   if (wvec) {
-    for (int i = threadIdx.x; i < K * CPR; i += blockDim.x) {
-      const int r = i / CPR, c8 = i - r * CPR;  // source row r = co*T + t
-      const int co = r / T, t = r - co * T;
-      const int kk = t * g.CO + co;
-      *(bf16x8*)(sw + kk * CI + 8 * (c8 ^ rc_swz(kk, CPR))) = *(const bf16x8*)(w + (long)i * 8);
+    // a batch's loads all leave before its LDS writes (one round trip per batch, not per chunk)
+    constexpr int NPT = (32 * KS * CPR + 255) / 256, BAT = NPT < 8 ? NPT : 8;
+    const int nch = K * CPR;
+#pragma unroll
+    for (int j0 = 0; j0 < NPT; j0 += BAT) {
+      bf16x8 wv[BAT];
+#pragma unroll
+      for (int j = 0; j < BAT; ++j) {
+        const int i = threadIdx.x + 256 * (j0 + j);
+        wv[j] = *(const bf16x8*)(w + (i < nch ? (long)i * 8 : 0));
+      }
+#pragma unroll
+      for (int j = 0; j < BAT; ++j) {
+        const int i = threadIdx.x + 256 * (j0 + j);
+        if (i < nch) {
+          const int r = i / CPR, c8 = i - r * CPR;  // source row r = co*T + t
+          const int co = r / T, t = r - co * T;
+          const int kk = t * g.CO + co;
+          *(bf16x8*)(sw + kk * CI + 8 * (c8 ^ rc_swz(kk, CPR))) = wv[j];
+        }
+      }
     }
   } else {
     for (int i = threadIdx.x; i < K * CI; i += blockDim.x) {
@@ -268,7 +307,7 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
       sw[kk * CI + 8 * ((ci >> 3) ^ rc_swz(kk, CPR)) + (ci & 7)] = w[i];
     }
   }
-  float* cwsum = csum + CM_WAVES * CI;  // [wave][CI][K0] (K0 > 0); csum is [wave][CI]
+  float* cwsum = csum + CM_RSLOTS * CI;  // [slot][CI][K0] (K0 > 0); csum is [slot][CI]
   __syncthreads();
   phase_mark(dbg, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -290,7 +329,13 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
   for (int g0 = (bid * CM_WAVES + wave) * UN; g0 < ngroups; g0 += nblk * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
     bf16x8 pmv[UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
-    float xk[UN][CPL][XK];
+    // input-layer pixels for the fused wgrad: RAW loads (uint8 or bf16 bits) with the validity kept
+    // aside and the conversion at the consumer — a conversion next to its load makes the compiler
+    // wait for each load in turn (one full memory round trip per tap)
+    unsigned xk[UN][CPL][XK];
+    unsigned long long xin = 0;  // bit (u*CPL+q)*XK+k
+    unsigned okm = 0;            // A-fragment validity, bit u*KS+kk
+    static_assert(UN * CPL * XK <= 64 && UN * KS <= 32, "validity masks");
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int px = (g0 + u) * 16 + fr;
@@ -310,18 +355,27 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
           // im2col row of the input layer at this pixel (= the input layer's output pixel)
           const int bb = g.fHW.div(pc), rr = pc - bb * (g.H * g.W);
           const int oh = g.fW.div(rr), ow = rr - oh * g.W;
+          long xo[K0];
 #pragma unroll
           for (int k = 0; k < K0; ++k) {
             const int kh = k / gi.KW, kw = k - kh * gi.KW;  // Cin = 1
             const int ih0 = oh * gi.sh - gi.ph + kh * gi.dh, iw0 = ow * gi.sw - gi.pw + kw * gi.dw;
             const bool in = okc && ih0 >= 0 && ih0 < gi.H && iw0 >= 0 && iw0 < gi.W;
-            const long xi = in ? ((long)bb * gi.H + ih0) * gi.W + iw0 : 0;
-            const float xv = xscale != 0.f ? fmaf((float)((const uint8_t*)x0)[xi], xscale, xshift)
-                                           : bf2f(((const bf16_raw*)x0)[xi]);
-            xk[u][q][k] = in ? xv : 0.f;
+            xo[k] = in ? ((long)bb * gi.H + ih0) * gi.W + iw0 : 0;
+            xin |= (unsigned long long)in << ((u * CPL + q) * XK + k);
+          }
+          if (xscale != 0.f) {  // uniform: the K0 loads of either form leave together
+#pragma unroll
+            for (int k = 0; k < K0; ++k) xk[u][q][k] = ((const uint8_t*)x0)[xo[k]];
+          } else {
+#pragma unroll
+            for (int k = 0; k < K0; ++k) xk[u][q][k] = ((const bf16_raw*)x0)[xo[k]];
           }
         }
       }
+      // raw gathers, validity kept aside and applied at the MFMA: no ALU op on a loaded value
+      // (and no branch) between the loads, so all of a trip's gathers are in flight together
+      long ao[KS];
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
         const int k0 = kk * 32 + 8 * fq;
@@ -330,10 +384,17 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
         const int kh = g.fKW.div(t), kw = t - kh * g.KW;
         const int oh = ih + g.ph - kh * g.dh, ow = iw + g.pw - kw * g.dw;  // stride 1
         const bool ok = pok && k0 < K && oh >= 0 && oh < g.OH && ow >= 0 && ow < g.OW;
-        const long o = ok ? (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co : 0;
-        bf16x8 v = zero_unless(*(const bf16x8*)(dy + o), ok);
-        if (y) mask8(v, *(const bf16x8*)(yp + o), yact);  // y is uniform: no load when dY is pre-masked
-        a[u][kk] = v;
+        ao[kk] = ok ? (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co : 0;
+        okm |= (unsigned)ok << (u * KS + kk);
+      }
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) a[u][kk] = *(const bf16x8*)(dy + ao[kk]);
+      if (y) {  // uniform: no load when dY is pre-masked
+        bf16x8 yv[KS];
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) yv[kk] = *(const bf16x8*)(yp + ao[kk]);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) mask8(a[u][kk], yv[kk], yact);
       }
     }
 #pragma unroll
@@ -354,7 +415,8 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
           const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (lds_v4_ptr)(sw + k2 * CI + 8 * ((col >> 3) ^ rc_swz(k2, CPR)) + (col & 7)));
           const bf16x8 bfr = (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-          acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][kk], bfr, acc[nf], 0, 0, 0);
+          acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(zero_unless(a[u][kk], (okm >> (u * KS + kk)) & 1), bfr,
+                                                             acc[nf], 0, 0, 0);
         }
       }
 #pragma unroll
@@ -372,12 +434,19 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
           bf16x8 v = *(const bf16x8*)(sc + row * CI + col);
           if (yprev) mask8(v, pmv[u][q], act_prev);
           if constexpr (K0 > 0) {
+            float xv[K0];
+#pragma unroll
+            for (int k = 0; k < K0; ++k) {
+              const unsigned r = xk[u][q][k];
+              const float f = xscale != 0.f ? fmaf((float)r, xscale, xshift) : bf2f((uint16_t)r);
+              xv[k] = (xin >> ((u * CPL + q) * XK + k)) & 1 ? f : 0.f;
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const float d = bf2f((uint16_t)v[j]);
               cacc[j] += d;
 #pragma unroll
-              for (int k = 0; k < K0; ++k) cw[j][k] = fmaf(d, xk[u][q][k], cw[j][k]);
+              for (int k = 0; k < K0; ++k) cw[j][k] = fmaf(d, xv[k], cw[j][k]);
             }
           } else {
             *(bf16x8*)(dx + (long)(base + row) * CI + col) = v;
@@ -391,38 +460,42 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
   }
   phase_mark(dbg, 2);
   if (colsum) {
-    // lanes l, l + CI/8, l + 2*CI/8, ... own the same 8 columns
+    // lanes l, l + CI/8, l + 2*CI/8, ... own the same 8 columns: fold them inside each 16-lane row
+    // with DPP rotations (plain VALU; ds_bpermute shuffles were ~160 LDS round trips here), then
+    // one LDS partial per (wave, row), summed after one barrier
+    constexpr int CW = CI / 8 < 16 ? CI / 8 : 16;
+    const int slot = wave * 4 + (lane >> 4), rl = lane & 15;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < 8; ++j) cacc[j] = row_fold<CW>(cacc[j]);
+    if (rl < CW) {
 #pragma unroll
-      for (int off = CI / 8; off < 64; off <<= 1) cacc[j] += __shfl_xor(cacc[j], off, 64);
-    // per-wave partial slots (LDS float atomics cost ~200 cycles each here), summed after one barrier
-    if (lane < CI / 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) csum[wave * CI + lane * 8 + j] = cacc[j];
+      for (int j = 0; j < 8; ++j) csum[slot * CI + rl * 8 + j] = cacc[j];
     }
     if constexpr (K0 > 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int k = 0; k < K0; ++k)
-          for (int off = CI / 8; off < 64; off <<= 1) cw[j][k] += __shfl_xor(cw[j][k], off, 64);
-      if (lane < CI / 8) {
+        for (int k = 0; k < K0; ++k) cw[j][k] = row_fold<CW>(cw[j][k]);
+      if (rl < CW) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int k = 0; k < K0; ++k) cwsum[wave * CI * K0 + (lane * 8 + j) * K0 + k] = cw[j][k];
+          for (int k = 0; k < K0; ++k) cwsum[slot * CI * K0 + (rl * 8 + j) * K0 + k] = cw[j][k];
       }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < CI; i += blockDim.x) {
-      const float v = csum[i] + csum[CI + i] + csum[2 * CI + i] + csum[3 * CI + i];
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < CM_RSLOTS; ++r) v += csum[r * CI + i];
       if (v != 0.f) atomicAdd(colsum + i, v);
     }
     if constexpr (K0 > 0) {
       // no-return f32 atomics: ~1 us for ~200 workgroups into these few rows (row 'Global float atomics')
       for (int i = threadIdx.x; i < CI * K0; i += blockDim.x) {
-        const float v = cwsum[i] + cwsum[CI * K0 + i] + cwsum[2 * CI * K0 + i] + cwsum[3 * CI * K0 + i];
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < CM_RSLOTS; ++r) v += cwsum[r * CI * K0 + i];
         if (v != 0.f) atomicAdd(dw0 + i, v);
       }
     }
@@ -635,7 +708,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(WgradArgs A) {
 // independent and each alone leaves most CUs idle at small batch; a second stream would run them
 // concurrently too, but a cross-queue dependency costs ~10 us per replayed graph, a launch ~1.5.
 template <int NF, int KS, int K0, int NFC>
-__global__ __launch_bounds__(256) void conv_bwd_pair_k(DgradArgs A, WgradArgs B, int nA, int nBx) {
+__global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs B, int nA, int nBx) {
   if ((int)blockIdx.x < nA) {
     conv_dgrad_body<NF, KS, K0, 2>(A, blockIdx.x, nA);
   } else {
@@ -647,8 +720,8 @@ __global__ __launch_bounds__(256) void conv_bwd_pair_k(DgradArgs A, WgradArgs B,
 // supported K-step counts (K is zero-padded up to one of them)
 int cm_ks(int ks) { return ks <= 2 ? 2 : ks <= 4 ? 4 : ks <= 8 ? 8 : ks <= 9 ? 9 : 16; }
 
-int cm_grid(long ngroups) {
-  long blocks = (ngroups + CM_WAVES * CM_UN - 1) / (CM_WAVES * CM_UN);
+int cm_grid(long ngroups, int un = CM_UN) {
+  long blocks = (ngroups + CM_WAVES * un - 1) / (CM_WAVES * un);
   if (blocks > 1024) blocks = 1024;
   return (int)(blocks < 1 ? 1 : blocks);
 }
@@ -753,7 +826,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   if (blocks > 1024) blocks = 1024;
   if (colsum && blocks > 512) blocks = 512;  // one colsum atomic per channel per workgroup
   const size_t shm = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                     (size_t)CM_WAVES * g.C * (1 + K0) * sizeof(float);
+                     (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float);
   const int wvec = (uintptr_t)w % 16 == 0;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
@@ -865,7 +938,7 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
   if (nA > 1024) nA = 1024;
   if (colsum && nA > 512) nA = 512;
   const size_t shmA = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                      (size_t)CM_WAVES * g.C * (1 + K0) * sizeof(float);
+                      (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float);
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
                      (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg};
@@ -912,12 +985,21 @@ extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* ge
   const int K = g.KH * g.KW * g.C;
   const int KS = cm_ks((K + 31) / 32);
   const long rows = (long)g.B * (g.OH / 2) * (g.OW / 2) * 4;
-  const int grid = cm_grid((rows + 15) / 16);
+  // one 16-row group per wave per trip when two would leave CUs idle (HOPSX_CMP_UN=1/2 forces)
+  static const int un_env = getenv("HOPSX_CMP_UN") ? atoi(getenv("HOPSX_CMP_UN")) : 0;
+  const long ngr = (rows + 15) / 16;
+  const int un = un_env == 1 || un_env == 2 ? un_env : (ngr < 2L * CM_WAVES * CM_UN * 256 ? 1 : 2);
+  const int grid = cm_grid(ngr, un);
   const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw);
-  const PoolEpi pe{(unsigned char*)am, rng, salt, p};
-#define HOPSX_CMP(NF, KSV)                                                                                     \
-  hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,       \
-                     (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe)
+  static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
+  const PoolEpi pe{(unsigned char*)am, rng, salt, p, dbg};
+#define HOPSX_CMP(NF, KSV)                                                                                      \
+  if (un == 1)                                                                                                  \
+    hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true, 1>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,  \
+                       (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe);                                \
+  else                                                                                                          \
+    hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true, 2>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,  \
+                       (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe)
 #define HOPSX_CMP_NF(NF)              \
   switch (KS) {                       \
     case 2: HOPSX_CMP(NF, 2); break;  \

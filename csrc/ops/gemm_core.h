@@ -46,14 +46,16 @@ __device__ __forceinline__ int rc_swz(int k, int cpr) {
 // Prologue fusion: multiply a loaded operand by act'(y) (y = the activation
 // output with the operand's layout) so backward GEMMs consume dY directly and
 // the separate activation-backward pass disappears.
+// (the act switch is hoisted out of the element loop: one uniform branch per call, straight-line
+// element code — a per-element switch compiled to ~8 branches per call)
 __device__ __forceinline__ void mask8(bf16x8& v, const bf16x8& y, int act) {
+  if (act == ACT_RELU) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (act == ACT_RELU) {
-      v[j] = (bf2f((uint16_t)y[j]) > 0.f) ? v[j] : (short)0;
-    } else {
+    for (int j = 0; j < 8; ++j) v[j] = (short)y[j] > 0 ? v[j] : (short)0;  // bf16 > 0 <=> positive int16 bits
+  } else if (act != ACT_NONE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
       v[j] = (short)f2bf(bf2f((uint16_t)v[j]) * act_grad_from_out(bf2f((uint16_t)y[j]), act));
-    }
   }
 }
 

@@ -480,5 +480,8 @@ def test_conv_pool_model_grads_match_unfused(monkeypatch, model):
         torch.cuda.synchronize()
         res.append((out.float().clone(), m._hx_arena.grad.float().clone()))
     assert not HF._PRESCATTERED
-    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
+    # (the conv+pool outputs themselves match bitwise: test_conv_fwd_pool_matches_conv_then_pool; the logits
+    # pass through split-K GEMMs whose fp32 atomics land in a run-dependent order, so two runs of the
+    # SAME path can differ by a bf16 ulp)
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=2e-2, atol=2e-3)
     torch.testing.assert_close(res[0][1], res[1][1], atol=3e-2 * res[1][1].abs().max().item(), rtol=3e-2)
