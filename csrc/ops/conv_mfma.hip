@@ -308,6 +308,18 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     }
   }
   float* cwsum = csum + CM_RSLOTS * CI;  // [slot][CI][K0] (K0 > 0); csum is [slot][CI]
+  // per (K step, fq) gather constants, built once per workgroup: output-pixel displacement of the
+  // tap and the element offset relative to the lane's own pixel (x: dh, y: dw, z: offset, w: valid)
+  int4* ktab = (int4*)(cwsum + CM_RSLOTS * CI * (K0 > 0 ? K0 : 0));
+  for (int i = threadIdx.x; i < KS * 4; i += blockDim.x) {
+    const int kk = i >> 2, q = i & 3;
+    const int k0 = kk * 32 + 8 * q;
+    const int kc = k0 < K ? k0 : 0;
+    const int t = g.fCO.div(kc), co = kc - t * g.CO;
+    const int kh = g.fKW.div(t), kw = t - kh * g.KW;
+    const int dh = g.ph - kh * g.dh, dwv = g.pw - kw * g.dw;  // stride 1: oh = ih + dh, ow = iw + dw
+    ktab[i] = make_int4(dh, dwv, (dh * g.OW + dwv) * g.CO + co, k0 < K);
+  }
   __syncthreads();
   phase_mark(dbg, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -326,6 +338,14 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
   constexpr int NCH = 16 * CI / 8;      // 16-B output chunks per 16-pixel group
   constexpr int CPL = (NCH + 63) / 64;  // of which this lane stores CPL (c = lane + 64 q)
   constexpr int XK = K0 > 0 ? K0 : 1;
+  int bo1[NF], bo2[NF];  // this lane's B-fragment LDS offsets at K step 0
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf) {
+    const int col = nf * 16 + 4 * (lane & 3);
+    const int k1 = 8 * fq + ((lane & 15) >> 2), k2 = k1 + 4;
+    bo1[nf] = k1 * CI + 8 * ((col >> 3) ^ rc_swz(k1, CPR)) + (col & 7);
+    bo2[nf] = k2 * CI + 8 * ((col >> 3) ^ rc_swz(k2, CPR)) + (col & 7);
+  }
   for (int g0 = (bid * CM_WAVES + wave) * UN; g0 < ngroups; g0 += nblk * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
     bf16x8 pmv[UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
@@ -336,6 +356,10 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     unsigned long long xin = 0;  // bit (u*CPL+q)*XK+k
     unsigned okm = 0;            // A-fragment validity, bit u*KS+kk
     static_assert(UN * CPL * XK <= 64 && UN * KS <= 32, "validity masks");
+    // 32-bit index math throughout (host: every tensor < 2^31 elements), tap constants from ktab
+    int4 kt[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) kt[kk] = ktab[kk * 4 + fq];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int px = (g0 + u) * 16 + fr;
@@ -350,18 +374,19 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
         const int p = (g0 + u) * 16 + row;
         const bool okc = c < NCH && (g0 + u) < ngroups && p < M;
         const int pc = okc ? p : 0;
-        pmv[u][q] = *(const bf16x8*)(ypp + (long)pc * CI + (okc ? col : 0));  // unconditional (ypp = yprev or dx)
+        pmv[u][q] = *(const bf16x8*)(ypp + (pc * CI + (okc ? col : 0)));  // unconditional (ypp = yprev or dx)
         if constexpr (K0 > 0) {
           // im2col row of the input layer at this pixel (= the input layer's output pixel)
           const int bb = g.fHW.div(pc), rr = pc - bb * (g.H * g.W);
           const int oh = g.fW.div(rr), ow = rr - oh * g.W;
-          long xo[K0];
+          const int ohs = oh * gi.sh - gi.ph, ows = ow * gi.sw - gi.pw, rowb = bb * gi.H;
+          int xo[K0];
 #pragma unroll
           for (int k = 0; k < K0; ++k) {
-            const int kh = k / gi.KW, kw = k - kh * gi.KW;  // Cin = 1
-            const int ih0 = oh * gi.sh - gi.ph + kh * gi.dh, iw0 = ow * gi.sw - gi.pw + kw * gi.dw;
-            const bool in = okc && ih0 >= 0 && ih0 < gi.H && iw0 >= 0 && iw0 < gi.W;
-            xo[k] = in ? ((long)bb * gi.H + ih0) * gi.W + iw0 : 0;
+            const int kh = gi.fKW.div(k), kw = k - kh * gi.KW;  // Cin = 1 (uniform: scalar ops)
+            const int ih0 = ohs + kh * gi.dh, iw0 = ows + kw * gi.dw;
+            const bool in = okc && (unsigned)ih0 < (unsigned)gi.H && (unsigned)iw0 < (unsigned)gi.W;
+            xo[k] = in ? (rowb + ih0) * gi.W + iw0 : 0;
             xin |= (unsigned long long)in << ((u * CPL + q) * XK + k);
           }
           if (xscale != 0.f) {  // uniform: the K0 loads of either form leave together
@@ -375,16 +400,13 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
       }
       // raw gathers, validity kept aside and applied at the MFMA: no ALU op on a loaded value
       // (and no branch) between the loads, so all of a trip's gathers are in flight together
-      long ao[KS];
+      const int pix = ((b * g.OH + ih) * g.OW + iw) * g.CO;
+      int ao[KS];
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        const int k0 = kk * 32 + 8 * fq;
-        const int kc = k0 < K ? k0 : 0;
-        const int t = g.fCO.div(kc), co = kc - t * g.CO;
-        const int kh = g.fKW.div(t), kw = t - kh * g.KW;
-        const int oh = ih + g.ph - kh * g.dh, ow = iw + g.pw - kw * g.dw;  // stride 1
-        const bool ok = pok && k0 < K && oh >= 0 && oh < g.OH && ow >= 0 && ow < g.OW;
-        ao[kk] = ok ? (((long)b * g.OH + oh) * g.OW + ow) * g.CO + co : 0;
+        const int oh = ih + kt[kk].x, ow = iw + kt[kk].y;
+        const bool ok = pok && kt[kk].w && (unsigned)oh < (unsigned)g.OH && (unsigned)ow < (unsigned)g.OW;
+        ao[kk] = ok ? pix + kt[kk].z : 0;
         okm |= (unsigned)ok << (u * KS + kk);
       }
 #pragma unroll
@@ -407,13 +429,10 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf) {
-          // transposed read (T10): lane 4q+p addresses rows k1 = 32kk+8fq+q (+4), ci = 16nf+4p..+3
-          const int col = nf * 16 + 4 * (lane & 3);
-          const int k1 = kk * 32 + 8 * fq + ((lane & 15) >> 2), k2 = k1 + 4;
-          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4_ptr)(sw + k1 * CI + 8 * ((col >> 3) ^ rc_swz(k1, CPR)) + (col & 7)));
-          const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4_ptr)(sw + k2 * CI + 8 * ((col >> 3) ^ rc_swz(k2, CPR)) + (col & 7)));
+          // transposed read (T10): lane 4q+p addresses rows k1 = 32kk+8fq+q (+4), ci = 16nf+4p..+3;
+          // rc_swz looks at k bits 0, 1 and 3 only, so the 32kk row step is a constant offset
+          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_ptr)(sw + bo1[nf] + kk * 32 * CI));
+          const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4_ptr)(sw + bo2[nf] + kk * 32 * CI));
           const bf16x8 bfr = (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
           acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(zero_unless(a[u][kk], (okm >> (u * KS + kk)) & 1), bfr,
                                                              acc[nf], 0, 0, 0);
@@ -745,7 +764,9 @@ bool hopsx_conv_fwd_pool_ok(const int* geom, int act) {
 // stride 1 only; K = KH*KW*CO <= 512, CO % 8 == 0, C in {16, 32, 64, 128}
 bool hopsx_conv_dgrad_mfma_ok(const int* geom) {
   const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * CO;
+  const long nx = (long)geom[0] * geom[1] * geom[2] * C, ny = (long)geom[0] * geom[4] * geom[5] * CO;
   return geom[9] == 1 && geom[10] == 1 && CO % 8 == 0 && K <= 512 && (C == 16 || C == 32 || C == 64 || C == 128) &&
+         nx < (1L << 31) && ny < (1L << 31) &&  // 32-bit gather offsets
          !hopsx_disabled("conv_mfma");
 }
 
@@ -826,7 +847,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   if (blocks > 1024) blocks = 1024;
   if (colsum && blocks > 512) blocks = 512;  // one colsum atomic per channel per workgroup
   const size_t shm = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                     (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float);
+                     (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float) + (size_t)KS * 4 * 16;
   const int wvec = (uintptr_t)w % 16 == 0;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
@@ -938,7 +959,7 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
   if (nA > 1024) nA = 1024;
   if (colsum && nA > 512) nA = 512;
   const size_t shmA = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                      (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float);
+                      (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float) + (size_t)KS * 4 * 16;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
                      (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg};
@@ -947,8 +968,18 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
   const long nchunks = ((long)g.B * g.OH * g.OW + WG_PX - 1) / WG_PX;
   constexpr int KB = 32;
   const int colblk = (Kw + KB - 1) / KB;
-  const long want_groups = std::max(1L, 384L / colblk);
-  const int cpw = (int)std::max(1L, (nchunks + 4 * want_groups - 1) / (4 * want_groups));
+  // size the weight-gradient part so the whole launch is resident at once (2 workgroups per CU at
+  // <= 256 VGPRs): otherwise its last workgroups only start when the first ones retire and the
+  // launch's tail is a second wave of them (measured: 340 of them started up to 8.4 us late)
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  static const int cpw_env = getenv("HOPSX_PAIR_CPW") ? atoi(getenv("HOPSX_PAIR_CPW")) : 0;
+  const long want_groups = std::max(1L, std::max(64L, 2L * n_cu - nA) / colblk);
+  const int cpw = cpw_env > 0 ? cpw_env : (int)std::max(1L, (nchunks + 4 * want_groups - 1) / (4 * want_groups));
   const long nBx = (nchunks + 4L * cpw - 1) / (4L * cpw);
   const size_t stage = (size_t)4 * WG_PX * (g.CO + KB) * sizeof(bf16_raw);
   const size_t redb = ((size_t)4 * (g.CO / 16) * 2 * 64 * 4 + 4 * g.CO + (size_t)g.CO * KB) * sizeof(float);
