@@ -49,7 +49,8 @@ def _worker(rank, world, port, mode, q):
     for _ in range(5):
         step(x, y)
     master = dp.gather_master() if hasattr(dp, "gather_master") else m._hx_arena.master
-    q.put((rank, master.clone()))
+    # a numpy copy: a shared-memory tensor's fd can outlive the (exiting) child and not be fetchable
+    q.put((rank, master.detach().cpu().numpy().copy()))
     hdist.barrier()
     torch.distributed.destroy_process_group()
 
@@ -61,7 +62,7 @@ def _run(mode):
     ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
+    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=120) for _ in ps)}
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
@@ -118,7 +119,7 @@ def _bf16_worker(rank, world, port, q):
     dp = DataParallel(m, grad_dtype=torch.bfloat16)
     dp.arena.grad.fill_(0.5 + rank)
     dp.allreduce_all()  # the between-graph-segments path, bf16 on the wire
-    q.put((rank, dp.arena.grad.clone()))
+    q.put((rank, dp.arena.grad.detach().cpu().numpy().copy()))
     hdist.barrier()
     torch.distributed.destroy_process_group()
 
@@ -130,7 +131,7 @@ def test_bf16_wire_allreduce_all():
     ps = [ctx.Process(target=_bf16_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
+    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=120) for _ in ps)}
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
