@@ -177,6 +177,15 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_bn_fwd_train(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(mean), P<float>(rstd),
                               P<float>(rm), P<float>(rv), mom, eps, M, C, P<void>(res), act, P<float>(acc), S(st));
   });
+  m.def("bn_fwd_apply_fin", [](u x, u y, u g, u b, u mean, u rstd, u rm, u rv, float mom, float eps, int M, int C,
+                               u res, int act, u acc, u st) {
+    return hopsx_bn_fwd_apply_fin(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(mean), P<float>(rstd),
+                                  P<float>(rm), P<float>(rv), mom, eps, M, C, P<void>(res), act, P<float>(acc), S(st));
+  });
+  m.def("bn_prestats_ok", [](int C) { return hopsx_bn_prestats_ok(C); });
+  m.def("conv2d_fwd_bnstats", [](u x, u w, std::vector<int> g, u out, u acc, u st) {
+    return hopsx_conv2d_fwd_bnstats(P<void>(x), P<void>(w), g.data(), P<void>(out), P<float>(acc), S(st));
+  });
   m.def("bn_fwd_infer", [](u x, u y, u g, u b, u rm, u rv, float eps, int M, int C, u res, int act, u st) {
     return hopsx_bn_fwd_infer(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(rm), P<float>(rv), eps, M, C,
                               P<void>(res), act, S(st));

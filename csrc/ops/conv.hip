@@ -317,6 +317,21 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
   return (int)hipGetLastError();
 }
 
+extern "C" int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int* geom, void* out, float* bnacc,
+                                        hipStream_t st) {
+  if (!bnacc || hopsx_disabled("bnstats") || !hopsx_bn_prestats_ok(geom[6])) return -2;
+  if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)out) % 16 != 0) return -2;
+  if (hopsx_conv_fwd_mfma_ok(geom)) return hopsx_conv2d_fwd_mfma_ex(x, w, geom, out, nullptr, 0, bnacc, st);
+  ConvGeom g = make_geom(geom);
+  if (g.C % 8 != 0) return -2;
+  const int M = g.B * g.OH * g.OW, N = g.CO, K = g.KH * g.KW * g.C;
+  Im2colLoader al{(const bf16_raw*)x, g, 1};
+  DenseLoader bl{(const bf16_raw*)w, K, is_vec_ok(w, K)};
+  EpiBnStatsBF16 e{(bf16_raw*)out, N, bnacc};
+  launch_gemm<true, true>(al, bl, e, M, N, K, false, st);
+  return (int)hipGetLastError();
+}
+
 // dX = conv_transpose(dY, W).  If `yprev` is given, the result is multiplied by
 // act'(yprev) — the backward of the activation that produced this conv's input
 // — and `colsum` receives that layer's bias gradient.

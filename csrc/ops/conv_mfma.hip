@@ -59,10 +59,15 @@ struct PoolEpi {
   int dbg;  // HOPSX_PHASE_DBG: per-workgroup phase stamps (tools/dbg_convfwd.py)
 };
 
-template <int NF, int KS, bool POOL = false, int UN = CM_UN>
+// BNS: the output feeds a training-mode BatchNorm — the epilogue also accumulates per-channel sum and
+// sum of squares of the stored (bf16) outputs into the zero-at-rest replicas
+// bnacc[blockIdx % HOPSX_BN_NREP][2 CO] (norm.hip bn_apply_fin8_k finishes them), so the BN never
+// re-reads its input for statistics.
+template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false>
 __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
                                                       const float* __restrict__ bias, bf16_raw* __restrict__ y,
-                                                      ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{}) {
+                                                      ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{},
+                                                      float* __restrict__ bnacc = nullptr) {
   constexpr int CO = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
   constexpr int cpr = KS * 4;  // 16-B chunks per weight row (K padded to 32*KS)
@@ -102,6 +107,9 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) bv[nf] = bias ? bias[nf * 16 + fr] : 0.f;
   const uint64_t dkey = POOL && pe.p > 0.f ? drop_key(pe.rng, pe.salt) : 0;
+  float st1[NF], st2[NF];  // BNS: this lane's channel partials (channel nf*16 + fr)
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf) { st1[nf] = 0.f; st2[nf] = 0.f; }
   for (int g0 = (blockIdx.x * CM_WAVES + wave) * UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
 #pragma unroll
@@ -187,20 +195,57 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
         continue;
       }
       // epilogue through the wave's LDS scratch: C map col = lane&15 (co), row = (lane>>4)*4 + r (pixel)
+      const int base = (g0 + u) * 16;
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          sc[(fq * 4 + r) * CO + nf * 16 + fr] = f2bf(apply_act(acc[nf][r] + bv[nf], act));
+        for (int r = 0; r < 4; ++r) {
+          const bf16_raw o = f2bf(apply_act(acc[nf][r] + bv[nf], act));
+          sc[(fq * 4 + r) * CO + nf * 16 + fr] = o;
+          if constexpr (BNS) {
+            const float v = base + fq * 4 + r < M ? bf2f(o) : 0.f;
+            st1[nf] += v;
+            st2[nf] = fmaf(v, v, st2[nf]);
+          }
+        }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes landed
       __builtin_amdgcn_wave_barrier();
-      const int base = (g0 + u) * 16;
 #pragma unroll
       for (int c = lane; c < 16 * CO / 8; c += 64) {
         const int row = c / (CO / 8), col = (c - row * (CO / 8)) * 8;
         if (base + row < M) *(bf16x8*)(y + (long)(base + row) * CO + col) = *(const bf16x8*)(sc + row * CO + col);
       }
       __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if constexpr (BNS) {
+    // fold the 4 pixel quads of each channel (lanes fr, fr+16, fr+32, fr+48), then the 4 waves in
+    // LDS (the staging scratch is free once every wave left the loop), one atomic per channel and
+    // statistic per workgroup into this workgroup's replica row
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf) {
+      st1[nf] += __shfl_xor(st1[nf], 16, 64);
+      st1[nf] += __shfl_xor(st1[nf], 32, 64);
+      st2[nf] += __shfl_xor(st2[nf], 16, 64);
+      st2[nf] += __shfl_xor(st2[nf], 32, 64);
+    }
+    __syncthreads();
+    float* red = (float*)scratch;  // [CM_WAVES][2][CO] floats <= the [CM_WAVES][16][CO] bf16 scratch
+    if (fq == 0) {
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) {
+        red[(wave * 2) * CO + nf * 16 + fr] = st1[nf];
+        red[(wave * 2 + 1) * CO + nf * 16 + fr] = st2[nf];
+      }
+    }
+    __syncthreads();
+    float* dst = bnacc + (long)(blockIdx.x % HOPSX_BN_NREP) * 2 * CO;
+    for (int e = threadIdx.x; e < 2 * CO; e += 256) {
+      const int which = e / CO, c = e - which * CO;
+      float t = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < CM_WAVES; ++wv) t += red[(wv * 2 + which) * CO + c];
+      atomicAdd(dst + e, t);
     }
   }
   if (pe.dbg) {
@@ -772,6 +817,12 @@ bool hopsx_conv_dgrad_mfma_ok(const int* geom) {
 
 extern "C" int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* out, const float* bias,
                                      int act, hipStream_t st) {
+  return hopsx_conv2d_fwd_mfma_ex(x, w, geom, out, bias, act, nullptr, st);
+}
+
+// bnacc != null: also accumulate the BatchNorm statistics of the output (conv_fwd_mfma_k BNS)
+extern "C" int hopsx_conv2d_fwd_mfma_ex(const void* x, const void* w, const int* geom, void* out, const float* bias,
+                                        int act, float* bnacc, hipStream_t st) {
   ConvGeom g;
   g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
   g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
@@ -783,8 +834,12 @@ extern "C" int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* ge
   const int grid = cm_grid((M + 15) / 16);
   const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw);
 #define HOPSX_CMF(NF, KSV)                                                                                     \
-  hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,            \
-                     (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K)
+  if (bnacc)                                                                                                   \
+    hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, false, CM_UN, true>), dim3(grid), dim3(256), shm, st,          \
+                       (const bf16_raw*)x, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, PoolEpi{}, bnacc); \
+  else                                                                                                         \
+    hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,          \
+                       (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K)
 #define HOPSX_CMF_NF(NF)          \
   switch (KS) {                   \
     case 2: HOPSX_CMF(NF, 2); break;  \
@@ -894,7 +949,8 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
 // short-conv weight gradient on MFMA: C % 8 == 0, CO in {16, 32, 64}, K = KH*KW*C <= 256
 bool hopsx_conv_wgrad_mfma_ok(const int* geom) {
   const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * C;
-  return C % 8 == 0 && K <= 256 && (CO == 16 || CO == 32 || CO == 64) && !hopsx_disabled("wgrad_mfma");
+  static const long maxk = hopsx_env_int("HOPSX_WGRAD_MFMA_MAXK", 256);
+  return C % 8 == 0 && K <= maxk && (CO == 16 || CO == 32 || CO == 64) && !hopsx_disabled("wgrad_mfma");
 }
 
 extern "C" int hopsx_conv2d_wgrad_mfma(const void* dy, const void* x, const int* geom, float* dw, float* dbias,
@@ -977,8 +1033,13 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
+  // When the dgrad part alone already fills every slot (nA >= 2 per CU, e.g. ResNet-20 stage 1:
+  // 1024 dgrad workgroups) the launch runs in several waves anyway: size the weight-gradient part
+  // by work (~384 workgroups) — squeezing it into the leftover slots made 12 x 5 workgroups walk
+  // 2048 chunks (86 us instead of 27 us per launch).
   static const int cpw_env = getenv("HOPSX_PAIR_CPW") ? atoi(getenv("HOPSX_PAIR_CPW")) : 0;
-  const long want_groups = std::max(1L, std::max(64L, 2L * n_cu - nA) / colblk);
+  const long slots = nA >= 2L * n_cu ? 384L : std::max(64L, 2L * n_cu - nA);
+  const long want_groups = std::max(1L, slots / colblk);
   const int cpw = cpw_env > 0 ? cpw_env : (int)std::max(1L, (nchunks + 4 * want_groups - 1) / (4 * want_groups));
   const long nBx = (nchunks + 4L * cpw - 1) / (4L * cpw);
   const size_t stage = (size_t)4 * WG_PX * (g.CO + KB) * sizeof(bf16_raw);
@@ -997,7 +1058,7 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
 #define HOPSX_PAIR_K0(NFv, KSv, NFCv) HOPSX_PAIR(NFv, KSv, 0, NFCv) HOPSX_PAIR(NFv, KSv, 4, NFCv)
 #define HOPSX_PAIR_NFC(NFv, KSv) HOPSX_PAIR_K0(NFv, KSv, 1) HOPSX_PAIR_K0(NFv, KSv, 2) HOPSX_PAIR_K0(NFv, KSv, 4)
   HOPSX_PAIR_NFC(1, 4) HOPSX_PAIR_NFC(1, 8) HOPSX_PAIR_NFC(2, 4) HOPSX_PAIR_NFC(2, 8) HOPSX_PAIR_NFC(4, 4)
-  HOPSX_PAIR_NFC(4, 8)
+  HOPSX_PAIR_NFC(4, 8) HOPSX_PAIR_K0(2, 9, 2)
 #undef HOPSX_PAIR_NFC
 #undef HOPSX_PAIR_K0
 #undef HOPSX_PAIR

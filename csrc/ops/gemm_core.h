@@ -232,6 +232,20 @@ struct EpiStoreBF16 {  // out = act(alpha*acc + bias[n])
   }
 };
 
+// out = bf16(acc) for a conv feeding a training BatchNorm: the column statistics (sum and sum of
+// squares of the stored bf16 values) go to colsum = the replicas [HOPSX_BN_NREP][2N] (kSq)
+struct EpiBnStatsBF16 {
+  static constexpr bool kSq = true;
+  bf16_raw* out;
+  long ldo;
+  float* colsum;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    const bf16_raw b = f2bf(v);
+    out[(long)m * ldo + n] = b;
+    return bf2f(b);
+  }
+};
+
 struct EpiStoreF32 {  // out = act(alpha*acc + bias[n]) + beta*out
   float* out;
   long ldo;
@@ -298,6 +312,10 @@ template <class EP, class = void>
 struct has_ticket { static constexpr bool value = false; };
 template <class EP>
 struct has_ticket<EP, decltype((void)EP::kTicket)> { static constexpr bool value = EP::kTicket; };
+template <class EP, class = void>
+struct has_sq { static constexpr bool value = false; };
+template <class EP>
+struct has_sq<EP, decltype((void)EP::kSq)> { static constexpr bool value = EP::kSq; };
 template <class EP, class = void>
 struct has_pre { static constexpr bool value = false; };
 template <class EP>
@@ -554,9 +572,9 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
   }
 
   // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + reg
-  float cs[FN];
+  float cs[FN], cs2[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) cs[j] = 0.f;
+  for (int j = 0; j < FN; ++j) { cs[j] = 0.f; cs2[j] = 0.f; }
   if constexpr (has_pre<EP>::value) {
     // gather-then-scatter epilogues: issue every gather first (the scatter stores may alias them
     // as far as the compiler knows, which would serialise one load latency per element)
@@ -592,7 +610,11 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-          if (m < M && n < N) cs[j] += ep(m, n, acc[i][j][r]);
+          if (m < M && n < N) {
+            const float v = ep(m, n, acc[i][j][r]);
+            cs[j] += v;
+            if constexpr (has_sq<EP>::value) cs2[j] = fmaf(v, v, cs2[j]);
+          }
         }
       }
     }
@@ -605,7 +627,18 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
         const int n = n0 + wn * WTN + j * 16 + fr;
-        if (fq == 0 && n < N) atomicAdd(ep.colsum + n, v);
+        if constexpr (has_sq<EP>::value) {
+          float q = cs2[j];
+          q += __shfl_xor(q, 16, 64);
+          q += __shfl_xor(q, 32, 64);
+          float* d = ep.colsum + (long)(bid % HOPSX_BN_NREP) * 2 * N;
+          if (fq == 0 && n < N) {
+            atomicAdd(d + n, v);
+            atomicAdd(d + N + n, q);
+          }
+        } else {
+          if (fq == 0 && n < N) atomicAdd(ep.colsum + n, v);
+        }
       }
     }
   } else {

@@ -120,7 +120,7 @@ __global__ void bn_grad_acc_k(const float* __restrict__ ws, float* __restrict__ 
 // zero-at-rest accumulator (NREP-fold less same-address atomic contention); the finalize
 // kernels fold the replicas, re-zero them and (fwd) update the running statistics, so no
 // memset launches remain.  The scalar kernels above serve odd channel counts.
-constexpr int BN_NREP = 8;
+constexpr int BN_NREP = HOPSX_BN_NREP;
 constexpr int BN_UNR = 4;
 
 __device__ __forceinline__ void ld8f(const bf16_raw* p, float* v) {
@@ -199,19 +199,48 @@ __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__
     }
   }
   __shared__ float red[256 * 16];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    red[threadIdx.x * 16 + j] = s1[j];
-    red[threadIdx.x * 16 + 8 + j] = s2[j];
-  }
-  __syncthreads();
   float* dst = acc + (long)(blockIdx.x % BN_NREP) * 2 * C;
-  for (int e = threadIdx.x; e < 2 * C; e += 256) {  // e < C: sum1 of channel e, else sum2 of channel e - C
-    const int which = e >= C, c = e - which * C;
-    const int g = c >> 3, j = c & 7;
-    float t = 0.f;
-    for (int q = 0; q < RPI; ++q) t += red[(q * CG + g) * 16 + which * 8 + j];
-    if (t != 0.f) atomicAdd(dst + e, t);
+  if (CG < 64) {
+    // lanes of a wave with the same channel group (lane % CG) fold with xor shuffles, log2(64/CG)
+    // steps; then 4 wave partials per channel meet in LDS.  (A serial walk over the RPI row
+    // partials by 2C threads cost RPI dependent LDS round trips: 128 of them at C = 16.)
+    for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += __shfl_xor(s1[j], o, 64);
+        s2[j] += __shfl_xor(s2[j], o, 64);
+      }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane < CG) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wave * CG + lane) * 16 + j] = s1[j];
+        red[(wave * CG + lane) * 16 + 8 + j] = s2[j];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * C; e += 256) {  // e < C: sum1 of channel e, else sum2 of channel e - C
+      const int which = e >= C, c = e - which * C;
+      const int g = c >> 3, j = c & 7;
+      const float t = red[g * 16 + which * 8 + j] + red[(CG + g) * 16 + which * 8 + j] +
+                      red[(2 * CG + g) * 16 + which * 8 + j] + red[(3 * CG + g) * 16 + which * 8 + j];
+      if (t != 0.f) atomicAdd(dst + e, t);
+    }
+  } else {  // RPI <= 4 row partials per channel
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[threadIdx.x * 16 + j] = s1[j];
+      red[threadIdx.x * 16 + 8 + j] = s2[j];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * C; e += 256) {
+      const int which = e >= C, c = e - which * C;
+      const int g = c >> 3, j = c & 7;
+      float t = 0.f;
+      for (int q = 0; q < RPI; ++q) t += red[(q * CG + g) * 16 + which * 8 + j];
+      if (t != 0.f) atomicAdd(dst + e, t);
+    }
   }
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics are done
@@ -289,6 +318,79 @@ __global__ __launch_bounds__(256) void bn_apply8_k(const bf16_raw* __restrict__ 
   }
 }
 
+// Forward apply whose statistics the PRODUCING conv accumulated in its epilogue (conv_mfma.hip /
+// conv.hip `bnacc`: per-channel sum / sum of squares of the bf16 outputs into the zero-at-rest
+// replicas acc[BN_NREP][2C]).  Every workgroup folds the replicas into per-channel scale / shift
+// in LDS — no statistics pass over x and no finalize round trips on the critical path — workgroup
+// 0 publishes mean / rstd (for the backward) and the running statistics, and the last workgroup
+// to have read the replicas re-zeroes them (after its own elementwise work).
+__global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restrict__ x, bf16_raw* __restrict__ y,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float* __restrict__ acc, long nch, int M, int C,
+                                                       const bf16_raw* __restrict__ res, int act, BnFin fin) {
+  __shared__ float ssc[2048], ssh[2048];  // C <= 2048 (bn_vec_ok)
+  __shared__ int last;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int r = 0; r < BN_NREP; ++r) {
+      s += acc[(long)r * 2 * C + c];
+      q += acc[(long)r * 2 * C + C + c];
+    }
+    const float mu = s / M;
+    const float var = fmaxf(q / M - mu * mu, 0.f);
+    const float rs = rsqrtf(var + fin.eps);
+    const float sc = rs * (gamma ? gamma[c] : 1.f);
+    ssc[c] = sc;
+    ssh[c] = (beta ? beta[c] : 0.f) - mu * sc;
+    if (blockIdx.x == 0) {
+      fin.mean_out[c] = mu;
+      fin.rstd_out[c] = rs;
+      if (fin.rmean) {
+        const float unb = M > 1 ? var * M / (M - 1) : var;
+        fin.rmean[c] = (1.f - fin.momentum) * fin.rmean[c] + fin.momentum * mu;
+        fin.rvar[c] = (1.f - fin.momentum) * fin.rvar[c] + fin.momentum * unb;
+      }
+    }
+  }
+  __syncthreads();  // every replica value this workgroup needs has been consumed
+  if (threadIdx.x == 0) last = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
+  const int CG = C >> 3;
+  const long stride = (long)gridDim.x * blockDim.x;  // a multiple of CG: the channel group is per-thread
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(i0 % CG) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = ssc[c0 + j];
+    sh[j] = ssh[c0 + j];
+  }
+  for (long i = i0; i < nch; i += 2 * stride) {
+    float v[2][8], rv[2][8];
+    const long i1 = i + stride < nch ? i + stride : i;
+    ld8f(x + i * 8, v[0]);
+    ld8f(x + i1 * 8, v[1]);
+    if (res) {
+      ld8f(res + i * 8, rv[0]);
+      ld8f(res + i1 * 8, rv[1]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = fmaf(v[u][j], sc[j], sh[j]);
+        if (res) t += rv[u][j];
+        v[u][j] = apply_act(t, act);
+      }
+    }
+    st8f(y + i * 8, v[0]);
+    if (i + stride < nch) st8f(y + i1 * 8, v[1]);
+  }
+  __syncthreads();
+  if (last)
+    for (int e = threadIdx.x; e < BN_NREP * 2 * C; e += 256) acc[e] = 0.f;
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply8_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
                                                        const bf16_raw* __restrict__ y, const float* __restrict__ gamma,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -340,7 +442,10 @@ static bool bn_vec_ok(int C, std::initializer_list<const void*> ptrs) {
 
 static int colred_grid(int M, int C, int& rpb) {
   const int RPI = 256 / (C / 8);
-  long g = (M + (long)RPI * 8 - 1) / ((long)RPI * 8);  // ~8 rows per thread
+  // ~BN_UNR rows per thread: one trip of loads in flight per lane and >= 256 workgroups on the
+  // ResNet-20 stage-1 shapes (8 rows per thread left half the CUs idle there)
+  const long rpt = hopsx_env_int("HOPSX_BN_RPT", BN_UNR);
+  long g = (M + (long)RPI * rpt - 1) / ((long)RPI * rpt);
   if (g > 1024) g = 1024;
   if (g < 1) g = 1;
   rpb = (int)((M + g - 1) / g);
@@ -396,6 +501,23 @@ extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, co
                      mean_out, rstd_out, 0, eps, n, C, (const bf16_raw*)residual, act);
   return (int)hipGetLastError();
 }
+
+// Training forward whose statistics are already in `acc` (accumulated by the producing conv's
+// epilogue, hopsx_conv2d_fwd_bnstats): one launch, re-zeroes acc.  -2 if the vector path does
+// not apply (the caller must not have produced the statistics then: check hopsx_bn_prestats_ok).
+extern "C" int hopsx_bn_fwd_apply_fin(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
+                                      float* rstd_out, float* running_mean, float* running_var, float momentum,
+                                      float eps, int M, int C, const void* residual, int act, float* acc,
+                                      hipStream_t st) {
+  if (!acc || !bn_vec_ok(C, {x, y, residual})) return -2;
+  const long n = (long)M * C;
+  const BnFin fin{mean_out, rstd_out, running_mean, running_var, momentum, eps, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(bn_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x,
+                     (bf16_raw*)y, gamma, beta, acc, n / 8, M, C, (const bf16_raw*)residual, act, fin);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hopsx_bn_prestats_ok(int C) { return bn_vec_ok(C, {}) ? 1 : 0; }
 
 extern "C" int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, const float* beta,
                                   const float* running_mean, const float* running_var, float eps, int M, int C,

@@ -115,6 +115,16 @@ int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* o
 bool hopsx_conv_dgrad_mfma_ok(const int* geom);
 int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* out, const float* bias, int act,
                           hipStream_t st);
+int hopsx_conv2d_fwd_mfma_ex(const void* x, const void* w, const int* geom, void* out, const float* bias, int act,
+                             float* bnacc, hipStream_t st);
+// conv forward (bf16 out, no bias / act) whose epilogue also accumulates the BatchNorm statistics
+// of its output into bnacc [HOPSX_BN_NREP][2 CO] (zero at rest; hopsx_bn_fwd_apply_fin consumes and
+// re-zeroes it).  -2: not supported for this shape (nothing launched; use the plain BN path).
+int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int* geom, void* out, float* bnacc, hipStream_t st);
+int hopsx_bn_fwd_apply_fin(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
+                           float* rstd_out, float* running_mean, float* running_var, float momentum, float eps, int M,
+                           int C, const void* residual, int act, float* acc, hipStream_t st);
+int hopsx_bn_prestats_ok(int C);
 int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                             int act_prev, float* colsum, const void* y, int yact, hipStream_t st);
 // dgrad with the input layer's weight gradient fused into the epilogue (geom0: the input layer,

@@ -7,10 +7,11 @@
 * ``resnet50()`` — ImageNet ResNet-50 v1.5 (stride on the 3x3 conv; 25,557,032 params),
   the model of the reference benchmark notebook (notebooks/ml/Benchmarks/benchmark.ipynb).
 
-MI355X mapping: every conv is the implicit-GEMM MFMA kernel with no bias (BN follows);
-BatchNorm runs the fused NHWC kernel that applies ``act(bn(x) + residual)`` in one
-pass, so the residual add and the ReLU of every block cost no extra kernel or HBM
-round trip; the classifier head is global-average-pool + the MFMA linear kernel.
+MI355X mapping: every conv is the implicit-GEMM MFMA kernel with no bias (BN follows) whose
+epilogue also accumulates the BN batch statistics (sum / sum of squares per channel);
+BatchNorm then runs ONE fused NHWC kernel that finalizes them and applies
+``act(bn(x) + residual)`` in one pass, so the residual add and the ReLU of every block
+cost no extra kernel or HBM round trip; the classifier head is global-average-pool + the MFMA linear kernel.
 """
 from __future__ import annotations
 
@@ -26,7 +27,9 @@ class ConvBN(nn.Module):
         self.bn = hnn.BatchNorm2d(cout, activation=act)
 
     def forward(self, x, residual=None):
-        return self.bn(self.conv(x), residual)
+        # training: the conv epilogue accumulates the BN statistics (functional.conv2d bnstats), so
+        # the BN is one apply launch instead of a statistics pass + an apply
+        return self.bn(self.conv(x, bnstats=self.bn.training), residual)
 
 
 class BasicBlock(nn.Module):

@@ -90,8 +90,9 @@ class Conv2d(nn.Module):
         else:
             self.register_parameter("bias", None)
 
-    def forward(self, x):
-        return HF.conv2d(x, self.weight, self.bias, act=self.activation, in_affine=self.in_affine, **self.cfg)
+    def forward(self, x, bnstats: bool = False):
+        return HF.conv2d(x, self.weight, self.bias, act=self.activation, in_affine=self.in_affine, bnstats=bnstats,
+                         **self.cfg)
 
     def extra_repr(self):
         return f"{self.in_channels}, {self.out_channels}, k={self.kernel_size}, {self.cfg}, act={self.activation}"

@@ -279,9 +279,21 @@ def _plain_gemm_conv(g, b, act, in_affine, prev) -> bool:
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None, pool=None):
+    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None, pool=None, bnstats=False):
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
         ctx.pool = None
+        if bnstats and x.dtype == BF16 and b is None and not act and in_affine is None and _bnstats_conv(g):
+            # the output feeds a training BatchNorm: the conv epilogue accumulates its statistics
+            # (no statistics pass over y); the BN then runs bn_fwd_apply_fin
+            x = x.contiguous()
+            y = K.conv2d_fwd_bnstats(x, _arena.weight_bf16(w), g)
+            if y is not None:
+                ctx.save_for_backward(x, y)
+                ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
+                ctx.plain = False
+                ctx.set_materialize_grads(False)
+                y._hx_bnstats = True
+                return y
         if pool is not None:
             # conv + act + 2x2 max-pool (+ dropout) as one launch; only the pooled tensor and the
             # argmax exist afterwards (ReLU' is encoded in the argmax, see conv2d_fwd_pool)
@@ -321,7 +333,7 @@ class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return (None,) * 10
+            return (None,) * 11
         if ctx.plain:  # 1x1 conv as library GEMMs: dX = dY W, dW += dY^T X (fp32 out, bf16 in)
             x, _ = ctx.saved_tensors
             w, g = ctx.w, ctx.g
@@ -341,7 +353,7 @@ class _Conv2dFn(torch.autograd.Function):
                         K.conv2d_wgrad(dy2.view(dy.shape), x, g, gw)
             else:
                 gw.view(CO, C).add_(torch.mm(dy2.t(), x.view(-1, C), out_dtype=torch.float32))
-            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None, None)
+            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None, None, None)
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         if ctx.pool is not None:
             x, am = ctx.saved_tensors
@@ -379,7 +391,7 @@ class _Conv2dFn(torch.autograd.Function):
                     hooks.grad_ready(ctx.prev[0])
                     hooks.grad_ready(ctx.prev[1])
                 return (r, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None,
-                        None, None, None)
+                        None, None, None, None)
         side_ok = not K.conv_wgrad_uses_ticket(g, ctx.in_affine)
         if side_ok:  # wgrad || dgrad on a parallel branch (its kernels keep no shared ticket/workspace)
             with _on_side(dy.device, dy, x, ymask, flop=2.0 * dy.numel() * g[7] * g[8] * g[3]):
@@ -399,7 +411,7 @@ class _Conv2dFn(torch.autograd.Function):
         if not side_ok:
             K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
         return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 def conv2d_maxpool(x, w, b=None, stride=1, padding=0, dilation=1, act=None, pool_kernel=2, pool_stride=None,
@@ -444,11 +456,11 @@ def _disabled() -> str:
     return os.environ.get("HOPSX_DISABLE", "")
 
 
-def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None):
+def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None, bnstats=False):
     """Apply the conv Function; tag the output of an input layer (input needs no gradient) so
     the next conv can fuse this layer's weight gradient into its dgrad."""
     prev = _fusable_input_layer(x, K.conv_geom(x.shape, w.shape, st, pd, dl)) if x.requires_grad else None
-    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev, pool)
+    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev, pool, bnstats)
     if pool is not None:
         return y
     if a:
@@ -458,8 +470,13 @@ def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None):
     return y
 
 
-def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None):
+def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None, bnstats=False):
     """NHWC conv. x [B,H,W,C], w [CO,KH,KW,C]. padding: int, tuple, 'valid' or 'same' (stride 1).
+
+    ``bnstats=True``: the output feeds a training-mode ``batch_norm`` next (models/resnet.py ConvBN);
+    where the conv kernel has the epilogue, it accumulates the BN statistics itself and tags the
+    output (``_hx_bnstats``) so the BN skips its statistics pass.  The tagged output must go to
+    ``batch_norm`` before any other BN of the same width runs.
 
     ``in_affine=(scale, shift)`` with a uint8 ``x``: the input layer's normalisation
     ``x * scale + shift``; on the GPU it is fused into the conv kernels when the layer
@@ -497,7 +514,21 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
         th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
         x = F.pad(to_compute(x), (0, 0, tw // 2, tw - tw // 2, th // 2, th - th // 2))
         pd = (0, 0)
-    return _conv_apply(to_compute(x), w, b, st, pd, dl, a, None)
+    return _conv_apply(to_compute(x), w, b, st, pd, dl, a, None, bnstats=bnstats and x.is_cuda)
+
+
+def _bnstats_conv(g) -> bool:
+    """Conv shapes whose BN statistics ride on the conv epilogue: everything the hopsx kernels run,
+    except 1x1 convs big enough that the library GEMM (hipBLASLt) + a statistics pass beats them."""
+    if "bnstats" in _disabled() or not K.bn_prestats_ok(g[6]):
+        return False
+    B, H, W, C, OH, OW, CO, KH, KW = g[:9]
+    if KH == 1 and KW == 1 and 2.0 * B * OH * OW * CO * C > _BNSTATS_MAX_1X1_FLOP:
+        return False
+    return C % 8 == 0
+
+
+_BNSTATS_MAX_1X1_FLOP = float(os.environ.get("HOPSX_BNSTATS_MAX_1X1_FLOP", 1e9))
 
 
 # ==================================================================== pooling
@@ -634,13 +665,16 @@ def dropout(x, p: float, training: bool = True, salt: int = 0):
 # ================================================================== batchnorm
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act):
+    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act, prestats=False):
         C = x.shape[-1]
         x2 = x.contiguous().view(-1, C)
         mean = torch.empty(C, device=x.device)
         rstd = torch.empty(C, device=x.device)
         r2 = residual.contiguous().view(-1, C) if residual is not None else None
-        y = K.bn_fwd_train(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
+        if prestats:  # statistics accumulated by the producing conv's epilogue
+            y = K.bn_fwd_apply_fin(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
+        else:
+            y = K.bn_fwd_train(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
         ctx.save_for_backward(x2, y, mean, rstd)
         ctx.p = (gamma, beta, act, x.shape, residual is not None)
         return y.view(x.shape)
@@ -656,7 +690,7 @@ class _BNFn(torch.autograd.Function):
         dres = torch.empty_like(dy2) if has_res else None
         dx = K.bn_bwd(dy2, x2, y, gamma, mean, rstd, gg, gb, ws, act=act, dresidual=dres)
         return (dx.view(shape), _ret_grad(gamma, gg), _ret_grad(beta, gb), None, None, None, None,
-                dres.view(shape) if has_res else None, None)
+                dres.view(shape) if has_res else None, None, None)
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentum=0.1, eps=1e-5, residual=None,
@@ -670,10 +704,15 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentu
         if residual is not None:
             y = y + residual
         return _cpu_act(y, a)
+    pre = getattr(x, "_hx_bnstats", False)
+    if pre:
+        x._hx_bnstats = False  # the accumulated statistics are consumed (and re-zeroed) exactly once
+        if not training:
+            raise RuntimeError("conv2d(bnstats=True) output fed to an eval-mode batch_norm")
     x = to_compute(x)
     residual = to_compute(residual) if residual is not None else None
     if training:
-        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a)
+        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a, pre)
     y = K.bn_fwd_infer(x.contiguous().view(-1, C), gamma, beta, running_mean, running_var, eps,
                        residual=None if residual is None else residual.contiguous().view(-1, C), act=a)
     return y.view(x.shape)

@@ -468,6 +468,41 @@ def bn_fwd_train(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, resid
     return out
 
 
+def conv2d_fwd_bnstats(x, w, geom, out=None):
+    """Conv forward (bf16 out, no bias / activation) whose epilogue also accumulates the BatchNorm
+    statistics of its output into the per-width accumulator ``bn_acc`` (norm.hip layout).  Returns
+    None — nothing launched — when the shape has no such epilogue; otherwise the output, and the
+    next op on the stream MUST be ``bn_fwd_apply_fin`` on it (it consumes and re-zeroes acc)."""
+    _req(x, BF16, "x")
+    _req(w, BF16, "w")
+    B, OH, OW, CO = geom[0], geom[4], geom[5], geom[6]
+    if out is None:
+        out = torch.empty(B, OH, OW, CO, device=x.device, dtype=BF16)
+    rc = _C.ext().conv2d_fwd_bnstats(ptr(x), ptr(w), list(geom), ptr(out), ptr(bn_acc(x.device, CO)), stream())
+    if rc == -2:
+        return None
+    check(rc, "conv2d_fwd_bnstats")
+    return out
+
+
+def bn_prestats_ok(C) -> bool:
+    return bool(_C.ext().bn_prestats_ok(int(C)))
+
+
+def bn_fwd_apply_fin(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, residual=None, act=0, out=None):
+    """Training BN forward whose statistics the producing conv already accumulated
+    (conv2d_fwd_bnstats): one launch that finalizes them, applies act(bn(x) + residual) and
+    re-zeroes the accumulator."""
+    M, C = x2d.shape
+    if out is None:
+        out = torch.empty_like(x2d)
+    check(_C.ext().bn_fwd_apply_fin(ptr(x2d), ptr(out), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), ptr(rmean),
+                                    ptr(rvar), float(momentum), float(eps), M, C, ptr(residual), act_id(act),
+                                    ptr(bn_acc(x2d.device, C)), stream()),
+          "bn_fwd_apply_fin")
+    return out
+
+
 def bn_fwd_infer(x2d, gamma, beta, rmean, rvar, eps, residual=None, act=0, out=None):
     M, C = x2d.shape
     if out is None:

@@ -1,0 +1,119 @@
+"""Conv forward with the BatchNorm statistics in its epilogue (conv_mfma.hip BNS / conv.hip
+EpiBnStatsBF16) + the one-launch BN apply that finalizes them (norm.hip bn_apply_fin8_k), against
+plain PyTorch fp32 conv -> batch_norm -> (+ residual) -> ReLU, and a whole ResNet-20 step with the
+fusion on vs off."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from hops_examples_amd.ops import kernels as K  # noqa: E402
+
+dev = "cuda"
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def close(a, b, rtol=2e-2, atol=2e-2):
+    torch.testing.assert_close(a.float(), b.float(), rtol=rtol, atol=atol)
+
+
+# (B, H, W, C, CO, k, stride): direct-MFMA path (K <= 512) and the implicit-GEMM path (K = 576)
+SHAPES = [(8, 32, 32, 16, 16, 3, 1), (8, 16, 16, 32, 64, 3, 2), (8, 8, 8, 64, 64, 3, 1), (8, 32, 32, 16, 32, 1, 2),
+          (4, 14, 14, 128, 128, 3, 1)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_bnstats_then_apply(shape):
+    B, H, W, C, CO, k, s = shape
+    torch.manual_seed(3)
+    x = bf(torch.randn(B, H, W, C, device=dev))
+    w = bf(torch.randn(CO, k, k, C, device=dev) / (k * k * C) ** 0.5)
+    res = bf(torch.randn(B, (H + s - 1) // s, (W + s - 1) // s, CO, device=dev))
+    gamma = torch.rand(CO, device=dev) + 0.5
+    beta = torch.randn(CO, device=dev)
+    g = K.conv_geom(x.shape, w.shape, (s, s), (k // 2, k // 2), (1, 1))
+    for rep in range(2):  # twice: the accumulator must be back at zero after the first apply
+        y = K.conv2d_fwd_bnstats(x, w, g)
+        assert y is not None, "shape should have the statistics epilogue"
+        mean, rstd = torch.empty(CO, device=dev), torch.empty(CO, device=dev)
+        rm, rv = torch.zeros(CO, device=dev), torch.ones(CO, device=dev)
+        out = K.bn_fwd_apply_fin(y.view(-1, CO), gamma, beta, mean, rstd, rm, rv, 0.1, 1e-5,
+                                 residual=res.view(-1, CO), act="relu")
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(K.bn_acc(torch.device(dev), CO))) == 0
+    yr = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, s, k // 2)
+    close(y.permute(0, 3, 1, 2), yr, rtol=1e-2, atol=1e-2)
+    yb = y.float().view(-1, CO)  # statistics of the stored bf16 conv output, as the kernel sees it
+    rm2, rv2 = torch.zeros(CO, device=dev), torch.ones(CO, device=dev)
+    ref = (F.batch_norm(yb, rm2, rv2, gamma, beta, True, 0.1, 1e-5) + res.float().view(-1, CO)).relu()
+    close(out, ref)
+    close(mean, yb.mean(0), rtol=1e-3, atol=1e-4)
+    close(rstd, (yb.var(0, unbiased=False) + 1e-5).rsqrt(), rtol=1e-3, atol=1e-3)
+    close(rm, rm2, rtol=1e-3, atol=1e-4)
+    close(rv, rv2, rtol=1e-3, atol=1e-4)
+
+
+def _resnet_step(disable: str):
+    from hops_examples_amd.models.resnet import cifar_resnet
+
+    old = os.environ.get("HOPSX_DISABLE", "")
+    os.environ["HOPSX_DISABLE"] = disable
+    try:
+        torch.manual_seed(0)
+        m = cifar_resnet(20).to(dev).train()
+        x = torch.randint(0, 256, (16, 32, 32, 3), device=dev, dtype=torch.uint8)
+        y = torch.randint(0, 10, (16,), device=dev)
+        logits = m(x)
+        loss = F.cross_entropy(logits.float(), y)
+        loss.backward()
+        grads = torch.cat([p.grad.float().reshape(-1) for p in m.parameters() if p.grad is not None])
+        bufs = torch.cat([b.float().reshape(-1) for n, b in m.named_buffers() if "running" in n])
+        return logits.float().detach(), grads, bufs
+    finally:
+        os.environ["HOPSX_DISABLE"] = old
+
+
+def test_resnet20_step_bnstats_matches_unfused():
+    """Same logits / running statistics; the gradients agree as well as two runs of the unfused
+    path agree with each other (float-atomic summation order makes both nondeterministic, and a
+    last-bit change of a BN statistic flips bf16 roundings that 20 layers of backward amplify)."""
+    l0, g0, b0 = _resnet_step("bnstats")
+    _, g0b, _ = _resnet_step("bnstats")
+    l1, g1, b1 = _resnet_step("")
+    close(l1, l0, rtol=3e-2, atol=3e-2)
+    close(b1, b0, rtol=1e-2, atol=1e-2)
+    noise = float(F.cosine_similarity(g0b, g0, dim=0))
+    cos = float(F.cosine_similarity(g1, g0, dim=0))
+    assert cos > 0.97 and cos > noise - 0.01, (cos, noise)
+
+
+def test_convbn_layer_grads_bnstats_matches_unfused():
+    """One ConvBN (+ residual + ReLU) layer: forward and all gradients, fused vs unfused."""
+    from hops_examples_amd.models.resnet import ConvBN
+
+    out = {}
+    for dis in ("bnstats", ""):
+        old = os.environ.get("HOPSX_DISABLE", "")
+        os.environ["HOPSX_DISABLE"] = dis
+        try:
+            torch.manual_seed(1)
+            m = ConvBN(32, 32, 3).to(dev).train()
+            x = bf(torch.randn(32, 16, 16, 32, device=dev)).requires_grad_(True)
+            r = bf(torch.randn(32, 16, 16, 32, device=dev)).requires_grad_(True)
+            y = m(x, residual=r)
+            dy = bf(torch.randn_like(y.float()))
+            gx, gr = torch.autograd.grad(y, (x, r), dy, retain_graph=True)
+            out[dis] = (y.float(), gx.float(), gr.float())
+        finally:
+            os.environ["HOPSX_DISABLE"] = old
+    for a, b in zip(out[""], out["bnstats"]):
+        close(a, b, rtol=2e-2, atol=2e-2)

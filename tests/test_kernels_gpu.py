@@ -241,7 +241,8 @@ def test_dropout_mask_reuse():
     assert not torch.equal(y2, y)
 
 
-@pytest.mark.parametrize("M,C", [(4096, 96), (8192, 64), (3136, 2048), (1000, 16), (50001, 256)])
+@pytest.mark.parametrize("M,C", [(4096, 96), (8192, 64), (3136, 2048), (1000, 16), (50001, 256), (131072, 16),
+                                 (32768, 32)])
 def test_batchnorm(M, C):
     """Vectorized (C/8 | 256) and scalar (C = 96) BN paths; run twice so the zero-at-rest
     replica accumulators must have been re-zeroed by the first call's finalize kernels."""
