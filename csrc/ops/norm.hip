@@ -151,6 +151,7 @@ struct BnFin {
   float* ws;  // MODE 1: [sum dz | sum dz*xhat]
   float* dgamma;
   float* dbeta;
+  int defer;  // 1: leave the replicas for the consuming apply kernel (bn_apply_fin8_k / bn_bwd_apply_fin8_k)
 };
 
 template <int MODE>
@@ -242,6 +243,7 @@ __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__
       if (t != 0.f) atomicAdd(dst + e, t);
     }
   }
+  if (fin.defer) return;  // the apply launch folds the replicas: no arrival / exchange round trips here
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics are done
   __syncthreads();
@@ -433,6 +435,78 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_k(const bf16_raw* __restric
   }
 }
 
+// Backward apply that finishes the deferred column reduction itself (bn_colred8_k<1> with
+// fin.defer): every workgroup folds the replicas of the two sums into per-channel constants in
+// LDS, workgroup 0 publishes ws and accumulates dgamma / dbeta, the last workgroup to have read the
+// replicas re-zeroes them.  Saves the reduction launch's arrival + exchange round trips.
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __restrict__ dy,
+                                                           const bf16_raw* __restrict__ x,
+                                                           const bf16_raw* __restrict__ y,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, float* __restrict__ acc,
+                                                           bf16_raw* __restrict__ dx, bf16_raw* __restrict__ dres,
+                                                           long nch, int M, int C, int act, BnFin fin) {
+  __shared__ float sk1[2048], sk2[2048], smd[2048], smu[2048], srs[2048];  // C <= 2048 (bn_vec_ok)
+  __shared__ int last;
+  const float invM = 1.f / M;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int r = 0; r < BN_NREP; ++r) {
+      s += acc[(long)r * 2 * C + c];
+      q += acc[(long)r * 2 * C + C + c];
+    }
+    const float rs = rstd[c];
+    sk1[c] = (gamma ? gamma[c] : 1.f) * rs;  // dx = k1 * (dz - mean(dz) - xhat * mean(dz*xhat))
+    sk2[c] = q * invM;
+    smd[c] = s * invM;
+    smu[c] = mean[c];
+    srs[c] = rs;
+    if (blockIdx.x == 0) {
+      fin.ws[c] = s;
+      fin.ws[C + c] = q;
+      if (fin.dbeta) fin.dbeta[c] += s;
+      if (fin.dgamma) fin.dgamma[c] += q;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) last = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
+  const int CG = C >> 3;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(i0 % CG) * 8;
+  float k1[8], k2[8], md[8], mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = sk1[c0 + j];
+    k2[j] = sk2[c0 + j];
+    md[j] = smd[c0 + j];
+    mu[j] = smu[c0 + j];
+    rs[j] = srs[c0 + j];
+  }
+  for (long i = i0; i < nch; i += stride) {
+    float d[8], xv[8], yv[8];
+    ld8f(dy + i * 8, d);
+    ld8f(x + i * 8, xv);
+    if (act != ACT_NONE) {
+      ld8f(y + i * 8, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] *= act_grad_from_out(yv[j], act);
+    }
+    if (dres) st8f(dres + i * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xv[j] - mu[j]) * rs[j];
+      d[j] = k1[j] * (d[j] - md[j] - xh * k2[j]);
+    }
+    st8f(dx + i * 8, d);
+  }
+  __syncthreads();
+  if (last)
+    for (int e = threadIdx.x; e < BN_NREP * 2 * C; e += 256) acc[e] = 0.f;
+}
+
 static bool bn_vec_ok(int C, std::initializer_list<const void*> ptrs) {
   if (C % 8 != 0 || C / 8 > 256 || (256 % (C / 8)) != 0 || hopsx_disabled("bn_vec")) return false;
   for (const void* p : ptrs)
@@ -483,11 +557,16 @@ extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, co
   if (acc && bn_vec_ok(C, {x, y, residual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
     const int g = colred_grid(M, C, rpb);
-    const BnFin fin{mean_out, rstd_out, running_mean, running_var, momentum, eps, nullptr, nullptr, nullptr};
+    const int defer = hopsx_disabled("bn_defer") ? 0 : 1;
+    const BnFin fin{mean_out, rstd_out, running_mean, running_var, momentum, eps, nullptr, nullptr, nullptr, defer};
     hipLaunchKernelGGL(bn_colred8_k<0>, dim3(g), dim3(256), 0, st, (const bf16_raw*)x, nullptr, nullptr, nullptr,
                        nullptr, acc, M, C, rpb, 0, fin);
-    hipLaunchKernelGGL(bn_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y,
-                       gamma, beta, mean_out, rstd_out, 0, eps, n / 8, C, (const bf16_raw*)residual, act);
+    if (defer)  // the apply folds the replicas (the same launch the conv-epilogue statistics use)
+      hipLaunchKernelGGL(bn_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x,
+                         (bf16_raw*)y, gamma, beta, acc, n / 8, M, C, (const bf16_raw*)residual, act, fin);
+    else
+      hipLaunchKernelGGL(bn_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y,
+                         gamma, beta, mean_out, rstd_out, 0, eps, n / 8, C, (const bf16_raw*)residual, act);
     return (int)hipGetLastError();
   }
   hopsx_zero(mean_out, C * sizeof(float), st);
@@ -540,9 +619,16 @@ extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const 
   if (acc && bn_vec_ok(C, {dy, x, y, dx, dresidual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
     const int g = colred_grid(M, C, rpb);
-    const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta};
+    const int defer = hopsx_disabled("bn_defer") ? 0 : 1;
+    const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, defer};
     hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
                        (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act, fin);
+    if (defer) {
+      hipLaunchKernelGGL(bn_bwd_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
+                         (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, acc, (bf16_raw*)dx,
+                         (bf16_raw*)dresidual, n / 8, M, C, act, fin);
+      return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(bn_bwd_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
                        (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, ws, (bf16_raw*)dx,
                        (bf16_raw*)dresidual, n / 8, M, C, act);

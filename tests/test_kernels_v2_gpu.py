@@ -370,7 +370,7 @@ def test_paired_conv_backward_matches_separate_launches(monkeypatch, model):
     from hops_examples_amd.runtime.arena import ParamArena
 
     grads = []
-    for disable in ("", "bwd_pair"):
+    for disable in ("", "bwd_pair", ""):
         monkeypatch.setenv("HOPSX_DISABLE", disable)
         HF.seed_device_rng(3, dev)
         torch.manual_seed(0)
@@ -388,7 +388,14 @@ def test_paired_conv_backward_matches_separate_launches(monkeypatch, model):
         root.backward(g)
         torch.cuda.synchronize()
         grads.append(m._hx_arena.grad.float().clone())
-    torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
+    if model == "mirrored":
+        torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
+    else:
+        # BatchNorm statistics are float-atomic sums (run-to-run last-bit noise that 20 layers of BN
+        # backward amplify): the pair must agree with the separate launches as well as a rerun does
+        cos = lambda a, b: float(torch.nn.functional.cosine_similarity(a, b, dim=0))  # noqa: E731
+        noise, diff = cos(grads[0], grads[2]), cos(grads[0], grads[1])
+        assert diff > 0.97 and diff > noise - 0.01, (diff, noise)
 
 
 @pytest.mark.parametrize("model", ["mirrored", "torch"])
@@ -485,3 +492,24 @@ def test_conv_pool_model_grads_match_unfused(monkeypatch, model):
     # SAME path can differ by a bf16 ulp)
     torch.testing.assert_close(res[0][0], res[1][0], rtol=2e-2, atol=2e-3)
     torch.testing.assert_close(res[0][1], res[1][1], atol=3e-2 * res[1][1].abs().max().item(), rtol=3e-2)
+
+
+@pytest.mark.parametrize("B,H,C,CO", [(16, 32, 16, 16), (16, 16, 32, 32), (128, 16, 32, 32), (8, 12, 64, 32)])
+def test_conv_bwd_pair_kernel_vs_fp32(B, H, C, CO):
+    """conv_bwd_pair_k alone (dgrad + wgrad in one launch) against fp32 autograd, incl. the
+    ResNet-20 stage-2 shape (Kd = 288 -> KS = 9) and a batch whose dgrad part fills the chip."""
+    torch.manual_seed(5)
+    x = (torch.randn(B, H, H, C, device=dev)).to(torch.bfloat16)
+    w = (torch.randn(CO, 3, 3, C, device=dev) / (9 * C) ** 0.5).to(torch.bfloat16)
+    dy = torch.randn(B, H, H, CO, device=dev).to(torch.bfloat16)
+    g = K.conv_geom(x.shape, w.shape, (1, 1), (1, 1), (1, 1))
+    dw = torch.zeros(CO, 3, 3, C, device=dev)
+    dx = K.conv2d_bwd_pair(dy, w, g, x, dw)
+    if dx is False:
+        pytest.skip("shape not instantiated")
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+    gx, gw = torch.autograd.grad(yr, (xr, wr), dy.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dx.float(), gx.permute(0, 2, 3, 1), rtol=2e-2, atol=2e-2 * gx.abs().max().item())
+    torch.testing.assert_close(dw, gw.permute(0, 2, 3, 1), rtol=2e-2, atol=1e-2 * gw.abs().max().item())
