@@ -949,7 +949,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
 // short-conv weight gradient on MFMA: C % 8 == 0, CO in {16, 32, 64}, K = KH*KW*C <= 256
 bool hopsx_conv_wgrad_mfma_ok(const int* geom) {
   const int C = geom[3], CO = geom[6], K = geom[7] * geom[8] * C;
-  static const long maxk = hopsx_env_int("HOPSX_WGRAD_MFMA_MAXK", 256);
+  static const long maxk = hopsx_env_int("HOPSX_WGRAD_MFMA_MAXK", 640);  // 640: ResNet-20 +2 %, ResNet-56 +3.4 %, R50 flat
   return C % 8 == 0 && K <= maxk && (CO == 16 || CO == 32 || CO == 64) && !hopsx_disabled("wgrad_mfma");
 }
 
