@@ -783,6 +783,10 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs
 
 // supported K-step counts (K is zero-padded up to one of them)
 int cm_ks(int ks) { return ks <= 2 ? 2 : ks <= 4 ? 4 : ks <= 8 ? 8 : ks <= 9 ? 9 : 16; }
+// + a 5-step variant (K = 129..160: the 3x3, 16-channel convs of ResNet stage 1, K = 144) for the
+// plain forward, the plain dgrad and the pair, which would otherwise pad K to 256 and spend 3/8 of
+// their gathers and MFMAs on zeros; the pooled / fused-input variants keep cm_ks
+int cm_ks5(int ks) { return ks == 5 && !hopsx_disabled("ks5") ? 5 : cm_ks(ks); }
 
 int cm_grid(long ngroups, int un = CM_UN) {
   long blocks = (ngroups + CM_WAVES * un - 1) / (CM_WAVES * un);
@@ -829,7 +833,7 @@ extern "C" int hopsx_conv2d_fwd_mfma_ex(const void* x, const void* w, const int*
   g.dh = geom[13]; g.dw = geom[14];
   g.init_div();
   const int K = g.KH * g.KW * g.C;
-  const int KS = cm_ks((K + 31) / 32);
+  const int KS = cm_ks5((K + 31) / 32);
   const long M = (long)g.B * g.OH * g.OW;
   const int grid = cm_grid((M + 15) / 16);
   const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw);
@@ -844,6 +848,7 @@ extern "C" int hopsx_conv2d_fwd_mfma_ex(const void* x, const void* w, const int*
   switch (KS) {                   \
     case 2: HOPSX_CMF(NF, 2); break;  \
     case 4: HOPSX_CMF(NF, 4); break;  \
+    case 5: HOPSX_CMF(NF, 5); break;  \
     case 8: HOPSX_CMF(NF, 8); break;  \
     case 9: HOPSX_CMF(NF, 9); break;  \
     default: HOPSX_CMF(NF, 16); break; \
@@ -892,7 +897,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   const int K0 = fused ? geom0[7] * geom0[8] : 0;
   ConvGeom g = cm_geom(geom);
   const int K = g.KH * g.KW * g.CO;
-  const int KS = cm_ks((K + 31) / 32);
+  const int KS = fused ? cm_ks((K + 31) / 32) : cm_ks5((K + 31) / 32);
   const long M = (long)g.B * g.H * g.W;
   // two 16-pixel groups per wave per trip (HOPSX_DGRAD_UN=1: one)
   static const int un_env = getenv("HOPSX_DGRAD_UN") ? atoi(getenv("HOPSX_DGRAD_UN")) : 0;
@@ -914,6 +919,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   switch (KS) {                   \
     case 2: HOPSX_CMD(NF, 2, 0); break;  \
     case 4: HOPSX_CMD(NF, 4, 0); break;  \
+    case 5: HOPSX_CMD(NF, 5, 0); break;  \
     case 8: HOPSX_CMD(NF, 8, 0); break;  \
     case 9: HOPSX_CMD(NF, 9, 0); break;  \
     default: HOPSX_CMD(NF, 16, 0); break; \
@@ -1009,7 +1015,7 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
   const int K0 = fused ? geom0[7] * geom0[8] : 0;
   // ---- dgrad part
   const int Kd = g.KH * g.KW * g.CO;
-  const int KS = cm_ks((Kd + 31) / 32);
+  const int KS = cm_ks5((Kd + 31) / 32);
   const long Md = (long)g.B * g.H * g.W;
   long nA = ((Md + 15) / 16 + CM_WAVES * 2 - 1) / (CM_WAVES * 2);
   if (nA > 1024) nA = 1024;
@@ -1058,7 +1064,7 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
 #define HOPSX_PAIR_K0(NFv, KSv, NFCv) HOPSX_PAIR(NFv, KSv, 0, NFCv) HOPSX_PAIR(NFv, KSv, 4, NFCv)
 #define HOPSX_PAIR_NFC(NFv, KSv) HOPSX_PAIR_K0(NFv, KSv, 1) HOPSX_PAIR_K0(NFv, KSv, 2) HOPSX_PAIR_K0(NFv, KSv, 4)
   HOPSX_PAIR_NFC(1, 4) HOPSX_PAIR_NFC(1, 8) HOPSX_PAIR_NFC(2, 4) HOPSX_PAIR_NFC(2, 8) HOPSX_PAIR_NFC(4, 4)
-  HOPSX_PAIR_NFC(4, 8) HOPSX_PAIR_K0(2, 9, 2)
+  HOPSX_PAIR_NFC(4, 8) HOPSX_PAIR_K0(2, 9, 2) HOPSX_PAIR(1, 5, 0, 1)
 #undef HOPSX_PAIR_NFC
 #undef HOPSX_PAIR_K0
 #undef HOPSX_PAIR

@@ -90,7 +90,7 @@ def _torch_conv(x, w, b, pad):
 
 
 @pytest.mark.parametrize("k,C,CO,H,pad", [(2, 32, 64, 27, 0), (3, 32, 64, 28, 1), (4, 32, 64, 25, 0), (2, 16, 32, 9, 0),
-                                          (3, 64, 128, 10, 1), (1, 64, 16, 7, 0)])
+                                          (3, 64, 128, 10, 1), (1, 64, 16, 7, 0), (3, 16, 16, 12, 1), (3, 16, 32, 8, 1)])
 def test_conv_mfma_fwd(k, C, CO, H, pad):
     torch.manual_seed(2)
     B = 3
@@ -103,7 +103,8 @@ def test_conv_mfma_fwd(k, C, CO, H, pad):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("k,C,CO,H,pad", [(2, 32, 64, 27, 0), (3, 32, 64, 14, 1), (4, 32, 64, 13, 0), (2, 16, 32, 9, 0)])
+@pytest.mark.parametrize("k,C,CO,H,pad", [(2, 32, 64, 27, 0), (3, 32, 64, 14, 1), (4, 32, 64, 13, 0), (2, 16, 32, 9, 0),
+                                          (3, 16, 16, 12, 1)])
 def test_conv_mfma_dgrad_masks_colsum(k, C, CO, H, pad):
     torch.manual_seed(3)
     B = 2

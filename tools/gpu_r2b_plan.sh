@@ -5,6 +5,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 B="timeout -k 10 200 python -u benchmarks/run.py"
 : > gpurun_out/plan_ab.txt
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_kernels_v2_gpu.py tests/test_bnstats_gpu.py tests/test_kernels_gpu.py tests/test_models_gpu.py \
+  > gpurun_out/plan_tests.log 2>&1 || exit 1
 run() {  # label, env..., then benchmark args after --
   local label=$1; shift
   local envs=()
@@ -14,6 +17,7 @@ run() {  # label, env..., then benchmark args after --
   out=$(env "${envs[@]}" $B "$@" | tail -1 | cut -c1-150) || return 1
   echo "$label $* :: $out" >> gpurun_out/plan_ab.txt
 }
+run ks5off HOPSX_DISABLE=ks5 -- cifar_resnet --steps 20 --warmup 5 || exit 1
 for cfg in cifar_resnet "resnet50 --batch 64" "resnet50 --batch 8"; do
   run default X=0 -- $cfg --steps 20 --warmup 5 && \
   run t64min256 HOPSX_GEMM_T64_MIN=256 -- $cfg --steps 20 --warmup 5 && \
