@@ -183,6 +183,7 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                                   P<float>(rm), P<float>(rv), mom, eps, M, C, P<void>(res), act, P<float>(acc), S(st));
   });
   m.def("bn_prestats_ok", [](int C) { return hopsx_bn_prestats_ok(C); });
+  m.def("bn_coop_timeouts", [](u acc, int C) { return hopsx_bn_coop_timeouts(P<float>(acc), C); });
   m.def("conv2d_fwd_bnstats", [](u x, u w, std::vector<int> g, u out, u acc, u st) {
     return hopsx_conv2d_fwd_bnstats(P<void>(x), P<void>(w), g.data(), P<void>(out), P<float>(acc), S(st));
   });

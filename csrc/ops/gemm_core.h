@@ -717,19 +717,32 @@ inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu =
   GemmPlan p;
   const long t128 = ((M + 127) / 128) * ((N + 127) / 128);
   const long t64 = ((M + 63) / 64) * ((N + 63) / 64);
-  if (M >= 128 && N >= 128 && t128 >= num_cu) p.cfg = 0;
-  else if (M >= 48 && N >= 48 && t64 >= num_cu / 2) p.cfg = 1;
-  else if (M > 32 && N > 32 && t64 >= 32) p.cfg = 1;
+  // A/B knobs (host side, read once): HOPSX_GEMM_T64_MIN / _T128_MIN = the tile count below which a
+  // non-split GEMM drops to the next smaller tile (fewer, bigger tiles leave CUs idle on small-M
+  // convs); HOPSX_GEMM_SPLIT_CFG = tile config of the big-K split GEMMs (1: 64x64,
+  // 0: 128x128 where M, N >= 128); HOPSX_GEMM_SPLIT_TARGET = workgroups per CU a split aims at.
+  // default 2 x num_cu 64x64 tiles (two per CU) before a non-split GEMM uses them: vs the old floor
+  // num_cu/2, ResNet-20 +6 %, ResNet-50 B=8 +18 %, B=64 +3 % (profiles/r2s7_gemm_plan_ab.txt,
+  // r2s7_verify2_ab.txt); the old floor left half the CUs idle on small-M convs
+  static const long t64_min = hopsx_env_int("HOPSX_GEMM_T64_MIN", 2L * num_cu);
+  static const long t128_min = hopsx_env_int("HOPSX_GEMM_T128_MIN", num_cu);
+  static const long split_cfg = hopsx_env_int("HOPSX_GEMM_SPLIT_CFG", 1);
+  static const long split_target = hopsx_env_int("HOPSX_GEMM_SPLIT_TARGET", 2);
+  const long t64_lim = t64_min >= 0 ? t64_min : num_cu / 2;
+  if (M >= 128 && N >= 128 && t128 >= t128_min) p.cfg = 0;
+  else if (M >= 48 && N >= 48 && t64 >= t64_lim) p.cfg = 1;
+  else if (M > 32 && N > 32 && t64 >= 32 && !(t64_min >= 0 && t64 < t64_min)) p.cfg = 1;
   // split-K GEMMs (weight gradients, K = batch*pixels) get their parallelism from
   // the K split, so use the bigger tile: every operand element is then fetched by
   // fewer workgroups (64x64 halves the operand traffic of 32x32 tiles)
-  else if (allow_split && M >= 48 && N >= 48 && K >= 8192) p.cfg = 1;
+  else if (allow_split && M >= 48 && N >= 48 && K >= 8192)
+    p.cfg = (split_cfg == 0 && M >= 128 && N >= 128) ? 0 : 1;
   else p.cfg = 2;
   const int bm = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
   const long tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm);
   p.split = 1;
   if (allow_split) {
-    const long target = 2L * num_cu;
+    const long target = split_target * num_cu;
     if (tiles < target) {
       long s = (target + tiles - 1) / tiles;
       static const int minkt = [] {

@@ -1,6 +1,7 @@
 // BatchNorm over NHWC activations viewed as [M = B*H*W, C] (channel-fastest),
 // with the residual add and the activation fused into the apply pass
 // (ResNet: y = act(bn(x) + residual)) and into the backward.
+#include <algorithm>
 #include <initializer_list>
 
 #include "common.h"
@@ -154,6 +155,54 @@ struct BnFin {
   int defer;  // 1: leave the replicas for the consuming apply kernel (bn_apply_fin8_k / bn_bwd_apply_fin8_k)
 };
 
+// Fold a workgroup's per-lane column partials (8 channels c0..c0+7 of channel group threadIdx % CG,
+// sums s1 / s2) and add them to this workgroup's replica row dst[0:2C] (red: >= 256*16 floats LDS).
+__device__ __forceinline__ void bn_block_colsum(float* s1, float* s2, float* red, float* dst, int C, int CG,
+                                                int RPI) {
+  if (CG < 64) {
+    // lanes of a wave with the same channel group (lane % CG) fold with xor shuffles, log2(64/CG)
+    // steps; then 4 wave partials per channel meet in LDS.  (A serial walk over the RPI row
+    // partials by 2C threads cost RPI dependent LDS round trips: 128 of them at C = 16.)
+    for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += __shfl_xor(s1[j], o, 64);
+        s2[j] += __shfl_xor(s2[j], o, 64);
+      }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane < CG) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wave * CG + lane) * 16 + j] = s1[j];
+        red[(wave * CG + lane) * 16 + 8 + j] = s2[j];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * C; e += 256) {  // e < C: sum1 of channel e, else sum2 of channel e - C
+      const int which = e >= C, c = e - which * C;
+      const int g = c >> 3, j = c & 7;
+      const float t = red[g * 16 + which * 8 + j] + red[(CG + g) * 16 + which * 8 + j] +
+                      red[(2 * CG + g) * 16 + which * 8 + j] + red[(3 * CG + g) * 16 + which * 8 + j];
+      if (t != 0.f) atomicAdd(dst + e, t);
+    }
+  } else {  // RPI <= 4 row partials per channel
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[threadIdx.x * 16 + j] = s1[j];
+      red[threadIdx.x * 16 + 8 + j] = s2[j];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * C; e += 256) {
+      const int which = e >= C, c = e - which * C;
+      const int g = c >> 3, j = c & 7;
+      float t = 0.f;
+      for (int q = 0; q < RPI; ++q) t += red[(q * CG + g) * 16 + which * 8 + j];
+      if (t != 0.f) atomicAdd(dst + e, t);
+    }
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ x,
                                                     const bf16_raw* __restrict__ y, const float* __restrict__ mean,
@@ -201,48 +250,7 @@ __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__
   }
   __shared__ float red[256 * 16];
   float* dst = acc + (long)(blockIdx.x % BN_NREP) * 2 * C;
-  if (CG < 64) {
-    // lanes of a wave with the same channel group (lane % CG) fold with xor shuffles, log2(64/CG)
-    // steps; then 4 wave partials per channel meet in LDS.  (A serial walk over the RPI row
-    // partials by 2C threads cost RPI dependent LDS round trips: 128 of them at C = 16.)
-    for (int o = CG; o < 64; o <<= 1) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s1[j] += __shfl_xor(s1[j], o, 64);
-        s2[j] += __shfl_xor(s2[j], o, 64);
-      }
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane < CG) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wave * CG + lane) * 16 + j] = s1[j];
-        red[(wave * CG + lane) * 16 + 8 + j] = s2[j];
-      }
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 2 * C; e += 256) {  // e < C: sum1 of channel e, else sum2 of channel e - C
-      const int which = e >= C, c = e - which * C;
-      const int g = c >> 3, j = c & 7;
-      const float t = red[g * 16 + which * 8 + j] + red[(CG + g) * 16 + which * 8 + j] +
-                      red[(2 * CG + g) * 16 + which * 8 + j] + red[(3 * CG + g) * 16 + which * 8 + j];
-      if (t != 0.f) atomicAdd(dst + e, t);
-    }
-  } else {  // RPI <= 4 row partials per channel
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[threadIdx.x * 16 + j] = s1[j];
-      red[threadIdx.x * 16 + 8 + j] = s2[j];
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 2 * C; e += 256) {
-      const int which = e >= C, c = e - which * C;
-      const int g = c >> 3, j = c & 7;
-      float t = 0.f;
-      for (int q = 0; q < RPI; ++q) t += red[(q * CG + g) * 16 + which * 8 + j];
-      if (t != 0.f) atomicAdd(dst + e, t);
-    }
-  }
+  bn_block_colsum(s1, s2, red, dst, C, CG, RPI);
   if (fin.defer) return;  // the apply launch folds the replicas: no arrival / exchange round trips here
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics are done
@@ -507,6 +515,132 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
     for (int e = threadIdx.x; e < BN_NREP * 2 * C; e += 256) acc[e] = 0.f;
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-launch BN backward for tensors one trip of a resident grid covers (ResNet-20/56 every layer,
+// the small ResNet-50 layers): every lane keeps its R rows of dy / x / y in registers, the
+// workgroups add their column partials into the replicas, meet at a grid barrier, fold the
+// replicas and write dx (+ dres) from the registers — no second launch and no second read of the
+// three tensors.  The grid is sized to at most half the device's resident capacity (host side), so
+// every workgroup is resident and a concurrent resident-grid kernel (the P2P collectives, <= 1
+// workgroup per CU) still fits.  The barrier is sense-reversing on two zero-at-rest words after
+// the arrival words (count, generation) and its spin is bounded by the wall clock: a lost
+// workgroup cannot hang the device (the timeout is recorded in the third word).
+template <int R>
+__global__ __launch_bounds__(256) void bn_bwd_coop8_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
+                                                      const bf16_raw* __restrict__ y, const float* __restrict__ gamma,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      float* __restrict__ acc, bf16_raw* __restrict__ dx,
+                                                      bf16_raw* __restrict__ dres, int M, int C, int act, BnFin fin,
+                                                      long long spin) {
+  const int CG = C >> 3, RPI = 256 / CG;
+  const int cg = threadIdx.x % CG, rsub = threadIdx.x / CG;
+  const int c0 = cg * 8;
+  const int rbase = blockIdx.x * (RPI * R) + rsub;
+  float mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+  bf16x8 vd[R], vx[R], vy[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {  // every load of the lane first
+    const int r = rbase + u * RPI;
+    const long o = (long)(r < M ? r : 0) * C + c0;
+    vd[u] = *(const bf16x8*)(dy + o);
+    vx[u] = *(const bf16x8*)(x + o);
+    if (act != ACT_NONE) vy[u] = *(const bf16x8*)(y + o);
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    if (rbase + u * RPI >= M) break;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float dz = bf2f((uint16_t)vd[u][j]);
+      if (act != ACT_NONE) dz *= act_grad_from_out(bf2f((uint16_t)vy[u][j]), act);
+      s1[j] += dz;
+      s2[j] = fmaf(dz, (bf2f((uint16_t)vx[u][j]) - mu[j]) * rs[j], s2[j]);
+    }
+  }
+  extern __shared__ float coop_smem[];  // [max(256*16, 5C)] floats
+  float* red = coop_smem;
+  float* dst = acc + (long)(blockIdx.x % BN_NREP) * 2 * C;
+  bn_block_colsum(s1, s2, red, dst, C, CG, RPI);
+  // ---- grid barrier (sense reversal; count, generation, timeout flag after the arrival words)
+  unsigned* bar = (unsigned*)(acc + (long)BN_NREP * 2 * C) + kArriveWords;
+  __shared__ int lastw;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial atomics are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned gen0 = __hip_atomic_load(bar + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (atomicAdd(bar, 1u) == gridDim.x - 1) {
+      atomicExch(bar, 0u);
+      atomicAdd(bar + 32, 1u);
+    } else {
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load(bar + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
+        if ((long long)(wall_clock64() - t0) > spin) {
+          atomicExch(bar + 64, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  // ---- fold the replicas (atomic reads: the partials landed at the memory side)
+  float* sk1 = coop_smem;  // red is free again
+  float* sk2 = sk1 + C;
+  float* smd = sk2 + C;
+  const float invM = 1.f / M;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int r = 0; r < BN_NREP; ++r) {
+      s += __hip_atomic_load(acc + (long)r * 2 * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q += __hip_atomic_load(acc + (long)r * 2 * C + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sk1[c] = (gamma ? gamma[c] : 1.f) * rstd[c];
+    sk2[c] = q * invM;
+    smd[c] = s * invM;
+    if (blockIdx.x == 0) {
+      fin.ws[c] = s;
+      fin.ws[C + c] = q;
+      if (fin.dbeta) fin.dbeta[c] += s;
+      if (fin.dgamma) fin.dgamma[c] += q;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) lastw = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
+  float k1[8], k2[8], md[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { k1[j] = sk1[c0 + j]; k2[j] = sk2[c0 + j]; md[j] = smd[c0 + j]; }
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const int r = rbase + u * RPI;
+    if (r >= M) break;
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      d[j] = bf2f((uint16_t)vd[u][j]);
+      if (act != ACT_NONE) d[j] *= act_grad_from_out(bf2f((uint16_t)vy[u][j]), act);
+    }
+    const long o = (long)r * C + c0;
+    if (dres) st8f(dres + o, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (bf2f((uint16_t)vx[u][j]) - mu[j]) * rs[j];
+      d[j] = k1[j] * (d[j] - md[j] - xh * k2[j]);
+    }
+    st8f(dx + o, d);
+  }
+  __syncthreads();
+  if (lastw)
+    for (int e = threadIdx.x; e < BN_NREP * 2 * C; e += 256) acc[e] = 0.f;
+}
+
 static bool bn_vec_ok(int C, std::initializer_list<const void*> ptrs) {
   if (C % 8 != 0 || C / 8 > 256 || (256 % (C / 8)) != 0 || hopsx_disabled("bn_vec")) return false;
   for (const void* p : ptrs)
@@ -547,6 +681,57 @@ static void slab_grid(int M, int C, int& gx, int& gy, int& rpb) {
 static int ew_grid(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+// the one-launch backward (bn_bwd_coop8_k) when a resident grid covers the tensor in one trip
+template <int R>
+static bool bn_coop_try(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
+                        const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
+                        void* dres, float* acc, hipStream_t st) {
+  static int n_cu = 0, occ = 0;
+  const size_t shm = std::max<size_t>(256 * 16, 3 * (size_t)C) * sizeof(float);
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  static size_t occ_shm = 0;
+  if (!occ || occ_shm != shm) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bn_bwd_coop8_k<R>, 256, shm) != hipSuccess) occ = 0;
+    occ_shm = shm;
+  }
+  const int RPI = 256 / (C / 8);
+  const long G = ((long)M + (long)RPI * R - 1) / ((long)RPI * R);
+  const long cap = (long)n_cu * occ / 2;  // half the resident capacity: see bn_bwd_coop8_k
+  if (G < 1 || G > cap) return false;
+  const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, 1};
+  const long long spin = 200000000LL;  // 2 s of the 100 MHz wall clock
+  hipLaunchKernelGGL(bn_bwd_coop8_k<R>, dim3((unsigned)G), dim3(256), shm, st, (const bf16_raw*)dy,
+                     (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, acc, (bf16_raw*)dx, (bf16_raw*)dres, M,
+                     C, act, fin, spin);
+  return true;
+}
+
+static bool bn_bwd_coop(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
+                        const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
+                        void* dres, float* acc, hipStream_t st) {
+  // off by default: measured SLOWER than the two launches (ResNet-20 111.6k -> 102.7k img/s, ResNet-50
+  // B=64 4.15k -> 4.10k; profiles/r2s7_verify2_ab.txt) — fewer workgroups in flight per tensor and the
+  // barrier's round trips outweigh the saved launch and re-read.  HOPSX_BN_COOP=1 to A/B.
+  static const long on = hopsx_env_int("HOPSX_BN_COOP", 0);
+  if (!on) return false;
+  return bn_coop_try<1>(dy, x, y, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, C, act, dres, acc, st) ||
+         bn_coop_try<2>(dy, x, y, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, C, act, dres, acc, st) ||
+         bn_coop_try<4>(dy, x, y, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, C, act, dres, acc, st) ||
+         bn_coop_try<8>(dy, x, y, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, C, act, dres, acc, st);
+}
+
+// timeout flag of the coop barrier (tests)
+extern "C" int hopsx_bn_coop_timeouts(const float* acc, int C) {
+  unsigned v = 0;
+  const unsigned* bar = (const unsigned*)(acc + (long)BN_NREP * 2 * C) + kArriveWords;
+  if (hipMemcpy(&v, bar + 64, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (int)v;
 }
 
 extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
@@ -619,6 +804,8 @@ extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const 
   if (acc && bn_vec_ok(C, {dy, x, y, dx, dresidual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
     const int g = colred_grid(M, C, rpb);
+    if (bn_bwd_coop(dy, x, y, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, C, act, dresidual, acc, st))
+      return (int)hipGetLastError();
     const int defer = hopsx_disabled("bn_defer") ? 0 : 1;
     const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, defer};
     hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,

@@ -125,6 +125,7 @@ int hopsx_bn_fwd_apply_fin(const void* x, void* y, const float* gamma, const flo
                            float* rstd_out, float* running_mean, float* running_var, float momentum, float eps, int M,
                            int C, const void* residual, int act, float* acc, hipStream_t st);
 int hopsx_bn_prestats_ok(int C);
+int hopsx_bn_coop_timeouts(const float* acc, int C);
 int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                             int act_prev, float* colsum, const void* y, int yact, hipStream_t st);
 // dgrad with the input layer's weight gradient fused into the epilogue (geom0: the input layer,

@@ -22,6 +22,14 @@ Performance / communication knobs read where they act:
   HOPSX_GRAPH_COLLECTIVES  1 = capture the RCCL all-reduce inside the step graph
   HOPSX_OPT_GRID        optimizer grid cap (default 256 workgroups up to 8 M params, else 512)
   HOPSX_OPT_NT          1 = nontemporal master/state stores in the optimizer kernel
+  HOPSX_GEMM_T64_MIN / HOPSX_GEMM_T128_MIN  tile counts below which a non-split GEMM drops to the
+                        next smaller tile (csrc/ops/gemm_core.h plan_gemm; defaults 2 x CUs / CUs)
+  HOPSX_GEMM_SPLIT_CFG, HOPSX_GEMM_SPLIT_TARGET  split-K GEMM tile (1 = 64x64) / workgroups per CU
+  HOPSX_WGRAD_MFMA_MAXK  largest KH*KW*C on the direct MFMA weight gradient (default 640)
+  HOPSX_BNSTATS_MAX_1X1_FLOP  1x1 convs above this keep the library GEMM + a BN statistics pass
+  HOPSX_BN_COOP         1 = one-launch BN backward with a grid barrier (measured slower; off)
+  HOPSX_DISABLE         comma list of fast paths to turn off for A/B checks, e.g. bnstats, bn_defer,
+                        ks5, bwd_pair, conv_mfma, wgrad_mfma, blaslt_1x1, direct_conv
 """
 from __future__ import annotations
 

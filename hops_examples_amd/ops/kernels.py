@@ -451,8 +451,9 @@ def bn_acc(device, C) -> torch.Tensor:
     if t is None:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("BN accumulator must be created before graph capture (run an eager step first)")
-        # + the 9 x 32 arrival words of the in-launch finalize (common.h grid_arrive_last)
-        t = torch.zeros(BN_NREP * 2 * C + 9 * 32, device=device, dtype=F32)
+        # + the 9 x 32 arrival words of the in-launch finalize (common.h grid_arrive_last) + the
+        # one-launch backward's grid barrier (count, generation, timeout flag; norm.hip bn_bwd_coop8_k)
+        t = torch.zeros(BN_NREP * 2 * C + 9 * 32 + 3 * 32, device=device, dtype=F32)
         _BN_ACC[key] = t
     return t
 
@@ -483,6 +484,11 @@ def conv2d_fwd_bnstats(x, w, geom, out=None):
         return None
     check(rc, "conv2d_fwd_bnstats")
     return out
+
+
+def bn_coop_timeouts(device, C) -> int:
+    """Nonzero if a one-launch BN backward barrier of width C ever timed out (never expected)."""
+    return int(_C.ext().bn_coop_timeouts(ptr(bn_acc(device, C)), int(C)))
 
 
 def bn_prestats_ok(C) -> bool:
