@@ -340,6 +340,22 @@ __global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restric
                                                        const bf16_raw* __restrict__ res, int act, BnFin fin) {
   __shared__ float ssc[2048], ssh[2048];  // C <= 2048 (bn_vec_ok)
   __shared__ int last;
+  const long stride = (long)gridDim.x * blockDim.x;  // a multiple of CG: the channel group is per-thread
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // the first trip's operands are requested BEFORE the replica fold, so their latency overlaps the
+  // replica loads' (kept raw: a conversion here would wait for them right away).  apply_grid gives
+  // most launches exactly one trip.
+  const bool have0 = i0 < nch;
+  const long i1 = i0 + stride < nch ? i0 + stride : i0;
+  bf16x8 px[2], pr[2];
+  if (have0) {
+    px[0] = *(const bf16x8*)(x + i0 * 8);
+    px[1] = *(const bf16x8*)(x + i1 * 8);
+    if (res) {
+      pr[0] = *(const bf16x8*)(res + i0 * 8);
+      pr[1] = *(const bf16x8*)(res + i1 * 8);
+    }
+  }
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f, q = 0.f;
 #pragma unroll
@@ -366,8 +382,6 @@ __global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restric
   __syncthreads();  // every replica value this workgroup needs has been consumed
   if (threadIdx.x == 0) last = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
   const int CG = C >> 3;
-  const long stride = (long)gridDim.x * blockDim.x;  // a multiple of CG: the channel group is per-thread
-  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(i0 % CG) * 8;
   float sc[8], sh[8];
 #pragma unroll
@@ -376,25 +390,27 @@ __global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restric
     sh[j] = ssh[c0 + j];
   }
   for (long i = i0; i < nch; i += 2 * stride) {
-    float v[2][8], rv[2][8];
-    const long i1 = i + stride < nch ? i + stride : i;
-    ld8f(x + i * 8, v[0]);
-    ld8f(x + i1 * 8, v[1]);
-    if (res) {
-      ld8f(res + i * 8, rv[0]);
-      ld8f(res + i1 * 8, rv[1]);
+    const long ib = i + stride < nch ? i + stride : i;
+    if (i != i0) {
+      px[0] = *(const bf16x8*)(x + i * 8);
+      px[1] = *(const bf16x8*)(x + ib * 8);
+      if (res) {
+        pr[0] = *(const bf16x8*)(res + i * 8);
+        pr[1] = *(const bf16x8*)(res + ib * 8);
+      }
     }
+    float v[2][8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float t = fmaf(v[u][j], sc[j], sh[j]);
-        if (res) t += rv[u][j];
+        float t = fmaf(bf2f((uint16_t)px[u][j]), sc[j], sh[j]);
+        if (res) t += bf2f((uint16_t)pr[u][j]);
         v[u][j] = apply_act(t, act);
       }
     }
     st8f(y + i * 8, v[0]);
-    if (i + stride < nch) st8f(y + i1 * 8, v[1]);
+    if (i + stride < nch) st8f(y + ib * 8, v[1]);
   }
   __syncthreads();
   if (last)
@@ -458,6 +474,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
   __shared__ float sk1[2048], sk2[2048], smd[2048], smu[2048], srs[2048];  // C <= 2048 (bn_vec_ok)
   __shared__ int last;
   const float invM = 1.f / M;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // two chunks per trip, the first trip's operands requested before the replica fold (see
+  // bn_apply_fin8_k); apply_grid gives most launches exactly one trip
+  const long i1 = i0 + stride < nch ? i0 + stride : i0;
+  bf16x8 pd[2], px[2], py[2];
+  if (i0 < nch) {
+    pd[0] = *(const bf16x8*)(dy + i0 * 8);
+    pd[1] = *(const bf16x8*)(dy + i1 * 8);
+    px[0] = *(const bf16x8*)(x + i0 * 8);
+    px[1] = *(const bf16x8*)(x + i1 * 8);
+    if (act != ACT_NONE) {
+      py[0] = *(const bf16x8*)(y + i0 * 8);
+      py[1] = *(const bf16x8*)(y + i1 * 8);
+    }
+  }
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f, q = 0.f;
 #pragma unroll
@@ -481,8 +513,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
   __syncthreads();
   if (threadIdx.x == 0) last = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
   const int CG = C >> 3;
-  const long stride = (long)gridDim.x * blockDim.x;
-  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(i0 % CG) * 8;
   float k1[8], k2[8], md[8], mu[8], rs[8];
 #pragma unroll
@@ -493,22 +523,36 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
     mu[j] = smu[c0 + j];
     rs[j] = srs[c0 + j];
   }
-  for (long i = i0; i < nch; i += stride) {
-    float d[8], xv[8], yv[8];
-    ld8f(dy + i * 8, d);
-    ld8f(x + i * 8, xv);
-    if (act != ACT_NONE) {
-      ld8f(y + i * 8, yv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] *= act_grad_from_out(yv[j], act);
+  for (long i = i0; i < nch; i += 2 * stride) {
+    const long ib = i + stride < nch ? i + stride : i;
+    if (i != i0) {
+      pd[0] = *(const bf16x8*)(dy + i * 8);
+      pd[1] = *(const bf16x8*)(dy + ib * 8);
+      px[0] = *(const bf16x8*)(x + i * 8);
+      px[1] = *(const bf16x8*)(x + ib * 8);
+      if (act != ACT_NONE) {
+        py[0] = *(const bf16x8*)(y + i * 8);
+        py[1] = *(const bf16x8*)(y + ib * 8);
+      }
     }
-    if (dres) st8f(dres + i * 8, d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = (xv[j] - mu[j]) * rs[j];
-      d[j] = k1[j] * (d[j] - md[j] - xh * k2[j]);
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && i + stride >= nch) break;
+      const long o = (u == 0 ? i : ib) * 8;
+      float d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        d[j] = bf2f((uint16_t)pd[u][j]);
+        if (act != ACT_NONE) d[j] *= act_grad_from_out(bf2f((uint16_t)py[u][j]), act);
+      }
+      if (dres) st8f(dres + o, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (bf2f((uint16_t)px[u][j]) - mu[j]) * rs[j];
+        d[j] = k1[j] * (d[j] - md[j] - xh * k2[j]);
+      }
+      st8f(dx + o, d);
     }
-    st8f(dx + i * 8, d);
   }
   __syncthreads();
   if (last)
