@@ -781,6 +781,22 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs
   }
 }
 
+// The same horizontal fusion for layers whose input gradient takes the implicit GEMM (stride 2, or
+// KH*KW*CO > 512: ResNet stage-3 3x3x64 and the strided / projection convs): the first nA
+// workgroups are the dgrad GEMM's tiles (mfma_gemm_body, one K split), the rest the direct MFMA
+// weight gradient.  Each part alone leaves most CUs idle at these sizes.
+template <int BM, int NFC>
+__global__ __launch_bounds__(256) void conv_bwd_pair_gemm_k(ConvDgradALoader al, ConvWeightTLoader bl, EpiDActBF16 ep,
+                                                           int M, int N, int K, int kps, int nA, WgradArgs B,
+                                                           int nBx) {
+  if ((int)blockIdx.x < nA) {
+    mfma_gemm_body<BM, BM, 2, true, false>(al, bl, ep, M, N, K, kps, nullptr, blockIdx.x, nA, 0, 1);
+  } else {
+    const int j = blockIdx.x - nA;
+    conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx);
+  }
+}
+
 // supported K-step counts (K is zero-padded up to one of them)
 int cm_ks(int ks) { return ks <= 2 ? 2 : ks <= 4 ? 4 : ks <= 8 ? 8 : ks <= 9 ? 9 : 16; }
 // + a 5-step variant (K = 129..160: the 3x3, 16-channel convs of ResNet stage 1, K = 144) for the
@@ -998,6 +1014,62 @@ extern "C" int hopsx_wgrad_debug_times(unsigned long long* host_out, int n) {
                                   hipMemcpyDeviceToHost);
 }
 
+// wgrad part of a paired launch: 32-column blocks, chunks per wave sized for ~`slots` workgroups
+static void pair_wgrad_plan(const ConvGeom& g, long slots, int& cpw, long& nBx, int& colblk, size_t& shm) {
+  const int Kw = g.KH * g.KW * g.C;
+  const long nchunks = ((long)g.B * g.OH * g.OW + WG_PX - 1) / WG_PX;
+  constexpr int KB = 32;
+  colblk = (Kw + KB - 1) / KB;
+  const long want_groups = std::max(1L, slots / colblk);
+  cpw = (int)std::max(1L, (nchunks + 4 * want_groups - 1) / (4 * want_groups));
+  nBx = (nchunks + 4L * cpw - 1) / (4L * cpw);
+  const size_t stage = (size_t)4 * WG_PX * (g.CO + KB) * sizeof(bf16_raw);
+  const size_t redb = ((size_t)4 * (g.CO / 16) * 2 * 64 * 4 + 4 * g.CO + (size_t)g.CO * KB) * sizeof(float);
+  shm = std::max(stage, redb);
+}
+
+// dgrad on the implicit GEMM + wgrad on the direct MFMA kernel in one launch (conv_bwd_pair_gemm_k)
+static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                              int act_prev, float* colsum, const void* y, int yact, const void* x, float* dw,
+                              float* dbias, hipStream_t st) {
+  if (hopsx_disabled("bwd_pair_gemm")) return -2;
+  ConvGeom g = cm_geom(geom);
+  if (g.C % 8 != 0 || g.CO % 8 != 0 || ((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)w) % 16 != 0)
+    return -2;
+  const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
+  const GemmPlan p = plan_gemm(M, N, K, false);
+  if (p.cfg == 0 || p.split != 1) return -2;  // 128x128 tiles: the GEMM fills the chip on its own
+  const int BM = p.cfg == 1 ? 64 : 32;
+  const long nA = (long)((M + BM - 1) / BM) * ((N + BM - 1) / BM);
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  int cpw, colblk;
+  long nBx;
+  size_t shm;
+  pair_wgrad_plan(g, nA >= 2L * n_cu ? 384L : std::max(64L, 2L * n_cu - nA), cpw, nBx, colblk, shm);
+  const long total = nA + nBx * colblk;
+  if (shm > 65536 || total > (1L << 20)) return -2;
+  static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
+  const WgradArgs WA{(const bf16_raw*)dy, (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g,
+                     g.KH * g.KW * g.C, cpw, dbg};
+  ConvDgradALoader al{(const bf16_raw*)dy, g, 1, (const bf16_raw*)y, yact};
+  ConvWeightTLoader bl{(const bf16_raw*)w, g, 1};
+  EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act_prev, colsum};
+#define HOPSX_PG(BMv, NFCv)                                                                                   \
+  if (BM == BMv && g.CO / 16 == NFCv) {                                                                     \
+    hipLaunchKernelGGL((conv_bwd_pair_gemm_k<BMv, NFCv>), dim3((unsigned)total), dim3(256), shm, st, al, bl, e, M, \
+                       N, K, p.kps, (int)nA, WA, (int)nBx);                                                   \
+    return (int)hipGetLastError();                                                                          \
+  }
+  HOPSX_PG(32, 1) HOPSX_PG(32, 2) HOPSX_PG(32, 4) HOPSX_PG(64, 1) HOPSX_PG(64, 2) HOPSX_PG(64, 4)
+#undef HOPSX_PG
+  return -2;
+}
+
 // One launch for a conv layer's whole backward: dgrad (optionally carrying the input layer's
 // weight gradient, geom0 != null) + the layer's own weight gradient.  Same argument meaning as
 // hopsx_conv2d_dgrad_mfma_ex and hopsx_conv2d_wgrad_mfma; returns -2 for shapes outside the
@@ -1006,8 +1078,10 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
                                      int act_prev, float* colsum, const void* y, int yact, const int* geom0,
                                      const void* x0, float xscale, float xshift, float* dw0, const void* x,
                                      float* dw, float* dbias, hipStream_t st) {
-  if (hopsx_disabled("bwd_pair") || !hopsx_conv_dgrad_mfma_ok(geom) || !hopsx_conv_wgrad_mfma_ok(geom)) return -2;
+  if (hopsx_disabled("bwd_pair") || !hopsx_conv_wgrad_mfma_ok(geom)) return -2;
   const bool fused = geom0 != nullptr;
+  if (!hopsx_conv_dgrad_mfma_ok(geom))
+    return fused ? -2 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, st);
   if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
   if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)yprev) % 16 != 0) return -2;
   ConvGeom g = cm_geom(geom);

@@ -495,22 +495,26 @@ def test_conv_pool_model_grads_match_unfused(monkeypatch, model):
     torch.testing.assert_close(res[0][1], res[1][1], atol=3e-2 * res[1][1].abs().max().item(), rtol=3e-2)
 
 
-@pytest.mark.parametrize("B,H,C,CO", [(16, 32, 16, 16), (16, 16, 32, 32), (128, 16, 32, 32), (8, 12, 64, 32)])
-def test_conv_bwd_pair_kernel_vs_fp32(B, H, C, CO):
+@pytest.mark.parametrize("B,H,C,CO,k,s", [(16, 32, 16, 16, 3, 1), (16, 16, 32, 32, 3, 1), (128, 16, 32, 32, 3, 1),
+                                          (8, 12, 64, 32, 3, 1), (32, 8, 64, 64, 3, 1), (16, 16, 16, 32, 3, 2),
+                                          (16, 16, 32, 64, 1, 2), (128, 8, 64, 64, 3, 1)])
+def test_conv_bwd_pair_kernel_vs_fp32(B, H, C, CO, k, s):
     """conv_bwd_pair_k alone (dgrad + wgrad in one launch) against fp32 autograd, incl. the
-    ResNet-20 stage-2 shape (Kd = 288 -> KS = 9) and a batch whose dgrad part fills the chip."""
+    ResNet-20 stage-2 shape (Kd = 288 -> KS = 9), a batch whose dgrad part fills the chip, and the
+    GEMM-dgrad variant (conv_bwd_pair_gemm_k: stride 2, or KH*KW*CO = 576 > 512)."""
     torch.manual_seed(5)
     x = (torch.randn(B, H, H, C, device=dev)).to(torch.bfloat16)
-    w = (torch.randn(CO, 3, 3, C, device=dev) / (9 * C) ** 0.5).to(torch.bfloat16)
-    dy = torch.randn(B, H, H, CO, device=dev).to(torch.bfloat16)
-    g = K.conv_geom(x.shape, w.shape, (1, 1), (1, 1), (1, 1))
-    dw = torch.zeros(CO, 3, 3, C, device=dev)
+    w = (torch.randn(CO, k, k, C, device=dev) / (k * k * C) ** 0.5).to(torch.bfloat16)
+    OH = (H + 2 * (k // 2) - k) // s + 1
+    dy = torch.randn(B, OH, OH, CO, device=dev).to(torch.bfloat16)
+    g = K.conv_geom(x.shape, w.shape, (s, s), (k // 2, k // 2), (1, 1))
+    dw = torch.zeros(CO, k, k, C, device=dev)
     dx = K.conv2d_bwd_pair(dy, w, g, x, dw)
     if dx is False:
         pytest.skip("shape not instantiated")
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
-    yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+    yr = torch.nn.functional.conv2d(xr, wr, None, s, k // 2)
     gx, gw = torch.autograd.grad(yr, (xr, wr), dy.float().permute(0, 3, 1, 2))
     torch.testing.assert_close(dx.float(), gx.permute(0, 2, 3, 1), rtol=2e-2, atol=2e-2 * gx.abs().max().item())
     torch.testing.assert_close(dw, gw.permute(0, 2, 3, 1), rtol=2e-2, atol=1e-2 * gw.abs().max().item())
