@@ -100,10 +100,12 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                                  P<unsigned long long>(prng), psalt, pp, dw_store, S(st));
   });
   m.def("conv2d_bwd_pair", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact,
-                              std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u st) {
+                              std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u add,
+                              u st) {
     return hopsx_conv2d_bwd_pair(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act,
                                  P<float>(colsum), P<void>(y), yact, g0.empty() ? nullptr : g0.data(), P<void>(x0),
-                                 xscale, xshift, P<float>(dw0), P<void>(x), P<float>(dw), P<float>(db), S(st));
+                                 xscale, xshift, P<float>(dw0), P<void>(x), P<float>(dw), P<float>(db), P<void>(add),
+                                 S(st));
   });
   m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
                            float xscale, float xshift, u counter, u st) {

@@ -282,6 +282,9 @@ struct DgradArgs {
   ConvGeom gi;
   float* dw0;
   int dbg;
+  // optional gradient of the same input from another consumer (a ResNet block's identity shortcut):
+  // added before the act'(yprev) mask, replacing autograd's separate add launch
+  const bf16_raw* addend;
 };
 
 // bid / nblk: this workgroup's index and the number of workgroups doing dgrad work (a paired
@@ -496,6 +499,11 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
         const int row = c / (CI / 8), col = (c - row * (CI / 8)) * 8;
         if (c < NCH && base + row < M) {
           bf16x8 v = *(const bf16x8*)(sc + row * CI + col);
+          if (A.addend) {  // bf16 + bf16 -> bf16, exactly autograd's accumulation of the two parts
+            const bf16x8 a = *(const bf16x8*)(A.addend + (long)(base + row) * CI + col);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(bf2f((uint16_t)v[j]) + bf2f((uint16_t)a[j]));
+          }
           if (yprev) mask8(v, pmv[u][q], act_prev);
           if constexpr (K0 > 0) {
             float xv[K0];
@@ -927,7 +935,7 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   const int wvec = (uintptr_t)w % 16 == 0;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
-                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg};
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg, nullptr};
 #define HOPSX_CMD(NF, KSV, K0V)                                                                                \
   if (un == 1) hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 1>), dim3(blocks), dim3(256), shm, st, DA); \
   else hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 2>), dim3(blocks), dim3(256), shm, st, DA)
@@ -1077,11 +1085,15 @@ static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, vo
 extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                      int act_prev, float* colsum, const void* y, int yact, const int* geom0,
                                      const void* x0, float xscale, float xshift, float* dw0, const void* x,
-                                     float* dw, float* dbias, hipStream_t st) {
+                                     float* dw, float* dbias, const void* addend, hipStream_t st) {
   if (hopsx_disabled("bwd_pair") || !hopsx_conv_wgrad_mfma_ok(geom)) return -2;
   const bool fused = geom0 != nullptr;
-  if (!hopsx_conv_dgrad_mfma_ok(geom))
+  if (fused && addend) return -2;
+  if ((uintptr_t)addend % 16 != 0) return -3;
+  if (!hopsx_conv_dgrad_mfma_ok(geom)) {
+    if (addend) return -3;  // the GEMM variant has no addend: call again without it and add afterwards
     return fused ? -2 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, st);
+  }
   if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
   if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)yprev) % 16 != 0) return -2;
   ConvGeom g = cm_geom(geom);
@@ -1098,7 +1110,8 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
                       (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float) + (size_t)KS * 4 * 16;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
-                     (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg};
+                     (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg,
+                     (const bf16_raw*)addend};
   // ---- wgrad part (32-column blocks)
   const int Kw = g.KH * g.KW * g.C;
   const long nchunks = ((long)g.B * g.OH * g.OW + WG_PX - 1) / WG_PX;

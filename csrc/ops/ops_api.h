@@ -131,10 +131,12 @@ int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int* geom, void
 // dgrad with the input layer's weight gradient fused into the epilogue (geom0: the input layer,
 // x0 its raw input, uint8 when xscale != 0; dw0 its [CO0][K0] grad, colsum its bias grad; dx unused)
 bool hopsx_conv_wgrad_mfma_ok(const int* geom);
-// one launch for dgrad (+ fused input-layer wgrad when geom0) and this layer's wgrad; -2: unsupported
+// one launch for dgrad (+ fused input-layer wgrad when geom0) and this layer's wgrad; -2: unsupported,
+// -3: `addend` (added to dX in the epilogue) unsupported for this shape — nothing launched
 int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act_prev,
                           float* colsum, const void* y, int yact, const int* geom0, const void* x0, float xscale,
-                          float xshift, float* dw0, const void* x, float* dw, float* dbias, hipStream_t st);
+                          float xshift, float* dw0, const void* x, float* dw, float* dbias, const void* addend,
+                          hipStream_t st);
 int hopsx_wgrad_debug_times(unsigned long long* host_out, int n);
 int hopsx_conv2d_wgrad_mfma(const void* dy, const void* x, const int* geom, float* dw, float* dbias, const void* y,
                             int yact, hipStream_t st);

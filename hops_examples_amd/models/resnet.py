@@ -15,6 +15,9 @@ cost no extra kernel or HBM round trip; the classifier head is global-average-po
 """
 from __future__ import annotations
 
+import os
+
+import torch
 from torch import nn
 
 from .. import nn as hnn
@@ -26,10 +29,11 @@ class ConvBN(nn.Module):
         self.conv = hnn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False, init="he")
         self.bn = hnn.BatchNorm2d(cout, activation=act)
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, gslot=None, res_gslot=None):
         # training: the conv epilogue accumulates the BN statistics (functional.conv2d bnstats), so
-        # the BN is one apply launch instead of a statistics pass + an apply
-        return self.bn(self.conv(x, bnstats=self.bn.training), residual)
+        # the BN is one apply launch instead of a statistics pass + an apply.  gslot / res_gslot:
+        # see BasicBlock.forward
+        return self.bn(self.conv(x, bnstats=self.bn.training, gslot=gslot), residual, gslot=res_gslot)
 
 
 class BasicBlock(nn.Module):
@@ -42,6 +46,12 @@ class BasicBlock(nn.Module):
         self.short = ConvBN(cin, cout, 1, stride, act=None) if (stride != 1 or cin != cout) else None
 
     def forward(self, x):
+        if self.short is None and self.training and x.is_cuda and torch.is_grad_enabled() and \
+                "res_addend" not in os.environ.get("HOPSX_DISABLE", ""):
+            # identity shortcut: the residual's gradient (from b's BN backward, which always runs
+            # first) is handed to a's conv backward, whose dgrad epilogue adds it — no autograd add
+            slot = {}
+            return self.b(self.a(x, gslot=slot), residual=x, res_gslot=slot)
         s = x if self.short is None else self.short(x)
         return self.b(self.a(x), residual=s)
 

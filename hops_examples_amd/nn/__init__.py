@@ -90,9 +90,9 @@ class Conv2d(nn.Module):
         else:
             self.register_parameter("bias", None)
 
-    def forward(self, x, bnstats: bool = False):
+    def forward(self, x, bnstats: bool = False, gslot=None):
         return HF.conv2d(x, self.weight, self.bias, act=self.activation, in_affine=self.in_affine, bnstats=bnstats,
-                         **self.cfg)
+                         gslot=gslot, **self.cfg)
 
     def extra_repr(self):
         return f"{self.in_channels}, {self.out_channels}, k={self.kernel_size}, {self.cfg}, act={self.activation}"
@@ -180,9 +180,9 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(num_features))
         self.momentum, self.eps, self.activation = momentum, eps, activation
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, gslot=None):
         return HF.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                             self.momentum, self.eps, residual, self.activation)
+                             self.momentum, self.eps, residual, self.activation, gslot=gslot)
 
 
 class EmbeddingBag(nn.Module):

@@ -279,9 +279,14 @@ def _plain_gemm_conv(g, b, act, in_affine, prev) -> bool:
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None, pool=None, bnstats=False):
+    def forward(ctx, x, w, b, stride, padding, dilation, act, in_affine=None, prev=None, pool=None, bnstats=False,
+                gslot=None):
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
         ctx.pool = None
+        # gslot: a dict through which a later-backpropagated consumer of x (a ResNet block's identity
+        # shortcut, _BNFn) hands over its gradient of x; this dgrad adds it (in the epilogue where
+        # the kernel has one) instead of autograd launching an add
+        ctx.gslot = gslot
         if bnstats and x.dtype == BF16 and b is None and not act and in_affine is None and _bnstats_conv(g):
             # the output feeds a training BatchNorm: the conv epilogue accumulates its statistics
             # (no statistics pass over y); the BN then runs bn_fwd_apply_fin
@@ -333,7 +338,7 @@ class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return (None,) * 11
+            return (None,) * 12
         if ctx.plain:  # 1x1 conv as library GEMMs: dX = dY W, dW += dY^T X (fp32 out, bf16 in)
             x, _ = ctx.saved_tensors
             w, g = ctx.w, ctx.g
@@ -342,6 +347,9 @@ class _Conv2dFn(torch.autograd.Function):
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.mm(dy2, _arena.weight_bf16(w).view(CO, C)).view(x.shape)
+                addend = _take_addend(ctx)
+                if addend is not None:
+                    dx.add_(addend)
             gw = _wgrad_buf(w)
             if os.environ.get("HOPSX_BLASLT_WGRAD", "0") != "1":
                 # the library's fp32-out tall-skinny reductions (K = B*H*W) measured slower than the
@@ -353,7 +361,7 @@ class _Conv2dFn(torch.autograd.Function):
                         K.conv2d_wgrad(dy2.view(dy.shape), x, g, gw)
             else:
                 gw.view(CO, C).add_(torch.mm(dy2.t(), x.view(-1, C), out_dtype=torch.float32))
-            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None, None, None)
+            return (dx, _ret_grad(w, gw), None, None, None, None, None, None, None, None, None, None)
         w, b, g, act = ctx.w, ctx.b, ctx.g, ctx.act
         if ctx.pool is not None:
             x, am = ctx.saved_tensors
@@ -385,13 +393,19 @@ class _Conv2dFn(torch.autograd.Function):
             if ctx.prev is not None:
                 w0, b0, g0, act0, aff0, x0 = ctx.prev
                 pprev = (x0, g0, _arena.grad_target(w0), _arena.grad_target(b0), x, act0, aff0)
-            r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, dbias=gb, y=ymask, act=act, prev=pprev)
+            addend = ctx.gslot.get("g") if (ctx.gslot is not None and pprev is None) else None
+            r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, dbias=gb, y=ymask, act=act, prev=pprev,
+                                  addend=addend)
             if r is not False:
+                if addend is not None:
+                    ctx.gslot.pop("g", None)  # consumed by the launch
+                elif r is not None:
+                    r = _add_addend(ctx, r)
                 if ctx.prev is not None:
                     hooks.grad_ready(ctx.prev[0])
                     hooks.grad_ready(ctx.prev[1])
                 return (r, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None,
-                        None, None, None, None)
+                        None, None, None, None, None)
         side_ok = not K.conv_wgrad_uses_ticket(g, ctx.in_affine)
         if side_ok:  # wgrad || dgrad on a parallel branch (its kernels keep no shared ticket/workspace)
             with _on_side(dy.device, dy, x, ymask, flop=2.0 * dy.numel() * g[7] * g[8] * g[3]):
@@ -407,11 +421,22 @@ class _Conv2dFn(torch.autograd.Function):
             hooks.grad_ready(w0)
             hooks.grad_ready(b0)
         elif ctx.needs_input_grad[0]:
-            dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act)
+            dx = _add_addend(ctx, K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act))
         if not side_ok:
             K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
         return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None,
-                None, None, None)
+                None, None, None, None)
+
+
+def _take_addend(ctx):
+    return ctx.gslot.pop("g", None) if ctx.gslot is not None else None
+
+
+def _add_addend(ctx, dx):
+    addend = _take_addend(ctx)
+    if addend is not None and dx is not None:
+        dx.add_(addend.view(dx.shape))
+    return dx
 
 
 def conv2d_maxpool(x, w, b=None, stride=1, padding=0, dilation=1, act=None, pool_kernel=2, pool_stride=None,
@@ -456,11 +481,11 @@ def _disabled() -> str:
     return os.environ.get("HOPSX_DISABLE", "")
 
 
-def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None, bnstats=False):
+def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None, bnstats=False, gslot=None):
     """Apply the conv Function; tag the output of an input layer (input needs no gradient) so
     the next conv can fuse this layer's weight gradient into its dgrad."""
     prev = _fusable_input_layer(x, K.conv_geom(x.shape, w.shape, st, pd, dl)) if x.requires_grad else None
-    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev, pool, bnstats)
+    y = _Conv2dFn.apply(x, w, b, st, pd, dl, a, in_affine, prev, pool, bnstats, gslot)
     if pool is not None:
         return y
     if a:
@@ -470,13 +495,13 @@ def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None, bnstats=False):
     return y
 
 
-def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None, bnstats=False):
+def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None, bnstats=False, gslot=None):
     """NHWC conv. x [B,H,W,C], w [CO,KH,KW,C]. padding: int, tuple, 'valid' or 'same' (stride 1).
 
     ``bnstats=True``: the output feeds a training-mode ``batch_norm`` next (models/resnet.py ConvBN);
     where the conv kernel has the epilogue, it accumulates the BN statistics itself and tags the
     output (``_hx_bnstats``) so the BN skips its statistics pass.  The tagged output must go to
-    ``batch_norm`` before any other BN of the same width runs.
+    ``batch_norm`` before any other BN of the same width runs.  ``gslot``: see _Conv2dFn (GPU only).
 
     ``in_affine=(scale, shift)`` with a uint8 ``x``: the input layer's normalisation
     ``x * scale + shift``; on the GPU it is fused into the conv kernels when the layer
@@ -514,7 +539,8 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
         th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
         x = F.pad(to_compute(x), (0, 0, tw // 2, tw - tw // 2, th // 2, th - th // 2))
         pd = (0, 0)
-    return _conv_apply(to_compute(x), w, b, st, pd, dl, a, None, bnstats=bnstats and x.is_cuda)
+    return _conv_apply(to_compute(x), w, b, st, pd, dl, a, None, bnstats=bnstats and x.is_cuda,
+                       gslot=gslot if x.is_cuda else None)
 
 
 def _bnstats_conv(g) -> bool:
@@ -665,7 +691,7 @@ def dropout(x, p: float, training: bool = True, salt: int = 0):
 # ================================================================== batchnorm
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act, prestats=False):
+    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act, prestats=False, gslot=None):
         C = x.shape[-1]
         x2 = x.contiguous().view(-1, C)
         mean = torch.empty(C, device=x.device)
@@ -677,6 +703,7 @@ class _BNFn(torch.autograd.Function):
             y = K.bn_fwd_train(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
         ctx.save_for_backward(x2, y, mean, rstd)
         ctx.p = (gamma, beta, act, x.shape, residual is not None)
+        ctx.gslot = gslot  # the residual's gradient goes to the conv that also consumes it (_Conv2dFn)
         return y.view(x.shape)
 
     @staticmethod
@@ -689,13 +716,18 @@ class _BNFn(torch.autograd.Function):
         ws = torch.empty(2 * C, device=dy.device)
         dres = torch.empty_like(dy2) if has_res else None
         dx = K.bn_bwd(dy2, x2, y, gamma, mean, rstd, gg, gb, ws, act=act, dresidual=dres)
+        if has_res and ctx.gslot is not None:
+            ctx.gslot["g"] = dres.view(shape)
+            dres = None
         return (dx.view(shape), _ret_grad(gamma, gg), _ret_grad(beta, gb), None, None, None, None,
-                dres.view(shape) if has_res else None, None, None)
+                dres.view(shape) if dres is not None else None, None, None, None)
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentum=0.1, eps=1e-5, residual=None,
-               act=None):
-    """NHWC batch norm with fused residual add + activation: act(bn(x) + residual)."""
+               act=None, gslot=None):
+    """NHWC batch norm with fused residual add + activation: act(bn(x) + residual).  ``gslot``: hand
+    the residual's gradient to the conv that also consumes the residual (see _Conv2dFn) instead of
+    returning it to autograd."""
     a = ACT[act] if not isinstance(act, int) else act
     C = x.shape[-1]
     if not x.is_cuda:
@@ -712,7 +744,7 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentu
     x = to_compute(x)
     residual = to_compute(residual) if residual is not None else None
     if training:
-        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a, pre)
+        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a, pre, gslot)
     y = K.bn_fwd_infer(x.contiguous().view(-1, C), gamma, beta, running_mean, running_var, eps,
                        residual=None if residual is None else residual.contiguous().view(-1, C), act=a)
     return y.view(x.shape)

@@ -245,10 +245,12 @@ def conv2d_dgrad_fused_wgrad(dy, w, geom, yprev, act_prev, y, act, x0, geom0, dw
           "conv2d_dgrad_fused_wgrad")
 
 
-def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None):
+def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, addend=None):
     """A conv layer's dgrad and wgrad in ONE launch (conv_mfma.hip conv_bwd_pair_k).  ``prev`` =
     (x0, geom0, dw0, db0, yprev, act_prev, in_affine) fuses the input layer's weight gradient into the
-    dgrad (no dX).  Returns dX (None when fused), or False when the shapes are not covered."""
+    dgrad (no dX).  ``addend``: another consumer's gradient of the same input, added to dX in the
+    epilogue where the kernel has it (else added afterwards).  Returns dX (None when fused), or
+    False when the shapes are not covered."""
     B, H, W, C = geom[:4]
     if prev is None:
         dx = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
@@ -259,8 +261,15 @@ def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None):
         sc, sh = (float(aff[0]), float(aff[1])) if aff else (0.0, 0.0)
         args = (0, ptr(yprev), act_id(act_prev), ptr(db0), ptr(y), act_id(act), list(g0), ptr(x0), sc, sh, ptr(dw0))
     dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_, dw0p = args
+    if addend is not None:
+        _req(addend, BF16, "addend")
     rc = _C.ext().conv2d_bwd_pair(ptr(dy), ptr(w), list(geom), dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_, dw0p,
-                                  ptr(x), ptr(dw), ptr(dbias), stream())
+                                  ptr(x), ptr(dw), ptr(dbias), ptr(addend), stream())
+    if rc == -3:  # no epilogue addend for this shape: nothing launched; pair without it, then add
+        rc = _C.ext().conv2d_bwd_pair(ptr(dy), ptr(w), list(geom), dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_,
+                                      dw0p, ptr(x), ptr(dw), ptr(dbias), 0, stream())
+        if rc == 0 and dx is not None:
+            dx.add_(addend.view(dx.shape))
     if rc == -2:
         return False
     check(rc, "conv2d_bwd_pair")

@@ -117,3 +117,28 @@ def test_convbn_layer_grads_bnstats_matches_unfused():
             os.environ["HOPSX_DISABLE"] = old
     for a, b in zip(out[""], out["bnstats"]):
         close(a, b, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("C,H", [(16, 16), (32, 8), (64, 8)])
+def test_identity_block_residual_grad_in_dgrad_epilogue(C, H):
+    """BasicBlock with an identity shortcut: the residual's gradient handed to conv a's dgrad
+    (epilogue addend on the direct MFMA pair, a separate add on the GEMM variant) equals autograd's
+    accumulation of the two parts (HOPSX_DISABLE=res_addend)."""
+    from hops_examples_amd.models.resnet import BasicBlock
+
+    out = {}
+    for dis in ("res_addend", ""):
+        old = os.environ.get("HOPSX_DISABLE", "")
+        os.environ["HOPSX_DISABLE"] = dis
+        try:
+            torch.manual_seed(4)
+            m = BasicBlock(C, C).to(dev).train()
+            x = bf(torch.randn(32, H, H, C, device=dev)).requires_grad_(True)
+            y = m(x)
+            dy = bf(torch.randn_like(y.float()))
+            gx, = torch.autograd.grad(y, (x,), dy)
+            out[dis] = (y.float(), gx.float())
+        finally:
+            os.environ["HOPSX_DISABLE"] = old
+    for a, b in zip(out[""], out["res_addend"]):
+        close(a, b, rtol=2e-2, atol=2e-2)
