@@ -181,6 +181,7 @@ def wait_all(workers: list, timeout: float | None = None, heartbeat_timeout: flo
                     break
         time.sleep(poll_s)
     if failure is not None:
+        failure = _root_cause(workers, failure, pending)
         for w in workers:
             if w.proc.poll() is None:
                 w.proc.kill()
@@ -199,6 +200,40 @@ def wait_all(workers: list, timeout: float | None = None, heartbeat_timeout: flo
                 detail = f"\nuser function raised:\n{value}"
         raise TrialError(f"{why}; first failure in {w.log_path}{detail}\nlog tail:\n{_tail(w)}")
     return [collect(w) for w in workers]
+
+
+# errors a rank raises because a PEER died (its collective lost the connection), not the root cause
+_PEER_LOSS = ("Connection reset", "Connection closed", "Broken pipe", "gloo", "NCCL", "RCCL", "ProcessGroup",
+              "Socket Timeout", "recvBytes", "sendBytes")
+
+
+def _root_cause(workers, failure, pending, grace_s: float = 1.0):
+    """The first rank seen failing may only be reacting to a peer's death (its all-reduce lost the
+    connection).  Give the other ranks a short grace to exit, then name a rank whose own function
+    raised something other than a lost-peer error, if there is one."""
+    first, _ = failure
+    t_end = time.time() + grace_s
+    failed = [first]
+    while time.time() < t_end:
+        for i in sorted(pending):
+            rc = workers[i].proc.poll()
+            if rc is not None and (rc != 0 or not workers[i].result_path.exists()) and i not in failed:
+                failed.append(i)
+        if len(failed) == len(workers):
+            break
+        time.sleep(0.05)
+    for i in failed:
+        w = workers[i]
+        msg = ""
+        if w.result_path.exists():
+            try:
+                ok, value = cloudpickle.loads(w.result_path.read_bytes())
+                msg = "" if ok else str(value)
+            except Exception:  # noqa: BLE001 - a torn result file is no root cause either
+                msg = ""
+        if msg and not any(k in msg for k in _PEER_LOSS):
+            return (i, f"rank {i} exited with code {w.proc.poll()}") if i != first else failure
+    return failure
 
 
 def run_inline(fn, kwargs: dict, run_dir: Path, log_name="output.log"):
