@@ -273,7 +273,7 @@ def _plain_gemm_conv(g, b, act, in_affine, prev) -> bool:
     fused prologue or epilogue stays on the hand-written MFMA kernels."""
     B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw = g[:13]
     return (KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 and b is None and not act
-            and in_affine is None and prev is None and B * H * W >= 4096 and C % 8 == 0 and CO % 8 == 0
+            and in_affine is None and prev is None and B * H * W >= _PLAIN_MIN_PX and C % 8 == 0 and CO % 8 == 0
             and "blaslt_1x1" not in _disabled())
 
 
@@ -554,7 +554,12 @@ def _bnstats_conv(g) -> bool:
     return C % 8 == 0
 
 
-_BNSTATS_MAX_1X1_FLOP = float(os.environ.get("HOPSX_BNSTATS_MAX_1X1_FLOP", 1e9))
+# 1x1 routing (profiles/r2s7_plain_1x1_ab.txt): above 1e8 FLOP a 1x1 conv takes the library GEMM + a
+# BN statistics pass from 256 output pixels up (ResNet-50 B=8 +5.8 %, B=64 +1.3 % vs 1e9 / 4096; the
+# hand-written GEMM's 32x32 tiles are short of work on those long-K skinny shapes)
+_BNSTATS_MAX_1X1_FLOP = float(os.environ.get("HOPSX_BNSTATS_MAX_1X1_FLOP", 1e8))
+# fewest output pixels for which a plain 1x1 conv goes to the library GEMM (hipBLASLt)
+_PLAIN_MIN_PX = int(os.environ.get("HOPSX_PLAIN_MIN_PX", 256))
 
 
 # ==================================================================== pooling
