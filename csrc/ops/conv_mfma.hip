@@ -285,12 +285,15 @@ struct DgradArgs {
   // optional gradient of the same input from another consumer (a ResNet block's identity shortcut):
   // added before the act'(yprev) mask, replacing autograd's separate add launch
   const bf16_raw* addend;
+  // 1: XCD-aware block order (consecutive pixel groups, which share dY halo rows, on one XCD's L2)
+  int xcd;
 };
 
 // bid / nblk: this workgroup's index and the number of workgroups doing dgrad work (a paired
 // launch, conv_bwd_pair_k, hands the remaining workgroups to the weight gradient)
 template <int NF, int KS, int K0, int UN>
 __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int nblk) {
+  if (A.xcd) bid = xcd_remap(bid, nblk);
   const bf16_raw* __restrict__ dy = A.dy;
   const bf16_raw* __restrict__ w = A.w;
   bf16_raw* __restrict__ dx = A.dx;
@@ -935,7 +938,8 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   const int wvec = (uintptr_t)w % 16 == 0;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
-                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg, nullptr};
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg, nullptr,
+                     (int)hopsx_env_int("HOPSX_DGRAD_XCD", 0)};
 #define HOPSX_CMD(NF, KSV, K0V)                                                                                \
   if (un == 1) hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 1>), dim3(blocks), dim3(256), shm, st, DA); \
   else hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 2>), dim3(blocks), dim3(256), shm, st, DA)
@@ -1111,7 +1115,7 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
                      (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg,
-                     (const bf16_raw*)addend};
+                     (const bf16_raw*)addend, (int)hopsx_env_int("HOPSX_DGRAD_XCD", 0)};
   // ---- wgrad part (32-column blocks)
   const int Kw = g.KH * g.KW * g.C;
   const long nchunks = ((long)g.B * g.OH * g.OW + WG_PX - 1) / WG_PX;

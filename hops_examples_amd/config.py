@@ -29,6 +29,7 @@ Performance / communication knobs read where they act:
   HOPSX_BNSTATS_MAX_1X1_FLOP  1x1 convs above this keep the library GEMM + a BN statistics pass
                         (default 1e8); HOPSX_PLAIN_MIN_PX fewest output pixels for that library path (256)
   HOPSX_BN_COOP         1 = one-launch BN backward with a grid barrier (measured slower; off)
+  HOPSX_DGRAD_XCD       1 = XCD-aware block order in the direct MFMA dgrad (measured neutral; off)
   HOPSX_DISABLE         comma list of fast paths to turn off for A/B checks, e.g. bnstats, bn_defer,
                         ks5, bwd_pair, conv_mfma, wgrad_mfma, blaslt_1x1, direct_conv
 """
