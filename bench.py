@@ -11,7 +11,7 @@ Model   : the MirroredStrategy MNIST CNN of the reference
 Data    : synthetic uint8 28x28 images + labels resident in HBM (no dataset download possible).
 Scaling : weak — per-GPU batch fixed (reference: 32 x num_replicas_in_sync, :128-131).
 Step    : full training step inside the timed region — forward, fused loss, backward,
-          gradient exchange (world > 1), fused Adadelta update.  hipGraph replay, 8 consecutive
+          gradient exchange (world > 1), fused Adadelta update.  hipGraph replay, 32 consecutive
           steps per graph (Keras steps_per_execution: every step still trains on its own batch,
           the last kernel of each step prefetches the next one).
 World>1 : one process per GPU.  On one node the gradient exchange is the P2P xGMI path
@@ -23,7 +23,11 @@ World>1 : one process per GPU.  On one node the gradient exchange is the P2P xGM
 
 Also measures the Chicago-taxi wide&deep trainer (steps/sec) unless --no-taxi.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no rank environment the
+script launches its own N ranks (parallel/launch.py: one process per GPU, torchrun's env contract;
+refuses when fewer than N GPUs are visible unless --rehearse, which shares devices / uses the CPU
+with gloo); under torch.distributed.run it is one of the ranks.  n_gpus is the size of the process
+group the ranks actually formed, and config.ranks lists the device each rank drove.
 """
 from __future__ import annotations
 
@@ -48,21 +52,26 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-taxi", action="store_true")
     ap.add_argument("--taxi-batch", type=int, default=40)  # TFX taxi trainer batch
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow more ranks than GPUs (ranks share devices, gloo process group)")
     return ap.parse_args()
 
 
 def timed(step_fn, n, sync_dev):
     from hops_examples_amd.parallel import dist as hdist
 
+    cuda = sync_dev.type == "cuda"
     hdist.barrier()
-    torch.cuda.synchronize(sync_dev)
+    if cuda:
+        torch.cuda.synchronize(sync_dev)
     t0 = time.perf_counter()
     if hasattr(step_fn, "run_n"):
         step_fn.run_n(n)  # n steps, replayed steps_per_execution at a time
     else:
         for i in range(n):
             step_fn(i)
-    torch.cuda.synchronize(sync_dev)
+    if cuda:
+        torch.cuda.synchronize(sync_dev)
     hdist.barrier()
     el = time.perf_counter() - t0
     return hdist.all_reduce_scalar(el, "max")
@@ -70,11 +79,18 @@ def timed(step_fn, n, sync_dev):
 
 def main():
     a = parse()
+    from hops_examples_amd.parallel import launch
+
+    if a.gpus > 1 and not launch.is_rank_process():
+        # the launcher: spawns the N ranks and never touches the GPU itself
+        sys.exit(launch.launch(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:], rehearse=a.rehearse))
     from hops_examples_amd.parallel import dist as hdist
 
     rank, local_rank, world = hdist.init()
-    if world != a.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != a.gpus:
+        if rank == 0:
+            print(f"[bench] --gpus {a.gpus} but the process group has {world} ranks", file=sys.stderr)
+        sys.exit(2)
     dev = hdist.device()
     torch.manual_seed(1234 + rank)
 
@@ -119,8 +135,10 @@ def main():
     ips = B * world * a.steps / el
     replicas = None
     dp_path = dp.path if dp is not None else None
+    ranks = None
     if dp is not None:
         replicas = dp.verify_replicas()  # outside the timed region
+        ranks = launch.gather_rank_info(dev, {"p2p_world": dp.p2p_world})
         dp.close()  # collective; raises if a P2P collective failed during the run
 
     taxi = None
@@ -128,7 +146,7 @@ def main():
         try:
             from hops_examples_amd.models.widedeep import bench_taxi
 
-            taxi = bench_taxi(dev, a.taxi_batch, max(20, a.steps // 2), max(5, a.warmup // 2), timed, world,
+            taxi = None if dev.type != "cuda" else bench_taxi(dev, a.taxi_batch, max(20, a.steps // 2), max(5, a.warmup // 2), timed, world,
                               graph=not a.no_graph)
         except Exception as e:  # keep the headline metric even if the secondary one fails
             taxi = {"error": repr(e)[:300]}
@@ -145,7 +163,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic (a 60k-image uint8 28x28 epoch + labels resident in HBM, next batch prefetched "
                     "by the optimizer kernel), random-init weights",
             "config": {
@@ -154,9 +172,11 @@ def main():
                 "per_gpu_batch": B,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
-                "hipgraph": not a.no_graph,
+                "hipgraph": step.use_graph,
                 "steps_per_execution": step.steps_per_execution if step._gU is not None else 1,
                 "allreduce": dp_path,
+                "wire_bytes_per_param": None if dp is None else dp.wire_bytes_per_param,
+                "ranks": ranks,
             },
             "replicas_identical": None if replicas is None else replicas["identical"],
             "final_loss": round(loss, 4),

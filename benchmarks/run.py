@@ -1,7 +1,13 @@
 """Benchmark harness for every BASELINE.json config (+ the reference's ResNet-50 benchmark notebook).
 
-    python benchmarks/run.py <config> [--steps K] [--warmup W] [--batch B]
+    python benchmarks/run.py <config> [--gpus N] [--steps K] [--warmup W] [--batch B] [--rehearse]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 benchmarks/run.py <config>
+
+``--gpus N`` without a rank environment launches N ranks itself (parallel/launch.py; refuses when
+fewer than N GPUs are visible unless ``--rehearse``).  ``cifar_resnet`` runs through
+``experiment.collective_allreduce`` (BASELINE config 5): the workers are experiment workers
+(chief_0_output.log / worker_<i>_output.log in Experiments/<id>/) and the chief's returned
+record is the printed JSON line.
 
 configs:
   mnist_launch_cpu   MNIST 2-layer CNN through experiment.launch on CPU (plumbing; images/s)
@@ -47,11 +53,13 @@ def timed(fn, n, dev):
     return hdist.all_reduce_scalar(time.perf_counter() - t0, "max")
 
 
-def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=None):
+def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=None, box=None):
     from hops_examples_amd.parallel import ps as P
     from hops_examples_amd.runtime.step import TrainStep
 
     dp = P.make(model, opt) if world > 1 else None
+    if box is not None:
+        box["dp"] = dp
     st = TrainStep(model, opt, kind, dp=dp, graph=dev.type == "cuda", forward_fn=forward_fn)
     nb = len(xs)
     box = {}
@@ -65,15 +73,19 @@ def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=
     return el, float(box["r"]["loss"].reshape(-1)[0])
 
 
-def _emit(rank, metric, value, unit, steps, warmup, el, world, cfg, extra=None):
-    if rank != 0:
-        return
+def _record(metric, value, unit, steps, warmup, el, world, cfg, extra=None) -> dict:
     rec = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": steps,
            "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 4), "higher_is_better": True,
            "scaling": "weak", "dtype": "bf16", "data": "synthetic", "config": cfg}
     if extra:
         rec.update(extra)
-    print(json.dumps(rec), flush=True)
+    return rec
+
+
+def _emit(rank, metric, value, unit, steps, warmup, el, world, cfg, extra=None):
+    if rank != 0:
+        return
+    print(json.dumps(_record(metric, value, unit, steps, warmup, el, world, cfg, extra)), flush=True)
 
 
 def cfg_mnist_mirrored(a, dev, rank, world):
@@ -198,22 +210,72 @@ def cfg_titanic(a, dev, rank, world):
     _ = keras
 
 
-def cfg_cifar_resnet(a, dev, rank, world):
+def cifar_resnet_record(depth: int, batch: int, steps: int, warmup: int) -> dict:
+    """One rank of the CIFAR-10 ResNet benchmark (runs inside an experiment worker or a rank
+    process; the process group is initialised here).  Returns the JSON record on rank 0, {} else."""
     from hops_examples_amd import optim
     from hops_examples_amd.models.resnet import cifar_resnet
+    from hops_examples_amd.parallel import launch
     from hops_examples_amd.runtime.arena import ALIGN, ParamArena
 
-    B = a.batch or 128
-    m = cifar_resnet(a.depth).to(dev)
+    rank, _, world = hdist.init()
+    dev = hdist.device()
+    torch.manual_seed(1234 + rank)
+    B = batch or 128
+    m = cifar_resnet(depth).to(dev)
     ParamArena.from_module(m, dev, pad_multiple=max(1, world) * ALIGN)
     opt = optim.SGD(m, lr=0.1, momentum=0.9, weight_decay=1e-4)
     nb = 16
     xs = torch.randint(0, 256, (nb, B, 32, 32, 3), dtype=torch.uint8, device=dev)
     ys = torch.randint(0, 10, (nb, B), device=dev)
-    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world)
-    _emit(rank, f"images/sec CIFAR-10 ResNet-{a.depth} collective all-reduce", B * world * a.steps / el, "images/sec",
-          a.steps, a.warmup, el, world, {"model": f"ResNet-{a.depth}", "per_gpu_batch": B,
-                                          "parallelism": f"dp{world}"}, {"final_loss": round(loss, 4)})
+    box = {}
+    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, steps, warmup, dev, world, box=box)
+    dp = box.get("dp")
+    extra = {"final_loss": round(loss, 4)}
+    if dp is not None and hasattr(dp, "verify_replicas"):
+        extra["replicas_identical"] = dp.verify_replicas()["identical"]
+    ranks = launch.gather_rank_info(dev)
+    if dp is not None and hasattr(dp, "close"):
+        dp.close()
+    rec = _record(f"images/sec CIFAR-10 ResNet-{depth} collective all-reduce", B * world * steps / el, "images/sec",
+                  steps, warmup, el, world, {"model": f"ResNet-{depth}", "per_gpu_batch": B, "global_batch": B * world,
+                                             "parallelism": f"dp{world}", "launcher": "experiment.collective_allreduce",
+                                             "allreduce": getattr(dp, "path", None), "ranks": ranks},
+                  dict(extra, dtype="bf16" if dev.type == "cuda" else "fp32"))
+    hdist.shutdown()
+    return rec if rank == 0 else {}
+
+
+def cfg_cifar_resnet(a, dev, rank, world):
+    rec = cifar_resnet_record(a.depth, a.batch, a.steps, a.warmup)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
+def cifar_via_experiment(a) -> int:
+    """BASELINE config 5 as the reference names it: the training function runs under
+    ``experiment.collective_allreduce`` (one worker process per GPU, RCCL / P2P over xGMI)."""
+    from hops_examples_amd import experiment
+    from hops_examples_amd.parallel import launch
+
+    n = a.gpus
+    if launch.visible_gpus() < n and not a.rehearse:
+        print(f"[run] {n} workers requested but {launch.visible_gpus()} GPU(s) visible; refusing", file=sys.stderr)
+        return 2
+    if launch.visible_gpus() < n:
+        os.environ.setdefault("HOPSX_DIST_BACKEND", "gloo")  # rehearsal: ranks share a device / the CPU
+    depth, batch, steps, warmup = a.depth, a.batch, a.steps, a.warmup
+
+    def train():
+        sys.path.insert(0, ROOT)
+        return cifar_resnet_record(depth, batch, steps, warmup)
+
+    exp_dir, res = experiment.collective_allreduce(train, name=f"cifar_resnet{depth}_bench", num_workers=n,
+                                                   metric_key="value")
+    res = dict(res)
+    res["experiment_dir"] = exp_dir
+    print(json.dumps(res), flush=True)
+    return 0
 
 
 def cfg_resnet50(a, dev, rank, world):
@@ -246,7 +308,16 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--depth", type=int, default=20)
     ap.add_argument("--rows", type=int, default=891 * 1000)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--rehearse", action="store_true", help="allow more ranks than GPUs (shared devices, gloo)")
     a = ap.parse_args()
+    from hops_examples_amd.parallel import launch
+
+    if not launch.is_rank_process():
+        if a.config == "cifar_resnet":
+            sys.exit(cifar_via_experiment(a))
+        if a.gpus > 1:
+            sys.exit(launch.launch(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:], rehearse=a.rehearse))
     rank, _, world = hdist.init()
     dev = hdist.device()
     torch.manual_seed(1234 + rank)

@@ -9,10 +9,11 @@
 //   * two-shot: rank r reduces slice r (reduce-scatter), then gathers the other owners' reduced
 //     slices: 2(N-1)/N of the bytes per GPU instead of (N-1).
 //   * dp_step (the data-parallel training step's tail, one launch): stage + zero the gradient,
-//     reduce slice r, apply the optimizer to slice r only, publish the new fp32 weights of slice r,
-//     gather every other slice's new weights (fp32 master + bf16 shadow).  Same xGMI bytes as a
-//     two-shot all-reduce, but the optimizer touches 1/N of the parameters and there is no
-//     separate optimizer launch.  Every replica ends with the owners' bit-identical weights.
+//     reduce slice r, apply the optimizer to slice r only, publish the new weights of slice r,
+//     gather every other slice's new weights.  Default wire: fp32 gradient + bf16 weights
+//     (ZeRO-1: 6 B per parameter instead of a two-shot all-reduce's 8; opt-in bf16 gradients: 4).
+//     The optimizer touches 1/N of the parameters and there is no separate optimizer launch.
+//     Every replica ends with the owners' bit-identical compute weights.
 // Staging is double-buffered by epoch parity; a rank cannot be two epochs ahead of a reader (it
 // needs that reader's flag of the epoch in between), so reuse is safe.  The epoch is a
 // per-workgroup counter in device memory (not a kernel argument), so the launches can be captured
@@ -45,11 +46,13 @@ using u = uintptr_t;
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 128;  // <= one workgroup per CU: every block of every rank is resident
+constexpr int kMaxBlocks = 256;  // <= one workgroup per CU: every block of every rank is resident
 constexpr int kThreads = 256;
+constexpr int kParity = 3;  // staging floats per parity, in units of cap: input, reduced fp32, reduced bf16
+constexpr int kWireChunk = 64;  // weight-wire mask granularity (= the arena's parameter alignment)
 
 struct Peers {
-  float* buf[kMaxRanks];        // staging buffers, [parity][input | reduced] = 4 * cap floats each
+  float* buf[kMaxRanks];        // staging buffers, [parity][input | reduced | reduced bf16] = 6 * cap floats
   unsigned* flag[kMaxRanks];    // signal pages, [3 rows][kMaxRanks][kMaxBlocks] uint32 each
 };
 
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_ar_k(const float* __restrict
   if (poisoned(sy.err)) return;
   const int b = blockIdx.x, G = gridDim.x;
   const unsigned e = sy.epochs[b] + 1;
-  const long off = (long)(e & 1u) * 2 * cap;  // same parity layout as two-shot (modes may mix)
+  const long off = (long)(e & 1u) * kParity * cap;  // same parity layout as two-shot (modes may mix)
   // 16-B aligned chunk per workgroup
   long per = (n + G - 1) / G;
   per = (per + 3) & ~3L;
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void twoshot_ar_k(const float* __restrict
   if (poisoned(sy.err)) return;
   const int b = blockIdx.x;
   const unsigned e = sy.epochs[b] + 1;
-  const long base = (long)(e & 1u) * 2 * cap;
+  const long base = (long)(e & 1u) * kParity * cap;
   const Slices S(n, world, gridDim.x);
   long lo, hi;
   for (int sl = 0; sl < world; ++sl) {
@@ -213,8 +216,18 @@ __global__ __launch_bounds__(kThreads) void twoshot_ar_k(const float* __restrict
 }
 
 // ------------------------------------------------------------------ fused data-parallel step
+// Wire formats (what crosses xGMI per parameter and step; each GPU reads (N-1)/N of it):
+//   gradients  GB = 0: fp32 reduce-scatter (4 B)   GB = 1: bf16, accumulated in fp32 (2 B)
+//   weights, per 64-element chunk of the arena (wmask; nullptr = every chunk fp32):
+//     fp32 (4 B): every replica receives the owner's fp32 master (parameters some kernel reads
+//                 in fp32: biases, norm scales, embedding tables);
+//     bf16 (2 B): ZeRO-1 for parameters the kernels read only through the bf16 compute copy
+//                 (conv / dense weights): only the owner keeps their fp32 master current, the
+//                 replicas share the bf16 shadow bit-for-bit, and the host gathers the owners'
+//                 fp32 slices at sync points (checkpoint, verification, close).
+// Staging per rank and parity: [input: cap floats | reduced fp32: cap floats | reduced bf16: cap].
 struct DpArgs {
-  float* master;      // fp32 [n] parameters (every replica ends with identical values)
+  float* master;      // fp32 [n] parameters (owner slice always current; fp32-wire chunks everywhere)
   float* grad;        // fp32 [n] local gradient; staged and zeroed here
   float* s1;          // optimizer state (full-size buffers; only this rank's slice is kept current)
   float* s2;
@@ -226,14 +239,73 @@ struct DpArgs {
   float* step_dev;    // completed-step counter (bias correction)
   unsigned* arrive;   // arrival counter of the bookkeeping (kArriveWords, zero at rest)
   unsigned long long* rng;
+  const unsigned char* wmask;  // [ceil(n / 64)] 1 = bf16 weight wire for that chunk
   Prefetch pf;
 };
 
-template <int KIND>
-__device__ inline void owner_update(const DpArgs& a, const Peers& peers, int world, long base, float* red, long i,
-                                    const OptHP& h, float bc1, float bc2) {
+// the 4 elements at i (i % 4 == 0) share one 64-element chunk
+__device__ __forceinline__ bool wire16(const DpArgs& a, long i) { return a.wmask && a.wmask[i / kWireChunk]; }
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+__device__ __forceinline__ uint2 pack4(const float4& w) {
+  return make_uint2((uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16),
+                    (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16));
+}
+
+// 4 staged values at element index i of a staging region holding fp32 (BF = false) or bf16
+template <bool BF>
+__device__ __forceinline__ float4 ld4(const float* region, long i) {
+  if (BF) {
+    const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_raw*>(region) + i);
+    return make_float4(bf2f(v.x & 0xffffu), bf2f(v.x >> 16), bf2f(v.y & 0xffffu), bf2f(v.y >> 16));
+  }
+  return *reinterpret_cast<const float4*>(region + i);
+}
+template <bool BF>
+__device__ __forceinline__ float ld1(const float* region, long j) {
+  if (BF) return bf2f(reinterpret_cast<const bf16_raw*>(region)[j]);
+  return region[j];
+}
+template <bool BF>
+__device__ __forceinline__ void st4(float* region, long i, const float4& v) {
+  if (BF) {
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_raw*>(region) + i) = pack4(v);
+  } else {
+    *reinterpret_cast<float4*>(region + i) = v;
+  }
+}
+template <bool BF>
+__device__ __forceinline__ void st1(float* region, long j, float v) {
+  if (BF) {
+    reinterpret_cast<bf16_raw*>(region)[j] = f2bf(v);
+  } else {
+    region[j] = v;
+  }
+}
+
+// rank-ordered sum of the staged gradients (every owner sums in the same order: replicas agree)
+template <bool GB>
+__device__ __forceinline__ float4 gsum4(const Peers& peers, int world, long base, long i) {
+  float4 s = ld4<GB>(peers.buf[0] + base, i);
+  for (int p = 1; p < world; ++p) {
+    const float4 v = ld4<GB>(peers.buf[p] + base, i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  return s;
+}
+template <bool GB>
+__device__ __forceinline__ float gsum1(const Peers& peers, int world, long base, long j) {
+  float s = ld1<GB>(peers.buf[0] + base, j);
+  for (int p = 1; p < world; ++p) s += ld1<GB>(peers.buf[p] + base, j);
+  return s;
+}
+
+// red: this rank's reduced-fp32 region; red16: its reduced-bf16 region
+template <int KIND, bool GB>
+__device__ inline void owner_update(const DpArgs& a, const Peers& peers, int world, long base, float* red,
+                                    bf16_raw* red16, long i, const OptHP& h, float bc1, float bc2) {
   constexpr int NS = nstate<KIND>();
-  const float4 g = sum4(peers, world, base + i);
+  const float4 g = gsum4<GB>(peers, world, base, i);
   float4 w = *reinterpret_cast<const float4*>(a.master + i);
   float4 x = NS >= 1 ? *reinterpret_cast<const float4*>(a.s1 + i) : make_float4(0, 0, 0, 0);
   float4 y = NS >= 2 ? *reinterpret_cast<const float4*>(a.s2 + i) : make_float4(0, 0, 0, 0);
@@ -246,33 +318,41 @@ __device__ inline void owner_update(const DpArgs& a, const Peers& peers, int wor
   if (NS >= 1) *reinterpret_cast<float4*>(a.s1 + i) = x;
   if (NS >= 2) *reinterpret_cast<float4*>(a.s2 + i) = y;
   if (NS >= 3) *reinterpret_cast<float4*>(a.s3 + i) = z;
-  *reinterpret_cast<float4*>(red + i) = w;
-  const uint32_t lo = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
-  const uint32_t hi = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
-  *reinterpret_cast<uint2*>(a.shadow + i) = make_uint2(lo, hi);
+  const uint2 wb = pack4(w);
+  if (wire16(a, i)) {
+    *reinterpret_cast<uint2*>(red16 + i) = wb;
+  } else {
+    *reinterpret_cast<float4*>(red + i) = w;
+  }
+  *reinterpret_cast<uint2*>(a.shadow + i) = wb;
 }
 
-template <int KIND>
-__device__ inline void owner_update1(const DpArgs& a, const Peers& peers, int world, long base, float* red, long j,
-                                     const OptHP& h, float bc1, float bc2) {
+template <int KIND, bool GB>
+__device__ inline void owner_update1(const DpArgs& a, const Peers& peers, int world, long base, float* red,
+                                     bf16_raw* red16, long j, const OptHP& h, float bc1, float bc2) {
   constexpr int NS = nstate<KIND>();
-  const float g = sum1(peers, world, base + j);
+  const float g = gsum1<GB>(peers, world, base, j);
   float x = NS >= 1 ? a.s1[j] : 0.f, y = NS >= 2 ? a.s2[j] : 0.f, z = NS >= 3 ? a.s3[j] : 0.f;
   const float w = upd<KIND>(a.master[j], g * h.gscale, x, y, z, h, bc1, bc2);
   a.master[j] = w;
   if (NS >= 1) a.s1[j] = x;
   if (NS >= 2) a.s2[j] = y;
   if (NS >= 3) a.s3[j] = z;
-  red[j] = w;
-  a.shadow[j] = f2bf(w);
+  const bf16_raw wb = f2bf(w);
+  if (wire16(a, j)) {
+    red16[j] = wb;
+  } else {
+    red[j] = w;
+  }
+  a.shadow[j] = wb;
 }
 
-template <int KIND>
+template <int KIND, bool GB>
 __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int rank, int world, Peers peers, Sync sy) {
   if (poisoned(sy.err)) return;
   const int b = blockIdx.x;
   const unsigned e = sy.epochs[b] + 1;
-  const long base = (long)(e & 1u) * 2 * cap;
+  const long base = (long)(e & 1u) * kParity * cap;
   const Slices S(a.n, world, gridDim.x);
   const OptHP h = load_hp(a.h, a.hp_dev);
   const float t = (a.step_dev ? a.step_dev[0] : 0.f) + 1.f;  // read by every workgroup before the last bumps it
@@ -281,17 +361,17 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
   float* mine = peers.buf[rank] + base;
   long lo, hi;
 
-  // phase 0: stage this workgroup's share of every slice and zero the local gradient for the next
-  // step's atomic accumulation; the next batch's prefetch overlaps the wait for the peers
+  // phase 0: stage this workgroup's share of every slice (in the gradient wire format) and zero the
+  // local gradient for the next step's accumulation; the next batch's prefetch overlaps the wait
   for (int sl = 0; sl < world; ++sl) {
     S.sub(sl, b, lo, hi);
     for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
       if (i + 3 < hi) {
-        *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(a.grad + i);
+        st4<GB>(mine, i, *reinterpret_cast<const float4*>(a.grad + i));
         *reinterpret_cast<float4*>(a.grad + i) = make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         for (long j = i; j < hi; ++j) {
-          mine[j] = a.grad[j];
+          st1<GB>(mine, j, a.grad[j]);
           a.grad[j] = 0.f;
         }
       }
@@ -300,35 +380,43 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
   prefetch_copy(a.pf);
   if (!flag_round(peers, rank, world, 1, b, e, sy)) return;
 
-  // phase 1: reduce + update this rank's slice; publish the new weights
+  // phase 1: reduce + update this rank's slice; publish the new weights in their wire format
   float* red = mine + cap;
+  bf16_raw* red16 = reinterpret_cast<bf16_raw*>(mine + 2 * cap);
   S.sub(rank, b, lo, hi);
   for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
     if (i + 3 < hi) {
-      owner_update<KIND>(a, peers, world, base, red, i, h, bc1, bc2);
+      owner_update<KIND, GB>(a, peers, world, base, red, red16, i, h, bc1, bc2);
     } else {
-      for (long j = i; j < hi; ++j) owner_update1<KIND>(a, peers, world, base, red, j, h, bc1, bc2);
+      for (long j = i; j < hi; ++j) owner_update1<KIND, GB>(a, peers, world, base, red, red16, j, h, bc1, bc2);
     }
   }
   if (!flag_round(peers, rank, world, 2, b, e, sy)) return;
 
-  // phase 2: every other owner's new weights -> fp32 master + bf16 shadow
+  // phase 2: every other owner's new weights -> bf16 shadow (+ fp32 master on fp32-wire chunks)
   for (int k = 1; k < world; ++k) {
     const int p = (rank + k) % world;
     const float* src = peers.buf[p] + base + cap;
+    const bf16_raw* src16 = reinterpret_cast<const bf16_raw*>(peers.buf[p] + base + 2 * cap);
     S.sub(p, b, lo, hi);
     for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
       if (i + 3 < hi) {
-        const float4 w = *reinterpret_cast<const float4*>(src + i);
-        *reinterpret_cast<float4*>(a.master + i) = w;
-        const uint32_t l2 = (uint32_t)f2bf(w.x) | ((uint32_t)f2bf(w.y) << 16);
-        const uint32_t h2 = (uint32_t)f2bf(w.z) | ((uint32_t)f2bf(w.w) << 16);
-        *reinterpret_cast<uint2*>(a.shadow + i) = make_uint2(l2, h2);
+        if (wire16(a, i)) {
+          *reinterpret_cast<uint2*>(a.shadow + i) = *reinterpret_cast<const uint2*>(src16 + i);
+        } else {
+          const float4 w = *reinterpret_cast<const float4*>(src + i);
+          *reinterpret_cast<float4*>(a.master + i) = w;
+          *reinterpret_cast<uint2*>(a.shadow + i) = pack4(w);
+        }
       } else {
         for (long j = i; j < hi; ++j) {
-          const float w = src[j];
-          a.master[j] = w;
-          a.shadow[j] = f2bf(w);
+          if (wire16(a, j)) {
+            a.shadow[j] = src16[j];
+          } else {
+            const float w = src[j];
+            a.master[j] = w;
+            a.shadow[j] = f2bf(w);
+          }
         }
       }
     }
@@ -367,7 +455,9 @@ PYBIND11_MODULE(_hopsx_comm, m) {
   m.attr("MAX_RANKS") = kMaxRanks;
   m.attr("MAX_BLOCKS") = kMaxBlocks;
   m.attr("THREADS") = kThreads;
-  m.attr("FLAG_ROWS") = 3;  // row 0: one-shot, rows 1-2: the two rounds of two-shot / dp_step
+  m.attr("FLAG_ROWS") = 3;
+  m.attr("STAGING_FLOATS_PER_CAP") = 2 * kParity;  // staging buffer = this * cap floats
+  m.attr("WIRE_CHUNK") = kWireChunk;  // row 0: one-shot, rows 1-2: the two rounds of two-shot / dp_step
 
   // staging memory (coarse-grained) or an uncached signal page; zeroed; returns (ptr, ipc handle)
   m.def("alloc", [](long bytes, bool uncached) {
@@ -397,7 +487,7 @@ PYBIND11_MODULE(_hopsx_comm, m) {
   // out = sum over ranks of in (fp32, n elements, n <= cap); blocks <= MAX_BLOCKS, identical on all
   // ranks; epochs: int32[MAX_BLOCKS] device counters (zeroed once); err: int32 sticky device flag;
   // timeout: seconds a workgroup waits for a peer before it gives up (sets err, writes nothing)
-  // two_shot: reduce-scatter + all-gather variant (staging must hold 4 * cap floats)
+  // two_shot: reduce-scatter + all-gather variant (staging: STAGING_FLOATS_PER_CAP * cap floats)
   m.def("allreduce_f32", [](u in, u out, long n, long cap, int rank, int world, std::vector<u> bufs,
                             std::vector<u> flags, u epochs, u err, int blocks, u stream, bool two_shot,
                             double timeout) {
@@ -419,7 +509,7 @@ PYBIND11_MODULE(_hopsx_comm, m) {
                       u hp_dev, u step_dev, u arrive, u rng, std::vector<u> pf_src, std::vector<u> pf_dst,
                       std::vector<long> pf_bytes, u pf_cursor, int pf_nbatch, long cap, int rank, int world,
                       std::vector<u> bufs, std::vector<u> flags, u epochs, u err, int blocks, u stream,
-                      double timeout) {
+                      double timeout, bool grad_bf16, u wmask) {
     const Peers pr = make_peers(rank, world, bufs, flags);
     if (n < 0 || n > cap) throw std::runtime_error("arena exceeds the staging capacity");
     if (blocks < 1 || blocks > kMaxBlocks) throw std::runtime_error("blocks out of range");
@@ -440,6 +530,7 @@ PYBIND11_MODULE(_hopsx_comm, m) {
     a.step_dev = reinterpret_cast<float*>(step_dev);
     a.arrive = reinterpret_cast<unsigned*>(arrive);
     a.rng = reinterpret_cast<unsigned long long*>(rng);
+    a.wmask = reinterpret_cast<const unsigned char*>(wmask);
     a.pf = Prefetch{};
     const size_t nj = std::min<size_t>(2, std::min(pf_src.size(), std::min(pf_dst.size(), pf_bytes.size())));
     if (nj > 0 && pf_cursor && pf_nbatch > 0 && arrive) {
@@ -455,9 +546,13 @@ PYBIND11_MODULE(_hopsx_comm, m) {
     if ((step_dev || rng || a.pf.njobs) && !arrive) throw std::runtime_error("bookkeeping needs the arrival counter");
     const Sync sy{reinterpret_cast<unsigned*>(epochs), reinterpret_cast<int*>(err), spin_ticks(timeout)};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define DP_CASE(K)                                                                                      \
-  case K:                                                                                               \
-    hipLaunchKernelGGL(dp_step_k<K>, dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy); \
+#define DP_CASE(K)                                                                                  \
+  case K:                                                                                           \
+    if (grad_bf16) {                                                                                \
+      hipLaunchKernelGGL((dp_step_k<K, true>), dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy); \
+    } else {                                                                                        \
+      hipLaunchKernelGGL((dp_step_k<K, false>), dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy); \
+    }                                                                                               \
     break;
     switch (kind) {
       DP_CASE(0) DP_CASE(1) DP_CASE(2) DP_CASE(3) DP_CASE(4) DP_CASE(5) DP_CASE(6)

@@ -243,8 +243,14 @@ class TrainingDataset(CamelCaseAPI):
     def to_device(self, target_name: str, split: str | None = None, feature_names=None, device=None, shard=None):
         """(features fp32 [n, k], target fp32 [n]) resident in HBM.  Parquet parts stream through
         io.parquet.ParquetDeviceReader (Arrow decode -> pinned staging -> side-stream H2D -> fp32
-        conversion on the GPU); other formats go through ``read()``.  ``shard=(n, i)``: every n-th
-        row group of every part (petastorm-style sharding)."""
+        conversion on the GPU); other formats go through ``read()``.
+
+        ``shard=(n, i)``: rank i of n gets an EQUAL number of rows (data-parallel ranks must run the
+        same number of steps).  Row-group sharding (petastorm's ``shard_count`` / ``cur_shard``: every
+        n-th row group, only those are read) when every shard gets at least half the rows of the
+        largest; else — e.g. a small dataset written as ONE row group — every rank reads all rows
+        and keeps rows i, i+n, ... (the DeviceLoader rule).  Either way each shard is truncated to
+        the smallest shard's row count, computed from the Parquet metadata on every rank alike."""
         from ..io.parquet import ParquetDeviceReader
 
         targets = [target_name] if isinstance(target_name, str) else list(target_name)
@@ -254,14 +260,35 @@ class TrainingDataset(CamelCaseAPI):
         if parts is None:
             x, y = _xy(self.read(split), target_name, feature_names)
             dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-            return torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
-        readers = [ParquetDeviceReader(p, feats + targets, device=device, shard=shard) for p in parts]
-        n = sum(r.rows for r in readers)
-        out = torch.empty(n, len(feats) + len(targets), dtype=torch.float32, device=readers[0].device)
+            x, y = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+            if shard is not None:
+                n, i = shard
+                m = x.shape[0] // n
+                x, y = x[i::n][:m].contiguous(), y[i::n][:m].contiguous()
+            return x, y
+        row_sharded = False
+        if shard is not None:
+            n, i = shard
+            per = [sum(ParquetDeviceReader(p, feats + targets, device=device, shard=(n, k)).rows for p in parts)
+                   for k in range(n)]
+            if min(per) == 0 or min(per) < max(per) // 2:
+                row_sharded, rg_shard, keep = True, None, None
+            else:
+                rg_shard, keep = shard, min(per)
+        else:
+            rg_shard, keep = None, None
+        readers = [ParquetDeviceReader(p, feats + targets, device=device, shard=rg_shard) for p in parts]
+        total = sum(r.rows for r in readers)
+        out = torch.empty(total, len(feats) + len(targets), dtype=torch.float32, device=readers[0].device)
         r0 = 0
         for r in readers:
             r.read(out[r0:r0 + r.rows])
             r0 += r.rows
+        if row_sharded:
+            n, i = shard
+            out = out[i::n][:total // n]
+        elif keep is not None:
+            out = out[:keep]
         y = out[:, len(feats):]
         return out[:, :len(feats)].contiguous(), (y[:, 0].contiguous() if len(targets) == 1 else y.contiguous())
 

@@ -59,7 +59,10 @@ class ParquetDeviceReader:
             else:
                 a = a.chunk(0)
             if a.null_count:
-                a = a.fill_null(0)
+                # missing values: NaN in float columns (what td.read() gives), 0 elsewhere
+                import pyarrow as pa
+
+                a = a.fill_null(float("nan") if pa.types.is_floating(a.type) else 0)
             try:
                 v = a.to_numpy(zero_copy_only=True)
             except Exception:  # bools / dictionary columns: one conversion on the host

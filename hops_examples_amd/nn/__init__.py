@@ -44,6 +44,7 @@ class Linear(nn.Module):
             w = torch.empty(out_features, in_features)
             nn.init.kaiming_uniform_(w, a=math.sqrt(5))
         self.weight = nn.Parameter(w)
+        self.weight._hx_wire_bf16 = True  # the kernels read it only through the bf16 shadow
         if bias:
             if init == "glorot":
                 b = torch.zeros(out_features)
@@ -84,6 +85,7 @@ class Conv2d(nn.Module):
             bound = 1 / math.sqrt(fan_in)
             w = torch.empty(out_channels, kh, kw, in_channels).uniform_(-bound, bound)
         self.weight = nn.Parameter(w)
+        self.weight._hx_wire_bf16 = True  # the kernels read it only through the bf16 shadow
         if bias:
             self.bias = nn.Parameter(torch.zeros(out_channels) if init != "torch" else
                                      torch.empty(out_channels).uniform_(-1 / math.sqrt(fan_in), 1 / math.sqrt(fan_in)))

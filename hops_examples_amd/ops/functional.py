@@ -745,6 +745,9 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentu
     if pre:
         x._hx_bnstats = False  # the accumulated statistics are consumed (and re-zeroed) exactly once
         if not training:
+            # the conv epilogue already accumulated this tensor's statistics: re-zero the shared
+            # accumulator rows before raising, or every later training BN of this width folds them in
+            K.bn_acc(x.device, C).zero_()
             raise RuntimeError("conv2d(bnstats=True) output fed to an eval-mode batch_norm")
     x = to_compute(x)
     residual = to_compute(residual) if residual is not None else None

@@ -92,6 +92,7 @@ class DataParallel:
         if self.world > 1 and (oneshot.enabled() if p2p is None else p2p) and self.arena.grad.is_cuda:
             self._oneshot = oneshot.P2PComm.create(cap_bytes=self.arena.numel * 4, device=self.arena.grad.device)
         self._fused_opt = None
+        self._wmask = None
         self._polls = 0
         self.poll_every = int(os.environ.get("HOPSX_P2P_POLL_EVERY", "64"))
         if broadcast and self.world > 1:
@@ -110,6 +111,7 @@ class DataParallel:
               and isinstance(opt, FusedOptimizer) and opt.arena is self.arena
               and opt._sl == slice(0, self.arena.numel) and self.arena.shadow is not None)
         self._fused_opt = opt if ok else None
+        self._wmask = self.arena.wire_mask() if ok and self._oneshot.weight_bf16 else None
         if ok and self.overlap:
             hooks.unsubscribe(self._on_ready)  # no per-bucket all-reduce: the step tail does it all
             self.overlap = False
@@ -118,7 +120,7 @@ class DataParallel:
         return self._fused_opt is not None and opt is self._fused_opt
 
     def fused_update(self, opt) -> None:
-        self._oneshot.dp_step(opt)
+        self._oneshot.dp_step(opt, self._wmask)
 
     def owner_slices(self) -> list[slice] | None:
         """Per-rank slices whose optimizer state only the owner keeps current (fused mode), else None."""
@@ -128,14 +130,54 @@ class DataParallel:
         L = ((n + w - 1) // w + 3) & ~3
         return [slice(min(n, r * L), min(n, (r + 1) * L)) for r in range(w)]
 
+    @property
+    def master_sharded(self) -> bool:
+        """ZeRO-1 wire (bf16 weight all-gather): the fp32 master is current only on each slice's
+        owner between sync points; the bf16 compute weights are complete on every rank."""
+        return self._fused_opt is not None and self._wmask is not None
+
+    def sync_master(self) -> None:
+        """Collective: make every rank's fp32 master complete (each slice from its owner).  Call on
+        every rank before reading parameters on the host (export, evaluation on the CPU);
+        checkpoint.save, verify_replicas and close do it themselves."""
+        sl = self.owner_slices()
+        if sl is None or not self.master_sharded:
+            return
+        _gather_slices(self.arena.master, sl, self._oneshot.rank)
+
     def gather_state(self) -> None:
-        """Collective: make every rank's optimizer-state buffers complete (each slice from its owner);
-        checkpoint.save calls this on every rank before rank 0 serialises."""
+        """Collective: make every rank's optimizer-state buffers (and, on the ZeRO-1 wire, the fp32
+        master) complete, each slice from its owner; checkpoint.save calls this on every rank before
+        rank 0 serialises."""
         sl = self.owner_slices()
         if sl is None:
             return
+        self.sync_master()
         for t in self.arena.states.values():
             _gather_slices(t, sl, self._oneshot.rank)
+
+    @property
+    def p2p_world(self) -> int:
+        """Ranks the P2P communicator spans (0: RCCL / process-group path)."""
+        if getattr(self, "_closed", None) is not None:
+            return self._closed[2]
+        return 0 if self._oneshot is None else self._oneshot.world
+
+    @property
+    def wire_bytes_per_param(self) -> int | None:
+        """Bytes per parameter per step in the exchange's wire format: fused step = gradient +
+        weight formats (each GPU reads (N-1)/N of them over xGMI); all-reduce = 2 x the gradient
+        format (reduce-scatter + all-gather halves of a ring / two-shot)."""
+        if getattr(self, "_closed", None) is not None:
+            return self._closed[1]
+        if self.world <= 1:
+            return None
+        if self._fused_opt is not None:
+            f = 0.0
+            if self._wmask is not None:
+                f = min(1.0, float(self._wmask.sum().item()) * 64 / max(1, self.arena.numel))
+            return self._oneshot.wire_bytes_per_param(f)
+        return 4 if self.grad_dtype == torch.bfloat16 and self._oneshot is None else 8
 
     # -------------------------------------------------------------- health
     def poll(self) -> None:
@@ -148,17 +190,33 @@ class DataParallel:
             self._oneshot.poll()
 
     def verify_replicas(self) -> dict:
-        """Collective consistency check: the fp32 master arena must be bit-identical on every rank
-        (after the same steps).  Returns {'identical': bool, 'max_abs_diff': float}."""
+        """Collective consistency check (after the same steps on every rank): the fp32 master and the
+        bf16 compute weights must be bit-identical on every rank, and the compute weights must be
+        the bf16 rounding of the master (a torn or stale all-gather fails this even on the ZeRO-1
+        wire, where the master is first reassembled from its owners).
+        Returns {'identical': bool, 'max_abs_diff': float}."""
+        self.sync_master()
         m = self.arena.master
         ref = m.clone()
         hdist.broadcast_(ref, 0)
         d = float((m - ref).abs().max().item()) if m.numel() else 0.0
+        sh = self.arena.shadow
+        if sh is not None and sh.numel():
+            bits = sh.view(torch.int16).to(torch.int32)  # int32: every backend can broadcast it
+            ref_bits = bits.clone()
+            hdist.broadcast_(ref_bits, 0)
+            if not torch.equal(bits, ref_bits):
+                d = max(d, float((bits - ref_bits).abs().max().item()))
+            mb = m.to(torch.bfloat16)
+            if not torch.equal(sh, mb):
+                d = max(d, float((sh.float() - mb.float()).abs().max().item()) or 1e-30)
         d = hdist.all_reduce_scalar(d, "max")
         return {"identical": d == 0.0, "max_abs_diff": d}
 
     @property
     def path(self) -> str:
+        if getattr(self, "_closed", None) is not None:
+            return self._closed[0]
         if self.world <= 1:
             return "none"
         if self._fused_opt is not None:
@@ -240,9 +298,13 @@ class DataParallel:
         return 1.0 / self.world
 
     def close(self) -> None:
-        """Collective.  Raises if a P2P collective failed since the last poll."""
+        """Collective.  Leaves the fp32 master complete on every rank; raises if a P2P collective
+        failed since the last poll."""
         hooks.unsubscribe(self._on_ready)
+        if getattr(self, "_closed", None) is None:
+            self._closed = (self.path, self.wire_bytes_per_param, self.p2p_world)  # reported after teardown
         if self._oneshot is not None:
+            self.sync_master()
             try:
                 self._oneshot.check()
             finally:

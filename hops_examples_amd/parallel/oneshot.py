@@ -7,14 +7,20 @@ flags every peer, and reads the peers' buffers itself:
 * one-shot all-reduce (small messages): every rank sums all N staging buffers;
 * two-shot all-reduce (mid-size): reduce-scatter + all-gather, 2(N-1)/N of the bytes;
 * ``dp_step``: the data-parallel step tail in ONE launch — reduce-scatter of the gradient, the
-  fused optimizer on this rank's slice only, all-gather of the new fp32 weights (+ bf16 shadow),
-  grad zeroing, step/RNG bookkeeping and the next-batch prefetch.  Every replica ends with the
-  owners' bit-identical weights; optimizer moments are kept current only on the slice owner
-  (``gather_states`` reassembles them for checkpoints).
+  fused optimizer on this rank's slice only, all-gather of the new weights, grad zeroing,
+  step/RNG bookkeeping and the next-batch prefetch.  Wire formats (``HOPSX_P2P_GRAD_WIRE`` /
+  ``HOPSX_P2P_WEIGHT_WIRE``): fp32 gradients + bf16 weights by default — ZeRO-1, 6 B per parameter
+  per step instead of 8: the fp32 master and the optimizer moments of a slice are current only on
+  its owner, the replicas share the bf16 compute weights bit-for-bit, and the engine gathers the
+  owners' fp32 slices at sync points (``DataParallel.sync_master``; checkpoints, close).  bf16
+  gradients (fp32 accumulation) bring it to 4 B.
 
 Setup exchanges ``hipIpcMemHandle`` bytes through the default process group (any backend), so it
-works for RCCL and gloo groups alike, then runs a self-test (a known all-reduce checked on every
-rank).  ``P2PComm.create`` returns None when any rank fails to map a peer or the self-test
+works for RCCL and gloo groups alike, then runs a self-test on every rank: known all-reduces in
+both modes AND the fused dp_step of every optimizer kind the benches use, several rounds each (both
+staging parities written, read and reused), checked against the single-rank optimizer kernel on
+the summed gradient.  ``HOPSX_P2P_SELFTEST_FAIL=<rank>`` forces that rank's verdict to "fail"
+(fault injection: every rank must then fall back to RCCL).  ``P2PComm.create`` returns None when any rank fails to map a peer or the self-test
 disagrees — the caller then stays on RCCL.  Launches are hipGraph-capturable (device-resident
 epochs).  A peer that never arrives makes the kernels set a sticky error flag and write nothing;
 ``poll()`` (cheap, asynchronous) and ``check()`` (synchronous) raise on it.
@@ -61,19 +67,49 @@ def enabled() -> bool:
 
 
 def _timeout() -> float:
-    return float(os.environ.get("HOPSX_P2P_TIMEOUT_S", "60"))
+    """Seconds a P2P workgroup waits for a peer before it declares it lost (sticky error, every rank
+    raises).  300 s by default: a rank-local phase (rank-0 evaluation, logging, a checkpoint write)
+    must not read as a dead peer; RCCL's own watchdog is 30 min.  A job with longer rank-local
+    phases raises ``HOPSX_P2P_TIMEOUT_S`` or puts a barrier before its next step."""
+    return float(os.environ.get("HOPSX_P2P_TIMEOUT_S", "300"))
 
 
-def _default_blocks(world: int) -> int:
-    """One workgroup per CU at most (the flag protocol needs every block resident).  Ranks that share
-    one GPU (multi-rank rehearsal on a one-GPU box) split its 256 CUs."""
+def _wire() -> tuple[bool, bool]:
+    """(bf16 gradients, bf16 weights) on the fused step's wire."""
+    g = os.environ.get("HOPSX_P2P_GRAD_WIRE", "fp32").lower() in ("bf16", "bfloat16")
+    w = os.environ.get("HOPSX_P2P_WEIGHT_WIRE", "bf16").lower() in ("bf16", "bfloat16")
+    return g, w
+
+
+def _default_blocks(ranks_per_device: int) -> int:
+    """One workgroup per CU at most (the flag protocol needs every block of every rank resident):
+    256 on a GPU of its own.  Ranks that share one physical GPU (multi-rank rehearsal on a one-GPU
+    box) split its 256 CUs.  ``ranks_per_device`` comes from the ranks' PCI ids (``_colocation``),
+    not from the visible device count: the experiment launcher pins every worker to one device with
+    HIP_VISIBLE_DEVICES, so each process sees one GPU even when the 8 workers drive 8 GPUs."""
     env = os.environ.get("HOPSX_P2P_BLOCKS")
     if env:
         return int(env)
-    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 1
-    if ndev < world:  # several ranks per device
-        return max(8, min(64, 256 // (2 * world)))
-    return 128
+    if ranks_per_device > 1:
+        return max(8, min(64, 256 // (2 * ranks_per_device)))
+    return 256
+
+
+def device_id(dev) -> str:
+    """Physical identity of a device: PCI domain:bus:device (+ uuid when the runtime reports one)."""
+    p = torch.cuda.get_device_properties(dev)
+    uid = str(getattr(p, "uuid", "") or "")
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}/{uid}"
+
+
+def _colocation(dev) -> int:
+    """Collective: the largest number of ranks that drive the same physical GPU."""
+    me = device_id(dev)
+    if hdist.world_size() <= 1:
+        return 1
+    ids = [None] * hdist.world_size()
+    dist.all_gather_object(ids, me)
+    return max(ids.count(i) for i in ids)
 
 
 class OneShotAllReduce:
@@ -88,11 +124,13 @@ class OneShotAllReduce:
             raise ValueError(f"P2P collectives support <= {C.MAX_RANKS} ranks (one node)")
         self.device = device or hdist.device()
         self.cap = (int(cap_bytes) // 4 + 3) & ~3
-        self.blocks = max(1, min(int(blocks or _default_blocks(self.world)), C.MAX_BLOCKS))
+        self.ranks_per_device = _colocation(self.device) if self.device.type == "cuda" else 1
+        self.blocks = max(1, min(int(blocks or _default_blocks(self.ranks_per_device)), C.MAX_BLOCKS))
         self.timeout = float(timeout or _timeout())
+        self.grad_bf16, self.weight_bf16 = _wire()
         self._buf = self._flag = None
         self._opened: list[int] = []
-        self._buf, hb = C.alloc(4 * self.cap * 4, False)
+        self._buf, hb = C.alloc(C.STAGING_FLOATS_PER_CAP * self.cap * 4, False)
         self._flag, hf = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
         # two-shot (reduce-scatter + all-gather) above this size when N > 2: 2(N-1)/N * n of xGMI
         # reads per GPU instead of (N-1) * n
@@ -145,9 +183,10 @@ class OneShotAllReduce:
                             (mode or self.mode(t.numel())) == "two_shot", self.timeout)
         return out
 
-    def dp_step(self, opt) -> None:
+    def dp_step(self, opt, wmask: torch.Tensor | None = None) -> None:
         """Reduce-scatter the arena gradient, run ``opt``'s update on this rank's slice, all-gather the
-        new weights; one launch (see the module docstring).  ``opt`` must own the whole arena."""
+        new weights; one launch (see the module docstring).  ``opt`` must own the whole arena.
+        ``wmask`` (arena.wire_mask()): chunks whose weights travel in bf16 (ZeRO-1)."""
         from ..ops._C import OPTIM
 
         a = opt.arena
@@ -169,7 +208,14 @@ class OneShotAllReduce:
                       opt.step_count.data_ptr(), opt._arrive.data_ptr(),
                       opt.rng.data_ptr() if opt.rng is not None else 0, srcs, dsts, nbytes, cur, nb, self.cap,
                       self.rank, self.world, self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(),
-                      self.blocks, torch.cuda.current_stream(self.device).cuda_stream, self.timeout)
+                      self.blocks, torch.cuda.current_stream(self.device).cuda_stream, self.timeout,
+                      self.grad_bf16, wmask.data_ptr() if (wmask is not None and self.weight_bf16) else 0)
+
+    def wire_bytes_per_param(self, bf16_fraction: float = 1.0) -> float:
+        """Bytes per parameter per step of the fused step's wire (each GPU reads (N-1)/N of them);
+        ``bf16_fraction``: share of the parameters on the bf16 weight wire."""
+        f = bf16_fraction if self.weight_bf16 else 0.0
+        return round((2 if self.grad_bf16 else 4) + 2 * f + 4 * (1 - f), 2)
 
     # ------------------------------------------------------------ failure detection
     def check(self) -> None:
@@ -224,6 +270,85 @@ def _agree(ok: bool) -> bool:
     return hdist.all_reduce_scalar(1.0 if ok else 0.0, "min") > 0.5
 
 
+# optimizer kinds the dp_step self-test covers (everything the benches and examples train with)
+SELFTEST_KINDS = ("sgd", "adam", "adadelta", "rmsprop")
+
+
+def _dp_selftest_hp(kind: str, world: int) -> list[float]:
+    return {"sgd": [0.5, 1.0 / world, 0.0, 0.9, 0.0, 0.0], "adam": [1e-2, 1.0 / world, 0.0, 0.9, 0.999, 1e-8],
+            "adadelta": [1.0, 1.0 / world, 0.0, 0.95, 1e-7], "rmsprop": [1e-2, 1.0 / world, 0.0, 0.9, 1e-7, 0.0, 0.0]}[kind]
+
+
+def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3) -> bool:
+    """The fused dp_step on a synthetic arena, every optimizer kind, ``rounds`` steps each (both
+    staging parities, reused): this rank's owner slice of the fp32 master and the whole bf16
+    shadow must match the single-rank optimizer kernel run on the exactly-summed gradient, and
+    the shadows must agree across ranks bit-for-bit.  Gradients are small integers, exact in fp32
+    and bf16 in any summation order, so only stale or torn peer data can fail the test."""
+    from ..ops import kernels as K
+    from ..ops._C import OPTIM
+
+    C = ext()
+    dev, W, r = comm.device, comm.world, comm.rank
+    n = min(comm.cap, 8192 * W + 20)
+    n -= n % 4
+    idx = torch.arange(n, device=dev, dtype=torch.float32)
+    L = ((n + W - 1) // W + 3) & ~3
+    own = slice(min(n, r * L), min(n, (r + 1) * L))
+    st = torch.cuda.current_stream(dev).cuda_stream
+    # weight wire: every other 64-element chunk in bf16 (both formats cross every slice boundary)
+    chunks = -(-n // C.WIRE_CHUNK)
+    wmask = (torch.arange(chunks, device=dev) % 2).to(torch.uint8) if comm.weight_bf16 else None
+    f32 = torch.ones(n, dtype=torch.bool, device=dev)
+    if wmask is not None:
+        f32 = (wmask == 0).repeat_interleave(C.WIRE_CHUNK)[:n]
+    for kind in kinds:
+        k = OPTIM[kind]
+        hp = _dp_selftest_hp(kind, W)
+        hp_dev = torch.tensor((hp + [0.0] * 8)[:8], device=dev)
+        master = (idx % 13) * 0.25 - 1.5
+        ref_m = master.clone()
+        states = [torch.zeros(n, device=dev) for _ in range(3)]
+        ref_s = [torch.zeros(n, device=dev) for _ in range(3)]
+        shadow = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        ref_sh = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        step, ref_step = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+        arrive = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
+        ref_arrive = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
+        for it in range(rounds):
+            grad = ((idx * (it + 3)) % 23) - 11.0 + r
+            gsum = sum(((idx * (it + 3)) % 23) - 11.0 + q for q in range(W))
+            C.dp_step(k, master.data_ptr(), grad.data_ptr(), states[0].data_ptr(), states[1].data_ptr(),
+                      states[2].data_ptr(), shadow.data_ptr(), n, hp, hp_dev.data_ptr(), step.data_ptr(),
+                      arrive.data_ptr(), 0, [], [], [], 0, 0, comm.cap, r, W, comm.bufs, comm.flags,
+                      comm.epochs.data_ptr(), comm.err.data_ptr(), comm.blocks, st, comm.timeout,
+                      comm.grad_bf16, 0 if wmask is None else wmask.data_ptr())
+            K.optim_step(k, ref_m, gsum, ref_s[0], ref_s[1], ref_s[2], ref_sh, hp, ref_step, zero_grad=True,
+                         arrive=ref_arrive, hp_dev=hp_dev)
+            torch.cuda.synchronize(dev)
+            if int(comm.err.item()) != 0 or bool(grad.abs().max().item() != 0.0):
+                return False
+            tol = 1e-5 * (1.0 + ref_m.abs())
+            if not bool(((master[own] - ref_m[own]).abs() <= tol[own]).all().item()):
+                return False
+            if not bool(((master - ref_m).abs() <= tol)[f32].all().item()):
+                return False  # fp32-wire chunks: every rank holds the owners' fp32 master
+            # the gathered bf16 weights: each owner's rounding of its fp32 result (1 bf16 ulp slack
+            # against the reference kernel's own rounding)
+            d = (shadow.float() - ref_sh.float()).abs()
+            if not bool((d <= ref_sh.float().abs() * 2.0 ** -7 + 1e-6).all().item()):
+                return False
+            if float(step.item()) != float(it + 1):
+                return False
+        if W > 1:
+            sh = shadow.view(torch.int32).clone()  # n % 4 == 0: bf16 pairs as int32 (any backend)
+            ref = sh.clone()
+            hdist.broadcast_(ref, 0)
+            if not torch.equal(sh, ref):
+                return False
+    return True
+
+
 def self_test(comm: OneShotAllReduce, rounds: int = 3) -> bool:
     """Known all-reduces in both modes, checked exactly on this rank (integer-valued floats: every
     summation order gives the same result).  Several rounds with changing values, so both staging
@@ -240,6 +365,11 @@ def self_test(comm: OneShotAllReduce, rounds: int = 3) -> bool:
             torch.cuda.synchronize(dev)
             if int(comm.err.item()) != 0 or not torch.equal(x, want):
                 return False
+    if os.environ.get("HOPSX_P2P_SELFTEST_DP", "1") == "1" and not dp_self_test(comm, rounds=rounds):
+        return False
+    forced = os.environ.get("HOPSX_P2P_SELFTEST_FAIL")
+    if forced is not None and forced.strip() in (str(comm.rank), "all"):
+        return False  # fault injection: this rank reports a failed self-test
     return True
 
 
@@ -293,15 +423,17 @@ def _create_local(cap_bytes: int, device) -> OneShotAllReduce:
     comm.rank, comm.world = hdist.rank(), hdist.world_size()
     comm.device = device or hdist.device()
     comm.cap = (int(cap_bytes) // 4 + 3) & ~3
-    comm.blocks = max(1, min(_default_blocks(comm.world), C.MAX_BLOCKS))
+    comm.ranks_per_device = _colocation(comm.device)
+    comm.blocks = max(1, min(_default_blocks(comm.ranks_per_device), C.MAX_BLOCKS))
     comm.timeout = _timeout()
+    comm.grad_bf16, comm.weight_bf16 = _wire()
     comm.two_shot_min = int(os.environ.get("HOPSX_TWOSHOT_MIN_KB", "256")) * 1024 // 4
     comm._buf = comm._flag = None
     comm._opened = []
     err = None
     hb = hf = None
     try:
-        comm._buf, hb = C.alloc(4 * comm.cap * 4, False)
+        comm._buf, hb = C.alloc(C.STAGING_FLOATS_PER_CAP * comm.cap * 4, False)
         comm._flag, hf = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
         hb, hf = bytes(hb), bytes(hf)
     except Exception as e:  # noqa: BLE001

@@ -83,6 +83,16 @@ class ParamArena:
         else:
             self.shadow.copy_(self.master)
 
+    def wire_mask(self) -> torch.Tensor | None:
+        """uint8 [ceil(numel / 64)] per 64-element chunk: 1 where the chunk belongs to a parameter
+        the kernels read only through the bf16 shadow (``_hx_wire_bf16``: conv / dense weights).
+        The fused P2P step all-gathers those chunks in bf16 (ZeRO-1); None if there are none."""
+        m = torch.zeros(-(-self.numel // ALIGN), dtype=torch.uint8)
+        for p, o in zip(self.params, self.offsets):
+            if getattr(p, "_hx_wire_bf16", False):
+                m[o // ALIGN:-(-(o + p.numel()) // ALIGN)] = 1
+        return m.to(self.device) if bool(m.any()) else None
+
     def zero_grad(self) -> None:
         self.grad.zero_()
 

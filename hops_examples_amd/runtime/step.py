@@ -178,6 +178,7 @@ class TrainStep:
     def eager(self, x, y):
         r = self._fwd_bwd(x, y)
         self._tail(eager=True)
+        self._after_replay()  # the P2P failure flag is polled on the eager path too
         return r
 
     # ------------------------------------------------------------- graph path

@@ -200,3 +200,24 @@ def test_training_dataset_to_device_parquet(fs):
     np.testing.assert_allclose(x.numpy(), df[feats].to_numpy(np.float32))
     np.testing.assert_allclose(y.numpy(), df["weekly_sales"].to_numpy(np.float32))
     assert x.dtype == torch.float32 and x.shape == (len(df), len(feats))
+
+
+def test_training_dataset_to_device_shards_equal_rows_and_keeps_nan(fs):
+    """A small Parquet TD is one row group: sharding by row group would give rank 1 nothing (its
+    loader would run 0 steps while rank 0 runs N -> a collective hang).  to_device falls back to
+    row sharding, every shard gets the same row count, and missing floats stay NaN."""
+    df = _sales(300)
+    df.loc[df.index[:5], "weekly_sales"] = np.nan
+    s = fs.create_feature_group("sales_nan", 1, primary_key=["store", "dept", "date"])
+    s.save(df)
+    td = fs.create_training_dataset("sales_shard", version=1, data_format="parquet", label=["weekly_sales"])
+    td.save(s.select_all())
+    full = td.read()
+    shards = [td.to_device("weekly_sales", device="cpu", shard=(2, i)) for i in range(2)]
+    assert shards[0][0].shape[0] == shards[1][0].shape[0] == len(full) // 2
+    ys = np.concatenate([sh[1].numpy() for sh in shards])
+    assert np.isnan(ys).sum() == full["weekly_sales"].isna().sum() - (len(full) % 2 and
+                                                                     np.isnan(full["weekly_sales"].iloc[-1]))
+    x0, _ = shards[0]
+    feats = [c for c in full.columns if c != "weekly_sales"]
+    np.testing.assert_allclose(x0.numpy(), full[feats].to_numpy(np.float32)[0::2][:len(full) // 2])

@@ -26,7 +26,7 @@ def test_p2p_timeout_writes_nothing_and_poisons():
     n, cap = 4096, 4096
     bufs, flags = [], []
     for _ in range(2):
-        b, _h = C.alloc(4 * cap * 4, False)
+        b, _h = C.alloc(C.STAGING_FLOATS_PER_CAP * cap * 4, False)
         f, _h = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
         bufs.append(b)
         flags.append(f)
@@ -54,7 +54,7 @@ def test_p2p_timeout_writes_nothing_and_poisons():
         arrive = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
         C.dp_step(3, master.data_ptr(), grad.data_ptr(), s1.data_ptr(), s2.data_ptr(), 0, shadow.data_ptr(), n,
                   [1.0, 0.5, 0.0, 0.95, 1e-7], hp.data_ptr(), step.data_ptr(), arrive.data_ptr(), 0, [], [], [], 0, 0,
-                  cap, 0, 2, bufs, flags, epochs.data_ptr(), err.data_ptr(), 8, st, 0.05)
+                  cap, 0, 2, bufs, flags, epochs.data_ptr(), err.data_ptr(), 8, st, 0.05, False, 0)
         torch.cuda.synchronize()
         assert torch.equal(master, m0) and torch.equal(grad, g0) and float(step.item()) == 0.0
     finally:
@@ -90,3 +90,19 @@ def test_dp_fused_step_two_ranks():
     r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                        timeout=110)
     assert r.returncode == 0 and "DPFUSED" in r.stdout, r.stdout[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grad_bf16,weight_bf16", [(False, False), (False, True), (True, False), (True, True)])
+def test_dp_step_self_test_every_wire_format(grad_bf16, weight_bf16):
+    """The fused step's arithmetic in every wire format (world 1: the rank is its own peer) against
+    the single-rank optimizer kernel, every optimizer kind the self-test covers, 3 rounds each."""
+    from hops_examples_amd.parallel.oneshot import OneShotAllReduce, dp_self_test
+
+    ar = OneShotAllReduce(cap_bytes=1 << 18, device=torch.device("cuda", 0))
+    ar.grad_bf16, ar.weight_bf16 = grad_bf16, weight_bf16
+    try:
+        assert dp_self_test(ar)
+        assert ar.wire_bytes_per_param(1.0) == (2 if grad_bf16 else 4) + (2 if weight_bf16 else 4)
+    finally:
+        ar.close()

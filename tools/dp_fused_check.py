@@ -64,7 +64,9 @@ def main():
         if hasattr(ma, "salt"):
             mb.salt = ma.salt
     assert dpB.path in ("rccl", "gloo"), dpB.path
-    res = {"world": world, "path": dpA.path, "blocks": dpA._oneshot.blocks}
+    res = {"world": world, "path": dpA.path, "blocks": dpA._oneshot.blocks,
+           "ranks_per_device": dpA._oneshot.ranks_per_device, "wire_bytes_per_param": dpA.wire_bytes_per_param,
+           "master_sharded": dpA.master_sharded}
 
     # eager warm-up (2), capture + one-step replays, then one steps_per_execution replay (4 steps);
     # A then B from the same dropout-RNG state (the RNG tensor is per device, shared by both)
@@ -78,6 +80,7 @@ def main():
         for i in range(6):
             st.step_resident(xs, ys)
             if i == 0:
+                st.dp.sync_master()  # ZeRO-1 wire: reassemble the owners' fp32 slices
                 torch.cuda.synchronize()
                 first[name] = st.opt.arena.master.clone()
         st.run_resident(xs, ys, 4)
@@ -95,6 +98,7 @@ def main():
     # decisions, so trajectories drift apart chaotically — two runs of the SAME engine reach ~2.4%
     # relative drift by step 10 (tools/dbg_dpfused.py).  A wrong exchange (a missing 1/N, a stale
     # slice) is off by tens of percent from the first step.
+    dpA.sync_master()
     dA, dB = optA.arena.master, optB.arena.master
     rel = float((dA - dB).norm() / (dB - init).norm())
     res["rel_drift_vs_allreduce_10_steps"] = rel
@@ -125,8 +129,10 @@ def main():
 
     # lr change after capture reaches the replayed graph (device hyper-parameters)
     optA.param_groups[0]["lr"] = 0.0
+    dpA.sync_master()
     before = optA.arena.master.clone()
     stA.run_resident(xs, ys, 4)
+    dpA.sync_master()
     torch.cuda.synchronize()
     res["lr0_frozen"] = bool(torch.equal(before, optA.arena.master))
     assert res["lr0_frozen"]
@@ -144,6 +150,15 @@ def main():
     res["us_per_fused_step_tail_shared_gpu"] = round((time.perf_counter() - t0) / 50 * 1e6, 1)
     dpA.close()
     dpB.close()
+
+    # fault injection: one rank's self-test verdict forced to "fail" -> EVERY rank falls back
+    os.environ["HOPSX_P2P"] = "auto"
+    os.environ["HOPSX_P2P_SELFTEST_FAIL"] = str(world - 1)
+    _, _, dpC, _ = build(dev, None)
+    res["forced_selftest_fail_path"] = dpC.path
+    assert dpC.path in ("rccl", "gloo"), dpC.path
+    dpC.close()
+    del os.environ["HOPSX_P2P_SELFTEST_FAIL"]
     if rank == 0:
         res["ok"] = True
         print("DPFUSED " + json.dumps(res), flush=True)
