@@ -149,11 +149,12 @@ def cfg_taxi(a, dev, rank, world):
     from hops_examples_amd.models.widedeep import TRAIN_BATCH_SIZE, bench_taxi
 
     B = a.batch or TRAIN_BATCH_SIZE
-    r = bench_taxi(dev, B, a.steps, a.warmup, timed, world, graph=dev.type == "cuda")
+    r = bench_taxi(dev, B, a.steps, a.warmup, timed, world, graph=dev.type == "cuda", from_transform=a.from_transform)
     _emit(rank, "steps/sec Chicago-taxi wide&deep", r["steps_per_sec"], "steps/sec", a.steps, a.warmup,
           r["ms_per_step"] * a.steps / 1e3, world, {"model": f"TaxiWideDeep {r['params']} params", "per_gpu_batch": B,
                                                      "parallelism": f"dp{world}"},
-          {"examples_per_sec": r["examples_per_sec"], "final_loss": r["loss"]})
+          {"examples_per_sec": r["examples_per_sec"], "final_loss": r["loss"], "data": r["data"],
+           "transform_s": r.get("transform_s")})
 
 
 def cfg_titanic(a, dev, rank, world):
@@ -310,6 +311,8 @@ def main():
     ap.add_argument("--rows", type=int, default=891 * 1000)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--rehearse", action="store_true", help="allow more ranks than GPUs (shared devices, gloo)")
+    ap.add_argument("--from-transform", action="store_true",
+                    help="taxi: train on the TFX Transform stage's output (raw trips analyzed + transformed on the GPU)")
     a = ap.parse_args()
     from hops_examples_amd.parallel import launch
 

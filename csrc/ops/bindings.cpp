@@ -217,4 +217,20 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   m.def("gram", [](u x, u mean, int rows, int cols, u gram, u st) {
     return hopsx_gram(P<float>(x), P<float>(mean), rows, cols, P<float>(gram), S(st));
   });
+  m.def("taxi_transform", [](u raw, u vids, long n, std::vector<int> ints, std::vector<float> flts,
+                             std::vector<long> offs, u dense, u cat, u label, u st) {
+    return hopsx_taxi_transform(P<float>(raw), P<int>(vids), n, ints.data(), flts.data(), offs.data(), P<float>(dense),
+                                P<long>(cat), P<float>(label), S(st));
+  });
+  m.def("transform_max_bounds", []() { return hopsx_transform_max_bounds(); });
+  m.def("prefix_sum_f64", [](u v, long n, u pref, u work, u st) {
+    return hopsx_prefix_sum_f64(P<double>(v), n, P<double>(pref), P<double>(work), S(st));
+  });
+  m.def("range_window", [](u ts, u seg, u seg_off, u pref, long n, u lo, u hi, int W, u sum, u cnt, u st) {
+    return hopsx_range_window(P<long>(ts), P<int>(seg), P<long>(seg_off), P<double>(pref), n, P<long>(lo), P<long>(hi), W,
+                              P<double>(sum), P<int>(cnt), S(st));
+  });
+  m.def("column_stats64", [](u x, int rows, int cols, u out, u st) {
+    return hopsx_column_stats64(P<double>(x), rows, cols, P<double>(out), S(st));
+  });
 }

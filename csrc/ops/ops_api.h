@@ -161,4 +161,21 @@ int hopsx_column_stats(const float* x, int rows, int cols, float* out_stats, hip
 int hopsx_column_hist(const float* x, int rows, int cols, const float* mins, const float* maxs, int bins,
                       unsigned* hist, hipStream_t st);
 int hopsx_gram(const float* x, const float* mean, int rows, int cols, float* gram, hipStream_t st);
+
+// ---- TFX Transform apply (transform.hip) ----
+// raw fp32 [n][F] (NaN = missing), vids int32 [n][nv] host vocabulary ids; see transform.hip for the
+// ints / flts / offs layout.  -2: spec out of range
+int hopsx_taxi_transform(const float* raw, const int* vids, long n, const int* ints, const float* flts,
+                         const long* offs, float* dense, long* cat, float* label, hipStream_t st);
+int hopsx_transform_max_bounds();
+
+// ---- range-window aggregates (window.hip) ----
+// P[0..n] = exclusive fp64 prefix sum of v; work >= ceil(n / 4096) doubles
+int hopsx_prefix_sum_f64(const double* v, long n, double* P, double* work, hipStream_t st);
+// rows sorted by (partition, ts); seg[i] = partition of row i, seg_off[s..s+1) its rows; W windows
+// [ts + lo[w], ts + hi[w]] -> sum[i][w] (NaN if empty) and cnt[i][w]
+int hopsx_range_window(const long* ts, const int* seg, const long* seg_off, const double* P, long n,
+                       const long* lo, const long* hi, int W, double* sum, int* cnt, hipStream_t st);
+// fp64 column statistics for the validation rules: [cols][7] = count, sum, sumsq, min, max, #>=0, #>0
+int hopsx_column_stats64(const double* x, int rows, int cols, double* out_stats, hipStream_t st);
 }

@@ -94,6 +94,80 @@ __global__ __launch_bounds__(256) void gram_k(const float* __restrict__ x, const
   if (i < cols && j < cols) atomicAdd(gram + (long)i * cols + j, acc);
 }
 
+// fp64 variant for the data-validation rules (Deequ computes in double): per column
+// out[c*7 + {0..6}] = {count, sum, sumsq, min, max, #(v >= 0), #(v > 0)} over non-NaN values.
+// One workgroup per (64-column slab, row chunk), fp64 partials combined with fp64 atomics; min/max
+// via a CAS loop on the double's bits (caller initialises min = +inf, max = -inf).
+__device__ inline void atomic_min_d(double* a, double v) {
+  unsigned long long* p = (unsigned long long*)a;
+  unsigned long long old = *p;
+  while (v < __longlong_as_double((long long)old)) {
+    const unsigned long long prev = atomicCAS(p, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+__device__ inline void atomic_max_d(double* a, double v) {
+  unsigned long long* p = (unsigned long long*)a;
+  unsigned long long old = *p;
+  while (v > __longlong_as_double((long long)old)) {
+    const unsigned long long prev = atomicCAS(p, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
+__global__ __launch_bounds__(256) void colstats64_k(const double* __restrict__ x, int rows, int cols, int rpb,
+                                                    double* __restrict__ st) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  double n = 0, s = 0, q = 0, mn = INFINITY, mx = -INFINITY, nn = 0, np_ = 0;
+  if (c < cols)
+    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) {
+      const double v = x[(long)r * cols + c];
+      if (v != v) continue;
+      n += 1;
+      s += v;
+      q += v * v;
+      mn = fmin(mn, v);
+      mx = fmax(mx, v);
+      nn += v >= 0;
+      np_ += v > 0;
+    }
+  __shared__ double red[7][4][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  red[0][w][l] = n; red[1][w][l] = s; red[2][w][l] = q; red[3][w][l] = mn; red[4][w][l] = mx;
+  red[5][w][l] = nn; red[6][w][l] = np_;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < cols) {
+    double a[7] = {0, 0, 0, INFINITY, -INFINITY, 0, 0};
+    for (int k = 0; k < 4; ++k) {
+      a[0] += red[0][k][l]; a[1] += red[1][k][l]; a[2] += red[2][k][l];
+      a[3] = fmin(a[3], red[3][k][l]); a[4] = fmax(a[4], red[4][k][l]);
+      a[5] += red[5][k][l]; a[6] += red[6][k][l];
+    }
+    double* o = st + (long)c * 7;
+    atomicAdd(o + 0, a[0]);
+    atomicAdd(o + 1, a[1]);
+    atomicAdd(o + 2, a[2]);
+    if (a[3] != INFINITY) atomic_min_d(o + 3, a[3]);
+    if (a[4] != -INFINITY) atomic_max_d(o + 4, a[4]);
+    atomicAdd(o + 5, a[5]);
+    atomicAdd(o + 6, a[6]);
+  }
+}
+
+extern "C" int hopsx_column_stats64(const double* x, int rows, int cols, double* out_stats, hipStream_t st) {
+  const int gx = (cols + 63) / 64;
+  int gy = (rows + 2047) / 2048;
+  const int max_gy = (2048 + gx - 1) / gx;
+  if (gy > max_gy) gy = max_gy;
+  if (gy < 1) gy = 1;
+  const int rpb = (rows + gy - 1) / gy;
+  hipLaunchKernelGGL(colstats64_k, dim3(gx, gy), dim3(256), 0, st, x, rows, cols, rpb, out_stats);
+  return (int)hipGetLastError();
+}
+
 extern "C" int hopsx_column_stats(const float* x, int rows, int cols, float* out_stats, hipStream_t st) {
   const int gx = (cols + 63) / 64;
   int gy = (rows + 1023) / 1024;

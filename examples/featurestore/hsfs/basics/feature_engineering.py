@@ -1,25 +1,33 @@
 # %% [markdown]
 # # Feature engineering: retail sales feature groups
-# Mirrors notebooks/featurestore/hsfs/basics/feature_engineering.ipynb: rolling aggregates per store/dept
-# over 30/90/180/365 days, feature groups with primary/partition keys, online flag and statistics,
-# insert (append), append_features, delete.  Synthetic retail data (the reference CSV is not shipped).
+# Mirrors notebooks/featurestore/hsfs/basics/feature_engineering.ipynb: weekly sales summed over the
+# last 30/90/180/365 days per (store, dept) and per store — Spark's
+# `F.sum("weekly_sales").over(Window.partitionBy(...).orderBy(timestamp).rangeBetween(days(-N), days(-1)))`
+# (:229-249) as `featurestore.window` range sums (GPU window.hip kernel on large frames) — then feature
+# groups with primary/partition keys, online flag and statistics, insert (append), append_features,
+# delete.  Synthetic weekly retail data (the reference's sales CSV is not shipped).
 # %%
 import numpy as np
 import pandas as pd
 
 import hsfs
+from hops_examples_amd.featurestore.window import days, with_range_sums
 
 conn = hsfs.connection()
 fs = conn.get_feature_store()
 rng = np.random.default_rng(0)
-days = pd.date_range("2021-01-01", periods=400, freq="D")
-sales = pd.DataFrame([(s, d, day, rng.normal(20000, 4000)) for s in range(1, 4) for d in range(1, 4) for day in days],
+weeks = pd.date_range("2010-02-05", periods=143, freq="7D")  # the retail data's weekly dates
+sales = pd.DataFrame([(s, d, day, rng.normal(20000, 4000)) for s in range(1, 4) for d in range(1, 4) for day in weeks],
                      columns=["store", "dept", "date", "weekly_sales"])
-sales = sales.sort_values(["store", "dept", "date"])
-for w in (30, 90, 180, 365):
-    sales[f"sales_last_{w}_days"] = (sales.groupby(["store", "dept"]).weekly_sales
-                                     .transform(lambda s: s.rolling(w, min_periods=1).mean()))
+sales["timestamp"] = sales.date.astype("int64") // 10**9  # F.unix_timestamp("date")
+periods = {"month": 30, "quarter": 90, "six_month": 180, "year": 365}
+sales = with_range_sums(sales, {f"sales_last_{p}_store_dep": (days(-n), days(-1)) for p, n in periods.items()},
+                        ["store", "dept"], "timestamp", "weekly_sales")
+sales = with_range_sums(sales, {f"sales_last_{p}_store": (days(-n), days(-1)) for p, n in periods.items()},
+                        "store", "timestamp", "weekly_sales")
+sales = sales.drop(columns=["timestamp"]).fillna(0)
 sales["date"] = sales.date.dt.strftime("%Y-%m-%d")
+days = weeks
 
 # %%
 fg = fs.create_feature_group("sales_fg", version=1, description="Sales related features",

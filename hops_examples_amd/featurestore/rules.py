@@ -5,9 +5,10 @@ Validation result JSON (``validationId``, ``validationTime``, ``expectationResul
 Failure message "Value: 2022.0 does not meet the constraint requirement! HAS_MAX": :655.
 Validation types STRICT / WARNING / ALL / NONE: :686-691.
 
-Numeric aggregates (min/max/mean/sum/stddev/completeness) come from the GPU
-column-statistics kernel when the frame is large and a GPU is present
-(statistics.column_stats), otherwise from numpy.
+Numeric aggregates (count / min / max / mean / sum / stddev and the IS_NON_NEGATIVE / IS_POSITIVE
+fractions) come from ONE fp64 GPU column-statistics launch over every numeric feature the rules
+touch (stats.hip ``colstats64_k``; Deequ computes in double too) when the frame has at least
+``GPU_MIN_ROWS`` rows and a GPU is present, otherwise from numpy.  ``validate`` reports which.
 """
 from __future__ import annotations
 
@@ -193,6 +194,52 @@ def _entropy(s: pd.Series) -> float:
     return float(-(p * np.log(p)).sum()) if len(p) else 0.0
 
 
+GPU_MIN_ROWS = 100_000
+_NUMERIC_RULES = ("HAS_MIN", "HAS_MAX", "HAS_MEAN", "HAS_SUM", "HAS_STANDARD_DEVIATION", "IS_NON_NEGATIVE",
+                  "IS_POSITIVE")
+
+
+def prefill_stats(df: pd.DataFrame, feats, stats_cache: dict, device=None) -> str:
+    """Aggregates of every numeric feature in ``feats`` in one pass (GPU fp64 kernel on large frames);
+    returns the device used ('gpu' / 'cpu')."""
+    feats = [f for f in dict.fromkeys(feats) if f in df.columns and f not in stats_cache]
+    if not feats:
+        return stats_cache.get("_device", "cpu")
+    x = np.stack([_num(df[f]) for f in feats], 1) if len(df) else np.zeros((0, len(feats)))
+    use_gpu = False
+    try:
+        import torch
+
+        use_gpu = torch.cuda.is_available() and (
+            (device is not None and torch.device(device).type == "cuda") or (device is None and len(df) >= GPU_MIN_ROWS))
+    except Exception:  # pragma: no cover
+        pass
+    if use_gpu and len(df):
+        import torch
+
+        from ..ops import kernels as K
+
+        xt = torch.from_numpy(np.ascontiguousarray(x)).pin_memory().cuda(non_blocking=True)
+        st = K.column_stats64(xt).cpu().numpy()
+        dev = "gpu"
+    else:
+        valid = ~np.isnan(x)
+        xz = np.where(valid, x, 0.0)
+        st = np.stack([valid.sum(0), xz.sum(0), (xz * xz).sum(0), np.where(valid, x, np.inf).min(0, initial=np.inf),
+                       np.where(valid, x, -np.inf).max(0, initial=-np.inf), (valid & (xz >= 0)).sum(0),
+                       (valid & (xz > 0)).sum(0)], 1).astype(np.float64)
+        dev = "cpu"
+    for j, f in enumerate(feats):
+        cnt, s, sq, mn, mx, nn, npos = (float(v) for v in st[j])
+        mean = s / cnt if cnt else math.nan
+        std = math.sqrt(max(sq / cnt - mean * mean, 0.0)) if cnt else math.nan
+        stats_cache[f] = {"count": int(cnt), "n": len(df), "min": mn if cnt else math.nan,
+                          "max": mx if cnt else math.nan, "sum": s, "mean": mean, "std": std,
+                          "nonneg": nn / cnt if cnt else 1.0, "pos": npos / cnt if cnt else 1.0}
+    stats_cache["_device"] = dev
+    return dev
+
+
 def _metric(rule: Rule, df: pd.DataFrame, feat: str, stats_cache: dict):
     """The measured value for rule on feature (None for row-wise predicates)."""
     n = rule.name
@@ -201,20 +248,14 @@ def _metric(rule: Rule, df: pd.DataFrame, feat: str, stats_cache: dict):
         return float(len(df))
     if s is None:
         raise KeyError(f"feature {feat!r} not in dataframe")
-    if n in ("HAS_MIN", "HAS_MAX", "HAS_MEAN", "HAS_SUM", "HAS_STANDARD_DEVIATION", "HAS_COMPLETENESS"):
-        st = stats_cache.get(feat)
-        if st is None:
-            x = _num(s)
-            valid = ~np.isnan(x)
-            cnt = int(valid.sum())
-            xv = x[valid]
-            st = {"count": cnt, "n": len(x), "min": float(xv.min()) if cnt else math.nan,
-                  "max": float(xv.max()) if cnt else math.nan, "sum": float(xv.sum()),
-                  "mean": float(xv.mean()) if cnt else math.nan, "std": float(xv.std()) if cnt else math.nan}
-            stats_cache[feat] = st
+    if n == "HAS_COMPLETENESS":
+        return float(s.notna().sum() / max(1, len(s)))
+    if n in _NUMERIC_RULES:
+        if feat not in stats_cache:
+            prefill_stats(df, [feat], stats_cache)
+        st = stats_cache[feat]
         return {"HAS_MIN": st["min"], "HAS_MAX": st["max"], "HAS_MEAN": st["mean"], "HAS_SUM": st["sum"],
-                "HAS_STANDARD_DEVIATION": st["std"],
-                "HAS_COMPLETENESS": (s.notna().sum() / max(1, len(s)))}[n]
+                "HAS_STANDARD_DEVIATION": st["std"], "IS_NON_NEGATIVE": st["nonneg"], "IS_POSITIVE": st["pos"]}[n]
     if n == "HAS_NUMBER_OF_DISTINCT_VALUES" or n == "HAS_APPROX_COUNT_DISTINCT":
         return float(s.nunique(dropna=True))
     if n == "HAS_DISTINCTNESS":
@@ -230,12 +271,6 @@ def _metric(rule: Rule, df: pd.DataFrame, feat: str, stats_cache: dict):
     if n == "HAS_APPROX_QUANTILE":
         q = 0.5 if rule.legal_values is None else float(rule.legal_values[0])
         return float(np.nanquantile(_num(s), q))
-    if n == "IS_NON_NEGATIVE":
-        x = _num(s)
-        return float(np.mean(x[~np.isnan(x)] >= 0)) if len(x) else 1.0
-    if n == "IS_POSITIVE":
-        x = _num(s)
-        return float(np.mean(x[~np.isnan(x)] > 0)) if len(x) else 1.0
     if n == "HAS_PATTERN":
         pat = re.compile(rule.pattern or ".*")
         vals = s.dropna().astype(str)
@@ -294,6 +329,9 @@ def check(rule: Rule, value) -> bool:
 def validate(df: pd.DataFrame, expectations: list[Expectation], validation_id: int,
              commit_time=None) -> FeatureGroupValidation:
     cache: dict = {}
+    # one aggregate pass (GPU fp64 kernel on large frames) over every feature a numeric rule reads
+    prefill_stats(df, [f for e in expectations for r in e.rules if r.name in _NUMERIC_RULES for f in e.features],
+                  cache)
     results = []
     for e in expectations:
         rs = []
@@ -315,4 +353,6 @@ def validate(df: pd.DataFrame, expectations: list[Expectation], validation_id: i
                 msg = "Success" if ok else f"Value: {v} does not meet the constraint requirement! {rule.name}"
                 rs.append(ValidationResult(status, msg, str(v), f, rule))
         results.append(ExpectationResult(e, rs))
-    return FeatureGroupValidation(validation_id, int(time.time() * 1000), results, commit_time)
+    v = FeatureGroupValidation(validation_id, int(time.time() * 1000), results, commit_time)
+    v.aggregates_device = cache.get("_device", "cpu")
+    return v

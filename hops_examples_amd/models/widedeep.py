@@ -325,8 +325,11 @@ def synth_taxi(n: int, seed: int = 0, device="cpu"):
 
 
 def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, graph: bool = True,
-               pool_examples: int = 200_000) -> dict:
-    """Steps/sec of the taxi trainer (per-GPU batch ``batch``; DP all-reduce when world > 1)."""
+               pool_examples: int = 200_000, from_transform: bool = False) -> dict:
+    """Steps/sec of the taxi trainer (per-GPU batch ``batch``; DP all-reduce when world > 1).
+    ``from_transform``: the training examples come from the TFX Transform stage (tfx.transform:
+    raw synthetic trips analyzed + transformed on the device) instead of pre-transformed features;
+    the analyze/apply time is reported, not timed with the steps."""
     from ..parallel.dp import DataParallel
     from ..runtime.arena import ParamArena
     from ..runtime.step import TrainStep
@@ -336,7 +339,21 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
     opt = make_optimizer(model)
     dp = DataParallel(model) if world > 1 else None
     nb = max(8, -(-pool_examples // batch))
-    dense, cat, label = synth_taxi(nb * batch, seed=7, device=dev)
+    transform_s = None
+    if from_transform:
+        import time as _time
+
+        from ..tfx import analyze, synth_raw_trips
+
+        raw = synth_raw_trips(nb * batch, seed=7)
+        t0 = _time.perf_counter()
+        tf = analyze(raw, device=dev)
+        dense, cat, label = tf.apply(raw, device=dev)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        transform_s = round(_time.perf_counter() - t0, 3)
+    else:
+        dense, cat, label = synth_taxi(nb * batch, seed=7, device=dev)
     cat = cat.view(nb, batch, -1)
     label = label.view(nb, batch, 1)
     out = {}
@@ -371,4 +388,6 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
     loss = float(out["r"]["loss"].reshape(-1)[0])
     return {"steps_per_sec": round(steps / el, 1), "examples_per_sec": round(batch * world * steps / el, 1),
             "ms_per_step": round(el / steps * 1e3, 4), "batch_per_gpu": batch, "loss": round(loss, 4),
-            "params": sum(p.numel() for p in model.parameters()), "hidden_units": hidden_units(), "step": path}
+            "params": sum(p.numel() for p in model.parameters()), "hidden_units": hidden_units(), "step": path,
+            "data": "tfx-transform" if from_transform else "synthetic-transformed",
+            **({"transform_s": transform_s} if transform_s is not None else {})}

@@ -559,6 +559,42 @@ def embedding_bag_bwd(dout, idx, offsets, mode, dtable, nbags, ldo=None, bag_len
     return dtable
 
 
+# --------------------------------------------------------- TFX transform (transform.hip)
+def taxi_transform(raw, vids, ints, flts, offs, nd, nc, with_label=True):
+    """Apply an analyzed Chicago-taxi transform to raw fp32 rows [n, F] on the GPU (one launch):
+    returns (dense fp32 [n, nd], cat int64 [n, nc] global wide ids, label fp32 [n, 1] | None)."""
+    n = raw.shape[0]
+    dense = torch.empty(n, nd, device=raw.device, dtype=F32)
+    cat = torch.empty(n, nc, device=raw.device, dtype=torch.int64)
+    label = torch.empty(n, 1, device=raw.device, dtype=F32) if with_label else None
+    check(_C.ext().taxi_transform(ptr(raw), ptr(vids), n, [int(v) for v in ints], [float(v) for v in flts],
+                                  [int(v) for v in offs], ptr(dense), ptr(cat), ptr(label), stream()),
+          "taxi_transform")
+    return dense, cat, label
+
+
+# --------------------------------------------------------- range windows (window.hip)
+def prefix_sum_f64(v):
+    """Exclusive fp64 prefix sum P[0..n] of a 1-D fp64 tensor (P[n] = total)."""
+    n = v.numel()
+    P = torch.empty(n + 1, device=v.device, dtype=torch.float64)
+    work = torch.empty(max(1, -(-n // 4096)), device=v.device, dtype=torch.float64)
+    check(_C.ext().prefix_sum_f64(ptr(v), n, ptr(P), ptr(work), stream()), "prefix_sum_f64")
+    return P
+
+
+def range_window(ts, seg, seg_off, v, lo, hi, want_count=False):
+    """Range-window sums (Spark rangeBetween) of rows sorted by (partition, ts): returns fp64 [n, W]
+    (NaN where the range is empty) and, with ``want_count``, int32 [n, W] row counts."""
+    n, W = ts.numel(), lo.numel()
+    P = prefix_sum_f64(v)
+    out = torch.empty(n, W, device=ts.device, dtype=torch.float64)
+    cnt = torch.empty(n, W, device=ts.device, dtype=torch.int32) if want_count else None
+    check(_C.ext().range_window(ptr(ts), ptr(seg), ptr(seg_off), ptr(P), n, ptr(lo), ptr(hi), W, ptr(out), ptr(cnt),
+                                stream()), "range_window")
+    return (out, cnt) if want_count else out
+
+
 # --------------------------------------------------------- column statistics
 def column_stats(x):
     """x [rows, cols] f32 on GPU -> [cols, 5] = count, sum, sumsq, min, max (NaN = missing)."""
@@ -567,6 +603,16 @@ def column_stats(x):
     out[:, 3] = float("inf")
     out[:, 4] = float("-inf")
     check(_C.ext().column_stats(ptr(x), rows, cols, ptr(out), stream()), "column_stats")
+    return out
+
+
+def column_stats64(x):
+    """x [rows, cols] f64 on GPU -> [cols, 7] f64 = count, sum, sumsq, min, max, #(>= 0), #(> 0)."""
+    rows, cols = x.shape
+    out = torch.zeros(cols, 7, device=x.device, dtype=torch.float64)
+    out[:, 3] = float("inf")
+    out[:, 4] = float("-inf")
+    check(_C.ext().column_stats64(ptr(x), rows, cols, ptr(out), stream()), "column_stats64")
     return out
 
 
