@@ -120,6 +120,103 @@ static py::bytes encode_example(py::dict feats) {
   return py::bytes(ex);
 }
 
+// Columnar TFRecord writer: one tf.train.Example per row from whole columns (the training-dataset
+// writer's hot loop).  columns = [(name, kind, data)]: kind 'float' / 'int64' with a 1-D numpy array
+// of n values, or 'bytes' with a list of n bytes/str.  Rows are encoded + framed by `nthreads`
+// threads into per-thread buffers (contiguous row ranges) and written in row order.
+static long write_tfrecord_columnar(const std::string& path, py::list columns, long n, int nthreads) {
+  struct Col {
+    std::string key;  // pre-encoded "name" field of the feature-map entry
+    int kind;         // 0 float, 1 int64, 2 bytes
+    const float* f = nullptr;
+    const int64_t* i = nullptr;
+    std::vector<std::string> b;
+  };
+  std::vector<Col> cols;
+  std::vector<py::object> keep;  // keep the numpy buffers alive
+  for (auto c : columns) {
+    py::tuple t = py::reinterpret_borrow<py::tuple>(c);
+    Col col;
+    const std::string name = py::str(t[0]);
+    put_len(col.key, 1, name);
+    const std::string kind = py::str(t[1]);
+    if (kind == "float") {
+      auto a = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(t[2]);
+      if (!a || a.size() != n) throw std::runtime_error("float column " + name + " must have n values");
+      col.kind = 0;
+      col.f = a.data();
+      keep.push_back(a);
+    } else if (kind == "int64") {
+      auto a = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(t[2]);
+      if (!a || a.size() != n) throw std::runtime_error("int64 column " + name + " must have n values");
+      col.kind = 1;
+      col.i = a.data();
+      keep.push_back(a);
+    } else if (kind == "bytes") {
+      col.kind = 2;
+      py::list l = py::reinterpret_borrow<py::list>(t[2]);
+      if ((long)l.size() != n) throw std::runtime_error("bytes column " + name + " must have n values");
+      col.b.reserve(n);
+      for (auto v : l) col.b.push_back(py::isinstance<py::bytes>(v) ? v.cast<std::string>() : py::str(v).cast<std::string>());
+    } else {
+      throw std::runtime_error("column kind must be float/int64/bytes");
+    }
+    cols.push_back(std::move(col));
+  }
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot open " + path);
+  const int T = std::max(1, std::min(nthreads, (int)std::max(1L, n / 1024)));
+  std::vector<std::string> out(T);
+  {
+    py::gil_scoped_release nogil;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) {
+      th.emplace_back([&, t] {
+        const long lo = n * t / T, hi = n * (t + 1) / T;
+        std::string& o = out[t];
+        std::string features, entry, feature, list, packed, ex;
+        for (long r = lo; r < hi; ++r) {
+          features.clear();
+          for (const Col& c : cols) {
+            list.clear();
+            feature.clear();
+            if (c.kind == 0) {
+              packed.assign((const char*)(c.f + r), 4);
+              put_len(list, 1, packed);
+              put_len(feature, 2, list);
+            } else if (c.kind == 1) {
+              packed.clear();
+              put_varint(packed, (uint64_t)c.i[r]);
+              put_len(list, 1, packed);
+              put_len(feature, 3, list);
+            } else {
+              put_len(list, 1, c.b[r]);
+              put_len(feature, 1, list);
+            }
+            entry = c.key;
+            put_len(entry, 2, feature);
+            put_len(features, 1, entry);
+          }
+          ex.clear();
+          put_len(ex, 1, features);
+          o += hopsx_io::frame_record((const uint8_t*)ex.data(), ex.size());
+        }
+      });
+    }
+    for (auto& x : th) x.join();
+  }
+  long bytes = 0;
+  for (auto& o : out) {
+    if (fwrite(o.data(), 1, o.size(), f) != o.size()) {
+      fclose(f);
+      throw std::runtime_error("TFRecord write failed");
+    }
+    bytes += (long)o.size();
+  }
+  fclose(f);
+  return bytes;
+}
+
 static py::dict decode_example(py::bytes rec) {
   std::string s = rec;
   auto m = parse_example((const uint8_t*)s.data(), (const uint8_t*)s.data() + s.size());
@@ -267,6 +364,8 @@ PYBIND11_MODULE(_hopsx_io, m) {
       .def("__exit__", [](TFRecordWriter& w, py::args) { w.close(); });
   m.def("read_tfrecords", &read_tfrecords, py::arg("path"), py::arg("verify") = true);
   m.def("encode_example", &encode_example);
+  m.def("write_tfrecord_columnar", &write_tfrecord_columnar, py::arg("path"), py::arg("columns"), py::arg("n"),
+        py::arg("nthreads") = 8);
   m.def("decode_example", &decode_example);
   m.def("decode_examples_columnar", &decode_examples_columnar, py::arg("records"), py::arg("schema"),
         py::arg("nthreads") = 8);

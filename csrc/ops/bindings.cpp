@@ -233,4 +233,9 @@ PYBIND11_MODULE(_hopsx_ops, m) {
   m.def("column_stats64", [](u x, int rows, int cols, u out, u st) {
     return hopsx_column_stats64(P<double>(x), rows, cols, P<double>(out), S(st));
   });
+  m.def("u8_normalize_chan", [](u x, u y, long pixels, int C, std::vector<float> scale, std::vector<float> shift,
+                                int rev, u st) {
+    if ((int)scale.size() < C || (int)shift.size() < C) return -2;
+    return hopsx_u8_normalize_chan(P<unsigned char>(x), P<void>(y), pixels, C, scale.data(), shift.data(), rev, S(st));
+  });
 }

@@ -52,6 +52,21 @@ __global__ void u8_norm_k(const unsigned char* __restrict__ x, bf16_raw* __restr
     y[i] = f2bf(x[i] * scale + shift);
 }
 
+// Per-channel image normalisation of uint8 NHWC pixels (C <= 4) -> bf16, optionally reversing the
+// channel order (RGB -> BGR for caffe-style models): y[p][c] = x[p][rev ? C-1-c : c] * scale[c] + shift[c].
+// One launch replaces the torch addcmul + bf16 cast pair (two at::native kernels) on the input path.
+struct ChanAffine {
+  float scale[4], shift[4];
+};
+__global__ void u8_norm_chan_k(const unsigned char* __restrict__ x, bf16_raw* __restrict__ y, long pixels, int C,
+                               ChanAffine a, int rev) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < pixels; p += (long)gridDim.x * blockDim.x) {
+    const unsigned char* px = x + p * C;
+    bf16_raw* py = y + p * C;
+    for (int c = 0; c < C; ++c) py[c] = f2bf(px[rev ? C - 1 - c : c] * a.scale[c] + a.shift[c]);
+  }
+}
+
 // out[n] += sum_m x[m][n]; one workgroup owns a column strip, rows split over gridDim.y
 __global__ __launch_bounds__(256) void colsum_k(const bf16_raw* __restrict__ x, float* __restrict__ out, int M,
                                                 int N, int rows_per_block) {
@@ -127,6 +142,20 @@ extern "C" int hopsx_cast_f32_bf16(const float* x, void* y, long n, hipStream_t 
 }
 extern "C" int hopsx_cast_bf16_f32(const void* x, float* y, long n, hipStream_t st) {
   hipLaunchKernelGGL(cast_bf16_f32_k, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_raw*)x, y, n);
+  return (int)hipGetLastError();
+}
+extern "C" int hopsx_u8_normalize_chan(const unsigned char* x, void* y, long pixels, int C, const float* scale,
+                                       const float* shift, int rev, hipStream_t st) {
+  if (C < 1 || C > 4 || pixels < 0) return -2;
+  ChanAffine a{};
+  for (int c = 0; c < C; ++c) {
+    a.scale[c] = scale[c];
+    a.shift[c] = shift[c];
+  }
+  long g = (pixels + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(u8_norm_chan_k, dim3((unsigned)g), dim3(256), 0, st, x, (bf16_raw*)y, pixels, C, a, rev);
   return (int)hipGetLastError();
 }
 extern "C" int hopsx_u8_normalize(const unsigned char* x, void* y, long n, float scale, float shift, hipStream_t st) {

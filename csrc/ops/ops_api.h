@@ -178,4 +178,7 @@ int hopsx_range_window(const long* ts, const int* seg, const long* seg_off, cons
                        const long* lo, const long* hi, int W, double* sum, int* cnt, hipStream_t st);
 // fp64 column statistics for the validation rules: [cols][7] = count, sum, sumsq, min, max, #>=0, #>0
 int hopsx_column_stats64(const double* x, int rows, int cols, double* out_stats, hipStream_t st);
+// per-channel uint8 NHWC -> bf16 image normalisation (C <= 4, optional channel reversal)
+int hopsx_u8_normalize_chan(const unsigned char* x, void* y, long pixels, int C, const float* scale,
+                            const float* shift, int rev, hipStream_t st);
 }

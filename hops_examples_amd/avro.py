@@ -151,3 +151,114 @@ def encode(schema, record) -> bytes:
 
 def decode(schema, data: bytes):
     return _dec(_schema(schema), io.BytesIO(data))
+
+
+# ------------------------------------------------------------------ object container files
+# Avro 1.x Object Container File: magic "Obj\x01", file metadata map {avro.schema, avro.codec},
+# a 16-byte sync marker, then blocks of (record count, byte size, records, sync).  Used by the
+# "avro" training-dataset format (notebooks/featurestore/hsfs/basics/training_datasets.ipynb:125-340).
+_MAGIC = b"Obj\x01"
+
+
+def _write_bytes(out, b: bytes):
+    _write_long(out, len(b))
+    out.write(b)
+
+
+def _read_bytes(inp) -> bytes:
+    return inp.read(_read_long(inp))
+
+
+def schema_of_frame(df, name: str = "record") -> dict:
+    """A record schema for a pandas frame: every field nullable (["null", type])."""
+    fields = []
+    for c in df.columns:
+        k = df[c].dtype.kind
+        t = "boolean" if k == "b" else ("long" if k in "iu" else ("double" if k == "f" else "string"))
+        fields.append({"name": str(c), "type": ["null", t]})
+    safe = "".join(ch if ch.isalnum() or ch == "_" else "_" for ch in str(name)) or "record"
+    return {"type": "record", "name": safe, "fields": fields}
+
+
+def _py(v):
+    """numpy scalars -> Python values the encoder matches (NaT / None -> null)."""
+    if v is None:
+        return None
+    if hasattr(v, "item"):
+        v = v.item()
+    if isinstance(v, float) and v != v:
+        return v  # NaN is a valid double
+    return v
+
+
+def write_container(path, schema, records, block_records: int = 4096, sync: bytes | None = None) -> int:
+    """Write ``records`` (dicts) as an Avro object container file; returns the record count."""
+    import os
+
+    sch = _schema(schema)
+    sync = sync or os.urandom(16)
+    kinds = {f["name"]: f["type"] for f in sch["fields"]}
+    n = 0
+    with open(path, "wb") as f:
+        f.write(_MAGIC)
+        meta = {"avro.schema": json.dumps(sch).encode(), "avro.codec": b"null"}
+        _write_long(f, len(meta))
+        for k, v in meta.items():
+            _write_bytes(f, k.encode())
+            _write_bytes(f, v)
+        _write_long(f, 0)
+        f.write(sync)
+        block, cnt = io.BytesIO(), 0
+        for rec in records:
+            r = {k: _py(rec.get(k)) for k in kinds}
+            for k, t in kinds.items():  # ints stored in a double column, strings for object values
+                if isinstance(t, list) and "string" in t and r[k] is not None and not isinstance(r[k], str):
+                    r[k] = str(r[k])
+            _enc(sch, r, block)
+            cnt += 1
+            if cnt == block_records:
+                _write_long(f, cnt)
+                _write_bytes(f, block.getvalue())
+                f.write(sync)
+                n += cnt
+                block, cnt = io.BytesIO(), 0
+        if cnt:
+            _write_long(f, cnt)
+            _write_bytes(f, block.getvalue())
+            f.write(sync)
+            n += cnt
+    return n
+
+
+def read_container(path):
+    """(schema, [records]) of an Avro object container file (null codec)."""
+    with open(path, "rb") as f:
+        buf = f.read()
+    inp = io.BytesIO(buf)
+    if inp.read(4) != _MAGIC:
+        raise ValueError(f"{path}: not an Avro object container file")
+    meta = {}
+    while True:
+        cnt = _read_long(inp)
+        if cnt == 0:
+            break
+        if cnt < 0:
+            _read_long(inp)
+            cnt = -cnt
+        for _ in range(cnt):
+            k = _read_bytes(inp).decode()
+            meta[k] = _read_bytes(inp)
+    if meta.get("avro.codec", b"null") not in (b"null", b""):
+        raise ValueError(f"{path}: codec {meta['avro.codec']!r} not supported")
+    sch = json.loads(meta["avro.schema"])
+    sync = inp.read(16)
+    out = []
+    while inp.tell() < len(buf):
+        cnt = _read_long(inp)
+        size = _read_long(inp)
+        blk = io.BytesIO(inp.read(size))
+        for _ in range(cnt):
+            out.append(_dec(sch, blk))
+        if inp.read(16) != sync:
+            raise ValueError(f"{path}: sync marker mismatch")
+    return sch, out

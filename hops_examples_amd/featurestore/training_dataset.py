@@ -6,8 +6,10 @@ batch_size=32)`` -> ((32, 14), (32,)) float32 batches :429-447), coalesce
 (hsfs/training/training-data-coalesced.ipynb:58-64), online serving vectors
 (hsfs/serving/feature_vector_model_serving.ipynb:151-254).
 
-Formats: csv, tsv, parquet, tfrecord (tf.train.Example via the C++ codec),
-npy, orc/avro/hdf5/petastorm are stored as Parquet.  Model input: ``tf_data``
+Formats: csv, tsv, parquet, tfrecord (tf.train.Example rows encoded by the C++ IO library from
+whole columns), npy, orc (pyarrow.orc), avro (object container files, avro.py), petastorm (Parquet
++ the inferred Unischema in ``_common_metadata``, readable by the petastorm readers); hdf5 needs
+h5py, which this image lacks, and is refused at creation rather than silently written as Parquet.  Model input: ``tf_data``
 yields numpy batches with the TF API's shapes; ``torch_data`` streams batches
 into HBM through pinned host buffers on a side stream (DeviceLoader).
 """
@@ -50,6 +52,12 @@ class TrainingDataset(CamelCaseAPI):
         fmt = (data_format or "tfrecords").lower()
         if fmt not in FORMATS:
             raise ValueError(f"unsupported data format {data_format}")
+        if fmt == "hdf5":
+            try:
+                import h5py  # noqa: F401
+            except ImportError as e:
+                raise ValueError("hdf5 training datasets need h5py, which is not installed") from e
+            raise ValueError("hdf5 training datasets are not supported by this feature store")
         self.data_format = "tfrecord" if fmt == "tfrecords" else fmt
         self.coalesce = coalesce
         self.storage_connector = storage_connector
@@ -118,6 +126,8 @@ class TrainingDataset(CamelCaseAPI):
         parts = self._split(df)
         for split, part in parts.items():
             self._write_split(part.reset_index(drop=True), split)
+        if self.data_format == "petastorm":
+            self._write_unischema(df)
         if self.statistics_config.enabled:
             try:
                 (self._location / "statistics.json").write_text(
@@ -157,23 +167,50 @@ class TrainingDataset(CamelCaseAPI):
             if fmt in ("csv", "tsv"):
                 part.to_csv(f"{base}.{fmt}", index=False, sep="," if fmt == "csv" else "\t")
             elif fmt == "tfrecord":
-                with hio.TFRecordWriter(f"{base}.tfrecord") as w:
-                    cols = list(part.columns)
-                    kinds = []
-                    for c in cols:
-                        k = part[c].dtype.kind
-                        kinds.append("int64" if k in "iub" else ("float" if k == "f" else "bytes"))
-                    arrs = [part[c].to_numpy() for c in cols]
-                    for r in range(len(part)):
-                        feats = {}
-                        for c, kind, a in zip(cols, kinds, arrs):
-                            v = a[r]
-                            feats[c] = (kind, [str(v).encode()] if kind == "bytes" else np.asarray([v]))
-                        w.write(hio.encode_example(feats))
+                # whole columns to the native writer: rows encoded + framed by C++ threads
+                cols = []
+                for c in part.columns:
+                    k = part[c].dtype.kind
+                    if k in "iub":
+                        cols.append((c, "int64", part[c].to_numpy(np.int64)))
+                    elif k == "f":
+                        cols.append((c, "float", part[c].to_numpy(np.float32)))
+                    else:
+                        cols.append((c, "bytes", [str(v).encode() for v in part[c].tolist()]))
+                hio.write_tfrecord_columns(f"{base}.tfrecord", cols, len(part))
             elif fmt == "npy":
                 np.save(f"{base}.npy", part.to_records(index=False), allow_pickle=False)
-            else:  # parquet / orc / avro / hdf5 / petastorm -> parquet files
+            elif fmt == "orc":
+                import pyarrow as pa
+                import pyarrow.orc as paorc
+
+                paorc.write_table(pa.Table.from_pandas(part, preserve_index=False), f"{base}.orc")
+            elif fmt == "avro":
+                from .. import avro
+
+                avro.write_container(f"{base}.avro", avro.schema_of_frame(part, self.name),
+                                     part.to_dict(orient="records"))
+            elif fmt in ("parquet", "petastorm"):
+                # petastorm datasets ARE Parquet (+ the Unischema in _common_metadata, written in save())
                 part.to_parquet(f"{base}.parquet", index=False)
+            else:
+                raise ValueError(f"training dataset format {fmt!r} is not supported here")
+
+    def _write_unischema(self, df: pd.DataFrame) -> None:
+        """petastorm metadata: a Unischema of scalar fields (dtype from the frame) in every split's
+        ``_common_metadata``, so ``petastorm.make_reader(td.location)`` can open the dataset."""
+        from ..petastorm.codecs import ScalarCodec
+        from ..petastorm.etl.dataset_metadata import META
+        from ..petastorm.unischema import Unischema, UnischemaField
+
+        fields = []
+        for c in df.columns:
+            k = df[c].dtype.kind
+            dt = (np.int64 if k in "iu" else np.float64 if k == "f" else np.bool_ if k == "b" else np.str_)
+            fields.append(UnischemaField(str(c), dt, (), ScalarCodec(), bool(df[c].isna().any())))
+        js = json.dumps({"unischema": Unischema(self.name, fields).to_json(), "row_group_size_mb": None})
+        for split in (self.splits or {"": None}):
+            (self._split_dir(split) / META).write_text(js)
 
     # --------------------------------------------------------------- read
     def _files(self, split: str | None):
@@ -196,6 +233,14 @@ class TrainingDataset(CamelCaseAPI):
                 frames.append(pd.DataFrame(np.load(p, allow_pickle=False)))
             elif p.suffix == ".tfrecord":
                 frames.append(self._read_tfrecord(p))
+            elif p.suffix == ".orc":
+                import pyarrow.orc as paorc
+
+                frames.append(paorc.read_table(str(p)).to_pandas())
+            elif p.suffix == ".avro":
+                from .. import avro
+
+                frames.append(pd.DataFrame(avro.read_container(str(p))[1]))
         if not frames:
             return pd.DataFrame(columns=cols)
         return pd.concat(frames, ignore_index=True)

@@ -88,10 +88,10 @@ class CifarResNet(nn.Module):
         self.pool = hnn.GlobalAvgPool2d()
         self.fc = hnn.Linear(cin, num_classes, init="torch", out_f32=True)
         self.depth = depth
-        _norm_buffers(self)
+        _norm_buffers(self, "cifar")
 
     def forward(self, x):
-        x = _as_nhwc_image(x, self.img_shift, self.img_scale)
+        x = _as_nhwc_image(x, self)
         return self.fc(self.pool(self.blocks(self.stem(x))))
 
 
@@ -108,35 +108,49 @@ class ResNet50(nn.Module):
         self.blocks = nn.Sequential(*blocks)
         self.pool = hnn.GlobalAvgPool2d()
         self.fc = hnn.Linear(cin, num_classes, init="torch", out_f32=True)
-        _norm_buffers(self)
+        _norm_buffers(self, "caffe")
 
     def forward(self, x):
-        x = _as_nhwc_image(x, self.img_shift, self.img_scale)
+        x = _as_nhwc_image(x, self)
         return self.fc(self.pool(self.blocks(self.maxpool(self.stem(x)))))
 
 
-_MEAN = (0.4914, 0.4822, 0.4465)
-_STD = (0.2470, 0.2435, 0.2616)
+# per-channel input normalisation of the two model families (uint8 NHWC pixels in):
+#   cifar : (x / 255 - mean) / std with the CIFAR-10 statistics
+#   caffe : Keras ResNet50 preprocess_input — RGB -> BGR, minus the ImageNet BGR means, no scaling
+#           (notebooks/ml/Inference/Inference_Hello_World.ipynb:263-266); inference.preprocess_input
+#           produces exactly this float tensor on the host, which the model then takes unchanged
+_NORM = {
+    "cifar": dict(mean=(0.4914, 0.4822, 0.4465), std=(0.2470, 0.2435, 0.2616), scale255=True, reverse=False),
+    "caffe": dict(mean=(103.939, 116.779, 123.68), std=(1.0, 1.0, 1.0), scale255=False, reverse=True),
+}
 
 
-def _norm_buffers(m):
-    """Per-channel (x/255 - mean)/std folded into one scale/shift pair, kept as buffers so the
-    normalisation is capture-safe (no host->device constants inside a hipGraph)."""
+def _norm_buffers(m, kind: str = "cifar"):
+    """Per-channel scale/shift of the input normalisation, kept on the module (host floats: the
+    normalisation kernel takes them by value, so it is capture-safe)."""
+    spec = _NORM[kind]
+    m.img_norm = kind
+    m.img_reverse = spec["reverse"]
+    m.img_scale_c = [1.0 / ((255.0 if spec["scale255"] else 1.0) * s) for s in spec["std"]]
+    m.img_shift_c = [-mu / s for mu, s in zip(spec["mean"], spec["std"])]
+
+
+def _as_nhwc_image(x, m):
+    """uint8 NHWC images are normalised per channel on the device (one hopsx kernel: bf16 out);
+    float inputs are taken as already preprocessed."""
     import torch
 
-    std = torch.tensor(_STD)
-    m.register_buffer("img_scale", 1.0 / (255.0 * std), persistent=False)
-    m.register_buffer("img_shift", -torch.tensor(_MEAN) / std, persistent=False)
+    if x.dtype != torch.uint8:
+        return x
+    if x.is_cuda:
+        from ..ops import kernels as K
 
-
-def _as_nhwc_image(x, shift, scale):
-    """uint8 NHWC images are normalised per channel on the device; float inputs pass through."""
-    import torch
-
-    if x.dtype == torch.uint8:
-        y = torch.addcmul(shift, x, scale)  # one fused elementwise pass: shift + x * scale
-        return y.to(torch.bfloat16) if x.is_cuda else y
-    return x
+        return K.u8_normalize_chan(x.contiguous(), m.img_scale_c, m.img_shift_c, reverse=m.img_reverse)
+    y = x.float()
+    if m.img_reverse:
+        y = y.flip(-1)
+    return y * torch.tensor(m.img_scale_c) + torch.tensor(m.img_shift_c)
 
 
 def cifar_resnet(depth: int = 20, num_classes: int = 10) -> CifarResNet:

@@ -413,6 +413,17 @@ def cast_f32_bf16(x, out=None):
     return out
 
 
+def u8_normalize_chan(x, scale, shift, reverse=False, out=None):
+    """uint8 NHWC [..., C] -> bf16, per channel x * scale[c] + shift[c] (channel order reversed first
+    with ``reverse``: RGB -> BGR)."""
+    C = x.shape[-1]
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    check(_C.ext().u8_normalize_chan(ptr(x), ptr(out), x.numel() // C, C, [float(v) for v in scale],
+                                     [float(v) for v in shift], int(bool(reverse)), stream()), "u8_normalize_chan")
+    return out
+
+
 def u8_normalize(x, scale, shift, out=None):
     if out is None:
         out = torch.empty(x.shape, device=x.device, dtype=BF16)

@@ -44,3 +44,22 @@ def test_batch_predict_shards(project_root, monkeypatch):
     assert {"top1_label", "top2_label", "top3_label"} <= set(df.columns)
     assert (df.top1_score >= df.top2_score).all()
     assert len(list((project_root / "Resources" / "labels.parquet").glob("part-*.parquet"))) == 2
+
+
+def test_resnet50_uint8_normalisation_equals_preprocess_input():
+    """ResNet-50 takes raw uint8 RGB pixels and applies Keras' caffe preprocessing itself (RGB -> BGR,
+    minus the ImageNet BGR means); a float input is taken as already preprocess_input-ed.  Both
+    routes must give the model the same tensor (round 2 normalised ResNet-50 with CIFAR statistics)."""
+    import numpy as np
+    import torch
+
+    from hops_examples_amd import inference as I
+    from hops_examples_amd.models.resnet import _as_nhwc_image, cifar_resnet, resnet50
+
+    x = np.random.default_rng(0).integers(0, 256, (2, 5, 5, 3), dtype=np.uint8)
+    m = resnet50()
+    got = _as_nhwc_image(torch.from_numpy(x), m).numpy()
+    np.testing.assert_allclose(got, I.preprocess_input(x), rtol=0, atol=1e-4)
+    c = cifar_resnet(20)
+    want = (x / 255.0 - np.array([0.4914, 0.4822, 0.4465])) / np.array([0.2470, 0.2435, 0.2616])
+    np.testing.assert_allclose(_as_nhwc_image(torch.from_numpy(x), c).numpy(), want, atol=1e-5)
