@@ -244,15 +244,19 @@ static py::dict decode_examples_columnar(py::list records, py::list schema, int 
     int len;
     std::vector<float> f;
     std::vector<int64_t> i;
+    std::vector<uint8_t> u;  // kind 3: the first bytes value, fixed length (e.g. a raw uint8 image)
   };
   std::vector<Col> cols;
   for (auto it : schema) {
     py::tuple t = py::reinterpret_borrow<py::tuple>(it);
     Col c;
     c.name = py::str(t[0]);
-    c.kind = std::string(py::str(t[1])) == "float" ? 1 : 2;
+    const std::string k = py::str(t[1]);
+    c.kind = k == "float" ? 1 : (k == "bytes" ? 3 : 2);
     c.len = t[2].cast<int>();
+    if (c.len < 0) throw std::runtime_error("column length must be >= 0");
     if (c.kind == 1) c.f.assign(n * c.len, NAN);
+    else if (c.kind == 3) c.u.assign(n * c.len, 0);
     else c.i.assign(n * c.len, 0);
     cols.push_back(std::move(c));
   }
@@ -266,6 +270,13 @@ static py::dict decode_examples_columnar(py::list records, py::list schema, int 
         for (auto& c : cols) {
           auto it = m.find(c.name);
           if (it == m.end()) continue;
+          if (c.kind == 3) {
+            if (it->second.b.empty()) continue;
+            const std::string& v = it->second.b[0];
+            if ((int)v.size() != c.len) throw std::runtime_error("bytes feature " + c.name + " has the wrong length");
+            memcpy(c.u.data() + r * c.len, v.data(), c.len);
+            continue;
+          }
           if (c.kind == 1) {
             const auto& src = it->second.f.empty() && !it->second.i.empty() ? std::vector<float>() : it->second.f;
             if (!it->second.f.empty())
@@ -298,6 +309,10 @@ static py::dict decode_examples_columnar(py::list records, py::list schema, int 
     if (c.kind == 1) {
       py::array_t<float> a({(ssize_t)n, (ssize_t)c.len});
       memcpy(a.mutable_data(), c.f.data(), c.f.size() * 4);
+      out[py::str(c.name)] = a;
+    } else if (c.kind == 3) {
+      py::array_t<uint8_t> a({(ssize_t)n, (ssize_t)c.len});
+      if (!c.u.empty()) memcpy(a.mutable_data(), c.u.data(), c.u.size());
       out[py::str(c.name)] = a;
     } else {
       py::array_t<int64_t> a({(ssize_t)n, (ssize_t)c.len});

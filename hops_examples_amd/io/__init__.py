@@ -167,7 +167,9 @@ def decode_example(rec: bytes) -> dict:
 
 
 def decode_batch(records: list[bytes], schema: list[tuple[str, str, int]], nthreads: int = 8) -> dict:
-    """Columnar decode of many Examples: schema [(name, 'float'|'int64', length)] -> {name: ndarray[n, length]}."""
+    """Columnar decode of many Examples: schema [(name, 'float'|'int64'|'bytes', length)] ->
+    {name: ndarray[n, length]} ('bytes': the first value of the feature, exactly ``length`` bytes, as
+    uint8 — a raw image)."""
     if _io is not None:
         return _io.decode_examples_columnar(records, schema, nthreads)
     out = {n: np.zeros((len(records), L), np.float32 if k == "float" else np.int64) for n, k, L in schema}

@@ -42,26 +42,40 @@ def test_jobs_lifecycle(project_root):
     assert [j["name"] for j in jobs.get_jobs()] == ["bad", "pi"]
 
 
-def test_flink_runner_lifecycle_runs_pipeline_as_job(project_root):
-    """hops.beam runner lifecycle (jobs-client/flink/jobs_flink_client.py:45-51): a pipeline is only
-    accepted by a RUNNING runner and executes as a tracked job."""
+def test_flink_runner_lifecycle_and_rest_client(project_root):
+    """hops.beam runner lifecycle and the Flink REST flow of jobs-client/flink/jobs_flink_client.py:
+    the runner is a job that becomes RUNNING once its REST endpoint is up (polled like the reference's
+    90 s loop), a second client reuses it, programs are uploaded and run in task slots, REST errors
+    raise RestAPIError with the reference's message shape, stop ends the runner job."""
     from hops_examples_amd import beam, jobs
+    from hops_examples_amd.exceptions import RestAPIError
 
-    app = _prog(project_root, "wordcount.py", """
-        import collections, sys
-        words = "the quick brown fox jumps over the lazy dog the end".split()
+    app = project_root / "Resources" / "wordcount.py"
+    app.parent.mkdir(parents=True, exist_ok=True)
+    app.write_text(textwrap.dedent("""
+        import collections, sys, time
+        words = sys.argv[1:] or "the quick brown fox jumps over the lazy dog the end".split()
         print(dict(collections.Counter(words).most_common(1)))
-    """)
-    cfg = beam.create_runner("flinkrunner", num_of_taskmanagers=2, num_task_slots=4)
-    assert cfg["state"] == "CREATED" and beam.get_runner_state("flinkrunner") == "CREATED"
+        time.sleep(float(__import__("os").environ.get("WC_SLEEP", "0")))
+    """))
+    beam.create_runner("flinkrunner", num_of_taskmanagers=1, num_task_slots=1)
+    assert beam.find_running("flinkrunner") is None
     with pytest.raises(RuntimeError):
-        beam.run_pipeline("flinkrunner", app)
+        beam.run_pipeline("flinkrunner", str(app))
     beam.start_runner("flinkrunner")
-    ex = beam.run_pipeline("flinkrunner", app)
-    st = jobs.wait_for_execution("flinkrunner-pipeline", ex["id"], timeout=60)
-    assert st["finalStatus"] == "SUCCEEDED"
-    assert "{'the': 3}" in jobs.get_logs("flinkrunner-pipeline")
-    assert beam.stop_runner("flinkrunner")["state"] == "STOPPED"
+    e = beam.wait_until_running("flinkrunner", wait=60, step=0.1)
+    assert e is not None and beam.get_runner_state("flinkrunner") == "RUNNING"
+    assert beam.find_running("flinkrunner")["endpoint"] == e["endpoint"]  # reuse, no second cluster
+    ov = beam.overview(e["endpoint"])
+    assert ov["slots-total"] == 1 and ov["jobs-running"] == 0
+    r = beam.run_pipeline("flinkrunner", str(app), args="a b b c")
+    s = beam.wait_job(r["endpoint"], r["jobid"], timeout=60)
+    assert s["state"] == "FINISHED" and s["exit-code"] == 0
+    with pytest.raises(RestAPIError, match="HTTP code: 404"):
+        beam.run_program(e["endpoint"], "no_such_program.py")
+    beam.stop_runner("flinkrunner")
+    ex = jobs.wait_for_execution("flinkrunner", jobs.get_executions("flinkrunner")[-1]["id"], timeout=30)
+    assert ex["state"] == "KILLED" and beam.find_running("flinkrunner") is None
 
 
 def test_dag_job_chain_and_failure_propagation(project_root):
