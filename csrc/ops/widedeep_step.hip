@@ -15,7 +15,11 @@
 //     (each row claimed once by an atomic exchange of its summed gradient, which also leaves
 //     the gradient buffer zero), step counters / RNG bumps as the optimizer kernels would,
 //   * the batch is read straight from the HBM-resident epoch at a device cursor that the
-//     kernel advances itself: no copy launches.
+//     kernel advances itself: no copy launches;
+//   * ``nsteps`` > 1 (Keras steps_per_execution): the launch runs that many consecutive steps on
+//     consecutive batches — the deep weights and their Adagrad state stay in registers / LDS
+//     between steps (written back once, after the last), the wide rows' FTRL updates go through
+//     memory (the next step gathers them) — so a step costs neither a launch nor a reload.
 // Data parallel runs use apply_opt = 0: gradients land in the arena grad buffer for the RCCL
 // all-reduce and the regular optimizer kernels.
 // Parity: the reference's TFX taxi trainer (README.md:99-112) — same model,
@@ -60,6 +64,7 @@ struct WideDeepArgs {
   unsigned long long* rng;
   int rng_bumps;
   int apply_opt;
+  int nsteps;               // consecutive steps in this launch (1 unless apply_opt)
   unsigned long long* dbg;  // phase timestamps (wall clock, 100 MHz), or null
   const int* slot;          // [deep span]: LDS slot of each deep arena element (-1: padding), host-built
 };
@@ -116,14 +121,15 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int B = A.B, Bp = A.Bp;
-  const long long bi = A.cursor ? A.cursor[0] : 0;
+  const long long bi0 = A.cursor ? A.cursor[0] : 0;
   const long deep_lo = A.woff[0], deep_hi = A.boff[L - 1] + A.dims[L];
   wd_mark(A, 0);
 
   // ---------------------------------------------------------------- stage
   // Every global load of the step is issued here, independent of each other (one memory round
-  // trip): this thread's deep parameters + Adagrad state (kept in registers until the update),
-  // its wide (example, column) entry with that row's FTRL state, the batch.
+  // trip): this thread's deep parameters + Adagrad state (kept in registers until the update —
+  // and across the steps of a multi-step launch), its wide (example, column) entry with that
+  // row's FTRL state, the batch.
   float pw[WD_PF], ps[WD_PF];
   int psl[WD_PF];
 #pragma unroll
@@ -134,6 +140,10 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     ps[k] = A.apply_opt ? A.ada_s[xc] : 0.f;
     psl[k] = x < deep_hi ? A.slot[xc - deep_lo] : -1;
   }
+  for (int step = 0; step < A.nsteps; ++step) {
+  const bool last = step + 1 == A.nsteps;
+  const long long bi = (bi0 + step) % A.nbatch;
+  if (step) __syncthreads();  // the previous step's wide-row updates (same CU) are visible after this
   const long long* cb = A.cat + bi * (long long)B * A.nwide;
   const bool wide_t = tid < B * A.nwide;
   const long wrow = A.wide_off + (wide_t ? cb[tid] : 0);
@@ -295,9 +305,13 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
         if (A.apply_opt) {
           float s1 = ps[k], s2 = 0.f, s3 = 0.f;
           const float w = upd<5>(pw[k], g * A.ada.gscale, s1, s2, s3, A.ada, 1.f, 1.f);
-          A.master[x] = w;
-          A.ada_s[x] = s1;
-          if (A.shadow) A.shadow[x] = f2bf(w);
+          pw[k] = w;  // the next step of this launch starts from the updated weight
+          ps[k] = s1;
+          if (last) {
+            A.master[x] = w;
+            A.ada_s[x] = s1;
+            if (A.shadow) A.shadow[x] = f2bf(w);
+          }
         } else {
           A.grad[x] = g;
         }
@@ -317,13 +331,14 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       if (A.shadow) A.shadow[wrow] = f2bf(w);
     }
   }
+  }  // steps
   if (tid == 0) {
     if (A.apply_opt) {
-      if (A.step_ada) A.step_ada[0] += 1.f;
-      if (A.step_ftrl) A.step_ftrl[0] += 1.f;
-      if (A.rng) A.rng[1] += (unsigned long long)A.rng_bumps;
+      if (A.step_ada) A.step_ada[0] += (float)A.nsteps;
+      if (A.step_ftrl) A.step_ftrl[0] += (float)A.nsteps;
+      if (A.rng) A.rng[1] += (unsigned long long)A.rng_bumps * (unsigned long long)A.nsteps;
     }
-    if (A.cursor) A.cursor[0] = (bi + 1) % A.nbatch;
+    if (A.cursor) A.cursor[0] = (bi0 + A.nsteps) % A.nbatch;
   }
   wd_mark(A, 19);
 }
@@ -348,7 +363,7 @@ int wd_fill(WideDeepArgs& a, const uint64_t* p, int np, const long* iv, int ni, 
   a.step_ada = (float*)p[12];
   a.step_ftrl = (float*)p[13];
   a.rng = (unsigned long long*)p[14];
-  // ints: L B nbatch nwide wide_off apply_opt rng_bumps dims[L+1] woff[L] boff[L]
+  // ints: L B nbatch nwide wide_off apply_opt rng_bumps dims[L+1] woff[L] boff[L] [nsteps]
   if (ni < 7) return -2;
   a.L = (int)iv[0];
   a.B = (int)iv[1];
@@ -357,7 +372,10 @@ int wd_fill(WideDeepArgs& a, const uint64_t* p, int np, const long* iv, int ni, 
   a.wide_off = iv[4];
   a.apply_opt = (int)iv[5];
   a.rng_bumps = (int)iv[6];
-  if (a.L < 1 || a.L > WD_MAXL || ni != 7 + (a.L + 1) + 2 * a.L || a.B < 1 || a.nbatch < 1) return -2;
+  const int nbase = 7 + (a.L + 1) + 2 * a.L;
+  if (a.L < 1 || a.L > WD_MAXL || (ni != nbase && ni != nbase + 1) || a.B < 1 || a.nbatch < 1) return -2;
+  a.nsteps = ni == nbase + 1 ? (int)iv[nbase] : 1;
+  if (a.nsteps < 1 || (a.nsteps > 1 && !a.apply_opt)) return -2;  // DP: gradients leave after every step
   for (int i = 0; i <= a.L; ++i) a.dims[i] = (int)iv[7 + i];
   for (int i = 0; i < a.L; ++i) {
     a.woff[i] = iv[8 + a.L + i];

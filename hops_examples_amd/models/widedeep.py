@@ -122,7 +122,9 @@ class FusedWideDeepStep:
         self._graphU = None
         self._keyU = None
         self._graphR: dict = {}  # remainder graphs (Keras steps_per_execution tail): U -> graph
-        self.steps_per_execution = max(1, int(os.environ.get("HOPSX_STEPS_PER_EXEC", "8")))
+        # steps per replayed graph; on one GPU they run inside ONE launch (widedeep_step.hip nsteps)
+        self.steps_per_execution = max(1, int(os.environ.get("HOPSX_TAXI_STEPS_PER_EXEC",
+                                                             os.environ.get("HOPSX_STEPS_PER_EXEC", "32"))))
         self._slot_cache = {}
         self._n = 0
         dev = self.arena.device
@@ -133,10 +135,11 @@ class FusedWideDeepStep:
         self.dbg = (torch.zeros(20, device=dev, dtype=torch.int64)
                     if os.environ.get("HOPSX_PHASE_DBG") == "1" else None)
 
-    def _ints(self, B: int, nbatch: int) -> list[int]:
+    def _ints(self, B: int, nbatch: int, nsteps: int = 1) -> list[int]:
         L = len(self.lins)
-        return ([L, B, nbatch, N_WIDE, int(self.model.wide.weight._hx_off), int(self.dp is None), 2] + self.dims
-                + [int(m.weight._hx_off) for m in self.lins] + [int(m.bias._hx_off) for m in self.lins])
+        iv = ([L, B, nbatch, N_WIDE, int(self.model.wide.weight._hx_off), int(self.dp is None), 2] + self.dims
+              + [int(m.weight._hx_off) for m in self.lins] + [int(m.bias._hx_off) for m in self.lins])
+        return iv + [int(nsteps)] if nsteps > 1 else iv
 
     def ok(self, B: int) -> bool:
         from ..ops import _C
@@ -168,7 +171,7 @@ class FusedWideDeepStep:
         self.ftrl.lr = self.ftrl.param_groups[0]["lr"]
         return pad8(self.ada._hp()) + pad8(self.ftrl._hp())
 
-    def _launch(self, dense, cat, label, nbatch: int, cursor):
+    def _launch(self, dense, cat, label, nbatch: int, cursor, nsteps: int = 1):
         from ..ops import _C
         from ..ops.functional import rng_state
         from ..ops.kernels import check, stream
@@ -179,7 +182,7 @@ class FusedWideDeepStep:
                 ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label), ptr(cursor), ptr(self.loss),
                 ptr(self.correct), ptr(self.ada.step_count), ptr(self.ftrl.step_count), ptr(rng_state(a.device)),
                 ptr(self.dbg), ptr(self._slots(dense.shape[-2]))]
-        check(_C.ext().widedeep_step(ptrs, self._ints(dense.shape[-2], nbatch), self._floats(), stream()),
+        check(_C.ext().widedeep_step(ptrs, self._ints(dense.shape[-2], nbatch, nsteps), self._floats(), stream()),
               "widedeep_step")
 
     def _finish(self):
@@ -238,14 +241,19 @@ class FusedWideDeepStep:
             self.opt.sync_hp()
 
     def _capture_u(self, dense, cat, ys, U: int):
+        """U consecutive steps in one graph: ONE launch running U steps in-kernel on one GPU (the
+        weights stay on chip between them); U launches + gradient exchanges when data-parallel."""
         self._slots(dense.shape[-2])
         self._sync_hp()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with _capture_graph(g):
-            for _ in range(U):
-                self._launch(dense, cat, ys, dense.shape[0], self.cursor)
-                self._finish()
+            if self.dp is None and os.environ.get("HOPSX_TAXI_INKERNEL_LOOP", "1") == "1":
+                self._launch(dense, cat, ys, dense.shape[0], self.cursor, nsteps=U)
+            else:
+                for _ in range(U):
+                    self._launch(dense, cat, ys, dense.shape[0], self.cursor)
+                    self._finish()
         return g
 
     def prepare_resident(self, xs, ys, n: int | None = None) -> None:

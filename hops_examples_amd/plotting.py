@@ -188,3 +188,244 @@ def save(svg: str, path) -> str:
     p.parent.mkdir(parents=True, exist_ok=True)
     p.write_text(svg)
     return str(p)
+
+
+# ------------------------------------------------------------------ maps (folium / ipyleaflet)
+# notebooks/ml/Plotting/folium_heat_map.ipynb:37-111 (HeatMapWithTime over moving points) and
+# ipyleaflet.ipynb:21-251 (Map, layers, DrawControl with draw callbacks, two maps linked on
+# center/zoom).  No tile server or browser widget exists here: a map is a Web-Mercator canvas whose
+# layers render to SVG; drawing is an API call that fires the same callbacks with GeoJSON.
+def _mercator(lat, lon, center, zoom, w, h):
+    """(x, y) pixels of lat/lon for a Web-Mercator view of ``zoom`` centred on ``center``."""
+    def proj(la, lo):
+        s = 256 * 2 ** zoom
+        x = (lo + 180.0) / 360.0 * s
+        r = np.radians(np.clip(la, -85.05, 85.05))
+        y = (1 - np.log(np.tan(r) + 1 / np.cos(r)) / np.pi) / 2 * s
+        return x, y
+
+    cx, cy = proj(np.asarray(center[0], float), np.asarray(center[1], float))
+    x, y = proj(np.asarray(lat, float), np.asarray(lon, float))
+    return x - cx + w / 2, y - cy + h / 2
+
+
+class GeoJSON:
+    def __init__(self, data: dict, style: dict | None = None):
+        self.data, self.style = data, dict(style or {})
+
+
+class Marker:
+    def __init__(self, location, title: str = ""):
+        self.location, self.title = tuple(location), title
+
+
+class Polyline:
+    def __init__(self, locations, color: str = "#0000FF"):
+        self.locations, self.color = [tuple(p) for p in locations], color
+
+
+class Polygon(Polyline):
+    pass
+
+
+class Circle:
+    def __init__(self, location, radius: float = 1000.0, color: str = "#0000FF"):
+        self.location, self.radius, self.color = tuple(location), float(radius), color
+
+
+class GeoMap:
+    """An ipyleaflet ``Map`` / folium ``Map`` stand-in: ``center``, ``zoom``, ``add_layer``,
+    ``add_control``, ``to_svg`` / ``save``."""
+
+    def __init__(self, center=(0.0, 0.0), zoom: int = 5, width: int = 640, height: int = 400, layout=None):
+        self.center, self.zoom = tuple(center), int(zoom)
+        self.width, self.height = width, height
+        if layout:
+            self.width = int(str(layout.get("width", width)).rstrip("px"))
+            self.height = int(str(layout.get("height", height)).rstrip("px"))
+        self.layers: list = []
+        self.controls: list = []
+        self._links: list = []
+
+    def __setattr__(self, k, v):
+        object.__setattr__(self, k, v)
+        if k in ("center", "zoom"):
+            for other, attr in getattr(self, "_links", []):
+                if attr == k and getattr(other, k) != v:
+                    setattr(other, k, v)
+
+    def add_layer(self, layer):
+        self.layers.append(layer)
+        return self
+
+    def add_control(self, control):
+        self.controls.append(control)
+        control.map = self
+        return self
+
+    def _xy(self, lat, lon):
+        return _mercator(lat, lon, self.center, self.zoom, self.width, self.height)
+
+    def _geojson_svg(self, geom: dict, color: str) -> list[str]:
+        t, c = geom.get("type"), geom.get("coordinates")
+        out = []
+        if t == "Point":
+            x, y = self._xy(c[1], c[0])
+            out.append(f'<circle cx="{x:.1f}" cy="{y:.1f}" r="5" fill="{color}"/>')
+        elif t in ("LineString", "Polygon"):
+            ring = c[0] if t == "Polygon" else c
+            xs, ys = self._xy([p[1] for p in ring], [p[0] for p in ring])
+            pts = " ".join(f"{a:.1f},{b:.1f}" for a, b in zip(xs, ys))
+            tag = "polygon" if t == "Polygon" else "polyline"
+            out.append(f'<{tag} points="{pts}" fill="{color if t == "Polygon" else "none"}" fill-opacity="0.3" '
+                       f'stroke="{color}" stroke-width="2"/>')
+        elif t == "Feature":
+            out += self._geojson_svg(geom["geometry"], color)
+        elif t == "FeatureCollection":
+            for f in geom["features"]:
+                out += self._geojson_svg(f, color)
+        return out
+
+    def to_svg(self, title: str = "") -> str:
+        body = [f'<rect width="{self.width}" height="{self.height}" fill="#e8eef2"/>']
+        for L in self.layers:
+            if isinstance(L, Marker):
+                x, y = self._xy(L.location[0], L.location[1])
+                body.append(f'<circle cx="{x:.1f}" cy="{y:.1f}" r="6" fill="#d62728"/>')
+            elif isinstance(L, Polyline):
+                xs, ys = self._xy([p[0] for p in L.locations], [p[1] for p in L.locations])
+                pts = " ".join(f"{a:.1f},{b:.1f}" for a, b in zip(xs, ys))
+                tag = "polygon" if isinstance(L, Polygon) else "polyline"
+                body.append(f'<{tag} points="{pts}" fill="{L.color if tag == "polygon" else "none"}" '
+                            f'fill-opacity="0.3" stroke="{L.color}" stroke-width="2"/>')
+            elif isinstance(L, Circle):
+                x, y = self._xy(L.location[0], L.location[1])
+                m_per_px = 156543.03 * np.cos(np.radians(L.location[0])) / 2 ** self.zoom
+                body.append(f'<circle cx="{x:.1f}" cy="{y:.1f}" r="{L.radius / m_per_px:.1f}" fill="{L.color}" '
+                            'fill-opacity="0.3"/>')
+            elif isinstance(L, GeoJSON):
+                body += self._geojson_svg(L.data, L.style.get("color", "#0000FF"))
+            elif isinstance(L, HeatMapWithTime):
+                body += L._frame_svg(self, L.current)
+        return _svg(body, title, self.width, self.height)
+
+    def save(self, path, title: str = "") -> str:
+        return save(self.to_svg(title), path)
+
+
+Map = GeoMap
+
+
+def link(a: tuple, b: tuple):
+    """traitlets.link((m, 'center'), (m2, 'center')): the two attributes stay equal."""
+    (oa, attr), (ob, attr2) = a, b
+    if attr != attr2:
+        raise ValueError("link the same attribute of two maps")
+    setattr(ob, attr, getattr(oa, attr))
+    oa._links.append((ob, attr))
+    ob._links.append((oa, attr))
+    return (oa, ob, attr)
+
+
+class DrawControl:
+    """ipyleaflet ``DrawControl``: enabled shape tools, ``on_draw`` callbacks receiving
+    (control, action, geo_json), ``last_action`` / ``last_draw``, ``clear_*``.  Shapes are drawn
+    with :meth:`draw` (the programmatic counterpart of a mouse gesture)."""
+
+    _KIND = {"marker": "Point", "polyline": "LineString", "polygon": "Polygon", "rectangle": "Polygon",
+             "circle": "Point", "circlemarker": "Point"}
+
+    def __init__(self, **tools):
+        self.tools = {k: v for k, v in tools.items() if k in self._KIND}
+        self._handlers: list = []
+        self.shapes: list[dict] = []
+        self.last_action, self.last_draw = "", {"type": "Feature", "geometry": None}
+        self.map = None
+
+    def on_draw(self, fn):
+        self._handlers.append(fn)
+
+    def draw(self, kind: str, coordinates, **properties) -> dict:
+        if kind not in self.tools:
+            raise ValueError(f"draw tool {kind!r} is not enabled on this control")
+        if kind == "rectangle":
+            (la0, lo0), (la1, lo1) = coordinates
+            coordinates = [[[lo0, la0], [lo1, la0], [lo1, la1], [lo0, la1], [lo0, la0]]]
+        elif kind in ("marker", "circle", "circlemarker"):
+            coordinates = [coordinates[1], coordinates[0]]
+        elif kind == "polygon":
+            coordinates = [[[lo, la] for la, lo in coordinates] + [[coordinates[0][1], coordinates[0][0]]]]
+        elif kind == "polyline":
+            coordinates = [[lo, la] for la, lo in coordinates]
+        feat = {"type": "Feature", "properties": {"style": self.tools[kind].get("shapeOptions", {}), "kind": kind,
+                                                  **properties},
+                "geometry": {"type": self._KIND[kind], "coordinates": coordinates}}
+        self.shapes.append(feat)
+        self.last_action, self.last_draw = "created", feat
+        for fn in self._handlers:
+            fn(self, "created", feat)
+        return feat
+
+    def _clear(self, kinds):
+        self.shapes = [s for s in self.shapes if s["properties"]["kind"] not in kinds]
+        self.last_action = "deleted"
+
+    def clear_circles(self):
+        self._clear({"circle", "circlemarker"})
+
+    def clear_polylines(self):
+        self._clear({"polyline"})
+
+    def clear_rectangles(self):
+        self._clear({"rectangle"})
+
+    def clear_markers(self):
+        self._clear({"marker"})
+
+    def clear_polygons(self):
+        self._clear({"polygon"})
+
+    def clear(self):
+        self.shapes = []
+        self.last_action = "deleted"
+
+
+class HeatMapWithTime:
+    """folium ``plugins.HeatMapWithTime(data, index=None)``: one point-density frame per time step;
+    ``data[t]`` is a list of [lat, lon(, weight)].  ``frames(map)`` renders every step, ``current``
+    selects the step a map shows (the player slider)."""
+
+    def __init__(self, data, index=None, auto_play: bool = False, max_opacity: float = 0.6, min_speed: float = 0.1,
+                 radius: float = 12.0):
+        self.data = [np.asarray(t, dtype=np.float64).reshape(len(t), -1) for t in data]
+        self.index = list(index) if index is not None else list(range(len(self.data)))
+        if len(self.index) != len(self.data):
+            raise ValueError("index must have one entry per time step")
+        self.max_opacity, self.radius, self.current = float(max_opacity), float(radius), 0
+
+    def add_to(self, m: GeoMap):
+        m.add_layer(self)
+        return self
+
+    def _frame_svg(self, m: GeoMap, t: int) -> list[str]:
+        pts = self.data[t]
+        if not len(pts):
+            return []
+        w = pts[:, 2] if pts.shape[1] > 2 else np.ones(len(pts))
+        xs, ys = m._xy(pts[:, 0], pts[:, 1])
+        wmax = float(w.max()) or 1.0
+        return [f'<circle cx="{x:.1f}" cy="{y:.1f}" r="{self.radius}" fill="{_color(float(v) / wmax)}" '
+                f'fill-opacity="{self.max_opacity * 0.5:.2f}"/>' for x, y, v in zip(xs, ys, w)]
+
+    def frames(self, m: GeoMap) -> list[str]:
+        out = []
+        for t in range(len(self.data)):
+            self.current = t
+            out.append(m.to_svg(title=str(self.index[t])))
+        self.current = 0
+        return out
+
+    def centroids(self) -> np.ndarray:
+        """Weighted (lat, lon) centre of mass per time step — how the cloud moves."""
+        return np.array([np.average(d[:, :2], axis=0, weights=d[:, 2] if d.shape[1] > 2 else None)
+                         for d in self.data])
