@@ -67,7 +67,9 @@ def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=
     def run(i):
         box["r"] = st(xs[i % nb], ys[i % nb])
 
-    for i in range(warmup):
+    # TrainStep runs `st.warmup` eager steps and captures the graph on the next one: warm up past the
+    # capture, so the timed window holds replays only (whatever --warmup says)
+    for i in range(max(warmup, st.warmup + 2 if st.use_graph else warmup)):
         run(i)
     el = timed(run, steps, dev)
     return el, float(box["r"]["loss"].reshape(-1)[0])

@@ -384,8 +384,15 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
     return (int)hipGetLastError();
   }
   if (xscale != 0.f) return -3;
-  if (hopsx_conv_wgrad_mfma_ok(geom) && (uintptr_t)dy % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0)
-    return hopsx_conv2d_wgrad_mfma(dy, x, geom, dw, dbias, y, yact, st);
+  // LDS-DMA 128x128 kernel (wgrad_glds.hip) for the conv -> BN layers (no dY mask, no bias grad);
+  // the small-CO direct-MFMA kernel keeps its shapes unless HOPSX_WGRAD_GLDS_FIRST=1 (A/B knob)
+  static const int glds_first = hopsx_env_int("HOPSX_WGRAD_GLDS_FIRST", 0);
+  const bool mfma_ok =
+      hopsx_conv_wgrad_mfma_ok(geom) && (uintptr_t)dy % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0;
+  if (!y && !dbias && (glds_first || !mfma_ok) && hopsx_conv_wgrad_glds_ok(geom) &&
+      hopsx_conv2d_wgrad_glds(dy, x, geom, dw, st) == 0)
+    return 0;
+  if (mfma_ok) return hopsx_conv2d_wgrad_mfma(dy, x, geom, dw, dbias, y, yact, st);
   // the direct kernel re-loads dY and X per (k, co) thread: cheap for small pixel counts and the
   // only path for uint8 inputs; past 16k pixels the implicit-GEMM MFMA path wins (the CIFAR
   // ResNet stem, 131k pixels: 89 us direct)
