@@ -159,58 +159,120 @@ def cfg_taxi(a, dev, rank, world):
            "transform_s": r.get("transform_s")})
 
 
-def cfg_titanic(a, dev, rank, world):
-    """Parquet TD -> pinned host -> HBM ingest rate, then DNN training steps/s on the resident data."""
+def _titanic_td(rows: int, rank: int):
+    """The featurestore tour's Titanic training dataset at ``rows`` synthetic passengers: rank 0
+    builds the feature group and the Parquet TD (64k-row row groups) once, every rank opens it."""
     import numpy as np
     import pandas as pd
 
-    from hops_examples_amd import keras, optim
+    import hsfs
+
+    name = f"titanic_bench_{rows}"
+    fs = hsfs.connection().get_feature_store()
+    if rank == 0:
+        try:
+            fs.get_training_dataset(name, 1)
+        except Exception:  # noqa: BLE001 - first run: build it
+            rng = np.random.default_rng(0)
+            df = pd.DataFrame({"passenger_id": np.arange(rows), "pclass": rng.integers(1, 4, rows),
+                               "sex": rng.integers(0, 2, rows), "fare": rng.gamma(2.0, 16.0, rows),
+                               "age": rng.normal(30, 12, rows).clip(1, 80), "sibsp": rng.integers(0, 5, rows),
+                               "parch": rng.integers(0, 4, rows)})
+            df["survived"] = ((df.sex == 1) ^ (rng.random(rows) < 0.2)).astype(np.int64)
+            fg = fs.create_feature_group(f"{name}_fg", 1, primary_key=["passenger_id"],
+                                         statistics_config={"enabled": False})
+            fg.save(df)
+            td = fs.create_training_dataset(name, 1, data_format="parquet", label=["survived"],
+                                            statistics_config={"enabled": False})
+            td.save(fg.select(["pclass", "sex", "fare", "age", "sibsp", "parch", "survived"]))
+    hdist.barrier()
+    return fs.get_training_dataset(name, 1)
+
+
+def titanic_record(rows: int, batch: int, steps: int, warmup: int) -> dict:
+    """BASELINE config 4: the featurestore tour's Titanic training dataset (Parquet) -> a DNN, one
+    rank per GPU.  Every rank streams ONLY its row groups of the TD into HBM
+    (td.to_device(shard=(world, rank)): Arrow decode -> pinned staging -> side-stream H2D -> fp32
+    convert on the GPU; reference: PetastormHelloWorld.ipynb:864-899 shard_count / cur_shard), then
+    trains with the gradient all-reduce.  Returns the JSON record on rank 0."""
+    from hops_examples_amd import optim
     from hops_examples_amd.models.zoo import titanic_dnn
+    from hops_examples_amd.parallel import launch
     from hops_examples_amd.runtime.arena import ALIGN, ParamArena
 
-    B = a.batch or 10
-    n = a.rows
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"hopsx_titanic_{n}_{rank}.parquet")
-    if not os.path.exists(path):
-        rng = np.random.default_rng(rank)
-        df = pd.DataFrame({"pclass": rng.integers(1, 4, n), "sex": rng.integers(0, 2, n),
-                           "fare": rng.gamma(2.0, 16.0, n).astype(np.float32), "age": rng.normal(30, 12, n),
-                           "sibsp": rng.integers(0, 5, n), "parch": rng.integers(0, 4, n)})
-        df["survived"] = ((df.sex == 1) ^ (rng.random(n) < 0.2)).astype(np.float32)
-        df.to_parquet(path, index=False, row_group_size=65536)
-    hdist.barrier()
-    from hops_examples_amd.io.parquet import ParquetDeviceReader
-
-    # Parquet row groups -> Arrow C++ decode -> pinned staging -> one H2D per chunk on a side
-    # stream -> fp32 convert + interleave on the GPU (io/parquet.py); a first (untimed) read warms
-    # the page cache and the allocator, as a steady-state epoch reader would be
-    cols = ["pclass", "sex", "fare", "age", "sibsp", "parch", "survived"]
-    rd = ParquetDeviceReader(path, cols, device=dev)
-    rd.read()
+    rank, _, world = hdist.init()
+    dev = hdist.device()
+    torch.manual_seed(1234 + rank)
+    os.environ.setdefault("HOPSX_PROJECT_ROOT", os.path.join(os.environ.get("TMPDIR", "/tmp"), "hopsx_bench_project"))
+    B = batch or 10
+    td = _titanic_td(rows, rank)
+    feats = ["pclass", "sex", "fare", "age", "sibsp", "parch"]
+    td.to_device("survived", feature_names=feats, device=dev, shard=(world, rank) if world > 1 else None)  # warm
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    tab = rd.read()
+    xd, yd = td.to_device("survived", feature_names=feats, device=dev, shard=(world, rank) if world > 1 else None)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     ingest = time.perf_counter() - t0
-    xd, yd = tab[:, :6].contiguous(), tab[:, 6].contiguous()
-    gbps = tab.numel() * 4 / ingest / 1e9
-    raw_gbps = rd.bytes_read / ingest / 1e9
+    local_rows = xd.shape[0]
+    gbps = local_rows * 7 * 4 / ingest / 1e9
     m = titanic_dnn()
     m.build((6,))
     net = m.net.to(dev)
     ParamArena.from_module(net, dev, pad_multiple=max(1, world) * ALIGN)
     opt = optim.Adam(net, lr=1e-3, eps=1e-7)
-    nb = n // B
+    nb = local_rows // B
     xs = xd[: nb * B].view(nb, B, 6)
     ys = yd[: nb * B].view(nb, B, 1)
-    el, loss = _train_loop(net, opt, "bce", xs, ys, a.steps, a.warmup, dev, world)
-    _emit(rank, "steps/sec Titanic TD -> DNN", a.steps / el, "steps/sec", a.steps, a.warmup, el, world,
-          {"model": f"titanic_dnn {m.count_params()} params", "per_gpu_batch": B, "parallelism": f"dp{world}",
-           "rows": n}, {"ingest_GBps_parquet_to_hbm": round(gbps, 3), "ingest_raw_column_GBps": round(raw_gbps, 3),
-                         "final_loss": round(loss, 4)})
-    _ = keras
+    box = {}
+    el, loss = _train_loop(net, opt, "bce", xs, ys, steps, warmup, dev, world, box=box)
+    dp = box.get("dp")
+    extra = {"ingest_GBps_parquet_to_hbm_per_rank": round(gbps, 3), "rows_per_rank": int(local_rows),
+             "shard_mode": getattr(td, "last_shard_mode", None), "final_loss": round(loss, 4),
+             "dtype": "bf16" if dev.type == "cuda" else "fp32"}
+    if dp is not None and hasattr(dp, "verify_replicas"):
+        extra["replicas_identical"] = dp.verify_replicas()["identical"]
+    ranks = launch.gather_rank_info(dev, {"rows": int(local_rows), "ingest_s": round(ingest, 4)})
+    if dp is not None and hasattr(dp, "close"):
+        dp.close()
+    rec = _record("steps/sec Titanic TD -> DNN", steps / el, "steps/sec", steps, warmup, el, world,
+                  {"model": f"titanic_dnn {m.count_params()} params", "per_gpu_batch": B, "global_batch": B * world,
+                   "parallelism": f"dp{world}", "rows": rows, "launcher": "experiment.mirrored" if world > 1 else
+                   "process", "allreduce": getattr(dp, "path", None), "ranks": ranks}, extra)
+    hdist.shutdown()
+    return rec if rank == 0 else {}
+
+
+def cfg_titanic(a, dev, rank, world):
+    rec = titanic_record(a.rows, a.batch, a.steps, a.warmup)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
+def titanic_via_experiment(a) -> int:
+    """BASELINE config 4 at N ranks: the training function runs under ``experiment.mirrored``."""
+    from hops_examples_amd import experiment
+    from hops_examples_amd.parallel import launch
+
+    n = a.gpus
+    if launch.visible_gpus() < n and not a.rehearse:
+        print(f"[run] {n} workers requested but {launch.visible_gpus()} GPU(s) visible; refusing", file=sys.stderr)
+        return 2
+    if launch.visible_gpus() < n:
+        os.environ.setdefault("HOPSX_DIST_BACKEND", "gloo")  # rehearsal: ranks share a device / the CPU
+    os.environ.setdefault("HOPSX_PROJECT_ROOT", os.path.join(os.environ.get("TMPDIR", "/tmp"), "hopsx_bench_project"))
+    rows, batch, steps, warmup = a.rows, a.batch, a.steps, a.warmup
+
+    def train():
+        sys.path.insert(0, ROOT)
+        return titanic_record(rows, batch, steps, warmup)
+
+    exp_dir, res = experiment.mirrored(train, name="titanic_td_bench", num_workers=n, metric_key="value")
+    res = dict(res)
+    res["experiment_dir"] = exp_dir
+    print(json.dumps(res), flush=True)
+    return 0
 
 
 def cifar_resnet_record(depth: int, batch: int, steps: int, warmup: int) -> dict:
@@ -321,6 +383,8 @@ def main():
     if not launch.is_rank_process():
         if a.config == "cifar_resnet":
             sys.exit(cifar_via_experiment(a))
+        if a.config == "titanic" and a.gpus > 1:
+            sys.exit(titanic_via_experiment(a))
         if a.gpus > 1:
             sys.exit(launch.launch(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:], rehearse=a.rehearse))
     rank, _, world = hdist.init()

@@ -112,8 +112,8 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_wgrad(P<void>(dy), P<void>(x), g.data(), P<float>(dw), P<float>(db), P<void>(y), yact,
                               P<float>(ws), ws_elems, xscale, xshift, P<unsigned>(counter), S(st));
   });
-  m.def("conv2d_wgrad_glds", [](u dy, u x, std::vector<int> g, u dw, u st) {
-    return hopsx_conv2d_wgrad_glds(P<void>(dy), P<void>(x), g.data(), P<float>(dw), S(st));
+  m.def("conv2d_wgrad_glds", [](u dy, u x, std::vector<int> g, u dw, int force, u st) {
+    return hopsx_conv2d_wgrad_glds(P<void>(dy), P<void>(x), g.data(), P<float>(dw), force, S(st));
   });
   m.def("conv_wgrad_glds_ok", [](std::vector<int> g) { return hopsx_conv_wgrad_glds_ok(g.data()); });
   m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,

@@ -390,7 +390,7 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
   const bool mfma_ok =
       hopsx_conv_wgrad_mfma_ok(geom) && (uintptr_t)dy % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0;
   if (!y && !dbias && (glds_first || !mfma_ok) && hopsx_conv_wgrad_glds_ok(geom) &&
-      hopsx_conv2d_wgrad_glds(dy, x, geom, dw, st) == 0)
+      hopsx_conv2d_wgrad_glds(dy, x, geom, dw, 0, st) == 0)
     return 0;
   if (mfma_ok) return hopsx_conv2d_wgrad_mfma(dy, x, geom, dw, dbias, y, yact, st);
   // the direct kernel re-loads dY and X per (k, co) thread: cheap for small pixel counts and the

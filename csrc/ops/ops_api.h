@@ -141,7 +141,7 @@ int hopsx_wgrad_debug_times(unsigned long long* host_out, int n);
 // conv weight gradient through LDS-DMA staged 128x128 MFMA tiles (wgrad_glds.hip): no dY activation
 // mask, no bias gradient, C % 8 == 0, CO % 8 == 0; -2: unsupported (nothing launched)
 int hopsx_conv_wgrad_glds_ok(const int* geom);
-int hopsx_conv2d_wgrad_glds(const void* dy, const void* x, const int* geom, float* dw, hipStream_t st);
+int hopsx_conv2d_wgrad_glds(const void* dy, const void* x, const int* geom, float* dw, int force, hipStream_t st);
 int hopsx_conv2d_wgrad_mfma(const void* dy, const void* x, const int* geom, float* dw, float* dbias, const void* y,
                             int yact, hipStream_t st);
 bool hopsx_conv_dgrad_fused_wgrad_ok(const int* geom, const int* geom0);

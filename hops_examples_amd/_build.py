@@ -61,6 +61,32 @@ def _stale(o: Path, cmd: list[str], deps: list[Path]) -> tuple[bool, str]:
     return (not o.exists() or not stamp.exists() or stamp.read_text().strip() != dg), dg
 
 
+def _local_includes(src: Path, search: list[Path], seen: set | None = None) -> list[Path]:
+    """Transitive ``#include "x.h"`` headers of a source found in ``search`` (the rebuild digest of
+    an object covers exactly what it includes: editing one kernel's header no longer rebuilds every
+    translation unit)."""
+    seen = set() if seen is None else seen
+    out = []
+    try:
+        text = src.read_text(errors="ignore")
+    except OSError:
+        return out
+    for ln in text.splitlines():
+        ln = ln.strip()
+        if not ln.startswith("#include") or '"' not in ln:
+            continue
+        name = ln.split('"')[1]
+        for d in [src.parent, *search]:
+            h = d / name
+            if h.exists():
+                if h not in seen:
+                    seen.add(h)
+                    out.append(h)
+                    out.extend(_local_includes(h, search, seen))
+                break
+    return out
+
+
 def _check_undefined(lib: Path) -> None:
     """A symbol of our own left undefined in the extension would only fail when first called (lazy
     binding aborts the process): refuse such a link."""
@@ -110,7 +136,8 @@ def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra
                    *_py_includes(), f"-I{srcdir}", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
                    "-c", str(s), "-o", str(o)]
         # the digest is taken BEFORE compiling: an edit during the compile leaves a mismatching stamp
-        stale, dg = _stale(o, cmd, [s, *headers])
+        deps = _local_includes(s, [srcdir, *{h.parent for h in headers}])
+        stale, dg = _stale(o, cmd, [s, *sorted(set(deps) | set(extra_headers or []))])
         if force or stale:
             jobs_list.append((cmd, o, dg))
 

@@ -41,6 +41,7 @@ class TrainingDatasetFeature:
 
 
 class TrainingDataset(CamelCaseAPI):
+    row_group_rows = 65536  # Parquet row-group size: the data-parallel shard unit of to_device
     ENTITY_TYPE = "trainingdatasets"
 
     def __init__(self, fs, name, version, description="", data_format="tfrecords", coalesce=False,
@@ -191,8 +192,9 @@ class TrainingDataset(CamelCaseAPI):
                 avro.write_container(f"{base}.avro", avro.schema_of_frame(part, self.name),
                                      part.to_dict(orient="records"))
             elif fmt in ("parquet", "petastorm"):
-                # petastorm datasets ARE Parquet (+ the Unischema in _common_metadata, written in save())
-                part.to_parquet(f"{base}.parquet", index=False)
+                # petastorm datasets ARE Parquet (+ the Unischema in _common_metadata, written in save());
+                # 64k-row row groups: the unit data-parallel readers shard by (to_device(shard=...))
+                part.to_parquet(f"{base}.parquet", index=False, row_group_size=self.row_group_rows)
             else:
                 raise ValueError(f"training dataset format {fmt!r} is not supported here")
 
@@ -292,8 +294,8 @@ class TrainingDataset(CamelCaseAPI):
 
         ``shard=(n, i)``: rank i of n gets an EQUAL number of rows (data-parallel ranks must run the
         same number of steps).  Row-group sharding (petastorm's ``shard_count`` / ``cur_shard``: every
-        n-th row group, only those are read) when every shard gets at least half the rows of the
-        largest; else — e.g. a small dataset written as ONE row group — every rank reads all rows
+        n-th row group of the whole dataset, only those are read) when every shard gets at least half
+        the rows of the largest; else — e.g. a small dataset written as ONE row group — every rank reads all rows
         and keeps rows i, i+n, ... (the DeviceLoader rule).  Either way each shard is truncated to
         the smallest shard's row count, computed from the Parquet metadata on every rank alike."""
         from ..io.parquet import ParquetDeviceReader
@@ -312,17 +314,32 @@ class TrainingDataset(CamelCaseAPI):
                 x, y = x[i::n][:m].contiguous(), y[i::n][:m].contiguous()
             return x, y
         row_sharded = False
+        picks = None  # per part: the row groups this rank reads
+        keep = None
         if shard is not None:
+            import pyarrow.parquet as pq
+
             n, i = shard
-            per = [sum(ParquetDeviceReader(p, feats + targets, device=device, shard=(n, k)).rows for p in parts)
-                   for k in range(n)]
+            # dataset-wide row-group sharding: global row group j (over all parts in order) goes to
+            # rank j % n, so parts with few row groups still spread over every rank
+            sizes = [[pq.ParquetFile(str(p)).metadata.row_group(g).num_rows
+                      for g in range(pq.ParquetFile(str(p)).metadata.num_row_groups)] for p in parts]
+            per, mine, j = [0] * n, [[] for _ in parts], 0
+            for pi, rgs in enumerate(sizes):
+                for g, rows in enumerate(rgs):
+                    per[j % n] += rows
+                    if j % n == i:
+                        mine[pi].append(g)
+                    j += 1
             if min(per) == 0 or min(per) < max(per) // 2:
-                row_sharded, rg_shard, keep = True, None, None
+                row_sharded = True
             else:
-                rg_shard, keep = shard, min(per)
-        else:
-            rg_shard, keep = None, None
-        readers = [ParquetDeviceReader(p, feats + targets, device=device, shard=rg_shard) for p in parts]
+                picks, keep = mine, min(per)
+        self.last_shard_mode = None if shard is None else ("rows" if row_sharded else "row_groups")
+        readers = [ParquetDeviceReader(p, feats + targets, device=device,
+                                       row_groups=None if picks is None else picks[pi])
+                   for pi, p in enumerate(parts)]
+        readers = [r for r in readers if r.rows > 0] or readers[:1]
         total = sum(r.rows for r in readers)
         out = torch.empty(total, len(feats) + len(targets), dtype=torch.float32, device=readers[0].device)
         r0 = 0

@@ -24,10 +24,11 @@ class ParquetDeviceReader:
     """``ParquetDeviceReader(path, columns).read()`` -> fp32 tensor [rows, len(columns)] in HBM.
 
     ``shard=(n, i)`` keeps every n-th row group starting at i (petastorm's ``shard_count`` /
-    ``cur_shard``); ``depth`` pinned staging slots (double buffering by default)."""
+    ``cur_shard``), ``row_groups`` an explicit list; ``depth`` pinned staging slots (double buffering
+    by default)."""
 
     def __init__(self, path, columns, device=None, shard: tuple[int, int] | None = None, depth: int = 2,
-                 threads: bool = True):
+                 threads: bool = True, row_groups=None):
         import pyarrow.parquet as pq
 
         self.pf = pq.ParquetFile(str(path))
@@ -36,7 +37,9 @@ class ParquetDeviceReader:
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         md = self.pf.metadata
         groups = list(range(md.num_row_groups))
-        if shard is not None:
+        if row_groups is not None:  # an explicit subset (a dataset-wide row-group shard, see to_device)
+            groups = [g for g in row_groups if 0 <= g < md.num_row_groups]
+        elif shard is not None:
             n, i = shard
             groups = groups[i::n]
         self.groups = groups

@@ -89,3 +89,20 @@ def test_cifar_benchmark_runs_through_collective_allreduce(tmp_path):
     assert rec["n_gpus"] == 2 and rec["config"]["launcher"] == "experiment.collective_allreduce"
     assert rec["log"].endswith("chief_0_output.log") and rec["replicas_identical"] is True
     assert os.path.isdir(rec["experiment_dir"])
+
+
+def test_titanic_td_benchmark_four_ranks_row_group_sharded(tmp_path):
+    """BASELINE config 4 at 4 ranks (gloo rehearsal): the Titanic TD is written once as Parquet with
+    64k-row row groups and every rank of experiment.mirrored reads only its row groups."""
+    env = _env()
+    env["HOPSX_PROJECT_ROOT"] = str(tmp_path / "proj")
+    env["TMPDIR"] = str(tmp_path)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "run.py"), "titanic", "--gpus", "4",
+                        "--rehearse", "--steps", "2", "--warmup", "1", "--rows", "262144"], cwd=str(tmp_path),
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 4 and rec["config"]["launcher"] == "experiment.mirrored"
+    assert rec["shard_mode"] == "row_groups" and rec["rows_per_rank"] == 65536
+    assert [x["rows"] for x in rec["config"]["ranks"]] == [65536] * 4
+    assert rec["replicas_identical"] is True

@@ -45,7 +45,7 @@ def test_wgrad_glds_direct(B, H, C, CO, k, stride, pad):
         return
     base = torch.randn(CO, k * k * C, device=dev)
     dw = base.clone()
-    rc = _C.ext().conv2d_wgrad_glds(K.ptr(dy), K.ptr(x), g, K.ptr(dw), K.stream())
+    rc = _C.ext().conv2d_wgrad_glds(K.ptr(dy), K.ptr(x), g, K.ptr(dw), 1, K.stream())
     assert rc == 0
     torch.cuda.synchronize()
     ref = _ref(dy, x, CO, C, k, stride, pad)

@@ -53,11 +53,16 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true", help="also time PyTorch's weight gradient")
+    ap.add_argument("--glds-only", action="store_true", help="skip the conv2d_wgrad dispatch timing")
+    ap.add_argument("--only", default="", help="H,C,CO,k,s of the one layer to run (profiling)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
     tot = {"glds": 0.0, "dispatch": 0.0, "torch": 0.0}
+    only = tuple(int(v) for v in a.only.split(",")) if a.only else None
     for (H, C, CO, k, s, n) in LAYERS:
+        if only and (H, C, CO, k, s) != only:
+            continue
         B = a.batch
         x = torch.randn(B, H, H, C, device=dev).to(bf)
         g = K.conv_geom(x.shape, (CO, k, k, C), (s, s), (k // 2, k // 2), (1, 1))
@@ -66,13 +71,13 @@ def main():
         flop = 2.0 * B * g[4] * g[5] * CO * k * k * C
         row = {"H": H, "C": C, "CO": CO, "k": k, "s": s, "n": n}
         if _C.ext().conv_wgrad_glds_ok(g):
-            us = timeit(lambda: _C.ext().conv2d_wgrad_glds(K.ptr(dy), K.ptr(x), g, K.ptr(dw), K.stream()), a.iters)
+            us = timeit(lambda: _C.ext().conv2d_wgrad_glds(K.ptr(dy), K.ptr(x), g, K.ptr(dw), 1, K.stream()), a.iters)
             row["glds_us"] = round(us, 1)
             row["glds_tf"] = round(flop / us / 1e6, 1)
             tot["glds"] += us * n
-        us = timeit(lambda: K.conv2d_wgrad(dy, x, g, dw), a.iters)
+        us = timeit(lambda: K.conv2d_wgrad(dy, x, g, dw), a.iters) if not a.glds_only else 0.0
         row["disp_us"] = round(us, 1)
-        row["disp_tf"] = round(flop / us / 1e6, 1)
+        row["disp_tf"] = round(flop / us / 1e6, 1) if us else 0.0
         tot["dispatch"] += us * n
         if a.torch:
             xt = x.permute(0, 3, 1, 2)
