@@ -116,6 +116,12 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_wgrad_glds(P<void>(dy), P<void>(x), g.data(), P<float>(dw), force, S(st));
   });
   m.def("conv_wgrad_glds_ok", [](std::vector<int> g) { return hopsx_conv_wgrad_glds_ok(g.data()); });
+  m.def("cols_to_f32", [](std::vector<u> cols, std::vector<int> dtypes, long rows, u out, long ld, u st) {
+    std::vector<const void*> cp(cols.size());
+    for (size_t j = 0; j < cols.size(); ++j) cp[j] = P<void>(cols[j]);
+    if (dtypes.size() != cols.size()) return -2;
+    return hopsx_cols_to_f32(cp.data(), dtypes.data(), (int)cols.size(), rows, P<float>(out), ld, S(st));
+  });
   m.def("maxpool2d_fwd", [](u x, u y, u am, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int sh,
                             int sw, int ph, int pw, float p, u rng, unsigned salt, u st) {
     return hopsx_maxpool2d_fwd(P<void>(x), P<void>(y), P<unsigned char>(am), B, H, W, C, OH, OW, KH, KW, sh, sw, ph,

@@ -5,6 +5,7 @@
 // The gathers run inside the LDS staging of gemm_core.h, so no im2col buffer
 // ever touches HBM.
 #include "gemm_core.h"
+#include "gemm_glds.h"
 #include "ops_api.h"
 
 using namespace hopsx;
@@ -285,6 +286,32 @@ static bool direct_ok(const ConvGeom& g) {
   return K <= 64 && g.CO % 4 == 0 && g.CO <= 256 && K * g.CO <= 1024 && !hopsx_disabled("direct_conv");
 }
 
+// The gg engine (gemm_glds.h: LDS-DMA ring, 128x256 / 256x128 tiles) for the conv GEMMs it fills the
+// chip with; false -> nothing launched, the caller keeps gemm_core.h's engine.  A 1x1 / stride-1 /
+// unpadded conv reads X (forward) and dY (dgrad) as plain [pixels][channels] matrices.
+static bool gg_1x1(const ConvGeom& g) {
+  return g.KH == 1 && g.KW == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
+}
+
+template <class EP>
+static bool gg_conv_fwd(const void* x, const void* w, const ConvGeom& g, const EP& e, hipStream_t st) {
+  const int M = g.B * g.OH * g.OW, N = g.CO, K = g.KH * g.KW * g.C;
+  if (g.C % 8 || g.CO % 8 || ((uintptr_t)x | (uintptr_t)w) % 16 || hopsx_disabled("gg_fwd")) return false;
+  const GgDense ws{(const bf16_raw*)w, (long)K, N, K};
+  if (gg_1x1(g)) return launch_gg<true, true>(GgDense{(const bf16_raw*)x, (long)g.C, M, K}, ws, e, M, N, K, false, st);
+  return launch_gg<true, true>(GgIm2col{(const bf16_raw*)x, g, M, K}, ws, e, M, N, K, false, st);
+}
+
+template <class EP>
+static bool gg_conv_dgrad(const void* dy, const void* w, const ConvGeom& g, const EP& e, hipStream_t st) {
+  const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
+  if (g.C % 8 || g.CO % 8 || ((uintptr_t)dy | (uintptr_t)w) % 16 || hopsx_disabled("gg_dgrad")) return false;
+  const GgWeightT ws{(const bf16_raw*)w, g, K, N};
+  if (gg_1x1(g))
+    return launch_gg<true, false>(GgDense{(const bf16_raw*)dy, (long)g.CO, M, K}, ws, e, M, N, K, false, st);
+  return launch_gg<true, false>(GgDgradA{(const bf16_raw*)dy, g, M, K}, ws, e, M, N, K, false, st);
+}
+
 extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, void* out,
                                 const float* bias, int act, float* colsum, float xscale, float xshift,
                                 hipStream_t st) {
@@ -307,6 +334,7 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
   DenseLoader bl{(const bf16_raw*)w, K, is_vec_ok(w, K)};
   if (epi == EPI_STORE_BF16) {
     EpiStoreBF16 e{(bf16_raw*)out, N, bias, 1.f, act, colsum};
+    if (gg_conv_fwd(x, w, g, e, st)) return (int)hipGetLastError();
     launch_gemm<true, true>(al, bl, e, M, N, K, false, st);
   } else if (epi == EPI_STORE_F32) {
     EpiStoreF32 e{(float*)out, N, bias, 1.f, 0.f, act, colsum};
@@ -328,6 +356,7 @@ extern "C" int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int*
   Im2colLoader al{(const bf16_raw*)x, g, 1};
   DenseLoader bl{(const bf16_raw*)w, K, is_vec_ok(w, K)};
   EpiBnStatsBF16 e{(bf16_raw*)out, N, bnacc};
+  if (gg_conv_fwd(x, w, g, e, st)) return (int)hipGetLastError();
   launch_gemm<true, true>(al, bl, e, M, N, K, false, st);
   return (int)hipGetLastError();
 }
@@ -347,6 +376,7 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
                       (const bf16_raw*)y, yact};
   ConvWeightTLoader bl{(const bf16_raw*)w, g, (g.C % 8 == 0) && ((uintptr_t)w % 16 == 0)};
   EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act, colsum};
+  if (!y && gg_conv_dgrad(dy, w, g, e, st)) return (int)hipGetLastError();
   launch_gemm<true, false>(al, bl, e, M, N, K, false, st);
   return (int)hipGetLastError();
 }

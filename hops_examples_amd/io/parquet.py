@@ -2,17 +2,21 @@
 path (Parquet on HopsFS -> tensor) streams into 288 GB HBM via pinned hipMemcpyAsync on a side
 stream").
 
-Row groups are decoded by Arrow's C++ reader (multi-threaded); the RAW column buffers (int64,
-float64, float32, int32, bool — whatever the file stores) are copied into a reusable pinned
-staging ring, sent host->device on a side stream as ONE copy per chunk, and converted +
-interleaved into the row-major fp32 destination on the GPU.  The host never converts, stacks or
-re-pins anything, and the decode of chunk i+1 overlaps the transfer and conversion of chunk i.
+Row groups are decoded by Arrow's C++ reader on a pool of worker threads (one ParquetFile handle
+per thread; Arrow and torch's copy release the GIL); each worker packs its row group's RAW column
+buffers (int64, float64, float32, int32, bool — whatever the file stores) into a slot of a reusable
+pinned staging ring, and the main thread sends every slot host->device on a side stream as ONE
+copy and converts + interleaves all its columns into the row-major fp32 destination with ONE
+hopsx kernel (columns.hip).  The host never converts, stacks or re-pins anything; decodes of the
+next row groups overlap the transfer and conversion of the current one.
 
 Reference parity: the training-dataset readers the notebooks use (``td.read()``,
 ``tf_data(...).tf_record_dataset``; notebooks/featurestore/hsfs/basics/training_datasets.ipynb:
 463-526) and petastorm's Parquet readers (PetastormHelloWorld.ipynb:864-899, sharding by row group).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -28,10 +32,11 @@ class ParquetDeviceReader:
     by default)."""
 
     def __init__(self, path, columns, device=None, shard: tuple[int, int] | None = None, depth: int = 2,
-                 threads: bool = True, row_groups=None):
+                 threads: bool = True, row_groups=None, workers: int | None = None):
         import pyarrow.parquet as pq
 
-        self.pf = pq.ParquetFile(str(path))
+        self._path = str(path)
+        self.pf = pq.ParquetFile(self._path)
         self.columns = list(columns)
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
@@ -46,14 +51,16 @@ class ParquetDeviceReader:
         self.rows = sum(md.row_group(g).num_rows for g in groups)
         self.depth = max(1, depth)
         self.threads = threads
+        # row groups decoded + packed in parallel (Arrow and torch's copy release the GIL)
+        self.workers = workers or int(os.environ.get("HOPSX_PARQUET_WORKERS", min(8, os.cpu_count() or 4)))
         self._slots = None
         self._stream = None
         self.bytes_read = 0  # raw column bytes moved host -> device by the last read()
 
     # ---------------------------------------------------------------- host side
-    def _decode(self, g: int):
+    def _decode(self, g: int, pf=None):
         """One row group -> list of numpy views of the raw column buffers (zero-copy where Arrow allows)."""
-        tbl = self.pf.read_row_group(g, columns=self.columns, use_threads=self.threads)
+        tbl = (pf or self.pf).read_row_group(g, columns=self.columns, use_threads=self.threads)
         cols = []
         for c in self.columns:
             a = tbl.column(c)
@@ -106,34 +113,67 @@ class ParquetDeviceReader:
             return out
         if self._stream is None:
             self._stream = torch.cuda.Stream(self.device)
+        from ..ops import kernels as K
+
         cur = torch.cuda.current_stream(self.device)
         self._stream.wait_stream(cur)  # out may have been allocated / used on the current stream
-        r0 = 0
-        moved = 0
-        for i, g in enumerate(self.groups):
-            cols = self._decode(g)  # overlaps the previous chunk's copy + conversion on the GPU
-            m = len(cols[0])
+        n_g = len(self.groups)
+        nthreads = max(1, min(self.workers, n_g))
+        depth = max(self.depth, nthreads + 1)
+        if self._slots is not None and len(self._slots) < depth:
+            self._slots = None
+        self.depth = depth
+        import threading
+        from concurrent.futures import ThreadPoolExecutor
+
+        local = threading.local()
+
+        def decode_pack(i: int, g: int, wait_ev):
+            """Worker: decode row group g (its own ParquetFile handle: Arrow readers are not shared
+            across threads), then pack the raw column buffers into pinned slot i % depth once the
+            H2D copy that last read that slot has completed (wait_ev)."""
+            if not hasattr(local, "pf"):
+                import pyarrow.parquet as pq
+
+                local.pf = pq.ParquetFile(self._path)
+            cols = self._decode(g, local.pf)
             offs, nb = [], 0
             for v in cols:
                 offs.append(nb)
                 nb += -(-v.nbytes // _ALIGN) * _ALIGN
-            slots = self._slot(nb)
-            host, dev, ev = slots[i % self.depth]
-            if ev is not None:
-                ev.synchronize()  # the H2D that last read this pinned slot has completed
-            hv = host.numpy()
+            if wait_ev is not None:
+                wait_ev.synchronize()
+            host = self._slots[i % depth][0]
             for v, o in zip(cols, offs):
-                hv[o:o + v.nbytes] = v.view(np.uint8).reshape(-1)
-            with torch.cuda.stream(self._stream):
-                dev[:nb].copy_(host[:nb], non_blocking=True)  # one hipMemcpyAsync per chunk
-                for j, (v, o) in enumerate(zip(cols, offs)):
-                    src = dev[o:o + v.nbytes].view(_torch_dtype(v.dtype))
-                    out[r0:r0 + m, j].copy_(src)  # convert + interleave on the GPU
-                e = torch.cuda.Event()
-                e.record(self._stream)
-            slots[i % self.depth][2] = e
-            r0 += m
-            moved += nb
+                # torch's copy_ releases the GIL (the workers' packs run in parallel)
+                host[o:o + v.nbytes].copy_(torch.from_numpy(v.view(np.uint8).reshape(-1)))
+            return cols, offs, nb
+
+        # size the ring from the metadata before any worker writes into it
+        self._slot(0)
+        r0 = 0
+        moved = 0
+        events = [None] * depth
+        with ThreadPoolExecutor(max_workers=nthreads) as ex:
+            futs = {}
+            for i in range(min(depth, n_g)):
+                futs[i] = ex.submit(decode_pack, i, self.groups[i], None)
+            for i in range(n_g):
+                cols, offs, nb = futs.pop(i).result()
+                m = len(cols[0])
+                host, dev, _ = self._slots[i % depth]
+                with torch.cuda.stream(self._stream):
+                    dev[:nb].copy_(host[:nb], non_blocking=True)  # one hipMemcpyAsync per row group
+                    srcs = [dev[o:o + v.nbytes].view(_torch_dtype(v.dtype)) for v, o in zip(cols, offs)]
+                    K.cols_to_f32(srcs, out[r0:r0 + m])  # convert + interleave: one launch per row group
+                    e = torch.cuda.Event()
+                    e.record(self._stream)
+                events[i % depth] = e
+                nxt = i + depth
+                if nxt < n_g:
+                    futs[nxt] = ex.submit(decode_pack, nxt, self.groups[nxt], e)
+                r0 += m
+                moved += nb
         cur.wait_stream(self._stream)
         out.record_stream(cur)
         self.bytes_read = moved

@@ -413,6 +413,24 @@ def cast_f32_bf16(x, out=None):
     return out
 
 
+_COL_DT = {torch.float32: 0, torch.float64: 1, torch.int64: 2, torch.int32: 3, torch.int16: 4, torch.int8: 5,
+           torch.uint8: 6, torch.float16: 7}
+
+
+def cols_to_f32(cols, out):
+    """Interleave 1-D device columns (any of int8..int64 / f16 / f32 / f64, equal length) into the
+    fp32 matrix ``out`` [rows, >= len(cols)] (row stride out.stride(0)) in ONE launch."""
+    rows = out.shape[0]
+    if any(c.numel() != rows or c.device != out.device for c in cols):
+        raise ValueError("cols_to_f32: every column must have out.shape[0] elements on out's device")
+    _req(out, F32, "out", contiguous=False)
+    if out.stride(1) != 1:
+        raise ValueError("cols_to_f32: out must have unit column stride")
+    dts = [_COL_DT[c.dtype] for c in cols]
+    check(_C.ext().cols_to_f32([ptr(c) for c in cols], dts, rows, ptr(out), out.stride(0), stream()), "cols_to_f32")
+    return out
+
+
 def u8_normalize_chan(x, scale, shift, reverse=False, out=None):
     """uint8 NHWC [..., C] -> bf16, per channel x * scale[c] + shift[c] (channel order reversed first
     with ``reverse``: RGB -> BGR)."""

@@ -39,3 +39,22 @@ def test_parquet_reader_cpu(tmp_path):
 @pytest.mark.gpu
 def test_parquet_reader_gpu(tmp_path):
     _check(torch.device("cuda", 0), tmp_path)
+
+
+@pytest.mark.gpu
+def test_cols_to_f32_all_dtypes():
+    """columns.hip: every supported column dtype, a row stride wider than k, a partial last block."""
+    from hops_examples_amd.ops import kernels as K
+
+    dev = torch.device("cuda", 0)
+    n = 1000 + 37
+    g = torch.Generator().manual_seed(0)
+    cols = [torch.randn(n, generator=g).to(torch.float64), torch.randn(n, generator=g),
+            torch.randint(-2**40, 2**40, (n,), generator=g), torch.randint(-1000, 1000, (n,), generator=g).int(),
+            torch.randint(-300, 300, (n,), generator=g).short(), torch.randint(-100, 100, (n,), generator=g).to(torch.int8),
+            torch.randint(0, 255, (n,), generator=g).to(torch.uint8), torch.randn(n, generator=g).half()]
+    out = torch.full((n, len(cols) + 3), -7.0, device=dev)
+    K.cols_to_f32([c.to(dev) for c in cols], out[:, 1:1 + len(cols)])
+    want = torch.stack([c.to(torch.float32) for c in cols], 1)
+    torch.testing.assert_close(out[:, 1:1 + len(cols)].cpu(), want, rtol=0, atol=0)
+    assert (out[:, 0] == -7).all() and (out[:, -2:] == -7).all()

@@ -64,3 +64,32 @@ def test_wgrad_glds_via_dispatch():
     K.conv2d_wgrad(dy, x, g, dw)
     ref = _ref(dy, x, CO, C, 3, 1, 1)
     torch.testing.assert_close(dw.reshape(CO, -1), ref, atol=1e-2 * ref.abs().max().item(), rtol=1e-2)
+
+
+FWD_CASES = [  # B, H, C, CO, k, stride  (big enough that the gg engine takes them)
+    (8, 56, 64, 256, 1, 1),
+    (32, 28, 128, 128, 3, 1),
+    (32, 56, 64, 128, 3, 2),
+    (16, 28, 256, 512, 1, 2),
+]
+
+
+@pytest.mark.parametrize("B,H,C,CO,k,stride", FWD_CASES)
+def test_gg_conv_fwd_and_dgrad(B, H, C, CO, k, stride):
+    """Forward (KC x KC: dense or im2col rows) and dgrad (KC dY gather x RC transposed weight) on the gg
+    engine vs fp32 PyTorch."""
+    torch.manual_seed(7)
+    pad = k // 2
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    w = (torch.randn(CO, k, k, C, device=dev) * 0.05).to(bf)
+    g = K.conv_geom(x.shape, w.shape, (stride, stride), (pad, pad), (1, 1))
+    y = K.conv2d_fwd(x, w, g)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=stride, padding=pad)
+    ref = ref.permute(0, 2, 3, 1)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
+    dy = torch.randn(B, g[4], g[5], CO, device=dev).to(bf)
+    dx = K.conv2d_dgrad(dy, w, g)
+    xr = torch.zeros(B, C, H, H, device=dev, requires_grad=True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2), stride=stride, padding=pad).backward(dy.float().permute(0, 3, 1, 2))
+    rdx = xr.grad.permute(0, 2, 3, 1)
+    torch.testing.assert_close(dx.float(), rdx, atol=2e-2 * rdx.abs().max().item(), rtol=2e-2)
