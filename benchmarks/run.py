@@ -228,7 +228,9 @@ def titanic_record(rows: int, batch: int, steps: int, warmup: int) -> dict:
     box = {}
     el, loss = _train_loop(net, opt, "bce", xs, ys, steps, warmup, dev, world, box=box)
     dp = box.get("dp")
-    extra = {"ingest_GBps_parquet_to_hbm_per_rank": round(gbps, 3), "rows_per_rank": int(local_rows),
+    extra = {"ingest_GBps_parquet_to_hbm_per_rank": round(gbps, 3),
+             "ingest_raw_column_GBps_per_rank": round(getattr(td, "last_read_bytes", 0) / ingest / 1e9, 3),
+             "rows_per_rank": int(local_rows),
              "shard_mode": getattr(td, "last_shard_mode", None), "final_loss": round(loss, 4),
              "dtype": "bf16" if dev.type == "cuda" else "fp32"}
     if dp is not None and hasattr(dp, "verify_replicas"):

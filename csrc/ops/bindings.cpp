@@ -36,9 +36,10 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_conv2d_fwd(P<void>(x), P<void>(w), g.data(), epi, P<void>(out), P<float>(bias), act,
                             P<float>(colsum), xscale, xshift, S(st));
   });
-  m.def("conv2d_dgrad", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact, u st) {
+  m.def("conv2d_dgrad", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact, u addend,
+                           u st) {
     return hopsx_conv2d_dgrad(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act, P<float>(colsum),
-                              P<void>(y), yact, S(st));
+                              P<void>(y), yact, P<void>(addend), S(st));
   });
   m.def("widedeep_slots", [](std::vector<long> iv, u out, long n) {
     return hopsx_widedeep_slots(iv.data(), (int)iv.size(), P<int>(out), n);

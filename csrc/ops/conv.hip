@@ -302,11 +302,18 @@ static bool gg_conv_fwd(const void* x, const void* w, const ConvGeom& g, const E
   return launch_gg<true, true>(GgIm2col{(const bf16_raw*)x, g, M, K}, ws, e, M, N, K, false, st);
 }
 
-template <class EP>
-static bool gg_conv_dgrad(const void* dy, const void* w, const ConvGeom& g, const EP& e, hipStream_t st) {
+static bool gg_conv_dgrad(const void* dy, const void* w, const ConvGeom& g, const EpiDActBF16& e, hipStream_t st) {
   const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
   if (g.C % 8 || g.CO % 8 || ((uintptr_t)dy | (uintptr_t)w) % 16 || hopsx_disabled("gg_dgrad")) return false;
   const GgWeightT ws{(const bf16_raw*)w, g, K, N};
+  if (g.KH == 1 && g.KW == 1 && g.ph == 0 && g.pw == 0 && (g.sh > 1 || g.sw > 1) && g.H == g.OH * g.sh &&
+      g.W == g.OW * g.sw && !e.colsum && !hopsx_disabled("dgrad_scatter")) {
+    const int Mo = g.B * g.OH * g.OW;
+    EpiDgradScatterBF16 es{e.out, e.y, e.act, e.add, g.C, g.W, g.OW, g.OH * g.OW, g.sh, g.sw, {}, {}, nullptr};
+    es.fOW.init(g.OW);
+    es.fOHW.init(g.OH * g.OW);
+    return launch_gg<true, false>(GgDense{(const bf16_raw*)dy, (long)g.CO, Mo, K}, ws, es, Mo, N, K, false, st);
+  }
   if (gg_1x1(g))
     return launch_gg<true, false>(GgDense{(const bf16_raw*)dy, (long)g.CO, M, K}, ws, e, M, N, K, false, st);
   return launch_gg<true, false>(GgDgradA{(const bf16_raw*)dy, g, M, K}, ws, e, M, N, K, false, st);
@@ -365,8 +372,9 @@ extern "C" int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int*
 // act'(yprev) — the backward of the activation that produced this conv's input
 // — and `colsum` receives that layer's bias gradient.
 extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
-                                  int act, float* colsum, const void* y, int yact, hipStream_t st) {
-  if (hopsx_conv_dgrad_mfma_ok(geom) && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
+                                  int act, float* colsum, const void* y, int yact, const void* addend,
+                                  hipStream_t st) {
+  if (!addend && hopsx_conv_dgrad_mfma_ok(geom) && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
       ((uintptr_t)dx % 16 == 0) && ((uintptr_t)yprev % 16 == 0))
     return hopsx_conv2d_dgrad_mfma(dy, w, geom, dx, yprev, act, colsum, y, yact, st);
   ConvGeom g = make_geom(geom);
@@ -375,7 +383,7 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
                       (g.CO % 8 == 0) && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)y % 16 == 0),
                       (const bf16_raw*)y, yact};
   ConvWeightTLoader bl{(const bf16_raw*)w, g, (g.C % 8 == 0) && ((uintptr_t)w % 16 == 0)};
-  EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act, colsum};
+  EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act, colsum, (const bf16_raw*)addend};
   if (!y && gg_conv_dgrad(dy, w, g, e, st)) return (int)hipGetLastError();
   launch_gemm<true, false>(al, bl, e, M, N, K, false, st);
   return (int)hipGetLastError();

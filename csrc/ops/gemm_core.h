@@ -328,9 +328,11 @@ struct EpiDActBF16 {
   const bf16_raw* y;
   long ldy;
   int act;
-  float* colsum;  // optional: bias gradient of the layer that produced y
+  float* colsum;        // optional: bias gradient of the layer that produced y
+  const bf16_raw* add;  // optional: a gradient to add (a ResNet identity shortcut's), same layout as out
   __device__ __forceinline__ float operator()(int m, int n, float v) const {
     if (y) v *= act_grad_from_out(bf2f(y[(long)m * ldy + n]), act);
+    if (add) v += bf2f(add[(long)m * ldo + n]);
     out[(long)m * ldo + n] = f2bf(v);
     return v;
   }

@@ -201,6 +201,36 @@ struct EpiAtomicF32T {
   }
 };
 
+// dgrad of a 1x1 / stride-s / unpadded conv as a DENSE GEMM over dY's pixels (M = B*OH*OW): the
+// input pixel (oh*sh, ow*sw) gets the product, the rest of its s x s block only zeros (the implicit
+// GEMM over dX's pixels would stage and multiply zero taps for (s*s - 1) / (s*s) of its rows).
+// Requires H == OH*sh, W == OW*sw (the blocks tile dX exactly); act' of yprev and the added gradient
+// as EpiDActBF16; no column sum.
+struct EpiDgradScatterBF16 {
+  bf16_raw* out;
+  const bf16_raw* yprev;
+  int act;
+  const bf16_raw* add;
+  int C, W, OW, OHW, sh, sw;
+  FastDiv fOW, fOHW;
+  float* colsum;  // always null (interface)
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    const int b = fOHW.div(m), r = m - b * OHW;
+    const int oh = fOW.div(r), ow = r - oh * OW;
+    const long H = (long)OHW / OW * sh;
+    const long base = (((long)b * H + (long)oh * sh) * W + (long)ow * sw) * C + n;
+    for (int dy = 0; dy < sh; ++dy)
+      for (int dx = 0; dx < sw; ++dx) {
+        const long pos = base + ((long)dy * W + dx) * C;
+        float val = 0.f;
+        if (dy == 0 && dx == 0) val = yprev ? v * act_grad_from_out(bf2f(yprev[pos]), act) : v;
+        if (add) val += bf2f(add[pos]);
+        out[pos] = f2bf(val);
+      }
+    return v;
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------------------------

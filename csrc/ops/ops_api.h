@@ -28,7 +28,7 @@ int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, int epi, voi
                      float* colsum, float xscale, float xshift, hipStream_t st);
 // y/yact: this conv's activation output -> fused act' mask on dY (prologue fusion)
 int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act,
-                       float* colsum, const void* y, int yact, hipStream_t st);
+                       float* colsum, const void* y, int yact, const void* addend, hipStream_t st);
 // dbias (optional) receives sum over pixels of the (masked) dY = the conv bias gradient
 // ws (optional, >= 1024*(K*CO+CO) floats): slab workspace for the small-K direct kernel
 int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom, float* dw, float* dbias, const void* y,

@@ -336,16 +336,12 @@ class TrainingDataset(CamelCaseAPI):
             else:
                 picks, keep = mine, min(per)
         self.last_shard_mode = None if shard is None else ("rows" if row_sharded else "row_groups")
-        readers = [ParquetDeviceReader(p, feats + targets, device=device,
-                                       row_groups=None if picks is None else picks[pi])
-                   for pi, p in enumerate(parts)]
-        readers = [r for r in readers if r.rows > 0] or readers[:1]
-        total = sum(r.rows for r in readers)
-        out = torch.empty(total, len(feats) + len(targets), dtype=torch.float32, device=readers[0].device)
-        r0 = 0
-        for r in readers:
-            r.read(out[r0:r0 + r.rows])
-            r0 += r.rows
+        # every part through ONE reader pipeline (decode pool, pinned ring, one convert per row group)
+        rd = ParquetDeviceReader([str(p) for p in parts], feats + targets, device=device, row_groups=picks)
+        total = rd.rows
+        out = torch.empty(total, len(feats) + len(targets), dtype=torch.float32, device=rd.device)
+        rd.read(out)
+        self.last_read_bytes = rd.bytes_read
         if row_sharded:
             n, i = shard
             out = out[i::n][:total // n]

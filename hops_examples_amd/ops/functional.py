@@ -264,13 +264,17 @@ def _pad_same(k, d=1):
     return tot // 2
 
 
+# HOPSX_PLAIN_GEMM=blaslt: the epilogue-free 1x1 convs' forward / dgrad on the vendor library GEMM
+# (torch.mm -> hipBLASLt) instead of the hopsx kernels (gg engine where it fills the chip)
+_PLAIN_LIB = os.environ.get("HOPSX_PLAIN_GEMM", "hopsx") == "blaslt"
+
+
 def _plain_gemm_conv(g, b, act, in_affine, prev) -> bool:
     """A 1x1 / stride-1 / unpadded conv with no epilogue (bias, activation) and no fused input layer
-    is a plain GEMM over [B*H*W, C] x [C, CO]: its forward and dgrad go to the hipBLASLt library GEMM
-    (the plain-GEMM case the kernel library leaves to the vendor library; ResNet-50 B=64 +8 %), its
-    weight gradient (a K = B*H*W reduction) stays on the split-K MFMA kernel, which measured faster
-    than the library's fp32-out path there (HOPSX_BLASLT_WGRAD=1 to compare).  Everything with a
-    fused prologue or epilogue stays on the hand-written MFMA kernels."""
+    is a plain GEMM over [B*H*W, C] x [C, CO]: forward and dgrad run as dense GEMMs on the hopsx
+    kernels (gg engine, gemm_glds.h; the dgrad epilogue adds a shortcut's gradient), or on the
+    vendor library with HOPSX_PLAIN_GEMM=blaslt; the weight gradient (a K = B*H*W reduction) stays
+    on the hopsx kernels (HOPSX_BLASLT_WGRAD=1 to compare the library's fp32-out path)."""
     B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw = g[:13]
     return (KH == 1 and KW == 1 and sh == 1 and sw == 1 and ph == 0 and pw == 0 and b is None and not act
             and in_affine is None and prev is None and B * H * W >= _PLAIN_MIN_PX and C % 8 == 0 and CO % 8 == 0
@@ -317,7 +321,10 @@ class _Conv2dFn(torch.autograd.Function):
             x = x.contiguous()
             wb = _arena.weight_bf16(w)
             C, CO = g[3], g[6]
-            y = torch.mm(x.view(-1, C), wb.view(CO, C).t()).view(g[0], g[4], g[5], CO)
+            if _PLAIN_LIB:
+                y = torch.mm(x.view(-1, C), wb.view(CO, C).t()).view(g[0], g[4], g[5], CO)
+            else:
+                y = K.conv2d_fwd(x, wb, g)
             ctx.save_for_backward(x, y)
             ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
             ctx.plain = True
@@ -346,10 +353,14 @@ class _Conv2dFn(torch.autograd.Function):
             dy2 = dy.to(BF16).contiguous().view(-1, CO)
             dx = None
             if ctx.needs_input_grad[0]:
-                dx = torch.mm(dy2, _arena.weight_bf16(w).view(CO, C)).view(x.shape)
                 addend = _take_addend(ctx)
-                if addend is not None:
-                    dx.add_(addend)
+                if _PLAIN_LIB:
+                    dx = torch.mm(dy2, _arena.weight_bf16(w).view(CO, C)).view(x.shape)
+                    if addend is not None:
+                        dx.add_(addend)
+                else:  # the shortcut's gradient is added in the dgrad epilogue (no separate add launch)
+                    dx = K.conv2d_dgrad(dy2.view(dy.shape), _arena.weight_bf16(w), g,
+                                        addend=None if addend is None else addend.to(BF16).contiguous().view(x.shape))
             gw = _wgrad_buf(w)
             if os.environ.get("HOPSX_BLASLT_WGRAD", "0") != "1":
                 # the library's fp32-out tall-skinny reductions (K = B*H*W) measured slower than the
@@ -421,7 +432,10 @@ class _Conv2dFn(torch.autograd.Function):
             hooks.grad_ready(w0)
             hooks.grad_ready(b0)
         elif ctx.needs_input_grad[0]:
-            dx = _add_addend(ctx, K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act))
+            addend = _take_addend(ctx)  # a shortcut's gradient of x: added in the dgrad epilogue
+            if addend is not None:
+                addend = addend.to(BF16).contiguous().view(x.shape)
+            dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act, addend=addend)
         if not side_ok:
             K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
         return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None,

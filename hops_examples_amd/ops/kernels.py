@@ -215,13 +215,19 @@ def conv2d_fwd_pool(x, w, geom, bias=None, act=0, drop_p=0.0, rng=None, salt=0):
     return y, am
 
 
-def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=None, act=0):
+def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=None, act=0, addend=None):
+    """dX = conv_transpose(dY, W) (* act'(yprev)) (+ addend: a gradient of x from another consumer,
+    added in the epilogue; bf16, x's layout)."""
     _req(dy, BF16, "dy")
     B, H, W, C = geom[:4]
     if out is None:
         out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+    if addend is not None:
+        _req(addend, BF16, "addend")
+        if addend.shape != out.shape:
+            raise ValueError("conv2d_dgrad: addend must have the input gradient's shape")
     check(_C.ext().conv2d_dgrad(ptr(dy), ptr(w), geom, ptr(out), ptr(yprev), act_id(act_prev) if yprev is not None
-                                else 0, ptr(colsum), ptr(y), act_id(act), stream()), "conv2d_dgrad")
+                                else 0, ptr(colsum), ptr(y), act_id(act), ptr(addend), stream()), "conv2d_dgrad")
     return out
 
 

@@ -93,3 +93,20 @@ def test_gg_conv_fwd_and_dgrad(B, H, C, CO, k, stride):
     F.conv2d(xr, w.float().permute(0, 3, 1, 2), stride=stride, padding=pad).backward(dy.float().permute(0, 3, 1, 2))
     rdx = xr.grad.permute(0, 2, 3, 1)
     torch.testing.assert_close(dx.float(), rdx, atol=2e-2 * rdx.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,H,C,CO,k,stride", [(8, 56, 64, 256, 1, 1), (16, 28, 256, 512, 1, 2),
+                                               (32, 28, 128, 128, 3, 1)])
+def test_conv_dgrad_addend_epilogue(B, H, C, CO, k, stride):
+    """A shortcut's gradient passed as `addend` is added in the dgrad epilogue (no separate add)."""
+    torch.manual_seed(9)
+    pad = k // 2
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    w = (torch.randn(CO, k, k, C, device=dev) * 0.05).to(bf)
+    g = K.conv_geom(x.shape, w.shape, (stride, stride), (pad, pad), (1, 1))
+    dy = torch.randn(B, g[4], g[5], CO, device=dev).to(bf)
+    add = torch.randn(B, H, H, C, device=dev).to(bf)
+    plain = K.conv2d_dgrad(dy, w, g).float()
+    fused = K.conv2d_dgrad(dy, w, g, addend=add).float()
+    ref = plain + add.float()
+    torch.testing.assert_close(fused, ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
