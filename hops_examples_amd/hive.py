@@ -244,6 +244,11 @@ class HiveConnection:
     def cursor(self):
         return _Cursor(self)
 
+    def register_temp_view(self, name: str, df: pd.DataFrame) -> None:
+        """A session-scoped view over a DataFrame (Spark ``createOrReplaceTempView``): queryable by
+        name, never written to the metastore or the warehouse."""
+        df.to_sql(name, self._conn(), if_exists="replace", index=False)
+
     def close(self):
         for c in self._conns.values():
             c.close()
