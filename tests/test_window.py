@@ -49,3 +49,48 @@ def test_with_range_sums_fills_like_the_reference():
     first = out.sort_values("ts").groupby(["store", "dept"]).head(1)
     assert (first.sales_last_month_store_dep == 0.0).all()  # nothing before the first row -> null -> 0
     assert list(out.columns[:4]) == list(df.columns)
+
+
+def _dp_rank(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        df = _frame(seed=3)
+        wins = [(days(-30), days(-1)), (days(-90), days(-1))]
+        s, c = range_sums(df, ["store", "dept"], "ts", "weekly_sales", wins, device="cpu", with_count=True)
+        q.put((rank, s, c))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_range_sums_data_parallel_gloo():
+    """2 ranks each compute their partitions' windows and all-gather: every rank returns exactly the
+    single-process result (feature engineering as a data-parallel job)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    df = _frame(seed=3)
+    wins = [(days(-30), days(-1)), (days(-90), days(-1))]
+    want, wcnt = range_sums(df, ["store", "dept"], "ts", "weekly_sales", wins, device="cpu", with_count=True,
+                            process_group=False)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dp_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, s, c in res:
+        np.testing.assert_array_equal(np.isnan(s), np.isnan(want))
+        np.testing.assert_allclose(np.nan_to_num(s), np.nan_to_num(want), rtol=1e-12)
+        np.testing.assert_array_equal(c, wcnt)
