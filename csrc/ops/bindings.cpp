@@ -11,7 +11,15 @@
 #include "ops_api.h"
 
 namespace py = pybind11;
-extern "C" void hopsx_mlp_head_debug(void* p);  // loss.hip: phase stamps (tools/dbg_mlp_head.py)
+extern "C" void hopsx_mlp_head_debug(void* p);
+// conv_mfma.hip: the conv backward pair + a fused optimizer's arena-slice update (optim_slice.h)
+extern "C" int hopsx_conv2d_bwd_pair_opt(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                         int act_prev, float* colsum, const void* y, int yact, const int* geom0,
+                                         const void* x0, float xscale, float xshift, float* dw0, const void* x,
+                                         float* dw, float* dbias, const void* addend, int kind, float* p, float* g,
+                                         float* s1, float* s2, float* s3, void* shadow, long n, const float* f,
+                                         const float* hp_dev, const float* step_dev, int nblk, int opt_first,
+                                         hipStream_t st);  // loss.hip: phase stamps (tools/dbg_mlp_head.py)
 using u = uintptr_t;
 
 template <class T>
@@ -54,6 +62,16 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                               unsigned salt, u st) {
     return hopsx_conv2d_fwd_pool(P<void>(x), P<void>(w), g.data(), P<void>(out), P<void>(am), P<float>(bias), act, p,
                                  P<unsigned long long>(rng), salt, S(st));
+  });
+  m.def("conv2d_fwd_pool_in_ok", [](std::vector<int> g0, std::vector<int> g, int act) {
+    return hopsx_conv_fwd_pool_in_ok(g0.data(), g.data(), act);
+  });
+  m.def("conv2d_fwd_pool_in", [](u x0, float xscale, float xshift, u w0, u b0, int act0, std::vector<int> g0, u y1,
+                                 u w, std::vector<int> g, u out, u am, u bias, int act, float p, u rng, unsigned salt,
+                                 u st) {
+    return hopsx_conv2d_fwd_pool_in(P<void>(x0), xscale, xshift, P<void>(w0), P<float>(b0), act0, g0.data(),
+                                    P<void>(y1), P<void>(w), g.data(), P<void>(out), P<void>(am), P<float>(bias), act,
+                                    p, P<unsigned long long>(rng), salt, S(st));
   });
   m.def("conv2d_dgrad_fused_wgrad_ok", [](std::vector<int> g, std::vector<int> g0) {
     return hopsx_conv_dgrad_fused_wgrad_ok(g.data(), g0.data());
@@ -107,6 +125,18 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                                  P<float>(colsum), P<void>(y), yact, g0.empty() ? nullptr : g0.data(), P<void>(x0),
                                  xscale, xshift, P<float>(dw0), P<void>(x), P<float>(dw), P<float>(db), P<void>(add),
                                  S(st));
+  });
+  m.def("conv2d_bwd_pair_opt", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact,
+                                  std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u add,
+                                  int kind, u p, u gr, u s1, u s2, u s3, u sh, long n, std::vector<float> f, u hp_dev,
+                                  u step_dev, int nblk, int opt_first, u st) {
+    if (f.size() < 8) f.resize(8, 0.f);
+    return hopsx_conv2d_bwd_pair_opt(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act,
+                                     P<float>(colsum), P<void>(y), yact, g0.empty() ? nullptr : g0.data(), P<void>(x0),
+                                     xscale, xshift, P<float>(dw0), P<void>(x), P<float>(dw), P<float>(db),
+                                     P<void>(add), kind, P<float>(p), P<float>(gr), P<float>(s1), P<float>(s2),
+                                     P<float>(s3), P<void>(sh), n, f.data(), P<float>(hp_dev), P<float>(step_dev), nblk,
+                                     opt_first, S(st));
   });
   m.def("conv2d_wgrad", [](u dy, u x, std::vector<int> g, u dw, u db, u y, int yact, u ws, long ws_elems,
                            float xscale, float xshift, u counter, u st) {

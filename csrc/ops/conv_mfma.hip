@@ -15,6 +15,7 @@
 
 #include "gemm_core.h"
 #include "ops_api.h"
+#include "optim_slice.h"
 
 using namespace hopsx;
 
@@ -63,18 +64,44 @@ struct PoolEpi {
 // sum of squares of the stored (bf16) outputs into the zero-at-rest replicas
 // bnacc[blockIdx % HOPSX_BN_NREP][2 CO] (norm.hip bn_apply_fin8_k finishes them), so the BN never
 // re-reads its input for statistics.
-template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false>
+//
+// T0 > 0 (IN0): this conv's input is the output of the network's input layer (Cin0 = 1, stride 1, <= 9 taps:
+// the 2x2 / 3x3 first conv of the MNIST models), and that layer is computed INSIDE the operand
+// gather instead of by its own launch: each lane's 8-channel A chunk at (b, ih, iw) is
+// act0(b0 + sum_taps px * w0) from the raw uint8 pixels with the input affine applied, in the
+// same fp32 order as conv.hip conv_direct_fwd_k, rounded to bf16.  Every input-layer element is
+// also stored once (for the backward: this conv's weight gradient and the input layer's ReLU'):
+// by the lane whose conv tap is the first one covering it (kh == 0, or the last output row).
+struct In0 {
+  const void* x0;  // input-layer pixels [B][H0][W0] (C0 = 1), uint8
+  float xscale, xshift;  // the input affine, applied on the fly (xscale != 0)
+  const bf16_raw* w0;  // [C][KH0*KW0] bf16 (C = this conv's Cin)
+  const float* b0;
+  bf16_raw* y1;  // input-layer output [B][H][W][C], written here; nullptr: not kept (inference)
+  int H0, W0, KH0, KW0, ph0, pw0, act0;
+};
+
+template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false, int T0 = 0>
 __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
                                                       const float* __restrict__ bias, bf16_raw* __restrict__ y,
                                                       ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{},
-                                                      float* __restrict__ bnacc = nullptr) {
+                                                      float* __restrict__ bnacc = nullptr, In0 i0 = In0{}) {
   constexpr int CO = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
   constexpr int cpr = KS * 4;  // 16-B chunks per weight row (K padded to 32*KS)
   constexpr int RS = cm_rs(cpr);  // row stride in chunks: the XOR swizzle stays inside the row
   bf16_raw* sw = cm_smem;                                 // [CO][RS*8]
   bf16_raw* scratch = cm_smem + CO * RS * 8;              // [waves][16][CO]
+  // T0: input-layer weights [taps][C] and bias [C] as fp32 after the scratch
+  float* sw0 = (float*)(scratch + CM_WAVES * 16 * CO);
   phase_mark(pe.dbg, 0);
+  if constexpr (T0 > 0) {
+    const int taps = T0 * T0;
+    for (int i = threadIdx.x; i < (taps + 1) * g.C; i += 256) {
+      const int t = i / g.C, c = i - t * g.C;
+      sw0[i] = t < taps ? bf2f(i0.w0[c * taps + t]) : (i0.b0 ? i0.b0[c] : 0.f);
+    }
+  }
   {
     // every staging load leaves before the first LDS write: one memory round trip, not one per
     // chunk (a load + ds_write loop waits for each load in turn)
@@ -112,6 +139,12 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
   for (int nf = 0; nf < NF; ++nf) { st1[nf] = 0.f; st2[nf] = 0.f; }
   for (int g0 = (blockIdx.x * CM_WAVES + wave) * UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
+    // T0: the input layer's pixels / lane bookkeeping of this trip (sized 1 when unused)
+    constexpr int TU = T0 > 0 ? UN : 1, TK = T0 > 0 ? KS : 1, TT = T0 > 0 ? T0 * T0 : 1;
+    unsigned i0px[TU][TK][TT];
+    int i0ci[TU][TK];
+    long i0off[TU][TK];
+    bool i0ok[TU][TK], i0wr[TU][TK];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int px = (g0 + u) * 16 + fr;
@@ -139,8 +172,53 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
         const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
         const bool ok = pok && k0 < K && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
         const long off = ok ? (((long)b * g.H + ih) * g.W + iw) * g.C + ci : 0;
-        a[u][kk] = zero_unless(*(const bf16x8*)(x + off), ok);
+        if constexpr (T0 > 0) {
+          // input layer at (b, ih, iw): issue its T0 x T0 pixel loads now, evaluate after the loop
+          // (every load of the trip in flight before the first use)
+          i0ok[u][kk] = ok;
+          i0ci[u][kk] = ci;
+          i0off[u][kk] = off;
+          i0wr[u][kk] = ok && (kh == 0 || oh == g.OH - 1) && (kw == 0 || ow == g.OW - 1);
+#pragma unroll
+          for (int a0 = 0; a0 < T0; ++a0)
+#pragma unroll
+            for (int c0 = 0; c0 < T0; ++c0) {
+              const int y0 = ih - i0.ph0 + a0, x0c = iw - i0.pw0 + c0;
+              const bool in = ok && y0 >= 0 && y0 < i0.H0 && x0c >= 0 && x0c < i0.W0;
+              const long pi = in ? ((long)b * i0.H0 + y0) * i0.W0 + x0c : 0;
+              const unsigned raw = ((const uint8_t*)i0.x0)[pi];  // one unconditional byte load per tap
+              i0px[u][kk][a0 * T0 + c0] = in ? raw : 0xFFFFFFFFu;
+            }
+        } else {
+          a[u][kk] = zero_unless(*(const bf16x8*)(x + off), ok);
+        }
       }
+    }
+    if constexpr (T0 > 0) {
+      // input layer: act0(b0 + sum_taps px * w0) in conv_direct_fwd_k's fp32 order, bf16-rounded;
+      // stored once (designated lane) for the backward
+#pragma unroll
+      for (int u = 0; u < UN; ++u)
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int ci = i0ci[u][kk];
+          float acc[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = sw0[T0 * T0 * g.C + ci + j];
+#pragma unroll
+          for (int t = 0; t < T0 * T0; ++t) {
+            const unsigned raw = i0px[u][kk][t];
+            const float pv = raw == 0xFFFFFFFFu ? 0.f : fmaf((float)raw, i0.xscale, i0.xshift);
+            const float* wr = sw0 + t * g.C + ci;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = fmaf(pv, wr[j], acc[j]);
+          }
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(apply_act(acc[j], i0.act0));
+          a[u][kk] = zero_unless(v, i0ok[u][kk]);
+          if (i0.y1 && i0wr[u][kk]) *(bf16x8*)(i0.y1 + i0off[u][kk]) = v;
+        }
     }
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
@@ -782,12 +860,29 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(WgradArgs A) {
 // the weight-gradient workgroups (the rest, nBx x nBy) share ONE launch.  The two GEMMs are
 // independent and each alone leaves most CUs idle at small batch; a second stream would run them
 // concurrently too, but a cross-queue dependency costs ~10 us per replayed graph, a launch ~1.5.
+//
+// os.kind >= 0: os.nblk more workgroups run a fused optimizer's update of an arena slice whose
+// gradients are final (optim_slice.h) — first in the grid (opt_first) or after the conv part.
 template <int NF, int KS, int K0, int NFC>
-__global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs B, int nA, int nBx) {
-  if ((int)blockIdx.x < nA) {
-    conv_dgrad_body<NF, KS, K0, 2>(A, blockIdx.x, nA);
+__global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs B, int nA, int nBx,
+                                                          OptSlice os, int opt_first) {
+  int bid = blockIdx.x;
+  if (os.kind >= 0) {
+    if (opt_first) {
+      if (bid < os.nblk) {
+        opt_slice_run(os, bid);
+        return;
+      }
+      bid -= os.nblk;
+    } else if (bid >= (int)gridDim.x - os.nblk) {
+      opt_slice_run(os, bid - ((int)gridDim.x - os.nblk));
+      return;
+    }
+  }
+  if (bid < nA) {
+    conv_dgrad_body<NF, KS, K0, 2>(A, bid, nA);
   } else {
-    const int j = blockIdx.x - nA;
+    const int j = bid - nA;
     conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx);
   }
 }
@@ -1086,16 +1181,63 @@ static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, vo
 // weight gradient, geom0 != null) + the layer's own weight gradient.  Same argument meaning as
 // hopsx_conv2d_dgrad_mfma_ex and hopsx_conv2d_wgrad_mfma; returns -2 for shapes outside the
 // instantiated set (the caller then issues the two launches).
+static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                int act_prev, float* colsum, const void* y, int yact, const int* geom0, const void* x0,
+                                float xscale, float xshift, float* dw0, const void* x, float* dw, float* dbias,
+                                const void* addend, const OptSlice& os, int opt_first, hipStream_t st);
+
 extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                      int act_prev, float* colsum, const void* y, int yact, const int* geom0,
                                      const void* x0, float xscale, float xshift, float* dw0, const void* x,
                                      float* dw, float* dbias, const void* addend, hipStream_t st) {
+  OptSlice none{};
+  none.kind = -1;
+  return conv2d_bwd_pair_impl(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, geom0, x0, xscale, xshift, dw0, x, dw,
+                              dbias, addend, none, 0, st);
+}
+
+// The same launch + a fused optimizer's update of the arena slice [p, p + n) (its gradients final),
+// as `nblk` extra workgroups (optim_slice.h).  f[0..7] = the optimizer's hyper-parameter vector.
+// Returns -2 when the pair kernel does not take the shape (nothing launched: the caller runs the
+// unfused backward and the whole optimizer).
+extern "C" int hopsx_conv2d_bwd_pair_opt(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                         int act_prev, float* colsum, const void* y, int yact, const int* geom0,
+                                         const void* x0, float xscale, float xshift, float* dw0, const void* x,
+                                         float* dw, float* dbias, const void* addend, int kind, float* p, float* g,
+                                         float* s1, float* s2, float* s3, void* shadow, long n, const float* f,
+                                         const float* hp_dev, const float* step_dev, int nblk, int opt_first,
+                                         hipStream_t st) {
+  if (kind < 0 || kind > 6 || n <= 0 || n % 4 || nblk < 1 ||
+      ((uintptr_t)p | (uintptr_t)g | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)s3) % 16 || (uintptr_t)shadow % 8)
+    return -3;
+  OptSlice os{};
+  os.kind = kind;
+  os.nblk = nblk;
+  os.p = p;
+  os.g = g;
+  os.s1 = s1;
+  os.s2 = s2;
+  os.s3 = s3;
+  os.shadow = (bf16_raw*)shadow;
+  os.n4 = n / 4;
+  os.h = OptHP{f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7]};
+  os.hp_dev = hp_dev;
+  os.step_dev = step_dev;
+  return conv2d_bwd_pair_impl(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, geom0, x0, xscale, xshift, dw0, x, dw,
+                              dbias, addend, os, opt_first, st);
+}
+
+static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                int act_prev, float* colsum, const void* y, int yact, const int* geom0, const void* x0,
+                                float xscale, float xshift, float* dw0, const void* x, float* dw, float* dbias,
+                                const void* addend, const OptSlice& os, int opt_first, hipStream_t st) {
   if (hopsx_disabled("bwd_pair") || !hopsx_conv_wgrad_mfma_ok(geom)) return -2;
   const bool fused = geom0 != nullptr;
   if (fused && addend) return -2;
   if ((uintptr_t)addend % 16 != 0) return -3;
   if (!hopsx_conv_dgrad_mfma_ok(geom)) {
     if (addend) return -3;  // the GEMM variant has no addend: call again without it and add afterwards
+    if (os.kind >= 0) return -2;
     return fused ? -2 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, st);
   }
   if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
@@ -1143,13 +1285,13 @@ extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* g
   const size_t redb = ((size_t)4 * (g.CO / 16) * 2 * 64 * 4 + 4 * g.CO + (size_t)g.CO * KB) * sizeof(float);
   const size_t shm = std::max(shmA, std::max(stage, redb));
   const WgradArgs WA{(const bf16_raw*)dy, (const bf16_raw*)x, (const bf16_raw*)y, yact, dw, dbias, g, Kw, cpw, dbg};
-  const long total = nA + nBx * colblk;
+  const long total = nA + nBx * colblk + (os.kind >= 0 ? os.nblk : 0);
   if (shm > 65536 || total > (1L << 20)) return -2;
   const int NF = g.C / 16, NFC = g.CO / 16;
 #define HOPSX_PAIR(NFv, KSv, K0v, NFCv)                                                                      \
   if (NF == NFv && KS == KSv && K0 == K0v && NFC == NFCv) {                                                  \
     hipLaunchKernelGGL((conv_bwd_pair_k<NFv, KSv, K0v, NFCv>), dim3((unsigned)total), dim3(256), shm, st, DA, WA, \
-                       (int)nA, (int)nBx);                                                                     \
+                       (int)nA, (int)nBx, os, opt_first);                                                      \
     return (int)hipGetLastError();                                                                           \
   }
 #define HOPSX_PAIR_K0(NFv, KSv, NFCv) HOPSX_PAIR(NFv, KSv, 0, NFCv) HOPSX_PAIR(NFv, KSv, 4, NFCv)
@@ -1206,5 +1348,55 @@ extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* ge
   }
 #undef HOPSX_CMP_NF
 #undef HOPSX_CMP
+  return (int)hipGetLastError();
+}
+
+// input layer (geom0: Cin 1, stride 1, dilation 1, a 2x2 or 3x3 kernel) -> this conv + act + 2x2 max-pool
+// (+ dropout) in ONE launch (conv_fwd_mfma_k IN0); geom is this conv's geometry over the input
+// layer's output (stride 1, dilation 1)
+bool hopsx_conv_fwd_pool_in_ok(const int* geom0, const int* geom, int act) {
+  return hopsx_conv_fwd_pool_ok(geom, act) && geom0[3] == 1 && geom0[9] == 1 && geom0[10] == 1 && geom0[13] == 1 &&
+         geom0[14] == 1 && geom0[7] == geom0[8] && (geom0[7] == 2 || geom0[7] == 3) && geom0[4] == geom[1] && geom0[5] == geom[2] &&
+         geom0[6] == geom[3] && geom0[0] == geom[0] && geom[9] == 1 && geom[10] == 1 && geom[13] == 1 &&
+         geom[14] == 1 && geom[6] == 64 && geom[3] % 8 == 0 && geom[3] <= 64 &&
+         (cm_ks((geom[7] * geom[8] * geom[3] + 31) / 32) == 2 || cm_ks((geom[7] * geom[8] * geom[3] + 31) / 32) == 4 ||
+          cm_ks((geom[7] * geom[8] * geom[3] + 31) / 32) == 9) &&
+         !hopsx_disabled("conv_in_pool");
+}
+
+extern "C" int hopsx_conv2d_fwd_pool_in(const void* x0, float xscale, float xshift, const void* w0, const float* b0,
+                                        int act0, const int* geom0, void* y1, const void* w, const int* geom,
+                                        void* out, void* am, const float* bias, int act, float p,
+                                        const unsigned long long* rng, unsigned salt, hipStream_t st) {
+  if (!hopsx_conv_fwd_pool_in_ok(geom0, geom, act)) return -2;
+  if (((uintptr_t)w | (uintptr_t)out | (uintptr_t)y1) % 16 != 0 || xscale == 0.f) return -3;
+  ConvGeom g = cm_geom(geom);
+  const int K = g.KH * g.KW * g.C;
+  const int KS = cm_ks((K + 31) / 32);
+  const long rows = (long)g.B * (g.OH / 2) * (g.OW / 2) * 4;
+  // one 16-row group per wave per trip: the trip holds T0*T0 pixels per K-step in registers
+  const long ngr = (rows + 15) / 16;
+  const int grid = cm_grid(ngr, 1);
+  const int taps = geom0[7] * geom0[8];
+  const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw) +
+                     (size_t)(taps + 1) * g.C * sizeof(float);
+  static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
+  const PoolEpi pe{(unsigned char*)am, rng, salt, p, dbg};
+  const In0 i0{x0, xscale, xshift, (const bf16_raw*)w0, b0, (bf16_raw*)y1, geom0[1], geom0[2], geom0[7], geom0[8],
+               geom0[11], geom0[12], act0};
+#define HOPSX_CMPI(KSV, T0V)                                                                                      \
+  hipLaunchKernelGGL((conv_fwd_mfma_k<4, KSV, true, 1, false, T0V>), dim3(grid), dim3(256), shm, st, nullptr,      \
+                     (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe, nullptr, i0)
+  const int t0 = geom0[7];
+  switch (KS * 4 + t0) {
+    case 2 * 4 + 2: HOPSX_CMPI(2, 2); break;
+    case 4 * 4 + 2: HOPSX_CMPI(4, 2); break;
+    case 9 * 4 + 2: HOPSX_CMPI(9, 2); break;
+    case 2 * 4 + 3: HOPSX_CMPI(2, 3); break;
+    case 4 * 4 + 3: HOPSX_CMPI(4, 3); break;
+    case 9 * 4 + 3: HOPSX_CMPI(9, 3); break;
+    default: return -2;
+  }
+#undef HOPSX_CMPI
   return (int)hipGetLastError();
 }

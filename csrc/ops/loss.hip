@@ -474,6 +474,7 @@ struct MlpHeadArgs {
   int lf32;
   int vec2;
   unsigned long long* dbg;
+  int rot;  // rotate each workgroup's workspace atomics (HOPSX_MLP_ROT, default on)
 };
 
 
@@ -899,7 +900,14 @@ __global__ __launch_bounds__(1024) void mlp_head_k(MlpHeadArgs a) {
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < a.B * a.N1; i += blockDim.x) {
+  // every workgroup adds to every line of the workspace: start each one at a different 64-float
+  // line (a.rot != 0) so the memory-side atomics of concurrent workgroups hit different addresses
+  // instead of all queueing on the same line in the same order
+  const int tot = a.B * a.N1;
+  const int rot = a.rot ? (int)(((unsigned)blockIdx.x * 64u) % (unsigned)tot) & ~63 : 0;
+  for (int i0 = threadIdx.x; i0 < tot; i0 += blockDim.x) {
+    int i = i0 + rot;
+    if (i >= tot) i -= tot;
     const int row = i / a.N1, col = i - row * a.N1;
     atomicAdd(a.ws + i, st[row * SR + col]);
   }
@@ -935,9 +943,10 @@ extern "C" int hopsx_mlp_head(const void* x, const void* w1, const float* b1, in
   int G = (K + ks * 32 - 1) / (ks * 32);
   if (G > 256) G = 256;
   const int vec2 = N1 % 8 == 0 && (uintptr_t)w2 % 16 == 0;
+  static const int rot_on = (int)hopsx_env_int("HOPSX_MLP_ROT", 1);
   MlpHeadArgs a{(const bf16_raw*)x, (const bf16_raw*)w1, b1, act1, (bf16_raw*)y, ws, arrive, B, K, N1, kind, target, C,
                 grad_scale, (const bf16_raw*)w2, b2, dw2, db2, (bf16_raw*)dh, loss_sum, correct, logits_out,
-                logits_f32, vec2, g_mlp_dbg};
+                logits_f32, vec2, g_mlp_dbg, rot_on};
   const size_t lds = mlp_lds_bytes(C, N1);
   const int rf = B > 16 ? 2 : 1, cf = (N1 / 16 + 3) / 4;
 #define MLP_CASE(R, F)                                                                     \

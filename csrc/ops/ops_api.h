@@ -110,6 +110,11 @@ int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, co
 
 bool hopsx_conv_fwd_mfma_ok(const int* geom);
 bool hopsx_conv_fwd_pool_ok(const int* geom, int act);
+bool hopsx_conv_fwd_pool_in_ok(const int* geom0, const int* geom, int act);
+int hopsx_conv2d_fwd_pool_in(const void* x0, float xscale, float xshift, const void* w0, const float* b0, int act0,
+                             const int* geom0, void* y1, const void* w, const int* geom, void* out, void* am,
+                             const float* bias, int act, float p, const unsigned long long* rng, unsigned salt,
+                             hipStream_t st);
 int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* out, void* am, const float* bias, int act,
                           float p, const unsigned long long* rng, unsigned salt, hipStream_t st);
 bool hopsx_conv_dgrad_mfma_ok(const int* geom);

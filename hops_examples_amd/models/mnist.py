@@ -64,7 +64,7 @@ class KerasMnistCNN(_ImageModel):
         self._set_input_affine()
 
     def forward(self, x):
-        x = hnn.conv_pool(self.conv2, self.pool, self.conv1(self.prep(x)))
+        x = hnn.input_conv_pool(self.conv1, self.conv2, self.pool, self.prep(x))
         return self.fc2(self.drop2(self.fc1(x.reshape(x.shape[0], -1))))
 
 
@@ -81,7 +81,7 @@ class MirroredMnistCNN(_ImageModel):
         self._set_input_affine()
 
     def forward(self, x):
-        x = hnn.conv_pool(self.conv2, self.pool, self.conv1(self.prep(x)))  # conv2 + pool + dropout: 1 launch
+        x = hnn.input_conv_pool(self.conv1, self.conv2, self.pool, self.prep(x))  # conv1 + conv2 + pool + dropout: 1 launch
         return self.fc2(self.fc1(x.reshape(x.shape[0], -1)))
 
 
@@ -98,7 +98,7 @@ class FashionMnistCNN(_ImageModel):
         self._set_input_affine()
 
     def forward(self, x):
-        x = hnn.conv_pool(self.conv2, self.pool, self.conv1(self.prep(x)))
+        x = hnn.input_conv_pool(self.conv1, self.conv2, self.pool, self.prep(x))
         return self.fc2(self.drop2(self.fc1(x.reshape(x.shape[0], -1))))
 
 

@@ -131,6 +131,17 @@ def conv_pool(conv: Conv2d, pool: MaxPool2d, x):
                              training=pool.training, salt=pool.salt, **conv.cfg)
 
 
+def input_conv_pool(conv0: Conv2d, conv: Conv2d, pool: MaxPool2d, x):
+    """``pool(conv(conv0(x)))`` where ``conv0`` is the network's input layer (raw uint8 images):
+    ONE launch when the chain qualifies (functional.conv_input_maxpool: the input layer runs inside
+    the second conv's operand gather), else ``conv_pool(conv, pool, conv0(x))``."""
+    y = HF.conv_input_maxpool(x, conv0.weight, conv0.bias, conv0.activation, conv0.in_affine, conv0.cfg,
+                              conv.weight, conv.bias, conv.activation, conv.cfg, pool_kernel=pool.k,
+                              pool_stride=pool.s, pool_padding=pool.p, dropout_p=pool.dropout,
+                              training=pool.training, salt=pool.salt)
+    return y if y is not None else conv_pool(conv, pool, conv0(x))
+
+
 class GlobalAvgPool2d(nn.Module):
     def forward(self, x):
         return HF.global_avg_pool(x)

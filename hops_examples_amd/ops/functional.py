@@ -250,6 +250,41 @@ HEAD = {"probe": None, "defer": False}
 # placeholder first gets it computed (flush_pending).
 PREHEAD = {"w": None, "arm": False, "pending": {}}
 
+# Optimizer co-launch (set by runtime.step.TrainStep on one GPU with a fused optimizer): the last
+# backward launch (the input-side conv pair) also runs the optimizer's update of the arena slice
+# whose gradients are already final (csrc/ops/optim_slice.h); ``lo`` = where that slice starts once
+# launched, so the optimizer's own launch updates only [start, lo).  ``ready``: ids of the
+# parameters whose gradients are final (hooks.grad_ready during this backward).
+COLAUNCH = {"opt": None, "ready": None, "lo": None, "launched": 0}
+
+
+def _colaunch_slice(own):
+    """(lo, slice tuple for K.conv2d_bwd_pair) when the registered optimizer can update the arena
+    suffix whose gradients are final, excluding ``own`` (the params this launch produces)."""
+    opt = COLAUNCH["opt"]
+    if (opt is None or COLAUNCH["ready"] is None or COLAUNCH["lo"] is not None or _PENDING
+            or "opt_colaunch" in _disabled()):
+        return None
+    arena, sl = opt.arena, opt._sl
+    ready, own_ids = COLAUNCH["ready"], {id(p) for p in own if p is not None}
+    lo = sl.stop
+    for p, o, _ in sorted(arena.ranges(), key=lambda r: -r[1]):
+        if o >= sl.stop:
+            continue
+        if o < sl.start or id(p) not in ready or id(p) in own_ids:
+            break
+        lo = o
+    if lo >= sl.stop or lo % 64:
+        return None
+    from ._C import OPTIM
+
+    opt.sync_hp()
+    off = lo - sl.start
+    st = [t[off:] for t in opt._states] + [None] * (3 - len(opt._states))
+    sh = arena.shadow[lo:sl.stop] if arena.shadow is not None else None
+    return lo, (OPTIM[opt.kind], arena.master[lo:sl.stop], arena.grad[lo:sl.stop], st[0], st[1], st[2], sh,
+                opt._hp(), opt._hp_dev, opt.step_count)
+
 
 def flush_pending() -> None:
     """Compute every deferred pre-head output now (the unfused path)."""
@@ -405,8 +440,13 @@ class _Conv2dFn(torch.autograd.Function):
                 w0, b0, g0, act0, aff0, x0 = ctx.prev
                 pprev = (x0, g0, _arena.grad_target(w0), _arena.grad_target(b0), x, act0, aff0)
             addend = ctx.gslot.get("g") if (ctx.gslot is not None and pprev is None) else None
+            co = _colaunch_slice((w, b) + ((ctx.prev[0], ctx.prev[1]) if ctx.prev is not None else ())) \
+                if (ctx.prev is not None and addend is None) else None
             r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, dbias=gb, y=ymask, act=act, prev=pprev,
-                                  addend=addend)
+                                  addend=addend, opt_slice=co[1] if co is not None else None)
+            if co is not None and r is not False:
+                COLAUNCH["lo"] = co[0]  # the optimizer's launch now updates only the prefix
+                COLAUNCH["launched"] += 1
             if r is not False:
                 if addend is not None:
                     ctx.gslot.pop("g", None)  # consumed by the launch
@@ -475,6 +515,81 @@ def conv2d_maxpool(x, w, b=None, stride=1, padding=0, dilation=1, act=None, pool
             return _conv_apply(x, w, b, st, pd, dl, a, None, pool=(float(dropout_p) if training else 0.0, salt))
     y = conv2d(x, w, b, stride, padding, dilation, act)
     return max_pool2d(y, pool_kernel, pool_stride, pool_padding, dropout_p, training, salt)  # unfused
+
+
+class _ConvInPoolFn(torch.autograd.Function):
+    """pool(conv(input_layer(x0))) as ONE forward launch (conv_mfma.hip IN0: the input layer is
+    evaluated inside the conv's operand gather and its output stored once for the backward).  The
+    backward is the conv's own (_Conv2dFn), whose dgrad carries the input layer's weight and bias
+    gradients (conv_mfma.hip K0) — the input layer has no backward node of its own."""
+
+    @staticmethod
+    def forward(ctx, x0, w0, b0, w, b, act0, aff0, g0, g, act, drop_p, salt, keep):
+        rng = rng_state(x0.device) if drop_p > 0 else None
+        y, am, y1 = K.conv2d_fwd_pool_in(x0, _arena.weight_bf16(w0), b0, act0, g0, _arena.weight_bf16(w), g, bias=b,
+                                         act=act, drop_p=drop_p, rng=rng, salt=salt, in_affine=aff0, keep_y1=keep)
+        ctx.save_for_backward(y1, am)
+        ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine = w, b, g, act, None
+        ctx.prev = (w0, b0, g0, act0, aff0, x0)
+        ctx.plain, ctx.gslot, ctx.pool = False, None, (drop_p, rng, salt)
+        ctx.set_materialize_grads(False)
+        y._hx_pool = (am, False, (g[0], g[4], g[5], g[6]), (2, 2), 0, rng, salt, drop_p, True)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        r = _Conv2dFn.backward(ctx, dy)
+        return (None, None, None, r[1], r[2]) + (None,) * 8
+
+
+def _sym_pads(padding, ks, dl):
+    """Symmetric (ph, pw) for a padding spec, or None ('same' with an even kernel pads one side)."""
+    if padding == "valid":
+        return (0, 0)
+    if padding == "same":
+        if ks[0] % 2 == 0 or ks[1] % 2 == 0:
+            return None
+        return (_pad_same(ks[0], dl[0]), _pad_same(ks[1], dl[1]))
+    return (padding, padding) if isinstance(padding, int) else tuple(padding)
+
+
+def conv_input_maxpool(x, w0, b0, act0, in_affine0, cfg0, w, b, act, cfg, pool_kernel=2, pool_stride=None,
+                       pool_padding=0, dropout_p=0.0, training=True, salt=0):
+    """max_pool2d(conv2d(conv2d(x, w0, b0, in_affine0), w, b)) for the network's input layer (raw uint8
+    NHWC images, one channel) as ONE launch when the chain qualifies; returns None otherwise (the
+    caller then runs the layers one by one).  Results equal the unfused chain's (same fp32 order in
+    the input layer, same bf16 roundings)."""
+    if (not x.is_cuda or x.dtype != torch.uint8 or x.dim() != 4 or x.shape[-1] != 1 or in_affine0 is None
+            or float(in_affine0[0]) == 0.0 or "conv_in_pool" in _disabled() or b0 is None):
+        return None
+    pk = (pool_kernel, pool_kernel) if isinstance(pool_kernel, int) else tuple(pool_kernel)
+    ps = pk if pool_stride is None else ((pool_stride,) * 2 if isinstance(pool_stride, int) else tuple(pool_stride))
+    pp = (pool_padding,) * 2 if isinstance(pool_padding, int) else tuple(pool_padding)
+    if pk != (2, 2) or ps != (2, 2) or pp != (0, 0):
+        return None
+    geoms = []
+    shape = tuple(x.shape)
+    for wt, c in ((w0, cfg0), (w, cfg)):
+        st = (c.get("stride", 1),) * 2 if isinstance(c.get("stride", 1), int) else tuple(c["stride"])
+        dl = (c.get("dilation", 1),) * 2 if isinstance(c.get("dilation", 1), int) else tuple(c["dilation"])
+        pd = _sym_pads(c.get("padding", 0), tuple(wt.shape[1:3]), dl)
+        if pd is None or st != (1, 1) or dl != (1, 1):
+            return None
+        gg = K.conv_geom(shape, wt.shape, st, pd, dl)
+        geoms.append(gg)
+        shape = (gg[0], gg[4], gg[5], gg[6])
+    g0, g = geoms
+    a0 = ACT[act0] if not isinstance(act0, int) else act0
+    a = ACT[act] if not isinstance(act, int) else act
+    if not K.conv_u8_fusable(g0) or not K.conv_fwd_pool_in_ok(g0, g, a) or x.data_ptr() % 16:
+        return None
+    keep = torch.is_grad_enabled() and (w.requires_grad or w0.requires_grad)
+    if keep and (not w0.requires_grad or _arena.grad_target(w0) is None or _arena.grad_target(b0) is None
+                 or not K.conv_dgrad_fused_wgrad_ok(g, g0) or "fused_wgrad0" in _disabled()):
+        return None  # the input layer's gradients must ride on this conv's dgrad
+    aff = (float(in_affine0[0]), float(in_affine0[1]))
+    return _ConvInPoolFn.apply(x.contiguous(), w0, b0, w, b, a0, aff, g0, g, a,
+                               float(dropout_p) if training else 0.0, salt, keep)
 
 
 def _fusable_input_layer(x, geom):

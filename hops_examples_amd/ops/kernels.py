@@ -215,6 +215,33 @@ def conv2d_fwd_pool(x, w, geom, bias=None, act=0, drop_p=0.0, rng=None, salt=0):
     return y, am
 
 
+def conv_fwd_pool_in_ok(geom0, geom, act) -> bool:
+    """input layer (geom0) -> conv(geom, act) -> 2x2/2 max-pool can run as ONE launch
+    (conv_mfma.hip IN0: the input layer is evaluated inside the conv's operand gather)."""
+    return bool(_C.ext().conv2d_fwd_pool_in_ok(list(geom0), list(geom), act_id(act)))
+
+
+def conv2d_fwd_pool_in(x0, w0, b0, act0, geom0, w, geom, bias=None, act=0, drop_p=0.0, rng=None, salt=0,
+                       in_affine=None, keep_y1=True):
+    """pool(conv(input_layer(x0))) in one launch.  x0: raw uint8 pixels [B, H0, W0, 1], normalised
+    as ``x * scale + shift`` (``in_affine``) inside the kernel.  Returns (pooled, argmax, y1): y1 is the input layer's
+    output [B, H, W, C] bf16 (stored by the same launch for the backward; None if not ``keep_y1``)."""
+    _req(w0, BF16, "w0")
+    _req(w, BF16, "w")
+    _req(x0, torch.uint8, "x0")
+    if in_affine is None or float(in_affine[0]) == 0.0:
+        raise ValueError("conv2d_fwd_pool_in: uint8 pixels need in_affine=(scale != 0, shift)")
+    xs, xh = float(in_affine[0]), float(in_affine[1])
+    B, OH, OW, CO = geom[0], geom[4], geom[5], geom[6]
+    y = torch.empty(B, OH // 2, OW // 2, CO, device=x0.device, dtype=BF16)
+    am = torch.empty(B, OH // 2, OW // 2, CO, device=x0.device, dtype=torch.uint8)
+    y1 = torch.empty(B, geom[1], geom[2], geom[3], device=x0.device, dtype=BF16) if keep_y1 else None
+    check(_C.ext().conv2d_fwd_pool_in(ptr(x0), xs, xh, ptr(w0), ptr(b0), act_id(act0), list(geom0), ptr(y1), ptr(w),
+                                      list(geom), ptr(y), ptr(am), ptr(bias), act_id(act), float(drop_p), ptr(rng),
+                                      int(salt) & 0xFFFFFFFF, stream()), "conv2d_fwd_pool_in")
+    return y, am, y1
+
+
 def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=None, act=0, addend=None):
     """dX = conv_transpose(dY, W) (* act'(yprev)) (+ addend: a gradient of x from another consumer,
     added in the epilogue; bf16, x's layout)."""
@@ -251,7 +278,7 @@ def conv2d_dgrad_fused_wgrad(dy, w, geom, yprev, act_prev, y, act, x0, geom0, dw
           "conv2d_dgrad_fused_wgrad")
 
 
-def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, addend=None):
+def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, addend=None, opt_slice=None):
     """A conv layer's dgrad and wgrad in ONE launch (conv_mfma.hip conv_bwd_pair_k).  ``prev`` =
     (x0, geom0, dw0, db0, yprev, act_prev, in_affine) fuses the input layer's weight gradient into the
     dgrad (no dX).  ``addend``: another consumer's gradient of the same input, added to dX in the
@@ -269,6 +296,21 @@ def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, ad
     dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_, dw0p = args
     if addend is not None:
         _req(addend, BF16, "addend")
+    if opt_slice is not None:
+        # + a fused optimizer's update of an arena slice whose gradients are final (optim_slice.h):
+        # opt_slice = (kind, master, grad, s1, s2, s3, shadow, hp list, hp_dev, step_dev)
+        kind, p_, g_, s1, s2, s3, shd, hp, hp_dev, step_dev = opt_slice
+        nblk = int(os.environ.get("HOPSX_OPT_SLICE_BLK", "256"))
+        first = int(os.environ.get("HOPSX_OPT_SLICE_FIRST", "0"))
+        rc = _C.ext().conv2d_bwd_pair_opt(ptr(dy), ptr(w), list(geom), dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_,
+                                          dw0p, ptr(x), ptr(dw), ptr(dbias), ptr(addend), int(kind), ptr(p_),
+                                          ptr(g_), ptr(s1), ptr(s2), ptr(s3), ptr(shd), int(p_.numel()),
+                                          [float(v) for v in (list(hp) + [0.0] * 8)[:8]], ptr(hp_dev), ptr(step_dev),
+                                          nblk, first, stream())
+        if rc in (-2, -3):
+            return False
+        check(rc, "conv2d_bwd_pair_opt")
+        return dx
     rc = _C.ext().conv2d_bwd_pair(ptr(dy), ptr(w), list(geom), dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_, dw0p,
                                   ptr(x), ptr(dw), ptr(dbias), ptr(addend), stream())
     if rc == -3:  # no epilogue addend for this shape: nothing launched; pair without it, then add

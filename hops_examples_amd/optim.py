@@ -119,9 +119,17 @@ class FusedOptimizer:
             self.step_count += 1
             return loss
         if a.device.type == "cuda":
+            from .ops import functional as HF
             from .ops import kernels as K
 
             sl = self._sl
+            if HF.COLAUNCH["opt"] is self and HF.COLAUNCH["lo"] is not None:
+                # the slice [lo, stop) was updated by the last backward launch (optim_slice.h):
+                # this launch updates the prefix and does the step bookkeeping / prefetch
+                lo = HF.COLAUNCH["lo"]
+                HF.COLAUNCH["lo"] = None
+                s = [t[: lo - sl.start] if t is not None else None for t in s]
+                sl = slice(sl.start, lo)
             self.sync_hp()
             K.optim_step(OPTIM[self.kind], a.master[sl], a.grad[sl], s[0], s[1], s[2],
                          a.shadow[sl] if a.shadow is not None else None, self._hp(), self.step_count,

@@ -39,6 +39,12 @@ from ..parallel import dist as hdist
 from . import health
 
 
+def _mark_ready(p):
+    r = HF.COLAUNCH["ready"]
+    if r is not None:
+        r.add(id(p))
+
+
 def _clone(x):
     return tuple(t.clone() for t in x) if isinstance(x, (tuple, list)) else x.clone()
 
@@ -127,11 +133,28 @@ class TrainStep:
             HF.HEAD["defer"] = False
             HF.PREHEAD["w"] = None
 
+    def _colaunch_ok(self) -> bool:
+        """One GPU, a single fused optimizer over the arena: the last backward launch may carry the
+        optimizer's update of the layers whose gradients are already final (functional.COLAUNCH;
+        HOPSX_OPT_COLAUNCH=1)."""
+        from ..optim import FusedOptimizer
+
+        # opt-in: measured slower on the flagship (profiles/r3s7_flagship_ab.txt: the optimizer
+        # workgroups compete with the pair's 2-per-CU workgroups for slots, 0.0817 vs 0.0751 ms/step)
+        return (self.device.type == "cuda" and self.dp is None and isinstance(self.opt, FusedOptimizer)
+                and os.environ.get("HOPSX_OPT_COLAUNCH", "0") == "1")
+
     def _fwd_bwd(self, x, y):
         # every step starts from zeroed gradients (the optimizer / fused DP step zeroes them): a weight
         # used once in this forward may STORE its gradient instead of adding it (functional.STEP)
         HF.STEP["overwrite"] = self.device.type == "cuda" and os.environ.get("HOPSX_DW_STORE", "1") == "1"
         HF.STEP["uses"] = {}
+        co = self._colaunch_ok()
+        if co:
+            from . import hooks
+
+            HF.COLAUNCH.update(opt=self.opt, ready=set(), lo=None)
+            hooks.subscribe(_mark_ready)
         try:
             out = self._forward(x)
             loss, correct, count, root, grad = HF.loss_and_grad_root(out, y, self.loss_kind)
@@ -139,11 +162,17 @@ class TrainStep:
         finally:
             HF.STEP["overwrite"] = False
             HF.STEP["uses"] = {}
+            if co:
+                hooks.unsubscribe(_mark_ready)
+                HF.COLAUNCH["ready"] = None  # the optimizer step below still sees opt / lo
         HF.join_side_streams()  # gradients complete before all-reduce / optimizer
         return {"loss": loss, "correct": correct, "count": count}
 
     def _opt(self):
-        self.opt.step()
+        try:
+            self.opt.step()
+        finally:
+            HF.COLAUNCH.update(opt=None, ready=None, lo=None)
         if self.device.type != "cuda" or getattr(self.opt, "rng", None) is None:
             HF.advance_rng(self.device)  # on the GPU the optimizer kernel advances the RNG itself
 
