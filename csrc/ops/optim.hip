@@ -29,7 +29,8 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
                                                bf16_raw* __restrict__ shadow, long n, OptHP h,
                                                float* __restrict__ step_dev, unsigned* __restrict__ arrive,
                                                unsigned long long* __restrict__ rng, int zero_grad, int vec,
-                                               Prefetch pf, int nt, const float* __restrict__ hp_dev) {
+                                               Prefetch pf, int nt, const float* __restrict__ hp_dev,
+                                               int pf_early) {
   // step_dev holds the number of COMPLETED steps; this step is t = step + 1.
   // Every workgroup reads it before its final barrier; the last workgroup to
   // finish bumps it (and the dropout RNG counter).
@@ -38,6 +39,10 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
   float bc1, bc2;
   bias_corr<KIND>(h, t, bc1, bc2);
   constexpr int NS = nstate<KIND>();
+  // HOPSX_OPT_PF_EARLY=1: the next batch's copy first: its cursor -> source -> store
+  // chain does not depend on the update and nothing reads the input buffers any more, so its round
+  // trips overlap the update's instead of following them
+  if (pf_early) prefetch_copy(pf);
   const long n4 = vec ? (n >> 2) : 0;
   const long stride = (long)gridDim.x * blockDim.x;
   // UN float4 per thread per trip with every load issued before the first update: the launcher
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(256) void optim_k(float* __restrict__ p, float* __r
     if (NS >= 3) s3[i] = c;
     if (shadow) shadow[i] = f2bf(w);
   }
-  prefetch_copy(pf);
+  if (!pf_early) prefetch_copy(pf);
   step_bookkeeping(arrive, step_dev, t, rng, pf);
 }
 
@@ -135,6 +140,7 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
   static const int genv = getenv("HOPSX_OPT_GRID") ? atoi(getenv("HOPSX_OPT_GRID")) : 0;
   const int gcap = genv > 0 ? genv : 512;
   static const int nt = getenv("HOPSX_OPT_NT") ? atoi(getenv("HOPSX_OPT_NT")) : 0;
+  static const int pf_early = (int)hopsx_env_int("HOPSX_OPT_PF_EARLY", 0);  // measured neutral (profiles/r3s7_flagship_ab.txt)
   if (g > gcap) g = gcap;
   if (g < 1) g = 1;
   // 6 float4 per thread when that covers the whole arena in one trip, else 3 (VGPR budget)
@@ -148,10 +154,10 @@ extern "C" int hopsx_optim_step(int kind, float* param, float* grad, float* s1, 
   case K:                                                                                                       \
     if (un == 6)                                                                                                \
       hipLaunchKernelGGL((optim_k<K, 6>), dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, \
-                         arr, rng, zero_grad, (int)aligned, pf, nt, hp_dev);                                     \
+                         arr, rng, zero_grad, (int)aligned, pf, nt, hp_dev, pf_early);                           \
     else                                                                                                        \
       hipLaunchKernelGGL((optim_k<K, 3>), dim3(g), dim3(256), 0, st, param, grad, s1, s2, s3, sh, n, h, step_dev, \
-                         arr, rng, zero_grad, (int)aligned, pf, nt, hp_dev);                                     \
+                         arr, rng, zero_grad, (int)aligned, pf, nt, hp_dev, pf_early);                           \
     break;
   switch (kind) {
     OPT_CASE(0) OPT_CASE(1) OPT_CASE(2) OPT_CASE(3) OPT_CASE(4) OPT_CASE(5) OPT_CASE(6)
