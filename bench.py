@@ -184,6 +184,9 @@ def main():
         }
         print(json.dumps(rec), flush=True)
     hdist.shutdown()
+    from hops_examples_amd.parallel import launch
+
+    launch.rank_exit(0)  # a finished rank of the self-launch skips interpreter teardown (see launch.rank_exit)
 
 
 if __name__ == "__main__":

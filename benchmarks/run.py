@@ -393,6 +393,7 @@ def main():
     dev = hdist.device()
     torch.manual_seed(1234 + rank)
     CONFIGS[a.config](a, dev, rank, world)
+    launch.rank_exit(0)  # a finished rank of the self-launch skips interpreter teardown (see launch.rank_exit)
 
 
 if __name__ == "__main__":

@@ -35,6 +35,21 @@ def is_rank_process() -> bool:
     return "WORLD_SIZE" in os.environ and "RANK" in os.environ
 
 
+def rank_exit(code: int = 0) -> None:
+    """End a rank of OUR self-launch (``launch``) after its work and process-group teardown: flush the
+    streams and ``os._exit``, skipping interpreter teardown — a native thread / static destructor
+    racing at exit once turned a finished rehearsal rank into an abort (``terminate called without
+    an active exception``, exit -6).  A no-op for ranks of other launchers (torchrun) and for
+    single-process runs, which exit normally."""
+    if os.environ.get("HOPSX_SELF_LAUNCHED") != "1":
+        return
+    try:
+        sys.stdout.flush()
+        sys.stderr.flush()
+    finally:
+        os._exit(code)
+
+
 def visible_gpus() -> int:
     try:
         import torch
@@ -80,7 +95,8 @@ def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float
         env = dict(os.environ)
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc),
                     "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
-                    "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1"})
+                    "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1",
+                    "HOPSX_SELF_LAUNCHED": "1"})
         if rehearse and ngpu < nproc:
             env.setdefault("HOPSX_DIST_BACKEND", "gloo")
         if extra_env:
