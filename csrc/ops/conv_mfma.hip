@@ -863,11 +863,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(WgradArgs A) {
 //
 // os.kind >= 0: os.nblk more workgroups run a fused optimizer's update of an arena slice whose
 // gradients are final (optim_slice.h) — first in the grid (opt_first) or after the conv part.
-template <int NF, int KS, int K0, int NFC>
+// (OPT: only the instantiation that takes a slice contains the call — the out-of-line optimizer body
+// needs a scratch stack, which the plain pair launches must not pay for)
+template <int NF, int KS, int K0, int NFC, bool OPT = false>
 __global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs B, int nA, int nBx,
                                                           OptSlice os, int opt_first) {
   int bid = blockIdx.x;
-  if (os.kind >= 0) {
+  if constexpr (OPT) {
     if (opt_first) {
       if (bid < os.nblk) {
         opt_slice_run(os, bid);
@@ -1290,8 +1292,14 @@ static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, 
   const int NF = g.C / 16, NFC = g.CO / 16;
 #define HOPSX_PAIR(NFv, KSv, K0v, NFCv)                                                                      \
   if (NF == NFv && KS == KSv && K0 == K0v && NFC == NFCv) {                                                  \
-    hipLaunchKernelGGL((conv_bwd_pair_k<NFv, KSv, K0v, NFCv>), dim3((unsigned)total), dim3(256), shm, st, DA, WA, \
-                       (int)nA, (int)nBx, os, opt_first);                                                      \
+    if (os.kind >= 0) {                                                                                      \
+      if (NFv != 2 || KSv != 8 || K0v != 4 || NFCv != 4) return -2; /* slice only on the flagship shape */  \
+      hipLaunchKernelGGL((conv_bwd_pair_k<2, 8, 4, 4, true>), dim3((unsigned)total), dim3(256), shm, st, DA, WA, \
+                         (int)nA, (int)nBx, os, opt_first);                                                  \
+    } else {                                                                                                 \
+      hipLaunchKernelGGL((conv_bwd_pair_k<NFv, KSv, K0v, NFCv>), dim3((unsigned)total), dim3(256), shm, st, DA, \
+                         WA, (int)nA, (int)nBx, os, opt_first);                                              \
+    }                                                                                                        \
     return (int)hipGetLastError();                                                                           \
   }
 #define HOPSX_PAIR_K0(NFv, KSv, NFCv) HOPSX_PAIR(NFv, KSv, 0, NFCv) HOPSX_PAIR(NFv, KSv, 4, NFCv)

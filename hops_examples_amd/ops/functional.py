@@ -553,6 +553,13 @@ def _sym_pads(padding, ks, dl):
     return (padding, padding) if isinstance(padding, int) else tuple(padding)
 
 
+# opt-in (HOPSX_CONV_IN_POOL=1): one launch fewer and bit-identical, but measured 1-2 % slower on the
+# flagship at the driver's 20-step setting (profiles/r3s7_flagship_ab.txt): the in-gather input layer
+# lengthens conv2's operand phase by more than the separate launch costs
+def _conv_in_pool_on() -> bool:
+    return os.environ.get("HOPSX_CONV_IN_POOL", "0") == "1"
+
+
 def conv_input_maxpool(x, w0, b0, act0, in_affine0, cfg0, w, b, act, cfg, pool_kernel=2, pool_stride=None,
                        pool_padding=0, dropout_p=0.0, training=True, salt=0):
     """max_pool2d(conv2d(conv2d(x, w0, b0, in_affine0), w, b)) for the network's input layer (raw uint8
@@ -560,7 +567,8 @@ def conv_input_maxpool(x, w0, b0, act0, in_affine0, cfg0, w, b, act, cfg, pool_k
     caller then runs the layers one by one).  Results equal the unfused chain's (same fp32 order in
     the input layer, same bf16 roundings)."""
     if (not x.is_cuda or x.dtype != torch.uint8 or x.dim() != 4 or x.shape[-1] != 1 or in_affine0 is None
-            or float(in_affine0[0]) == 0.0 or "conv_in_pool" in _disabled() or b0 is None):
+            or float(in_affine0[0]) == 0.0 or not _conv_in_pool_on() or "conv_in_pool" in _disabled()
+            or b0 is None):
         return None
     pk = (pool_kernel, pool_kernel) if isinstance(pool_kernel, int) else tuple(pool_kernel)
     ps = pk if pool_stride is None else ((pool_stride,) * 2 if isinstance(pool_stride, int) else tuple(pool_stride))

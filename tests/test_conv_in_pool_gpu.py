@@ -65,13 +65,13 @@ def test_conv_in_pool_matches_unfused_and_fp32(B, HW, k0, k, pad, drop):
     assert none is None and torch.equal(y2.view(torch.int16), y.view(torch.int16))
 
 
-def _train_step_grads(disable: str):
+def _train_step_grads(fused: bool):
     from hops_examples_amd.models.mnist import MirroredMnistCNN
     from hops_examples_amd.ops import functional as HF
     from hops_examples_amd.runtime.arena import ParamArena
 
-    old = os.environ.get("HOPSX_DISABLE", "")
-    os.environ["HOPSX_DISABLE"] = disable
+    old = os.environ.get("HOPSX_CONV_IN_POOL")
+    os.environ["HOPSX_CONV_IN_POOL"] = "1" if fused else "0"  # opt-in path (off by default)
     try:
         torch.manual_seed(3)
         m = MirroredMnistCNN().to(dev)
@@ -85,14 +85,17 @@ def _train_step_grads(disable: str):
         torch.cuda.synchronize()
         return out.float().clone(), m._hx_arena.grad.clone()
     finally:
-        os.environ["HOPSX_DISABLE"] = old
+        if old is None:
+            os.environ.pop("HOPSX_CONV_IN_POOL", None)
+        else:
+            os.environ["HOPSX_CONV_IN_POOL"] = old
 
 
 def test_mirrored_mnist_fused_input_layer_same_step():
     """The flagship model's step with the fused input layer equals the unfused one (up to the order
     of fp32 atomic accumulation downstream)."""
-    out_f, g_f = _train_step_grads("")
-    out_u, g_u = _train_step_grads("conv_in_pool")
+    out_f, g_f = _train_step_grads(True)
+    out_u, g_u = _train_step_grads(False)
     # the conv chain is bit-identical (test above); fc1's split-K forward and the weight gradients
     # accumulate with fp32 atomics in run-dependent order, so the rest agrees to rounding noise
     assert (out_f - out_u).abs().max().item() <= 1e-2 * out_u.abs().max().item()
