@@ -293,10 +293,19 @@ static bool gg_1x1(const ConvGeom& g) {
   return g.KH == 1 && g.KW == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
 }
 
+// im2col convs with a narrow GEMM (N = output columns < HOPSX_GG_MIN_N, default 65) stay on gemm_core.h's
+// engine: the ResNet-50 stage-1 3x3 64->64 conv measured 210 vs 248 us forward and 249 vs 294 us dgrad
+// at B=256 there (profiles/r3s7_conv_gemm_vs_torch.txt); gg keeps every wider shape
+static bool gg_narrow(const ConvGeom& g, int N) {
+  static const int min_n = (int)hopsx_env_int("HOPSX_GG_MIN_N", 65);
+  return !(g.KH == 1 && g.KW == 1) && N < min_n;
+}
+
 template <class EP>
 static bool gg_conv_fwd(const void* x, const void* w, const ConvGeom& g, const EP& e, hipStream_t st) {
   const int M = g.B * g.OH * g.OW, N = g.CO, K = g.KH * g.KW * g.C;
-  if (g.C % 8 || g.CO % 8 || ((uintptr_t)x | (uintptr_t)w) % 16 || hopsx_disabled("gg_fwd")) return false;
+  if (g.C % 8 || g.CO % 8 || ((uintptr_t)x | (uintptr_t)w) % 16 || hopsx_disabled("gg_fwd") || gg_narrow(g, N))
+    return false;
   const GgDense ws{(const bf16_raw*)w, (long)K, N, K};
   if (gg_1x1(g)) return launch_gg<true, true>(GgDense{(const bf16_raw*)x, (long)g.C, M, K}, ws, e, M, N, K, false, st);
   return launch_gg<true, true>(GgIm2col{(const bf16_raw*)x, g, M, K}, ws, e, M, N, K, false, st);
@@ -304,7 +313,8 @@ static bool gg_conv_fwd(const void* x, const void* w, const ConvGeom& g, const E
 
 static bool gg_conv_dgrad(const void* dy, const void* w, const ConvGeom& g, const EpiDActBF16& e, hipStream_t st) {
   const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
-  if (g.C % 8 || g.CO % 8 || ((uintptr_t)dy | (uintptr_t)w) % 16 || hopsx_disabled("gg_dgrad")) return false;
+  if (g.C % 8 || g.CO % 8 || ((uintptr_t)dy | (uintptr_t)w) % 16 || hopsx_disabled("gg_dgrad") || gg_narrow(g, N))
+    return false;
   const GgWeightT ws{(const bf16_raw*)w, g, K, N};
   if (g.KH == 1 && g.KW == 1 && g.ph == 0 && g.pw == 0 && (g.sh > 1 || g.sw > 1) && g.H == g.OH * g.sh &&
       g.W == g.OW * g.sw && !e.colsum && !hopsx_disabled("dgrad_scatter")) {
