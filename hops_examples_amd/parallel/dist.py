@@ -41,6 +41,11 @@ def init(backend: str | None = None, timeout_s: float = 600.0) -> tuple[int, int
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        # every rank all-reduces a known vector at startup, so a broken fabric / wrong
+        # rendezvous fails here, loudly, instead of as silently diverging replicas later
+        if os.environ.get("HOPSX_DIST_SELFTEST", "1") == "1" and not self_test():
+            raise RuntimeError(f"collective self-test failed on rank {rank}: an all-reduce of rank+1 over "
+                               f"{world} ranks did not sum to {world * (world + 1) // 2} (backend {backend})")
     return rank, local_rank, world
 
 
@@ -92,7 +97,8 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
 def self_test() -> bool:
     """All-reduce checksum self-test: every rank contributes rank+1."""
     n = world_size()
-    t = torch.full((1024,), float(rank() + 1), device=device())
+    dev = device() if (not is_dist() or dist.get_backend() == "nccl") else torch.device("cpu")
+    t = torch.full((1024,), float(rank() + 1), device=dev)
     all_reduce_(t)
     ok = bool(torch.all(t == n * (n + 1) / 2).item())
     return ok
