@@ -45,7 +45,8 @@ sys.path.insert(0, ROOT)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    # default: the launcher's world size (torchrun without --gpus); an explicit --gpus must match it
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("HOPSX_BENCH_BATCH", "32")))
@@ -81,13 +82,16 @@ def main():
     a = parse()
     from hops_examples_amd.parallel import launch
 
+    explicit = a.gpus is not None
+    if not explicit:
+        a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 and not launch.is_rank_process():
         # the launcher: spawns the N ranks and never touches the GPU itself
         sys.exit(launch.launch(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:], rehearse=a.rehearse))
     from hops_examples_amd.parallel import dist as hdist
 
     rank, local_rank, world = hdist.init()
-    if world != a.gpus:
+    if world != a.gpus and explicit:
         if rank == 0:
             print(f"[bench] --gpus {a.gpus} but the process group has {world} ranks", file=sys.stderr)
         sys.exit(2)
@@ -106,9 +110,16 @@ def main():
     ParamArena.from_module(model, dev)
     opt = optim.Adadelta(model, lr=1.0)
     dp = DataParallel(model) if world > 1 else None
-    # 32 steps per replayed graph (Keras steps_per_execution; HOPSX_STEPS_PER_EXEC overrides): vs 8,
-    # +1.5 % at the driver's 20-step run and +1 % at 200 steps (profiles/r2s7_spe_ab.txt)
-    step = TrainStep(model, opt, "sparse_ce", dp=dp, graph=not a.no_graph, steps_per_execution=32)
+    from hops_examples_amd.runtime.persist import PersistentMnistStep
+
+    if dp is None and not a.no_graph and dev.type == "cuda" and PersistentMnistStep.supported(model, opt, B, world):
+        # one GPU: the whole step (fwd, loss, bwd, Adadelta) runs inside ONE persistent launch per 32
+        # steps, fc1 weights + optimizer state resident on chip (runtime/persist.py; HOPSX_PERSIST=0 off)
+        step = PersistentMnistStep(model, opt, steps_per_launch=32)
+    else:
+        # 32 steps per replayed graph (Keras steps_per_execution; HOPSX_STEPS_PER_EXEC overrides): vs 8,
+        # +1.5 % at the driver's 20-step run and +1 % at 200 steps (profiles/r2s7_spe_ab.txt)
+        step = TrainStep(model, opt, "sparse_ce", dp=dp, graph=not a.no_graph, steps_per_execution=32)
 
     # an MNIST-sized synthetic epoch (>= 60k images) resident in HBM, so the random
     # labels are not memorised within the timed window
@@ -130,6 +141,8 @@ def main():
         run(i)
     step.prepare_resident(xs, ys, n=a.steps)  # capture the steps_per_execution (+ remainder) graphs untimed
     el = timed(run, a.steps, dev)
+    if hasattr(step, "check"):
+        step.check()  # the persistent engine's sticky hand-off error word (outside the timed region)
     loss = float(out["r"]["loss"].item())
     ms = el / a.steps * 1e3
     ips = B * world * a.steps / el
@@ -172,8 +185,9 @@ def main():
                 "per_gpu_batch": B,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
+                "engine": type(step).__name__,
                 "hipgraph": step.use_graph,
-                "steps_per_execution": step.steps_per_execution if step._gU is not None else 1,
+                "steps_per_execution": step.steps_per_execution if getattr(step, "_gU", True) is not None else 1,
                 "allreduce": dp_path,
                 "wire_bytes_per_param": None if dp is None else dp.wire_bytes_per_param,
                 "ranks": ranks,

@@ -53,6 +53,15 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_widedeep_slots(iv.data(), (int)iv.size(), P<int>(out), n);
   });
   m.def("widedeep_step_lds", [](std::vector<long> iv) { return hopsx_widedeep_step_lds(iv.data(), (int)iv.size()); });
+  m.def("mnist_persist", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, u st) {
+    return hopsx_mnist_persist(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),
+                               S(st));
+  });
+  m.def("mnist_persist_geom", []() {
+    std::vector<long> g(10);
+    hopsx_mnist_persist_geom(g.data());
+    return g;
+  });
   m.def("widedeep_step", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, u st) {
     return hopsx_widedeep_step(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),
                                S(st));

@@ -107,6 +107,10 @@ long hopsx_widedeep_step_lds(const long* iv, int ni);
 int hopsx_widedeep_slots(const long* iv, int ni, int* out, long n);
 int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
                         hipStream_t st);
+// ---- flagship MNIST CNN: nsteps whole training steps in one persistent launch (mnist_persist.hip) ----
+int hopsx_mnist_persist(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
+                        hipStream_t st);
+void hopsx_mnist_persist_geom(long* g);
 
 bool hopsx_conv_fwd_mfma_ok(const int* geom);
 bool hopsx_conv_fwd_pool_ok(const int* geom, int act);

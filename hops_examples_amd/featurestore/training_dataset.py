@@ -322,8 +322,10 @@ class TrainingDataset(CamelCaseAPI):
             n, i = shard
             # dataset-wide row-group sharding: global row group j (over all parts in order) goes to
             # rank j % n, so parts with few row groups still spread over every rank
-            sizes = [[pq.ParquetFile(str(p)).metadata.row_group(g).num_rows
-                      for g in range(pq.ParquetFile(str(p)).metadata.num_row_groups)] for p in parts]
+            sizes = []
+            for p in parts:  # the footer of each part is read once
+                md = pq.ParquetFile(str(p)).metadata
+                sizes.append([md.row_group(g).num_rows for g in range(md.num_row_groups)])
             per, mine, j = [0] * n, [[] for _ in parts], 0
             for pi, rgs in enumerate(sizes):
                 for g, rows in enumerate(rgs):
@@ -331,10 +333,15 @@ class TrainingDataset(CamelCaseAPI):
                     if j % n == i:
                         mine[pi].append(g)
                     j += 1
-            if min(per) == 0 or min(per) < max(per) // 2:
+            # equal shards by truncation must not silently drop data: with more than one row group's
+            # worth of rows lost (e.g. 3 groups over 2 ranks), shard by rows instead (petastorm's
+            # cur_shard reads every row group and never truncates)
+            biggest = max((r for rgs in sizes for r in rgs), default=0)
+            if min(per) == 0 or sum(per) - n * min(per) > biggest:
                 row_sharded = True
             else:
                 picks, keep = mine, min(per)
+        self.last_shard_dropped = 0 if shard is None or row_sharded else sum(per) - n * keep
         self.last_shard_mode = None if shard is None else ("rows" if row_sharded else "row_groups")
         # every part through ONE reader pipeline (decode pool, pinned ring, one convert per row group)
         rd = ParquetDeviceReader([str(p) for p in parts], feats + targets, device=device, row_groups=picks)

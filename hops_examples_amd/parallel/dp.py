@@ -100,6 +100,13 @@ class DataParallel:
         self.arena._hx_engine = self  # checkpoint.save gathers the owner-only optimizer slices
         if self.overlap:
             hooks.subscribe(self._on_ready)
+        # ZeRO-1 wire: between sync points the fp32 master is current only on each slice's owner, so a
+        # host read of the module's state (export, keras save, a TFX model.pt) would see stale weights.
+        # sync_master is collective, so it cannot run from a state_dict() that one rank calls: refuse
+        # instead of writing stale weights.
+        self._stale = False
+        if isinstance(model_or_arena, torch.nn.Module) and hasattr(model_or_arena, "register_state_dict_pre_hook"):
+            model_or_arena.register_state_dict_pre_hook(self._state_dict_guard)
 
     # -------------------------------------------------------------- fused P2P step tail
     def bind_optimizer(self, opt) -> None:
@@ -121,6 +128,13 @@ class DataParallel:
 
     def fused_update(self, opt) -> None:
         self._oneshot.dp_step(opt, self._wmask)
+        self._stale = self.master_sharded
+
+    def _state_dict_guard(self, module, prefix, keep_vars) -> None:
+        if self._stale and self.master_sharded:
+            raise RuntimeError("DataParallel: the fp32 master is sharded across ranks (bf16 weight wire, "
+                               "HOPSX_P2P_WEIGHT_WIRE=bf16); call dp.sync_master() on EVERY rank (collective) "
+                               "before state_dict() / export / save, or dp.close() at the end of training")
 
     def owner_slices(self) -> list[slice] | None:
         """Per-rank slices whose optimizer state only the owner keeps current (fused mode), else None."""
@@ -144,6 +158,7 @@ class DataParallel:
         if sl is None or not self.master_sharded:
             return
         _gather_slices(self.arena.master, sl, self._oneshot.rank)
+        self._stale = False
 
     def gather_state(self) -> None:
         """Collective: make every rank's optimizer-state buffers (and, on the ZeRO-1 wire, the fp32
@@ -304,9 +319,12 @@ class DataParallel:
         if getattr(self, "_closed", None) is None:
             self._closed = (self.path, self.wire_bytes_per_param, self.p2p_world)  # reported after teardown
         if self._oneshot is not None:
-            self.sync_master()
             try:
+                # a failed P2P collective (dead peer, sticky error) raises here, BEFORE the collective
+                # master gather, which would otherwise block until the process-group timeout and copy
+                # slices the failed kernels never wrote
                 self._oneshot.check()
+                self.sync_master()
             finally:
                 self._oneshot.close()
                 self._oneshot = None

@@ -78,6 +78,27 @@ def _kill(procs) -> None:
             p.wait()
 
 
+class _Terminated(Exception):
+    def __init__(self, signum: int):
+        super().__init__(signum)
+        self.signum = signum
+
+
+def _raise_terminated(signum, frame):  # noqa: ARG001
+    raise _Terminated(signum)
+
+
+def _child_setup() -> None:
+    """In each rank before exec: die with the launcher (PR_SET_PDEATHSIG = SIGTERM), so a launcher
+    killed by SIGKILL leaves no rank spinning on the GPU in its own session."""
+    try:
+        import ctypes
+
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except Exception:  # noqa: BLE001
+        pass
+
+
 def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float | None = None,
            extra_env: dict | None = None) -> int:
     """Run ``sys.executable argv`` as ``nproc`` ranks on this node; returns the job's exit code.
@@ -91,6 +112,9 @@ def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float
         return 2
     port = free_port()
     procs = []
+    # a driver timeout / job manager stops the launcher with SIGTERM or SIGHUP: turn both into an
+    # exception so the finally block below kills every rank (they run in sessions of their own)
+    prev = {sig: signal.signal(sig, _raise_terminated) for sig in (signal.SIGTERM, signal.SIGHUP)}
     for r in range(nproc):
         env = dict(os.environ)
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc),
@@ -101,7 +125,8 @@ def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float
             env.setdefault("HOPSX_DIST_BACKEND", "gloo")
         if extra_env:
             env.update({k: str(v) for k, v in extra_env.items()})
-        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env, start_new_session=True))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env, start_new_session=True,
+                                      preexec_fn=_child_setup))
     t0 = time.time()
     rc = 0
     try:
@@ -121,8 +146,13 @@ def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float
             time.sleep(0.05)
     except KeyboardInterrupt:
         rc = 130
+    except _Terminated as e:
+        print(f"[launch] received signal {e.signum}; stopping every rank", file=sys.stderr, flush=True)
+        rc = 128 + e.signum
     finally:
         _kill(procs)
+        for sig, h in prev.items():
+            signal.signal(sig, h)
     return rc
 
 

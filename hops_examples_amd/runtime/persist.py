@@ -1,0 +1,236 @@
+"""PersistentMnistStep: the flagship MirroredStrategy MNIST CNN trained ``n`` steps per launch.
+
+Reference workload: notebooks/ml/Distributed_Training/mirrored_strategy/
+mirroredstrategy_mnist_example.ipynb:189-222 (model, Adadelta(1.0) compile, fit on 32 images per
+replica).  On one MI355X the whole training step — forward, softmax cross-entropy, backward and the
+Adadelta update of all 1,394,282 parameters — runs inside ONE persistent kernel per
+``steps_per_launch`` steps (csrc/ops/mnist_persist.hip): each of 169 workgroups owns one pooled
+position and keeps its fc1 weight slice and Adadelta state in registers for the whole launch; 32 head
+workgroups own one image each.  Four in-launch hand-offs per step replace six kernel launches and
+the per-step HBM round trip of the 1.38 M fc1 parameters and their optimizer state.
+
+Contract (same as TrainStep.run_resident on an HBM-resident epoch): every step trains on the next
+batch of ``xs``/``ys`` (cycling), with dropout masks keyed on the device RNG counter, and the arena
+(fp32 master, bf16 shadow, Adadelta accumulators), the optimizer's step count, the RNG counter and
+the batch cursor are up to date in HBM when a launch returns.  The result is deterministic: no float
+atomics, every cross-workgroup sum is a fixed-order loop.
+
+Limits: one GPU (data-parallel runs use TrainStep + the fused P2P step), batch 32, Adadelta, the
+MirroredMnistCNN architecture.  ``PersistentMnistStep.supported(...)`` says whether it applies.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_GEOM = None
+
+
+def _ext():
+    from ..ops import _C
+
+    return _C.ext()
+
+
+def geometry() -> dict:
+    """Kernel geometry (csrc/ops/mnist_persist.hip constants)."""
+    global _GEOM
+    if _GEOM is None:
+        g = _ext().mnist_persist_geom()
+        _GEOM = dict(zip(["batch", "npos", "nhead", "grid", "nconv", "nslice", "slice", "pay", "flag_words",
+                          "lds_bytes"], g))
+    return _GEOM
+
+
+class PersistentError(RuntimeError):
+    pass
+
+
+class PersistentMnistStep:
+    PARAMS = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "fc1.weight", "fc1.bias",
+              "fc2.weight", "fc2.bias")
+
+    @staticmethod
+    def supported(model, opt, batch: int, world: int = 1) -> bool:
+        from ..models.mnist import MirroredMnistCNN
+        from ..optim import Adadelta
+
+        if os.environ.get("HOPSX_PERSIST", "1") != "1":
+            return False
+        a = getattr(opt, "arena", None)
+        return (isinstance(model, MirroredMnistCNN) and isinstance(opt, Adadelta) and world == 1 and batch == 32
+                and a is not None and a.device.type == "cuda" and a.shadow is not None
+                and opt._sl.start == 0 and opt._sl.stop >= a.numel and model.training)
+
+    def __init__(self, model, opt, steps_per_launch: int = 32, debug_stamps: bool = False):
+        from ..ops.functional import rng_state
+
+        a = opt.arena
+        self.model, self.opt, self.arena = model, opt, a
+        dev = a.device
+        self.device = dev
+        g = geometry()
+        self.geom = g
+        named = dict(model.named_parameters())
+        self.offs = [int(named[n]._hx_off) for n in self.PARAMS]
+        self.s1 = a.state("adadelta_s0")
+        self.s2 = a.state("adadelta_s1")
+        self.spl = max(1, int(os.environ.get("HOPSX_PERSIST_STEPS", steps_per_launch)))
+        f32 = dict(device=dev, dtype=torch.float32)
+        B, npos, nh = g["batch"], g["npos"], g["nhead"]
+        self.slabA = torch.empty(2 * npos * B * 128, **f32)
+        self.slabB = torch.empty(2 * nh * g["pay"], **f32)
+        self.slabC = torch.empty(2 * npos * g["nconv"], **f32)
+        self.slabD = torch.empty(2 * g["nslice"] * g["slice"], **f32)
+        self.flags = torch.zeros(g["flag_words"], device=dev, dtype=torch.int32)
+        self.err = torch.zeros(4, device=dev, dtype=torch.int32)
+        self.out = torch.zeros(2 * self.spl, **f32)
+        self.cursor = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.rng = rng_state(dev)
+        self.dbg = torch.zeros(g["grid"] * self.spl * 8, device=dev, dtype=torch.int64) if debug_stamps else None
+        self.acquire = int(os.environ.get("HOPSX_PERSIST_ACQUIRE", "0"))
+        self.use_graph = False
+        self.steps_per_execution = self.spl
+        self._last = None
+        self._n = 0
+
+    # ------------------------------------------------------------------ launch
+    def _check_data(self, xs, ys):
+        B = self.geom["batch"]
+        if xs.dtype != torch.uint8 or not xs.is_contiguous() or xs.device != self.device:
+            raise ValueError("xs must be a contiguous uint8 tensor on the model's device")
+        if xs.numel() % (B * 784) or xs.dim() < 3 or xs.shape[1] != B:
+            raise ValueError(f"xs must be [nbatch, {B}, 28, 28(, 1)], got {tuple(xs.shape)}")
+        nb = xs.shape[0]
+        if ys.dtype != torch.int64 or tuple(ys.shape) != (nb, B) or not ys.is_contiguous() or ys.device != self.device:
+            raise ValueError(f"ys must be a contiguous int64 [{nb}, {B}] tensor on the model's device")
+        return nb
+
+    def _launch(self, xs, ys, nb: int, k: int) -> None:
+        from ..ops import _C
+
+        opt, a, m = self.opt, self.arena, self.model
+        opt.sync_hp()
+        hp = [float(v) for v in opt._hp()]  # lr gscale wd rho eps
+        ptrs = [a.master.data_ptr(), a.shadow.data_ptr(), self.s1.data_ptr(), self.s2.data_ptr(), xs.data_ptr(),
+                ys.data_ptr(), self.cursor.data_ptr(), self.rng.data_ptr(), opt.step_count.data_ptr(),
+                opt._hp_dev.data_ptr() if opt._hp_dev is not None else 0, self.slabA.data_ptr(),
+                self.slabB.data_ptr(), self.slabC.data_ptr(), self.slabD.data_ptr(), self.flags.data_ptr(),
+                self.err.data_ptr(), self.out.data_ptr()]
+        if self.dbg is not None:
+            ptrs.append(self.dbg.data_ptr())
+        pool = m.pool
+        drop = float(pool.dropout) if pool.training else 0.0
+        scale, shift = m.conv1.in_affine
+        iv = self.offs + [nb, int(pool.salt), int(k), self.geom["batch"], self.acquire]
+        fv = [drop, float(scale), float(shift)] + (hp + [0.0] * 5)[:5]
+        _C.check(self._ext.mnist_persist(ptrs, iv, fv, _C.stream()), "mnist_persist")
+
+    @property
+    def _ext(self):
+        return _ext()
+
+    def run_resident(self, xs, ys, n: int):
+        """``n`` training steps on the resident epoch, ``steps_per_launch`` per launch.  Returns the
+        last step's {"loss", "correct", "count"} as device tensors (no host sync)."""
+        nb = self._check_data(xs, ys)
+        k = 0
+        while n > 0:
+            k = min(n, self.spl)
+            self._launch(xs, ys, nb, k)
+            n -= k
+            self._n += k
+        if k:
+            self._last = {"loss": self.out[2 * (k - 1)], "correct": self.out[2 * k - 1],
+                          "count": self.geom["batch"]}
+        return self._last
+
+    def step_resident(self, xs, ys):
+        return self.run_resident(xs, ys, 1)
+
+    def prepare_resident(self, xs, ys, n=None) -> None:  # TrainStep API parity: nothing to capture
+        self._check_data(xs, ys)
+
+    def losses(self, k: int) -> torch.Tensor:
+        """[k, 2] (mean loss, correct) of the last launch's first k steps."""
+        return self.out[: 2 * k].view(k, 2)
+
+    def check(self) -> None:
+        """Raise if a hand-off of any launch timed out or was aborted (sticky device error word)."""
+        e = int(self.err[0].item()) & 0xFFFFFFFF
+        if e:
+            phase, step, wg = (e >> 24) & 0x7F, (e >> 12) & 0xFFF, e & 0xFFF
+            raise PersistentError(f"mnist_persist: hand-off wait timed out (phase {phase}, step {step}, "
+                                  f"workgroup {wg}); arena state of the failed launch is partial")
+
+    def phase_stamps(self, k: int) -> torch.Tensor:
+        """[grid, k, 8] wall-clock stamps (100 MHz ticks) of the last launch (debug_stamps=True)."""
+        if self.dbg is None:
+            raise RuntimeError("construct with debug_stamps=True")
+        return self.dbg.view(self.geom["grid"], self.spl, 8)[:, :k]
+
+
+# ---------------------------------------------------------------------------------------------
+# fp64 PyTorch reference of the same training steps (numerics tests, tools/persist_check.py)
+# ---------------------------------------------------------------------------------------------
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def dropout_keep(seed: int, ctr: int, salt: int, idx: torch.Tensor, p: float) -> torch.Tensor:
+    """The kernels' counter-based dropout mask (common.h drop_key / hash_u32 / uniform01) for int64
+    element indices < 2**32: True where the element is kept."""
+    m64 = (1 << 64) - 1
+    key = (seed ^ ((salt * 0xD1B54A32D192ED03) & m64) ^ ((ctr * 0x8CB92BA72F3D8DD7) & m64)) & m64
+    ka, kb = key & _M32, key >> 32
+    h = _mix32((_mix32((idx & _M32) ^ ka) + kb) & _M32)
+    return (h & 0xFFFFFF).to(torch.float64) * (1.0 / 16777216.0) >= p
+
+
+def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torch.Tensor, cursor: int, n: int,
+                    seed: int, ctr: int, salt: int, drop_p: float, lr: float, rho: float, eps: float,
+                    xscale: float = 1.0 / 255.0, xshift: float = -0.5):
+    """``n`` fp64 training steps of MirroredMnistCNN with the kernel's data order, dropout masks,
+    loss (mean sparse CE) and Adadelta.  params / s1 / s2: name -> tensor (hopsx layouts: conv OHWI,
+    dense [out, in]); updated in place (fp64 copies are returned).  Returns (params, s1, s2, losses)."""
+    import torch.nn.functional as F
+
+    P = {k: v.detach().to(torch.float64).clone() for k, v in params.items()}
+    S1 = {k: v.detach().to(torch.float64).clone() for k, v in s1.items()}
+    S2 = {k: v.detach().to(torch.float64).clone() for k, v in s2.items()}
+    nb, B = ys.shape
+    po = torch.arange(B * 169 * 64, dtype=torch.int64, device=xs.device)  # NHWC pooled element index
+    losses = []
+    for s in range(n):
+        bt = (cursor + s) % nb
+        x = xs[bt].reshape(B, 1, 28, 28).to(torch.float64) * xscale + xshift
+        y = ys[bt]
+        for v in P.values():
+            v.requires_grad_(True)
+        h = F.relu(F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"]))
+        h = F.relu(F.conv2d(h, P["conv2.weight"].permute(0, 3, 1, 2), P["conv2.bias"]))
+        h = F.max_pool2d(h, 2).permute(0, 2, 3, 1).reshape(B, -1)  # NHWC flatten
+        if drop_p > 0:
+            keep = dropout_keep(seed, ctr + s, salt, po, drop_p).reshape(B, -1)
+            h = h * keep.to(h.dtype) / (1.0 - drop_p)
+        h = F.relu(F.linear(h, P["fc1.weight"], P["fc1.bias"]))
+        logits = F.linear(h, P["fc2.weight"], P["fc2.bias"])
+        loss = F.cross_entropy(logits, y)
+        grads = torch.autograd.grad(loss, list(P.values()))
+        losses.append(float(loss))
+        with torch.no_grad():
+            for (k, w), g in zip(list(P.items()), grads):
+                w = w.detach()
+                S1[k].mul_(rho).addcmul_(g, g, value=1 - rho)
+                d = (S2[k] + eps).sqrt() / (S1[k] + eps).sqrt() * g
+                S2[k].mul_(rho).addcmul_(d, d, value=1 - rho)
+                P[k] = w - lr * d
+    return {k: v.detach() for k, v in P.items()}, S1, S2, losses

@@ -1,0 +1,118 @@
+"""The persistent flagship step (csrc/ops/mnist_persist.hip, runtime/persist.py) against an fp64
+PyTorch reference of the same training steps (same data order, dropout masks, loss, Adadelta), and
+its determinism / launch-boundary invariance.
+
+Reference workload: notebooks/ml/Distributed_Training/mirrored_strategy/
+mirroredstrategy_mnist_example.ipynb:189-222.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from hops_examples_amd import optim  # noqa: E402
+from hops_examples_amd.models.mnist import MirroredMnistCNN  # noqa: E402
+from hops_examples_amd.runtime.arena import ParamArena  # noqa: E402
+from hops_examples_amd.runtime import persist  # noqa: E402
+
+B = 32
+
+
+def _setup(seed=0, nb=5, spl=32, stamps=False):
+    torch.manual_seed(seed)
+    dev = torch.device("cuda", 0)
+    m = MirroredMnistCNN().to(dev)
+    ParamArena.from_module(m, dev)
+    opt = optim.Adadelta(m, lr=1.0)
+    g = torch.Generator().manual_seed(seed + 7)
+    xs = torch.randint(0, 256, (nb, B, 28, 28, 1), dtype=torch.uint8, generator=g).to(dev)
+    ys = torch.randint(0, 10, (nb, B), dtype=torch.int64, generator=g).to(dev)
+    eng = persist.PersistentMnistStep(m, opt, steps_per_launch=spl, debug_stamps=stamps)
+    return m, opt, eng, xs, ys
+
+
+def _snapshot(m, eng):
+    named = dict(m.named_parameters())
+    P = {k: named[k].detach().clone() for k in eng.PARAMS}
+    a = eng.arena
+    S1 = {k: eng.s1[named[k]._hx_off:named[k]._hx_off + named[k].numel()].view_as(named[k]).clone() for k in eng.PARAMS}
+    S2 = {k: eng.s2[named[k]._hx_off:named[k]._hx_off + named[k].numel()].view_as(named[k]).clone() for k in eng.PARAMS}
+    return P, S1, S2, a.master.clone()
+
+
+def _run_and_reference(n, seed=0):
+    m, opt, eng, xs, ys = _setup(seed)
+    P0, S10, S20, _ = _snapshot(m, eng)
+    rng0 = eng.rng.clone().cpu()
+    eng.run_resident(xs, ys, n)
+    torch.cuda.synchronize()
+    eng.check()
+    losses = eng.losses(n)[:, 0].cpu().double()
+    P1, S11, S21, _ = _snapshot(m, eng)
+    Pr, S1r, S2r, lr_ = persist.reference_steps(P0, S10, S20, xs, ys, 0, n, int(rng0[0]) & ((1 << 64) - 1),
+                                                int(rng0[1]), int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95,
+                                                1e-7)
+    return m, opt, eng, P0, P1, Pr, S11, S1r, losses, torch.tensor(lr_, dtype=torch.float64)
+
+
+def test_persistent_matches_fp64_reference():
+    n = 6
+    m, opt, eng, P0, P1, Pr, S1k, S1r, lk, lr_ = _run_and_reference(n)
+    # per-step loss: bf16 operands vs fp64, same data / masks
+    assert torch.allclose(lk, lr_.cpu(), rtol=2e-3, atol=2e-3), (lk, lr_)
+    for k in eng.PARAMS:
+        dk = (P1[k] - P0[k]).double().flatten()
+        dr = (Pr[k] - P0[k].double()).flatten()
+        cos = torch.nn.functional.cosine_similarity(dk, dr, dim=0).item()
+        rel = ((dk - dr).norm() / dr.norm()).item()
+        # Adadelta's first updates are ~ +-sqrt(eps / (1 - rho)) * sign(g): sign flips of tiny bf16
+        # gradients are the only large per-element differences, so bound the update vectors
+        assert cos > 0.995 and rel < 0.1, f"{k}: cos {cos:.5f} rel {rel:.4f}"
+        sk, sr = S1k[k].double().flatten(), S1r[k].flatten()
+        srel = ((sk - sr).norm() / sr.norm()).item()
+        assert srel < 0.05, f"{k}: E[g^2] rel {srel:.4f}"
+    # bookkeeping advanced on the device
+    assert int(eng.cursor.item()) == n % 5
+    assert float(opt.step_count.item()) == n
+    # the bf16 shadow the other kernels read is the rounded master
+    a = eng.arena
+    assert torch.equal(a.shadow, a.master.to(torch.bfloat16))
+
+
+def test_persistent_deterministic_and_launch_invariant():
+    """Two runs from the same state are bit-identical, and cutting 24 steps into 3 launches of 8
+    changes nothing (the state written back between launches is exact)."""
+    res = []
+    for spl in (24, 24, 8):
+        m, opt, eng, xs, ys = _setup(3, spl=spl)
+        eng.run_resident(xs, ys, 24)
+        torch.cuda.synchronize()
+        eng.check()
+        res.append((eng.arena.master.clone(), eng.s1.clone(), eng.s2.clone(), float(eng.out[2 * 7].item())))
+    (m0, a0, b0, _), (m1, a1, b1, _), (m2, a2, b2, _) = res
+    assert torch.equal(m0, m1) and torch.equal(a0, a1) and torch.equal(b0, b1)
+    assert torch.equal(m0, m2) and torch.equal(a0, a2) and torch.equal(b0, b2)
+
+
+def test_persistent_trains():
+    m, opt, eng, xs, ys = _setup(5, nb=2)
+    eng.run_resident(xs, ys, 60)  # two batches, memorised
+    torch.cuda.synchronize()
+    eng.check()
+    l = eng.losses(28)[:, 0].cpu()  # last launch: steps 32..59
+    assert float(l[-1]) < 0.5, l
+
+
+def test_persistent_phase_stamps():
+    m, opt, eng, xs, ys = _setup(1, spl=16, stamps=True)
+    eng.run_resident(xs, ys, 16)
+    torch.cuda.synchronize()
+    eng.check()
+    st = eng.phase_stamps(16).cpu()
+    pos = st[:169]
+    # per step the position workgroups pass their phases in order and every step takes time
+    assert bool((pos[:, :, 7] >= pos[:, :, 0]).all())
+    steps = (pos[0, 1:, 0] - pos[0, :-1, 0]).double() * 10e-3  # us (100 MHz)
+    assert float(steps.median()) > 0.0

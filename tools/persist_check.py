@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Persistent flagship step: numerics vs the fp64 reference and per-phase timing from in-kernel
+wall-clock stamps (runtime/persist.py, csrc/ops/mnist_persist.hip).
+
+  python tools/persist_check.py [--steps 8] [--timing 32]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from hops_examples_amd import optim  # noqa: E402
+from hops_examples_amd.models.mnist import MirroredMnistCNN  # noqa: E402
+from hops_examples_amd.runtime import persist  # noqa: E402
+from hops_examples_amd.runtime.arena import ParamArena  # noqa: E402
+
+
+def setup(seed, spl, stamps=False, nb=8):
+    torch.manual_seed(seed)
+    dev = torch.device("cuda", 0)
+    m = MirroredMnistCNN().to(dev)
+    ParamArena.from_module(m, dev)
+    opt = optim.Adadelta(m, lr=1.0)
+    xs = torch.randint(0, 256, (nb, 32, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (nb, 32), dtype=torch.int64, device=dev)
+    return m, opt, persist.PersistentMnistStep(m, opt, steps_per_launch=spl, debug_stamps=stamps), xs, ys
+
+
+def numerics(n):
+    m, opt, eng, xs, ys = setup(0, 32)
+    named = dict(m.named_parameters())
+    sl = lambda t, k: t[named[k]._hx_off:named[k]._hx_off + named[k].numel()].view_as(named[k]).clone()  # noqa: E731
+    P0 = {k: named[k].detach().clone() for k in eng.PARAMS}
+    S10 = {k: sl(eng.s1, k) for k in eng.PARAMS}
+    S20 = {k: sl(eng.s2, k) for k in eng.PARAMS}
+    rng0 = eng.rng.clone().cpu()
+    eng.run_resident(xs, ys, n)
+    torch.cuda.synchronize()
+    eng.check()
+    lk = eng.losses(n)[:, 0].cpu().tolist()
+    Pr, S1r, S2r, lr_ = persist.reference_steps(P0, S10, S20, xs, ys, 0, n, int(rng0[0]) & ((1 << 64) - 1),
+                                                int(rng0[1]), int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95, 1e-7)
+    print("loss kernel   ", [round(v, 5) for v in lk])
+    print("loss reference", [round(v, 5) for v in lr_])
+    for k in eng.PARAMS:
+        dk = (named[k].detach() - P0[k]).double().flatten()
+        dr = (Pr[k] - P0[k].double()).flatten()
+        cos = torch.nn.functional.cosine_similarity(dk, dr, dim=0).item()
+        rel = ((dk - dr).norm() / dr.norm()).item()
+        mx = (dk - dr).abs().max().item()
+        s1k = sl(eng.s1, k).double().flatten()
+        srel = ((s1k - S1r[k].flatten()).norm() / S1r[k].norm()).item()
+        print(f"{k:14s} cos {cos:.6f} rel {rel:.5f} maxabs {mx:.3e} |dref|max {dr.abs().max().item():.3e} "
+              f"s1 rel {srel:.5f}")
+
+
+def timing(n, reps=5):
+    m, opt, eng, xs, ys = setup(1, n, stamps=True, nb=64)
+    eng.run_resident(xs, ys, n)  # warm
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        eng.run_resident(xs, ys, n)
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) / n * 1e6)
+    eng.check()
+    st = eng.phase_stamps(n).cpu().double() * 0.01  # us
+    pos, head = st[:169], st[169:]
+    # per-step span on position workgroup 0 and medians of every phase over workgroups and steps 1..n-1
+    step_us = (pos[:, 2:, 0] - pos[:, 1:-1, 0]).median().item()
+    names = ["conv fwd", "fc1 part + publish A", "wait B (head)", "dh load + fc1 bwd + pool bwd",
+             "conv2 wgrad/dgrad + conv1 wgrad", "publish C + slice reduce/update", "wait D + load"]
+    print(f"host wall {min(ts):.2f} us/step (best of {reps}), in-kernel step {step_us:.2f} us")
+    for i, nm in enumerate(names):
+        d = (pos[:, 1:, i + 1] - pos[:, 1:, i]).median().item()
+        print(f"  P phase {i} {nm:36s} {d:7.2f} us")
+    hA = (head[:, 1:, 0] - pos[:, 1:, 2].max(dim=0).values.unsqueeze(0)).median().item()
+    print(f"  head: last A publish -> head A done {hA:.2f} us; head A->B publish "
+          f"{(head[:, 1:, 1] - head[:, 1:, 0]).median().item():.2f} us; B->update done "
+          f"{(head[:, 1:, 2] - head[:, 1:, 1]).median().item():.2f} us")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--timing", type=int, default=32)
+    a = ap.parse_args()
+    numerics(a.steps)
+    timing(a.timing)
