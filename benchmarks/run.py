@@ -12,6 +12,7 @@ record is the printed JSON line.
 configs:
   mnist_launch_cpu   MNIST 2-layer CNN through experiment.launch on CPU (plumbing; images/s)
   mnist_mirrored     MNIST CNN (E3, 1.39M params) bf16, DP over RCCL (images/s)       == bench.py
+  mnist_ps           the same model through experiment.parameter_server's sharded-PS engine (images/s)
   taxi               Chicago-taxi wide & deep trainer (steps/s)
   titanic            Titanic TD (Parquet) -> HBM ingest (GB/s) + 7.8k-param DNN (steps/s)
   cifar_resnet       CIFAR-10 ResNet-20/56, collective all-reduce (images/s)
@@ -53,11 +54,11 @@ def timed(fn, n, dev):
     return hdist.all_reduce_scalar(time.perf_counter() - t0, "max")
 
 
-def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=None, box=None):
+def _train_loop(model, opt, kind, xs, ys, steps, warmup, dev, world, forward_fn=None, box=None, mode=None):
     from hops_examples_amd.parallel import ps as P
     from hops_examples_amd.runtime.step import TrainStep
 
-    dp = P.make(model, opt) if world > 1 else None
+    dp = P.make(model, opt, mode) if world > 1 else None
     if box is not None:
         box["dp"] = dp
     st = TrainStep(model, opt, kind, dp=dp, graph=dev.type == "cuda", forward_fn=forward_fn)
@@ -90,7 +91,7 @@ def _emit(rank, metric, value, unit, steps, warmup, el, world, cfg, extra=None):
     print(json.dumps(_record(metric, value, unit, steps, warmup, el, world, cfg, extra)), flush=True)
 
 
-def cfg_mnist_mirrored(a, dev, rank, world):
+def cfg_mnist_mirrored(a, dev, rank, world, mode=None):
     from hops_examples_amd import optim
     from hops_examples_amd.models.mnist import MirroredMnistCNN
     from hops_examples_amd.runtime.arena import ALIGN, ParamArena
@@ -102,10 +103,20 @@ def cfg_mnist_mirrored(a, dev, rank, world):
     nb = max(8, -(-61440 // B))
     xs = torch.randint(0, 256, (nb, B, 28, 28, 1), dtype=torch.uint8, device=dev)
     ys = torch.randint(0, 10, (nb, B), device=dev)
-    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world)
-    _emit(rank, "images/sec MNIST CNN (E3) DP", B * world * a.steps / el, "images/sec", a.steps, a.warmup, el, world,
-          {"model": "MirroredMnistCNN 1,394,282 params", "per_gpu_batch": B, "parallelism": f"dp{world}"},
+    box = {}
+    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world, box=box, mode=mode)
+    dp = box.get("dp")
+    _emit(rank, "images/sec MNIST CNN (E3) DP" + (" parameter-server" if mode == "parameter_server" else ""),
+          B * world * a.steps / el, "images/sec", a.steps, a.warmup, el, world,
+          {"model": "MirroredMnistCNN 1,394,282 params", "per_gpu_batch": B, "parallelism": f"dp{world}",
+           "engine": type(dp).__name__ if dp is not None else None},
           {"final_loss": round(loss, 4)})
+
+
+def cfg_mnist_ps(a, dev, rank, world):
+    """experiment.parameter_server's engine (parallel/ps.py ShardedPS: reduce-scatter of the gradient to the
+    shard owners, owner-only optimizer update, bf16 all-gather of the weights) on the E3 model."""
+    cfg_mnist_mirrored(a, dev, rank, world, mode="parameter_server")
 
 
 def cfg_mnist_launch_cpu(a, dev, rank, world):
@@ -363,7 +374,8 @@ def cfg_resnet50(a, dev, rank, world):
                                 "parallelism": f"dp{world}"}, {"final_loss": round(loss, 4)})
 
 
-CONFIGS = {"mnist_launch_cpu": cfg_mnist_launch_cpu, "mnist_mirrored": cfg_mnist_mirrored, "taxi": cfg_taxi,
+CONFIGS = {"mnist_launch_cpu": cfg_mnist_launch_cpu, "mnist_mirrored": cfg_mnist_mirrored, "mnist_ps": cfg_mnist_ps,
+           "taxi": cfg_taxi,
            "titanic": cfg_titanic, "cifar_resnet": cfg_cifar_resnet, "resnet50": cfg_resnet50}
 
 

@@ -35,3 +35,20 @@ def download(dataset_path: str, local_path: str = ".") -> str:
 
 def delete(dataset_path: str) -> None:
     hdfs.rmr(dataset_path)
+
+
+def sample_data(name: str = "") -> str:
+    """Local path of a bundled sample dataset: the data files the reference notebooks ship
+    (notebooks/featurestore/aws/s3/data/telco_customer_churn.csv and its ``telco-delta`` Delta
+    table, notebooks/featurestore/aws/data/Sacramentorealestatetransactions.csv, the retail
+    ``hsfs/archive`` CSVs), copied into ``tests/fixtures``.  ``HOPSX_SAMPLE_DATA`` overrides the
+    directory."""
+    import os
+
+    base = os.environ.get("HOPSX_SAMPLE_DATA")
+    root = Path(base) if base else Path(os.environ.get("HOPSX_REPO", Path(__file__).resolve().parent.parent)) / \
+        "tests" / "fixtures"
+    p = root / name
+    if not p.exists():
+        raise FileNotFoundError(f"sample dataset {name!r} not found under {root}")
+    return str(p)

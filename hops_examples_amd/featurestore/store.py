@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import json
+import os
 import sqlite3
 import threading
 from pathlib import Path
@@ -103,18 +104,39 @@ class StorageConnector:
         self.options = dict(options or {})
         self.__dict__.update(kw)
 
+    def _sf(self, key: str):
+        if key == "password":  # credentials never live in connector metadata written by examples
+            return self.options.get("password") or os.environ.get("SNOWFLAKE_PASSWORD")
+        return self.options.get(key, getattr(self, key, None))
+
     def spark_options(self) -> dict:
+        """Options for ``spark.read.format(...)``: the Snowflake Spark connector's ``sf*`` keys for a
+        SNOWFLAKE connector (pyspark.ipynb:92-120), JDBC url/dbtable otherwise."""
+        if self.connector_type == "SNOWFLAKE":
+            o = {"sfURL": self._sf("url"), "sfUser": self._sf("user"), "sfPassword": self._sf("password"),
+                 "sfDatabase": self._sf("database"), "sfSchema": self._sf("schema"),
+                 "sfWarehouse": self._sf("warehouse"), "sfRole": self._sf("role"), "dbtable": self._sf("table")}
+            return {k: v for k, v in o.items() if v is not None}
         o = {"url": self.connection_string or f"jdbc:sqlite:{self.path}", "dbtable": self.options.get("table")}
         o.update(self.options)
         return {k: v for k, v in o.items() if v is not None}
 
     def snowflake_connector_options(self) -> dict:
-        return {"sfURL": self.options.get("url"), "sfUser": self.options.get("user"),
-                "sfDatabase": self.options.get("database"), "sfSchema": self.options.get("schema"),
-                "sfWarehouse": self.options.get("warehouse")}
+        """kwargs of ``snowflake.connector.connect`` (python.ipynb:51-75)."""
+        o = {"account": self._sf("account") or (self._sf("url") or "").split("//")[-1].split(".")[0] or None,
+             "user": self._sf("user"), "password": self._sf("password"), "database": self._sf("database"),
+             "schema": self._sf("schema"), "warehouse": self._sf("warehouse"), "role": self._sf("role")}
+        return {k: v for k, v in o.items() if v is not None}
 
     def read(self, query: str | None = None, data_format: str | None = None, path: str | None = None):
-        if self.connector_type in ("JDBC", "REDSHIFT", "SNOWFLAKE", "SQLITE"):
+        if self.connector_type == "SNOWFLAKE":
+            from .. import snowflake
+
+            q = query or f"SELECT * FROM {self._sf('table')}"
+            with snowflake.connect(**self.snowflake_connector_options()) as ctx:
+                df = ctx.cursor().execute(q).fetch_pandas_all()
+            return df.rename(columns=str.lower)  # feature names are lower-case in the feature store
+        if self.connector_type in ("JDBC", "REDSHIFT", "SQLITE"):
             db = self.connection_string or self.path
             for pre in ("jdbc:sqlite:", "sqlite:///"):
                 if db and db.startswith(pre):

@@ -122,7 +122,51 @@ class SparkDataFrame:
     registerTempTable = createOrReplaceTempView
 
 
+class _FormatReader:
+    """``spark.read.format(fmt).options(**o).load([path])``: csv / parquet / json files, ``jdbc`` (url +
+    dbtable or query over SQLite) and the Snowflake Spark connector ``net.snowflake.spark.snowflake``
+    (``sf*`` options + dbtable or query; hsfs/snowflake/pyspark.ipynb:92-120)."""
+
+    def __init__(self, fmt: str):
+        self.fmt, self.opts = fmt.lower(), {}
+
+    def option(self, key: str, value) -> "_FormatReader":
+        self.opts[key] = value
+        return self
+
+    def options(self, **kw) -> "_FormatReader":
+        self.opts.update(kw)
+        return self
+
+    def load(self, path: str | None = None) -> SparkDataFrame:
+        o = self.opts
+        if self.fmt in ("net.snowflake.spark.snowflake", "snowflake"):
+            from . import snowflake
+
+            q = o.get("query") or f"SELECT * FROM {o['dbtable']}"
+            with snowflake.connect(url=o.get("sfURL"), user=o.get("sfUser"), password=o.get("sfPassword"),
+                                   database=o.get("sfDatabase"), schema=o.get("sfSchema"),
+                                   warehouse=o.get("sfWarehouse"), role=o.get("sfRole")) as ctx:
+                return SparkDataFrame(ctx.cursor().execute(q).fetch_pandas_all())
+        if self.fmt == "jdbc":
+            import sqlite3
+
+            db = o["url"]
+            for pre in ("jdbc:sqlite:", "sqlite:///"):
+                db = db[len(pre):] if db.startswith(pre) else db
+            q = o.get("query") or f"SELECT * FROM {o['dbtable']}"
+            with sqlite3.connect(db) as c:
+                return SparkDataFrame(pd.read_sql_query(q, c))
+        r = _Reader()
+        if self.fmt == "csv":
+            return r.csv(path, header=str(o.get("header", True)).lower() == "true")
+        return getattr(r, self.fmt)(path)
+
+
 class _Reader:
+    def format(self, fmt: str) -> _FormatReader:
+        return _FormatReader(fmt)
+
     def parquet(self, path: str) -> SparkDataFrame:
         from . import hdfs
 
