@@ -59,7 +59,7 @@ constexpr int PAY_DH = 0, PAY_H = 128, PAY_DL = 256, PAY_LOSS = 268, PAY_COR = 2
 constexpr int FL_A = 0, FL_B = 256, FL_C = 512, FL_D = 768, FL_WORDS = 1024;
 
 // LDS row strides (bf16 elements), padded by 16 B against bank conflicts of the fragment reads
-constexpr int W1S = 72, W2S = 136, C1S = 40, PLS = 72, DHS = 136, DCS = 72;
+constexpr int W1S = 72, W2S = 136, C1S = 40, PLS = 72, DHS = 136, DCS = 136;
 
 // position-workgroup LDS map (bytes, every offset a multiple of 16)
 constexpr int L_W1 = 0;                           // bf16 [128 n][W1S]   fc1 slice
@@ -72,8 +72,8 @@ constexpr int L_C1 = L_XIN + B * 16 * 4;          // bf16 [32 b][9 pos][C1S] con
 constexpr int L_POOL = L_C1 + B * 9 * C1S * 2;    // bf16 [32 b][PLS]   pooled (+dropout)
 constexpr int L_AM = L_POOL + B * PLS * 2;        // u8   [32 b][64]    argmax tap / 0xFF = no grad
 constexpr int L_DH = L_AM + B * C2;               // bf16 [32 b][DHS]
-constexpr int L_DC2 = L_DH + B * DHS * 2;         // bf16 [128 (b,q)][DCS] conv2 output grad
-constexpr int L_STG = L_DC2 + 4 * B * DCS * 2;    // f32  staging: A partial [32][128] / C grads [8416]
+constexpr int L_DC2 = L_DH + B * DHS * 2;         // bf16 [64 co][DCS] conv2 output grad, (b,q) cols
+constexpr int L_STG = L_DC2 + C2 * DCS * 2;       // f32  staging: A partial [32][128] / C grads [8416]
 constexpr int L_RED = L_STG + NCONV * 4;          // f32  [NRED][SLICE] slice reduce / conv1 grad halves
 constexpr int L_SL = L_RED + 1024 * 4;            // f32  [3][SLICE] owned conv slice: master, s1, s2
 constexpr int LDS_BYTES = L_SL + 3 * 64 * 4;
@@ -445,18 +445,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         for (int i = 0; i < 2; ++i) dp[i] = mfma(lds8(DH + (i * 16 + fr) * DHS + kk * 32 + fq * 8), bfr, dp[i]);
       }
     }
-    __syncthreads();  // every read of the old W1 is done
-    // ---- Adadelta on the fc1 slice (registers), new bf16 weights for the next forward ----
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float s3 = 0.f;
-          wm[ii][j][r] = upd<3>(wm[ii][j][r], gw[ii][j][r] * hp.gscale, g1[ii][j][r], g2[ii][j][r], s3, hp, 1.f, 1.f);
-          W1[((2 * w + ii) * 16 + fq * 4 + r) * W1S + j * 16 + fr] = f2bf(wm[ii][j][r]);
-        }
+    // (no barrier: the phases up to the C publish write neither DH, POOL nor W1)
     // ---- dropout / max-pool / relu backward -> dconv2[(b,q)][co]; conv2 bias gradient ----
     {
       const int co = w * 16 + fr;
@@ -469,8 +458,9 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
           const int am = AM[b * C2 + co];
           const bf16_raw gb = am != 0xFF ? f2bf(dp[i][r] * inv) : (bf16_raw)0;
           db += bf2f(gb);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) DC2[(b * 4 + q) * DCS + co] = q == am ? gb : (bf16_raw)0;
+          // the image's 4 window taps are adjacent columns of row co: one 8-byte store
+          *(bf16x4*)(DC2 + co * DCS + b * 4) = (bf16x4){(short)(am == 0 ? gb : 0), (short)(am == 1 ? gb : 0),
+                                                        (short)(am == 2 ? gb : 0), (short)(am == 3 ? gb : 0)};
         }
       db += __shfl_xor(db, 16, 64);
       db += __shfl_xor(db, 32, 64);
@@ -486,7 +476,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int k1 = kk * 32 + 8 * fq + tq, b1 = k1 >> 2, q1 = k1 & 3;  // k1 + 4 = image b1 + 1, same q
-        const bf16x8 af = lds_tr(DC2 + k1 * DCS + w * 16 + 4 * tp, DC2 + (k1 + 4) * DCS + w * 16 + 4 * tp);
+        const bf16x8 af = lds8(DC2 + (w * 16 + fr) * DCS + kk * 32 + fq * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int t = j >> 1, ci0 = (j & 1) * 16 + 4 * tp;
@@ -511,9 +501,12 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         bf16x8 af[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = lds8(DC2 + ((mh * 4 + i) * 16 + fr) * DCS + kk * 32 + fq * 8);
         const int k1 = kk * 32 + 8 * fq + tq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m0 = (mh * 4 + i) * 16 + 4 * tp;
+          af[i] = lds_tr(DC2 + k1 * DCS + m0, DC2 + (k1 + 4) * DCS + m0);
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int c0 = (2 * t + h) * 16 + 4 * tp;
@@ -569,7 +562,11 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     stamp(a, s, 5);
     {  // publish C
       const auto R = rsrc(a.slabC + ((long)par * NPOS + p) * NCONV);
-      for (int idx = tid; idx < NCONV / 4; idx += 256) st_sc1(R, idx * 16, *(const f32x4*)(STG + idx * 4));
+#pragma unroll
+      for (int k = 0; k < (NCONV / 4 + 255) / 256; ++k) {
+        const int idx = tid + 256 * k;
+        if (idx < NCONV / 4) st_sc1(R, idx * 16, *(const f32x4*)(STG + idx * 4));
+      }
       drain();
       __syncthreads();
       if (tid == 0) flag_store(a.flags + FL_C + p, ep);
@@ -583,7 +580,15 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         if (e0 + 4 * j < NCONV) {
           const auto R = rsrc(a.slabC + (long)par * NPOS * NCONV);
-          for (int pp = g; pp < NPOS; pp += NRED) acc += ld_sc1(R, (pp * NCONV + e0 + 4 * j) * 4);
+          constexpr int NK = (NPOS + NRED - 1) / NRED;  // 9 partials per thread, all in flight
+          f32x4 v[NK];
+#pragma unroll
+          for (int k = 0; k < NK; ++k) {
+            const int pp = g + NRED * k;
+            v[k] = pp < NPOS ? ld_sc1(R, (pp * NCONV + e0 + 4 * j) * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int k = 0; k < NK; ++k) acc += v[k];
         }
         *(f32x4*)(RED + g * SLICE + 4 * j) = acc;
       }
@@ -604,13 +609,35 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         if (lane == 0) flag_store(a.flags + FL_D + p, ep);
       }
     }
+    // ---- Adadelta on the fc1 slice (registers) and the new bf16 weights for the next forward: off the
+    // critical path, while this workgroup waits for the D hand-off (W1 is next read after it) ----
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s3 = 0.f;
+          wm[ii][j][r] = upd<3>(wm[ii][j][r], gw[ii][j][r] * hp.gscale, g1[ii][j][r], g2[ii][j][r], s3, hp, 1.f, 1.f);
+          W1[((2 * w + ii) * 16 + fq * 4 + r) * W1S + j * 16 + fr] = f2bf(wm[ii][j][r]);
+        }
     stamp(a, s, 6);
     // ---- D: the updated conv parameters for the next step ----
     if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok)) return;
     {
       const auto R = rsrc(a.slabD + (long)par * NSLICE * SLICE);
-      for (int idx = tid; idx < NCONV / 4; idx += 256) {
-        const f32x4 v = ld_sc1(R, idx * 16);
+      constexpr int NK = (NCONV / 4 + 255) / 256;
+      f32x4 dv[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const int idx = tid + 256 * k;
+        dv[k] = idx < NCONV / 4 ? ld_sc1(R, idx * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const int idx = tid + 256 * k;
+        if (idx >= NCONV / 4) break;
+        const f32x4 v = dv[k];
         const int j = idx * 4;  // 4 params never straddle a region (8192, 8256, 8384 are multiples of 4)
         if (j < OFF_B2) {
           *(bf16x4*)(W2 + (j >> 7) * W2S + (j & 127)) =
@@ -709,8 +736,17 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     {
       const int n4 = tid & 31, g = tid >> 5;
       const auto R = rsrc(a.slabA + (long)par * NPOS * B * HID);
-      f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-      for (int pp = g; pp < NPOS; pp += 8) acc += ld_sc1(R, ((pp * B + i) * HID + n4 * 4) * 4);
+      // all 22 loads in flight before the (fixed-order) sum: a load -> add chain serialises 22 L2 trips
+      constexpr int NK = (NPOS + 7) / 8;
+      f32x4 v[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const int pp = g + 8 * k;
+        v[k] = pp < NPOS ? ld_sc1(R, ((pp * B + i) * HID + n4 * 4) * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      f32x4 acc = v[0];
+#pragma unroll
+      for (int k = 1; k < NK; ++k) acc += v[k];
       *(f32x4*)(RED + g * HID + n4 * 4) = acc;
     }
     __syncthreads();
@@ -767,7 +803,18 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(5, s), a.acquire, s_ok)) return;
     {
       const auto R = rsrc(a.slabB + (long)par * NHEAD * PAY);
-      for (int idx = tid; idx < NHEAD * PAY / 4; idx += 256) *(f32x4*)(ALL + idx * 4) = ld_sc1(R, idx * 16);
+      constexpr int NK = (NHEAD * PAY / 4 + 255) / 256;
+      f32x4 v[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const int idx = tid + 256 * k;
+        v[k] = idx < NHEAD * PAY / 4 ? ld_sc1(R, idx * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const int idx = tid + 256 * k;
+        if (idx < NHEAD * PAY / 4) *(f32x4*)(ALL + idx * 4) = v[k];
+      }
     }
     __syncthreads();
     for (int j = tid; j < NCLS * HID; j += 256) {

@@ -41,7 +41,7 @@ def rank_exit(code: int = 0) -> None:
     racing at exit once turned a finished rehearsal rank into an abort (``terminate called without
     an active exception``, exit -6).  A no-op for ranks of other launchers (torchrun) and for
     single-process runs, which exit normally."""
-    if os.environ.get("HOPSX_SELF_LAUNCHED") != "1":
+    if os.environ.get("HOPSX_SELF_LAUNCHED") != "1" or os.environ.get("HOPSX_RANK_FAST_EXIT", "1") == "0":
         return
     try:
         sys.stdout.flush()

@@ -195,14 +195,47 @@ def dropout_keep(seed: int, ctr: int, salt: int, idx: torch.Tensor, p: float) ->
     return (h & 0xFFFFFF).to(torch.float64) * (1.0 / 16777216.0) >= p
 
 
+class _RoundFwd(torch.autograd.Function):
+    """x -> bf16(x) in the forward, gradient passed straight through (an operand the kernel reads as bf16)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    """identity in the forward; the incoming gradient is rounded to bf16 (a gradient the kernel stores as a
+    bf16 MFMA operand)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
 def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torch.Tensor, cursor: int, n: int,
                     seed: int, ctr: int, salt: int, drop_p: float, lr: float, rho: float, eps: float,
-                    xscale: float = 1.0 / 255.0, xshift: float = -0.5):
+                    xscale: float = 1.0 / 255.0, xshift: float = -0.5, emulate_bf16: bool = False):
     """``n`` fp64 training steps of MirroredMnistCNN with the kernel's data order, dropout masks,
     loss (mean sparse CE) and Adadelta.  params / s1 / s2: name -> tensor (hopsx layouts: conv OHWI,
-    dense [out, in]); updated in place (fp64 copies are returned).  Returns (params, s1, s2, losses)."""
+    dense [out, in]).  Returns fp64 (params, s1, s2, losses).
+
+    ``emulate_bf16``: round exactly the tensors the persistent kernel stores as bf16 MFMA operands —
+    conv1 output, conv2 weight, the relu'd conv2 output (before the max-pool, as the kernel ties it),
+    the pooled+dropout activations, the fc1 weight, dh (fc1 output gradient, not its bias gradient) and
+    the conv2 output gradient — and nothing else, so the kernel differs from it only by fp32 vs fp64
+    accumulation (and the rare relu / max-pool tie that rounding flips)."""
     import torch.nn.functional as F
 
+    rf = _RoundFwd.apply if emulate_bf16 else (lambda t: t)
+    rg = _RoundGrad.apply if emulate_bf16 else (lambda t: t)
     P = {k: v.detach().to(torch.float64).clone() for k, v in params.items()}
     S1 = {k: v.detach().to(torch.float64).clone() for k, v in s1.items()}
     S2 = {k: v.detach().to(torch.float64).clone() for k, v in s2.items()}
@@ -215,17 +248,17 @@ def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torc
         y = ys[bt]
         for v in P.values():
             v.requires_grad_(True)
-        h = F.relu(F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"]))
-        h = F.relu(F.conv2d(h, P["conv2.weight"].permute(0, 3, 1, 2), P["conv2.bias"]))
+        h = rf(F.relu(F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"])))
+        h = rg(rf(F.relu(F.conv2d(h, rf(P["conv2.weight"]).permute(0, 3, 1, 2), P["conv2.bias"]))))
         h = F.max_pool2d(h, 2).permute(0, 2, 3, 1).reshape(B, -1)  # NHWC flatten
         if drop_p > 0:
             keep = dropout_keep(seed, ctr + s, salt, po, drop_p).reshape(B, -1)
             h = h * keep.to(h.dtype) / (1.0 - drop_p)
-        h = F.relu(F.linear(h, P["fc1.weight"], P["fc1.bias"]))
+        h = F.relu(rg(F.linear(rf(h), rf(P["fc1.weight"]))) + P["fc1.bias"])
         logits = F.linear(h, P["fc2.weight"], P["fc2.bias"])
         loss = F.cross_entropy(logits, y)
         grads = torch.autograd.grad(loss, list(P.values()))
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
         with torch.no_grad():
             for (k, w), g in zip(list(P.items()), grads):
                 w = w.detach()

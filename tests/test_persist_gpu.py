@@ -42,7 +42,7 @@ def _snapshot(m, eng):
     return P, S1, S2, a.master.clone()
 
 
-def _run_and_reference(n, seed=0):
+def _run_and_reference(n, seed=0, emulate_bf16=False):
     m, opt, eng, xs, ys = _setup(seed)
     P0, S10, S20, _ = _snapshot(m, eng)
     rng0 = eng.rng.clone().cpu()
@@ -53,32 +53,49 @@ def _run_and_reference(n, seed=0):
     P1, S11, S21, _ = _snapshot(m, eng)
     Pr, S1r, S2r, lr_ = persist.reference_steps(P0, S10, S20, xs, ys, 0, n, int(rng0[0]) & ((1 << 64) - 1),
                                                 int(rng0[1]), int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95,
-                                                1e-7)
+                                                1e-7, emulate_bf16=emulate_bf16)
     return m, opt, eng, P0, P1, Pr, S11, S1r, losses, torch.tensor(lr_, dtype=torch.float64)
 
 
-def test_persistent_matches_fp64_reference():
-    n = 6
-    m, opt, eng, P0, P1, Pr, S1k, S1r, lk, lr_ = _run_and_reference(n)
-    # per-step loss: bf16 operands vs fp64, same data / masks
-    assert torch.allclose(lk, lr_.cpu(), rtol=2e-3, atol=2e-3), (lk, lr_)
+def _delta_stats(P0, P1, Pr, k):
+    dk = (P1[k] - P0[k]).double().flatten()
+    dr = (Pr[k] - P0[k].double()).flatten()
+    cos = torch.nn.functional.cosine_similarity(dk, dr, dim=0).item()
+    err = (dk - dr).abs()
+    return cos, err, dr
+
+
+def test_persistent_one_step_matches_bf16_emulation():
+    """One step against the fp64 reference that rounds exactly the operands the kernel stores as bf16:
+    what is left is fp32-vs-fp64 accumulation, so every parameter update must agree to ~1e-6 of the
+    Adadelta step (1.41e-3 = sqrt(eps / (1 - rho)) for |g| >> sqrt(eps))."""
+    m, opt, eng, P0, P1, Pr, S1k, S1r, lk, lr_ = _run_and_reference(1, emulate_bf16=True)
+    assert abs(float(lk[0]) - float(lr_[0])) < 1e-5 * float(lr_[0]), (lk, lr_)
     for k in eng.PARAMS:
-        dk = (P1[k] - P0[k]).double().flatten()
-        dr = (Pr[k] - P0[k].double()).flatten()
-        cos = torch.nn.functional.cosine_similarity(dk, dr, dim=0).item()
-        rel = ((dk - dr).norm() / dr.norm()).item()
-        # Adadelta's first updates are ~ +-sqrt(eps / (1 - rho)) * sign(g): sign flips of tiny bf16
-        # gradients are the only large per-element differences, so bound the update vectors
-        assert cos > 0.995 and rel < 0.1, f"{k}: cos {cos:.5f} rel {rel:.4f}"
+        cos, err, dr = _delta_stats(P0, P1, Pr, k)
+        # an element whose gradient is within fp32 noise of 0 can take a different Adadelta step (the
+        # update is ~ g / sqrt(E[g^2] + eps)): allow that for < 0.1 % of the elements, bounded by 2 steps
+        bad = (err > 2e-6 + 1e-3 * dr.abs()).double().mean().item()
+        assert cos > 0.99999 and bad < 1e-3 and float(err.max()) <= 2 * 1.42e-3, \
+            f"{k}: cos {cos:.7f} frac off {bad:.5f} max {float(err.max()):.3e}"
         sk, sr = S1k[k].double().flatten(), S1r[k].flatten()
-        srel = ((sk - sr).norm() / sr.norm()).item()
-        assert srel < 0.05, f"{k}: E[g^2] rel {srel:.4f}"
-    # bookkeeping advanced on the device
-    assert int(eng.cursor.item()) == n % 5
-    assert float(opt.step_count.item()) == n
-    # the bf16 shadow the other kernels read is the rounded master
+        assert torch.allclose(sk, sr, rtol=1e-4, atol=1e-12), f"{k}: E[g^2]"
+    # bookkeeping advanced on the device; the bf16 shadow the other kernels read is the rounded master
+    assert int(eng.cursor.item()) == 1 and float(opt.step_count.item()) == 1
     a = eng.arena
     assert torch.equal(a.shadow, a.master.to(torch.bfloat16))
+
+
+def test_persistent_trajectory_tracks_references():
+    """Six steps: the loss trajectory stays on the bf16-emulating reference (rounding-boundary flips
+    decorrelate the updates of near-zero gradients slowly) and within bf16 noise of pure fp64."""
+    n = 6
+    *_, lk, lemu = _run_and_reference(n, emulate_bf16=True)
+    assert torch.allclose(lk, lemu.cpu(), rtol=1e-3, atol=0), (lk, lemu)
+    m, opt, eng, P0, P1, Pr, S1k, S1r, lk2, lref = _run_and_reference(n)
+    assert torch.equal(lk, lk2)  # deterministic
+    assert torch.allclose(lk2, lref.cpu(), rtol=5e-3, atol=0), (lk2, lref)
+    assert int(eng.cursor.item()) == n % 5 and float(opt.step_count.item()) == n
 
 
 def test_persistent_deterministic_and_launch_invariant():

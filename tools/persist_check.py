@@ -44,20 +44,23 @@ def numerics(n):
     torch.cuda.synchronize()
     eng.check()
     lk = eng.losses(n)[:, 0].cpu().tolist()
-    Pr, S1r, S2r, lr_ = persist.reference_steps(P0, S10, S20, xs, ys, 0, n, int(rng0[0]) & ((1 << 64) - 1),
-                                                int(rng0[1]), int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95, 1e-7)
-    print("loss kernel   ", [round(v, 5) for v in lk])
-    print("loss reference", [round(v, 5) for v in lr_])
-    for k in eng.PARAMS:
-        dk = (named[k].detach() - P0[k]).double().flatten()
-        dr = (Pr[k] - P0[k].double()).flatten()
-        cos = torch.nn.functional.cosine_similarity(dk, dr, dim=0).item()
-        rel = ((dk - dr).norm() / dr.norm()).item()
-        mx = (dk - dr).abs().max().item()
-        s1k = sl(eng.s1, k).double().flatten()
-        srel = ((s1k - S1r[k].flatten()).norm() / S1r[k].norm()).item()
-        print(f"{k:14s} cos {cos:.6f} rel {rel:.5f} maxabs {mx:.3e} |dref|max {dr.abs().max().item():.3e} "
-              f"s1 rel {srel:.5f}")
+    print("loss kernel        ", [round(v, 5) for v in lk])
+    for emu in (False, True):
+        Pr, S1r, S2r, lr_ = persist.reference_steps(P0, S10, S20, xs, ys, 0, n, int(rng0[0]) & ((1 << 64) - 1),
+                                                    int(rng0[1]), int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95,
+                                                    1e-7, emulate_bf16=emu)
+        print(f"loss ref (bf16={int(emu)})  ", [round(v, 5) for v in lr_])
+        for k in eng.PARAMS:
+            dk = (named[k].detach() - P0[k]).double().flatten()
+            dr = (Pr[k] - P0[k].double()).flatten()
+            cos = torch.nn.functional.cosine_similarity(dk, dr, dim=0).item()
+            rel = ((dk - dr).norm() / dr.norm()).item()
+            mx = (dk - dr).abs().max().item()
+            big = ((dk - dr).abs() > 1e-4).double().mean().item()
+            s1k = sl(eng.s1, k).double().flatten()
+            srel = ((s1k - S1r[k].flatten()).norm() / S1r[k].norm()).item()
+            print(f"  {k:14s} cos {cos:.6f} rel {rel:.5f} maxabs {mx:.3e} frac>1e-4 {big:.5f} "
+                  f"|dref|max {dr.abs().max().item():.3e} s1 rel {srel:.6f}")
 
 
 def timing(n, reps=5):
@@ -92,5 +95,6 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--timing", type=int, default=32)
     a = ap.parse_args()
+    numerics(1)
     numerics(a.steps)
     timing(a.timing)
