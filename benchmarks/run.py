@@ -254,7 +254,7 @@ def titanic_record(rows: int, batch: int, steps: int, warmup: int) -> dict:
     # gradient outside (0, 1) — read the linear output as a logit instead, so the benchmark trains
     el, loss = _train_loop(net, opt, "bce_logits", xs, ys, steps, warmup, dev, world, box=box, stats=lst)
     dp = box.get("dp")
-    if not loss < lst["initial_loss"]:
+    if steps + warmup >= 50 and not loss < lst["initial_loss"]:  # (a 2-step rehearsal proves nothing)
         raise SystemExit(f"[titanic] the model did not learn: loss {lst['initial_loss']:.4f} -> {loss:.4f}")
     extra = {"ingest_GBps_parquet_to_hbm_per_rank": round(gbps, 3),
              "ingest_raw_column_GBps_per_rank": round(getattr(td, "last_read_bytes", 0) / ingest / 1e9, 3),

@@ -106,3 +106,26 @@ def test_titanic_td_benchmark_four_ranks_row_group_sharded(tmp_path):
     assert rec["shard_mode"] == "row_groups" and rec["rows_per_rank"] == 65536
     assert [x["rows"] for x in rec["config"]["ranks"]] == [65536] * 4
     assert rec["replicas_identical"] is True
+
+
+def test_bench_eight_ranks_rehearsal():
+    """World size 8 (BASELINE configs 2 and 5 run on 8 GPUs): eight gloo ranks on the CPU."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--rehearse", "--steps", "2", "--warmup", "1",
+                        "--no-taxi"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["config"]["global_batch"] == 256 and rec["config"]["parallelism"] == "dp8"
+    assert rec["replicas_identical"] is True
+    assert [x["rank"] for x in rec["config"]["ranks"]] == list(range(8))
+
+
+def test_cifar_resnet_eight_workers_rehearsal(tmp_path):
+    """BASELINE config 5 at 8 workers through experiment.collective_allreduce (gloo rehearsal)."""
+    env = _env()
+    env["HOPSX_PROJECT_ROOT"] = str(tmp_path / "proj")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "run.py"), "cifar_resnet", "--gpus", "8",
+                        "--rehearse", "--depth", "20", "--batch", "4", "--steps", "1", "--warmup", "1"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["replicas_identical"] is True
