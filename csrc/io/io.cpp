@@ -9,6 +9,13 @@
 //  * tf.train.Example protobuf encode + columnar batch decode
 //  * numeric CSV parser -> float32 matrix (empty / non-numeric -> NaN)
 //  * gather_rows: shuffled mini-batch assembly by a thread pool
+//  * ParquetFile: native Parquet column decode (parquet_core.h) of mmapped files straight into the
+//    pinned staging ring of the Parquet -> HBM reader, GIL released
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -27,6 +34,7 @@
 #include <vector>
 
 #include "io_core.h"  // the parsers (bounds-checked, no Python types; fuzzed under ASan)
+#include "parquet_core.h"
 
 namespace py = pybind11;
 using hopsx_io::crc32c;
@@ -360,6 +368,81 @@ static void gather_rows(py::array src, py::array_t<int64_t, py::array::c_style |
   for (auto& x : th) x.join();
 }
 
+// ---------------------------------------------------------------- Parquet
+// A read-only mapping of one Parquet file + its parsed footer.  decode() writes the selected columns
+// of one row group into caller-owned (pinned) memory; many threads may decode one file at once.
+class PqFile {
+ public:
+  explicit PqFile(const std::string& path) : path_(path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("cannot open " + path);
+    struct stat st;
+    if (fstat(fd_, &st) != 0) {
+      ::close(fd_);
+      throw std::runtime_error("cannot stat " + path);
+    }
+    size_ = (size_t)st.st_size;
+    if (size_ < 12) {
+      ::close(fd_);
+      throw std::runtime_error("parquet: file too small: " + path);
+    }
+    void* p = mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (p == MAP_FAILED) {
+      ::close(fd_);
+      throw std::runtime_error("cannot mmap " + path);
+    }
+    data_ = (const uint8_t*)p;
+    madvise(p, size_, MADV_SEQUENTIAL);
+    try {
+      meta_ = hopsx_io::parse_footer(data_, size_);
+    } catch (...) {
+      munmap(p, size_);
+      ::close(fd_);
+      throw;
+    }
+  }
+  ~PqFile() {
+    if (data_) munmap((void*)data_, size_);
+    if (fd_ >= 0) ::close(fd_);
+  }
+  py::dict meta() const {
+    py::dict d;
+    d["num_rows"] = meta_.num_rows;
+    py::list cols, rgs;
+    for (const auto& c : meta_.columns) cols.append(py::make_tuple(c.name, c.type, c.repetition));
+    for (const auto& rg : meta_.row_groups) {
+      py::list ch;
+      for (const auto& c : rg.chunks) ch.append(py::make_tuple(c.type, c.codec, c.num_values, c.total_compressed));
+      rgs.append(py::make_tuple(rg.num_rows, ch));
+    }
+    d["columns"] = cols;
+    d["row_groups"] = rgs;
+    return d;
+  }
+  // columns: leaf indices; dst: host address; offsets: byte offset of each column's values.
+  void decode(int rg, std::vector<int> columns, uintptr_t dst, std::vector<int64_t> offsets) const {
+    if (rg < 0 || rg >= (int)meta_.row_groups.size()) throw std::out_of_range("row group");
+    if (columns.size() != offsets.size()) throw std::invalid_argument("columns / offsets");
+    const auto& g = meta_.row_groups[(size_t)rg];
+    for (int c : columns)
+      if (c < 0 || c >= (int)meta_.columns.size()) throw std::out_of_range("column");
+    py::gil_scoped_release nogil;
+    thread_local hopsx_io::PqScratch S;
+    for (size_t k = 0; k < columns.size(); ++k) {
+      const int c = columns[k];
+      hopsx_io::decode_chunk(data_, size_, meta_.columns[(size_t)c], g.chunks[(size_t)c], g.num_rows,
+                             (uint8_t*)dst + offsets[k], S);
+    }
+  }
+
+ private:
+  std::string path_;
+  int fd_ = -1;
+  const uint8_t* data_ = nullptr;
+  size_t size_ = 0;
+  hopsx_io::PqMeta meta_;
+};
+
 PYBIND11_MODULE(_hopsx_io, m) {
   m.doc() = "hopsx native data path: TFRecord/Example/CSV codecs and batch assembly";
   m.def("crc32c", [](py::bytes b) {
@@ -385,5 +468,10 @@ PYBIND11_MODULE(_hopsx_io, m) {
   m.def("decode_examples_columnar", &decode_examples_columnar, py::arg("records"), py::arg("schema"),
         py::arg("nthreads") = 8);
   m.def("parse_csv_numeric", &parse_csv_numeric, py::arg("path"), py::arg("delimiter") = ',', py::arg("header") = true);
+  py::register_exception<hopsx_io::Unsupported>(m, "ParquetUnsupported");
+  py::class_<PqFile>(m, "ParquetFile")
+      .def(py::init<const std::string&>())
+      .def("meta", &PqFile::meta)
+      .def("decode", &PqFile::decode, py::arg("row_group"), py::arg("columns"), py::arg("dst"), py::arg("offsets"));
   m.def("gather_rows", &gather_rows, py::arg("src"), py::arg("idx"), py::arg("dst"), py::arg("nthreads") = 8);
 }

@@ -125,6 +125,7 @@ class TrainingDataset(CamelCaseAPI):
             shutil.rmtree(self._location)
         self._location.mkdir(parents=True)
         parts = self._split(df)
+        self._wopts = dict(write_options or {})
         for split, part in parts.items():
             self._write_split(part.reset_index(drop=True), split)
         if self.data_format == "petastorm":
@@ -160,7 +161,9 @@ class TrainingDataset(CamelCaseAPI):
         d = self._split_dir(split)
         d.mkdir(parents=True, exist_ok=True)
         fmt = self.data_format
-        nparts = 1 if self.coalesce or len(df) < 200_000 else max(1, len(df) // 200_000)
+        wo = getattr(self, "_wopts", {})
+        part_rows = int(wo.get("part_rows", 200_000))
+        nparts = 1 if self.coalesce or len(df) < part_rows else max(1, len(df) // part_rows)
         chunks = np.array_split(np.arange(len(df)), nparts) if len(df) else [np.arange(0)]
         for i, idx in enumerate(chunks):
             part = df.iloc[idx]
@@ -194,7 +197,12 @@ class TrainingDataset(CamelCaseAPI):
             elif fmt in ("parquet", "petastorm"):
                 # petastorm datasets ARE Parquet (+ the Unischema in _common_metadata, written in save());
                 # 64k-row row groups: the unit data-parallel readers shard by (to_device(shard=...))
-                part.to_parquet(f"{base}.parquet", index=False, row_group_size=self.row_group_rows)
+                # write_options: row_group_size / compression / use_dictionary (a PLAIN, uncompressed
+                # TD is one memcpy per column chunk for the native reader: io/parquet.py)
+                part.to_parquet(f"{base}.parquet", index=False,
+                                row_group_size=int(wo.get("row_group_size", self.row_group_rows)),
+                                compression=wo.get("compression", "snappy"),
+                                use_dictionary=bool(wo.get("use_dictionary", True)))
             else:
                 raise ValueError(f"training dataset format {fmt!r} is not supported here")
 

@@ -2,13 +2,16 @@
 path (Parquet on HopsFS -> tensor) streams into 288 GB HBM via pinned hipMemcpyAsync on a side
 stream").
 
-Row groups are decoded by Arrow's C++ reader on a pool of worker threads (one ParquetFile handle
-per thread; Arrow and torch's copy release the GIL); each worker packs its row group's RAW column
-buffers (int64, float64, float32, int32, bool — whatever the file stores) into a slot of a reusable
-pinned staging ring, and the main thread sends every slot host->device on a side stream as ONE
-copy and converts + interleaves all its columns into the row-major fp32 destination with ONE
-hopsx kernel (columns.hip).  The host never converts, stacks or re-pins anything; decodes of the
-next row groups overlap the transfer and conversion of the current one.
+Row groups are decoded on a pool of worker threads straight into a slot of a reusable pinned
+staging ring: by the native decoder of ``_hopsx_io`` (csrc/io/parquet_core.h: mmapped file, Thrift
+footer, PLAIN / dictionary / RLE pages, snappy; the GIL released, no Arrow objects and no
+intermediate copy — a PLAIN page is one memcpy from the page cache into pinned memory), or, for
+files it does not cover (nested or string columns, other codecs), by Arrow's reader plus one pack
+copy.  The slot holds each column's RAW values (int64, float64, float32, int32, bool — whatever the
+file stores); the main thread sends every slot host->device on a side stream as ONE copy and
+converts + interleaves all its columns into the row-major fp32 destination with ONE hopsx kernel
+(columns.hip).  Decodes of the next row groups overlap the transfer and conversion of the current
+one.
 
 Reference parity: the training-dataset readers the notebooks use (``td.read()``,
 ``tf_data(...).tf_record_dataset``; notebooks/featurestore/hsfs/basics/training_datasets.ipynb:
@@ -73,6 +76,33 @@ def _staging(device: torch.device) -> _Staging:
     return st
 
 
+_NATIVE: dict = {}  # (path, size, mtime_ns) -> _hopsx_io.ParquetFile (footer parsed once, mmapped)
+_NP = {0: np.dtype(np.uint8), 1: np.dtype(np.int32), 2: np.dtype(np.int64), 4: np.dtype(np.float32),
+       5: np.dtype(np.float64)}  # Parquet physical type -> raw value dtype in the staging slot
+
+
+def _native_file(path: str):
+    """The native decoder's handle of ``path`` (cached per file version), or None when the native
+    library is unavailable or the file is outside its scope."""
+    if os.environ.get("HOPSX_PARQUET_NATIVE", "1") != "1":
+        return None
+    try:
+        st = os.stat(path)
+    except OSError:
+        return None
+    key = (path, st.st_size, st.st_mtime_ns)
+    f = _NATIVE.get(key, False)
+    if f is False:
+        try:
+            from .. import _hopsx_io as io
+
+            f = io.ParquetFile(path)
+        except Exception:  # noqa: BLE001 - not built, not Parquet, or unsupported layout: Arrow reads it
+            f = None
+        _NATIVE[key] = f
+    return f
+
+
 def _thread_file(path: str):
     files = getattr(_TLS, "files", None)
     if files is None:
@@ -106,17 +136,24 @@ class ParquetDeviceReader:
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         self.sources = []  # (path, row group, rows), in output order
+        self.native = {}   # path -> (native handle, column indices, raw dtypes) when natively decodable
         for p, rg in zip(paths, per_file):
-            md = pq.ParquetFile(p).metadata
-            groups = list(range(md.num_row_groups))
+            nf = _native_file(p)
+            plan = self._native_plan(nf) if nf is not None else None
+            if plan is not None:
+                self.native[p] = plan
+                rows_of = [r for r, _ in nf.meta()["row_groups"]]
+            else:
+                md = pq.ParquetFile(p).metadata
+                rows_of = [md.row_group(g).num_rows for g in range(md.num_row_groups)]
+            groups = list(range(len(rows_of)))
             if rg is not None:  # an explicit subset (a dataset-wide row-group shard, see to_device)
-                groups = [g for g in rg if 0 <= g < md.num_row_groups]
+                groups = [g for g in rg if 0 <= g < len(rows_of)]
             elif shard is not None:
                 n, i = shard
                 groups = groups[i::n]
-            self.sources += [(p, g, md.row_group(g).num_rows) for g in groups]
+            self.sources += [(p, g, rows_of[g]) for g in groups]
         self._path = paths[0]
-        self.pf = pq.ParquetFile(self._path)
         self.groups = [g for _, g, _ in self.sources]
         self.rows = sum(r for _, _, r in self.sources)
         self.depth = max(1, depth)
@@ -126,6 +163,45 @@ class ParquetDeviceReader:
         self.bytes_read = 0  # raw column bytes moved host -> device by the last read()
 
     # ---------------------------------------------------------------- host side
+    def _native_plan(self, nf):
+        """(handle, leaf indices, raw dtypes) of the requested columns, or None if any is outside
+        the native decoder's scope (missing, nested, string / INT96 / fixed-length, repeated)."""
+        md = nf.meta()
+        by_name = {name: (i, t, rep) for i, (name, t, rep) in enumerate(md["columns"])}
+        idx, dts = [], []
+        for c in self.columns:
+            e = by_name.get(c)
+            if e is None or e[1] not in _NP or e[2] == 2:
+                return None
+            idx.append(e[0])
+            dts.append(_NP[e[1]])
+        return nf, idx, dts
+
+    def _layout(self, src):
+        """Byte offsets of each column's raw values in a staging slot (native sources)."""
+        _, _, dts = self.native[src[0]]
+        offs, nb = [], 0
+        for dt in dts:
+            offs.append(nb)
+            nb += -(-src[2] * dt.itemsize // _ALIGN) * _ALIGN
+        return offs, nb
+
+    def _decode_native_into(self, src, host_ptr: int):
+        """Decode row group ``src`` straight into pinned memory at ``host_ptr``; returns
+        (per-column (dtype, nbytes), offsets, total bytes), or None when the native decoder refuses a
+        page (the caller falls back to Arrow for this row group)."""
+        nf, idx, dts = self.native[src[0]]
+        offs, nb = self._layout(src)
+        try:
+            nf.decode(src[1], idx, host_ptr, offs)  # releases the GIL
+        except Exception as e:  # noqa: BLE001
+            from .. import _hopsx_io as io
+
+            if isinstance(e, io.ParquetUnsupported):
+                return None
+            raise
+        return [(dt, src[2] * dt.itemsize) for dt in dts], offs, nb
+
     def _decode(self, src, threads: bool | None = None):
         """One (path, row group) -> list of numpy views of the raw column buffers (zero-copy where
         Arrow allows); the calling thread's own ParquetFile handle."""
@@ -163,13 +239,23 @@ class ParquetDeviceReader:
         if out is None:
             out = torch.empty(n, k, dtype=torch.float32, device=self.device)
         if self.device.type != "cuda":
-            r0 = 0
+            r0, moved = 0, 0
             for src in self.sources:
-                cols = self._decode(src)
-                m = len(cols[0])
+                m = src[2]
+                got = None
+                if src[0] in self.native:
+                    _, nb = self._layout(src)
+                    buf = torch.empty(nb, dtype=torch.uint8)
+                    got = self._decode_native_into(src, buf.data_ptr())
+                if got is not None:
+                    cols = [buf[o:o + n].numpy().view(dt) for (dt, n), o in zip(got[0], got[1])]
+                    moved += got[2]
+                else:
+                    cols = self._decode(src)
                 for j, v in enumerate(cols):
-                    out[r0:r0 + m, j] = torch.from_numpy(np.array(v, dtype=np.float32))
+                    out[r0:r0 + m, j] = torch.from_numpy(np.asarray(v, dtype=np.float32))
                 r0 += m
+            self.bytes_read = moved
             return out
         from ..ops import kernels as K
 
@@ -186,32 +272,39 @@ class ParquetDeviceReader:
             threads = self.threads and nthreads == 1  # Arrow's own column threads only without the pool
 
             def decode_pack(i: int, src):
-                """Worker: decode one row group, then pack its raw column buffers into ring slot
-                i % depth once the H2D copy that last read that slot has completed."""
+                """Worker: decode one row group into ring slot i % depth once the H2D copy that last
+                read that slot has completed — natively straight into the pinned slot, else Arrow
+                decode + one pack copy.  Returns ([(dtype, nbytes)], offsets, slot bytes)."""
+                host, _, ev = slots[i % depth]
+                if src[0] in self.native:
+                    if ev is not None:
+                        ev.synchronize()
+                    got = self._decode_native_into(src, host.data_ptr())
+                    if got is not None:
+                        return got
                 cols = self._decode(src, threads)
                 offs, nb = [], 0
                 for v in cols:
                     offs.append(nb)
                     nb += -(-v.nbytes // _ALIGN) * _ALIGN
-                host, _, ev = slots[i % depth]
                 if ev is not None:
                     ev.synchronize()
                 for v, o in zip(cols, offs):
                     # torch's copy releases the GIL: the workers' packs run in parallel
                     host[o:o + v.nbytes].copy_(torch.from_numpy(v.view(np.uint8).reshape(-1)))
-                return cols, offs, nb
+                return [(v.dtype, v.nbytes) for v in cols], offs, nb
 
             r0 = 0
             moved = 0
             futs = {i: pool.submit(decode_pack, i, self.sources[i]) for i in range(min(depth, n_g))}
             for i in range(n_g):
                 cols, offs, nb = futs.pop(i).result()
-                m = len(cols[0])
+                m = self.sources[i][2]
                 slot = slots[i % depth]
                 host, dev = slot[0], slot[1]
                 with torch.cuda.stream(st.stream):
                     dev[:nb].copy_(host[:nb], non_blocking=True)  # one hipMemcpyAsync per row group
-                    srcs = [dev[o:o + v.nbytes].view(_torch_dtype(v.dtype)) for v, o in zip(cols, offs)]
+                    srcs = [dev[o:o + n].view(_torch_dtype(dt)) for (dt, n), o in zip(cols, offs)]
                     K.cols_to_f32(srcs, out[r0:r0 + m])  # convert + interleave: one launch per row group
                     e = torch.cuda.Event()
                     e.record(st.stream)
