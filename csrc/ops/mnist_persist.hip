@@ -116,7 +116,7 @@ struct Args {
   unsigned* flags;  // [FL_WORDS], zeroed before the launch
   unsigned* err;    // sticky error word (0 = ok)
   float* out;       // [nsteps][2]: mean loss, correct count
-  unsigned long long* dbg;  // optional [GRID][nsteps][8] wall-clock phase stamps
+  unsigned long long* dbg;  // optional [GRID][nsteps][16] wall-clock phase stamps
   OptHP hp;
   float drop_p, xscale, xshift;
   unsigned salt;
@@ -177,6 +177,17 @@ __device__ __forceinline__ bool wait_all(const unsigned* flags, int n, unsigned 
   return g != 0;
 }
 
+// Adadelta (optim_core.h upd<3>, rho = a, eps = b) with the hardware square root / reciprocal square
+// root (1 ulp) instead of the correctly rounded sqrt + division sequences: ~8 instead of ~35 VALU ops
+// an element, and the fc1 slice update (32 elements a lane) sits on the step's critical path
+__device__ __forceinline__ float adadelta(float w, float g, float& s1, float& s2, const OptHP& h) {
+  g = fmaf(h.wd, w, g);
+  s1 = fmaf(h.a, s1, (1.f - h.a) * g * g);
+  const float delta = g * __builtin_amdgcn_sqrtf(s2 + h.b) * __builtin_amdgcn_rsqf(s1 + h.b);
+  s2 = fmaf(h.a, s2, (1.f - h.a) * delta * delta);
+  return fmaf(-h.lr, delta, w);
+}
+
 __device__ __forceinline__ unsigned ecode(int phase, int s) {
   return 0x80000000u | ((unsigned)phase << 24) | (((unsigned)s & 0xFFFu) << 12) | (blockIdx.x & 0xFFFu);
 }
@@ -201,7 +212,7 @@ __device__ __forceinline__ long conv_idx(const Args& a, int j) {
 }
 
 __device__ __forceinline__ void stamp(const Args& a, int s, int ph) {
-  if (a.dbg && threadIdx.x == 0) a.dbg[((long)blockIdx.x * a.nsteps + s) * 8 + ph] = (unsigned long long)wall_clock64();
+  if (a.dbg && threadIdx.x == 0) a.dbg[((long)blockIdx.x * a.nsteps + s) * 16 + ph] = (unsigned long long)wall_clock64();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -571,9 +582,11 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       __syncthreads();
       if (tid == 0) flag_store(a.flags + FL_C + p, ep);
     }
+    stamp(a, s, 6);
     // ---- slice owners: fixed-order reduce of 52 params over the 169 partials, Adadelta, publish D ----
     if (owner) {
       if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok)) return;
+      stamp(a, s, 7);
       const int e0 = p * SLICE;
       if (tid < 13 * NRED) {
         const int j = tid % 13, g = tid / 13;
@@ -598,8 +611,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         float gs = 0.f;
         for (int g = 0; g < NRED; ++g) gs += RED[g * SLICE + tid];
         if (e < NCONV) {
-          float s3 = 0.f;
-          SLm[tid] = upd<3>(SLm[tid], gs * hp.gscale, SL1[tid], SL2[tid], s3, hp, 1.f, 1.f);
+          SLm[tid] = adadelta(SLm[tid], gs * hp.gscale, SL1[tid], SL2[tid], hp);
           __hip_atomic_store((gu32*)(a.slabD + (long)par * NSLICE * SLICE + e), __float_as_uint(SLm[tid]),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -608,6 +620,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         drain();
         if (lane == 0) flag_store(a.flags + FL_D + p, ep);
       }
+      stamp(a, s, 8);
     }
     // ---- Adadelta on the fc1 slice (registers) and the new bf16 weights for the next forward: off the
     // critical path, while this workgroup waits for the D hand-off (W1 is next read after it) ----
@@ -617,13 +630,13 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float s3 = 0.f;
-          wm[ii][j][r] = upd<3>(wm[ii][j][r], gw[ii][j][r] * hp.gscale, g1[ii][j][r], g2[ii][j][r], s3, hp, 1.f, 1.f);
+          wm[ii][j][r] = adadelta(wm[ii][j][r], gw[ii][j][r] * hp.gscale, g1[ii][j][r], g2[ii][j][r], hp);
           W1[((2 * w + ii) * 16 + fq * 4 + r) * W1S + j * 16 + fr] = f2bf(wm[ii][j][r]);
         }
-    stamp(a, s, 6);
+    stamp(a, s, 9);
     // ---- D: the updated conv parameters for the next step ----
     if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok)) return;
+    stamp(a, s, 10);
     {
       const auto R = rsrc(a.slabD + (long)par * NSLICE * SLICE);
       constexpr int NK = (NCONV / 4 + 255) / 256;
@@ -649,7 +662,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       }
     }
     __syncthreads();
-    stamp(a, s, 7);
+    stamp(a, s, 11);
   }
 
   // ---- write back: fc1 slice and the owned conv slice (master, state, bf16 shadow) ----
@@ -822,21 +835,18 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
       float g = 0.f;
 #pragma unroll 8
       for (int b = 0; b < B; ++b) g = fmaf(ALL[b * PAY + PAY_DL + c], ALL[b * PAY + PAY_H + n], g);
-      float s3 = 0.f;
-      HW[j] = upd<3>(HW[j], g * hp.gscale, HW1[j], HW2[j], s3, hp, 1.f, 1.f);
+      HW[j] = adadelta(HW[j], g * hp.gscale, HW1[j], HW2[j], hp);
     }
     if (tid < HID) {
       float g = 0.f;
 #pragma unroll 8
       for (int b = 0; b < B; ++b) g += ALL[b * PAY + PAY_DH + tid];
-      float s3 = 0.f;
-      HB1[tid] = upd<3>(HB1[tid], g * hp.gscale, HB1[128 + tid], HB1[256 + tid], s3, hp, 1.f, 1.f);
+      HB1[tid] = adadelta(HB1[tid], g * hp.gscale, HB1[128 + tid], HB1[256 + tid], hp);
     }
     if (tid < NCLS) {
       float g = 0.f;
       for (int b = 0; b < B; ++b) g += ALL[b * PAY + PAY_DL + tid];
-      float s3 = 0.f;
-      HB2[tid] = upd<3>(HB2[tid], g * hp.gscale, HB2[16 + tid], HB2[32 + tid], s3, hp, 1.f, 1.f);
+      HB2[tid] = adadelta(HB2[tid], g * hp.gscale, HB2[16 + tid], HB2[32 + tid], hp);
     }
     if (i == 0 && tid == 255) {
       float l = 0.f, cc = 0.f;

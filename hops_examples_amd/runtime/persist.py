@@ -88,7 +88,7 @@ class PersistentMnistStep:
         self.out = torch.zeros(2 * self.spl, **f32)
         self.cursor = torch.zeros(1, device=dev, dtype=torch.int64)
         self.rng = rng_state(dev)
-        self.dbg = torch.zeros(g["grid"] * self.spl * 8, device=dev, dtype=torch.int64) if debug_stamps else None
+        self.dbg = torch.zeros(g["grid"] * self.spl * 16, device=dev, dtype=torch.int64) if debug_stamps else None
         self.acquire = int(os.environ.get("HOPSX_PERSIST_ACQUIRE", "0"))
         self.use_graph = False
         self.steps_per_execution = self.spl
@@ -165,10 +165,13 @@ class PersistentMnistStep:
                                   f"workgroup {wg}); arena state of the failed launch is partial")
 
     def phase_stamps(self, k: int) -> torch.Tensor:
-        """[grid, k, 8] wall-clock stamps (100 MHz ticks) of the last launch (debug_stamps=True)."""
+        """[grid, k, 16] wall-clock stamps (100 MHz ticks) of the last launch (debug_stamps=True).
+        Position workgroups: 0 step start, 1 conv fwd done, 2 A published, 3 B ready, 4 pool bwd done,
+        5 conv bwd done, 6 C published, 7 C ready (slice owners), 8 D published (owners), 9 fc1 slice
+        updated, 10 D ready, 11 step end.  Heads: 0 A ready, 1 B published, 2 fc2 update done."""
         if self.dbg is None:
             raise RuntimeError("construct with debug_stamps=True")
-        return self.dbg.view(self.geom["grid"], self.spl, 8)[:, :k]
+        return self.dbg.view(self.geom["grid"], self.spl, 16)[:, :k]
 
 
 # ---------------------------------------------------------------------------------------------

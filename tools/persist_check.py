@@ -76,18 +76,29 @@ def timing(n, reps=5):
     eng.check()
     st = eng.phase_stamps(n).cpu().double() * 0.01  # us
     pos, head = st[:169], st[169:]
-    # per-step span on position workgroup 0 and medians of every phase over workgroups and steps 1..n-1
+    own = pos[:162]
     step_us = (pos[:, 2:, 0] - pos[:, 1:-1, 0]).median().item()
-    names = ["conv fwd", "fc1 part + publish A", "wait B (head)", "dh load + fc1 bwd + pool bwd",
-             "conv2 wgrad/dgrad + conv1 wgrad", "publish C + slice reduce/update", "wait D + load"]
     print(f"host wall {min(ts):.2f} us/step (best of {reps}), in-kernel step {step_us:.2f} us")
-    for i, nm in enumerate(names):
-        d = (pos[:, 1:, i + 1] - pos[:, 1:, i]).median().item()
-        print(f"  P phase {i} {nm:36s} {d:7.2f} us")
-    hA = (head[:, 1:, 0] - pos[:, 1:, 2].max(dim=0).values.unsqueeze(0)).median().item()
-    print(f"  head: last A publish -> head A done {hA:.2f} us; head A->B publish "
-          f"{(head[:, 1:, 1] - head[:, 1:, 0]).median().item():.2f} us; B->update done "
+
+    def med(t, a, b):
+        return (t[:, 1:, b] - t[:, 1:, a]).median().item()
+
+    rows = [("conv fwd (input, conv1, conv2 MFMA, pool, dropout)", pos, 0, 1), ("fc1 partial + publish A", pos, 1, 2),
+            ("wait B (heads)", pos, 2, 3), ("dh load + fc1 wgrad/dgrad + pool bwd", pos, 3, 4),
+            ("conv2 wgrad/dgrad + conv1 wgrad", pos, 4, 5), ("publish C", pos, 5, 6),
+            ("owner: wait C", own, 6, 7), ("owner: slice reduce + update + publish D", own, 7, 8),
+            ("owner: fc1 slice Adadelta", own, 8, 9), ("wait D", pos, 9, 10), ("D load", pos, 10, 11)]
+    for nm, t, a, b in rows:
+        print(f"  {nm:48s} {med(t, a, b):7.2f} us")
+    lastA = pos[:, 1:, 2].max(dim=0).values
+    lastC = pos[:, 1:, 6].max(dim=0).values
+    lastD = own[:, 1:, 8].max(dim=0).values
+    print(f"  head: last A publish -> A ready {(head[:, 1:, 0] - lastA).median().item():.2f} us; head compute + "
+          f"B publish {(head[:, 1:, 1] - head[:, 1:, 0]).median().item():.2f} us; fc2 update "
           f"{(head[:, 1:, 2] - head[:, 1:, 1]).median().item():.2f} us")
+    print(f"  skew: C publish spread {(pos[:, 1:, 6].max(0).values - pos[:, 1:, 6].min(0).values).median().item():.2f} us; "
+          f"last C publish -> owners' C ready {(own[:, 1:, 7] - lastC).median().item():.2f} us; "
+          f"last D publish -> D ready {(pos[:, 1:, 10] - lastD).median().item():.2f} us")
 
 
 if __name__ == "__main__":
