@@ -73,11 +73,12 @@ def test_persistent_one_step_matches_bf16_emulation():
     assert abs(float(lk[0]) - float(lr_[0])) < 1e-5 * float(lr_[0]), (lk, lr_)
     for k in eng.PARAMS:
         cos, err, dr = _delta_stats(P0, P1, Pr, k)
-        # an element whose gradient is within fp32 noise of 0 can take a different Adadelta step (the
-        # update is ~ g / sqrt(E[g^2] + eps)): allow that for < 0.1 % of the elements, bounded by 2 steps
-        bad = (err > 2e-6 + 1e-3 * dr.abs()).double().mean().item()
-        assert cos > 0.99999 and bad < 1e-3 and float(err.max()) <= 2 * 1.42e-3, \
-            f"{k}: cos {cos:.7f} frac off {bad:.5f} max {float(err.max()):.3e}"
+        # the conv gradients are sums of ~50k products with cancellation: fp32 vs fp64 order moves an
+        # element's update by up to ~5 % of a step (measured max 6.5e-5); more than 7 % of a step (1e-4)
+        # is allowed for at most 1 element in 1000 (a gradient within noise of 0), bounded by 2 steps
+        nbad = int((err > 1e-4).sum())
+        assert cos > 0.99999 and nbad <= max(0, err.numel() // 1000) and float(err.max()) <= 2 * 1.42e-3, \
+            f"{k}: cos {cos:.7f} off {nbad}/{err.numel()} max {float(err.max()):.3e}"
         # E[g^2] = 0.05 g^2: the conv gradients are sums of ~50k terms with cancellation, where fp32
         # vs fp64 order moves the smallest entries by up to ~1 % (measured rel-L2 <= 3.2e-3)
         sk, sr = S1k[k].double().flatten(), S1r[k].flatten()
