@@ -57,6 +57,10 @@ constexpr int GRID = NPOS + NHEAD;  // 201 workgroups, one per CU
 constexpr int PAY = 272;            // head payload floats
 constexpr int PAY_DH = 0, PAY_H = 128, PAY_DL = 256, PAY_LOSS = 268, PAY_COR = 269;
 constexpr int FL_A = 0, FL_B = 256, FL_C = 512, FL_D = 768, FL_WORDS = 1024;
+// D payload (updated conv parameters): the conv2 weights as bf16 (what the MFMAs read), then the 224
+// small fp32 parameters [b2 | conv1 w | conv1 b]
+constexpr int D_F32 = OFF_B2 * 2;                 // byte offset of the fp32 part
+constexpr int D_BYTES = D_F32 + (NCONV - OFF_B2) * 4;
 
 // LDS row strides (bf16 elements), padded by 16 B against bank conflicts of the fragment reads
 constexpr int W1S = 72, W2S = 136, C1S = 40, PLS = 72, DHS = 136, DCS = 136;
@@ -76,7 +80,8 @@ constexpr int L_DC2 = L_DH + B * DHS * 2;         // bf16 [64 co][DCS] conv2 out
 constexpr int L_STG = L_DC2 + C2 * DCS * 2;       // f32  staging: A partial [32][128] / C grads [8416]
 constexpr int L_RED = L_STG + NCONV * 4;          // f32  [NRED][SLICE] slice reduce / conv1 grad halves
 constexpr int L_SL = L_RED + 1024 * 4;            // f32  [3][SLICE] owned conv slice: master, s1, s2
-constexpr int LDS_BYTES = L_SL + 3 * 64 * 4;
+constexpr int L_KEEP = L_SL + 3 * 64 * 4;         // u8   [32 b][64] next step's dropout keep mask
+constexpr int LDS_BYTES = L_KEEP + B * C2;
 
 // head-workgroup LDS map (aliases the same allocation)
 constexpr int H_W2 = 0;                       // f32 [3][10*128] fc2 weight: master, s1, s2
@@ -112,7 +117,7 @@ struct Args {
   float* slabA;  // [2][169][32][128]
   float* slabB;  // [2][32][PAY]
   float* slabC;  // [2][169][NCONV]
-  float* slabD;  // [2][NSLICE*SLICE]
+  float* slabD;  // [2][D_BYTES / 4]
   unsigned* flags;  // [FL_WORDS], zeroed before the launch
   unsigned* err;    // sticky error word (0 = ok)
   float* out;       // [nsteps][2]: mean loss, correct count
@@ -191,6 +196,10 @@ __device__ __forceinline__ float adadelta(float w, float g, float& s1, float& s2
 __device__ __forceinline__ unsigned ecode(int phase, int s) {
   return 0x80000000u | ((unsigned)phase << 24) | (((unsigned)s & 0xFFFu) << 12) | (blockIdx.x & 0xFFFu);
 }
+
+// fp32 -> bf16 round-to-nearest-even by the gfx950 conversion instruction (v_cvt_pk_bf16_f32):
+// the same bits as common.h's f2bf for every finite value, one instruction instead of five
+__device__ __forceinline__ bf16_raw f2bf(float f) { return __builtin_bit_cast(bf16_raw, (__bf16)f); }
 
 __device__ __forceinline__ bf16x8 lds8(const bf16_raw* p) { return *(const bf16x8*)p; }
 // transposed fragment read (ds_read_b64_tr_b16): this lane addresses row (k) 8*fq + tq (p1) and
@@ -283,6 +292,20 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
   };
   unsigned xv = xload(0);
   const float P = a.drop_p, inv = P > 0.f ? 1.f / (1.f - P) : 1.f;
+  unsigned char* KEEP = smem + L_KEEP;
+  // the dropout keep mask of step s for this position (common.h drop_key / uniform01 on the NHWC
+  // index of the pooled element): it depends only on the step, so it is drawn while the previous
+  // step waits for its D hand-off, off the critical path
+  auto draw_keep = [&](int s) {
+    const unsigned long long ctr = ctr0 + (unsigned long long)s;
+    const uint64_t dkey = (uint64_t)seed ^ ((uint64_t)a.salt * 0xD1B54A32D192ED03ull) ^
+                          ((uint64_t)ctr * 0x8CB92BA72F3D8DD7ull);
+    for (int e = threadIdx.x; e < B * C2; e += 256) {
+      const int b = e >> 6, co = e & 63;
+      KEEP[e] = P > 0.f ? (unsigned char)(uniform01(dkey, (uint64_t)((long)(b * NPOS + p) * C2 + co)) >= P) : 1;
+    }
+  };
+  draw_keep(0);
   __syncthreads();
 
   for (int s = 0; s < a.nsteps; ++s) {
@@ -345,9 +368,6 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
           for (int ii = 0; ii < 2; ++ii) acc[ii][j] = mfma(af[ii], bfr, acc[ii][j]);
         }
       }
-      const unsigned long long ctr = ctr0 + (unsigned long long)s;
-      const uint64_t dkey = (uint64_t)seed ^ ((uint64_t)a.salt * 0xD1B54A32D192ED03ull) ^
-                            ((uint64_t)ctr * 0x8CB92BA72F3D8DD7ull);  // common.h drop_key
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
@@ -365,13 +385,11 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
             }
           }
           if (!(best > 0.f)) bi = 0xFF;
-          if (P > 0.f) {
-            if (uniform01(dkey, (uint64_t)((long)(b * NPOS + p) * C2 + co)) >= P) {
-              best *= inv;
-            } else {
-              best = 0.f;
-              bi = 0xFF;
-            }
+          if (KEEP[b * C2 + co]) {
+            best *= inv;
+          } else {
+            best = 0.f;
+            bi = 0xFF;
           }
           POOL[b * PLS + co] = f2bf(best);
           AM[b * C2 + co] = (unsigned char)bi;
@@ -501,6 +519,16 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) STG[(w * 16 + fq * 4 + r) * 128 + j * 16 + fr] = acc[j][r];
     }
+    __syncthreads();
+    {  // publish C, part 1: the conv2 weight gradient (8192 floats) now; its write-through stores drain
+       // while the conv2 input gradient and the conv1 gradient below are computed
+      const auto R = rsrc(a.slabC + ((long)par * NPOS + p) * NCONV);
+#pragma unroll
+      for (int k = 0; k < OFF_B2 / 4 / 256; ++k) {
+        const int idx = tid + 256 * k;
+        st_sc1(R, idx * 16, *(const f32x4*)(STG + idx * 4));
+      }
+    }
     // ---- conv2 input gradient -> col2im -> relu' -> conv1 weight / bias gradient ----
     {
       const int mh = w >> 1, h = w & 1;
@@ -571,13 +599,10 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     }
     __syncthreads();
     stamp(a, s, 5);
-    {  // publish C
+    {  // publish C, part 2: the 224 small gradients [b2 | conv1 w | conv1 b]; every wave drains both parts
       const auto R = rsrc(a.slabC + ((long)par * NPOS + p) * NCONV);
-#pragma unroll
-      for (int k = 0; k < (NCONV / 4 + 255) / 256; ++k) {
-        const int idx = tid + 256 * k;
-        if (idx < NCONV / 4) st_sc1(R, idx * 16, *(const f32x4*)(STG + idx * 4));
-      }
+      const int idx = OFF_B2 / 4 + tid;
+      if (idx < NCONV / 4) st_sc1(R, idx * 16, *(const f32x4*)(STG + idx * 4));
       drain();
       __syncthreads();
       if (tid == 0) flag_store(a.flags + FL_C + p, ep);
@@ -610,10 +635,22 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         const int e = e0 + tid;
         float gs = 0.f;
         for (int g = 0; g < NRED; ++g) gs += RED[g * SLICE + tid];
+        float wn = 0.f;
         if (e < NCONV) {
           SLm[tid] = adadelta(SLm[tid], gs * hp.gscale, SL1[tid], SL2[tid], hp);
-          __hip_atomic_store((gu32*)(a.slabD + (long)par * NSLICE * SLICE + e), __float_as_uint(SLm[tid]),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          wn = SLm[tid];
+        }
+        // the D payload: conv2 weights as bf16 pairs (slices start at even indices), the rest fp32; every
+        // store a 4-byte write-through (sc1) store
+        const float wnext = __shfl_down(wn, 1, 64);
+        unsigned char* D = (unsigned char*)a.slabD + (long)par * D_BYTES;
+        if (e < OFF_B2) {
+          if (!(tid & 1))
+            __hip_atomic_store((gu32*)(D + e * 2), (unsigned)f2bf(wn) | ((unsigned)f2bf(wnext) << 16),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (e < NCONV) {
+          __hip_atomic_store((gu32*)(D + D_F32 + (e - OFF_B2) * 4), __float_as_uint(wn), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (w == 0) {
@@ -633,32 +670,28 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
           wm[ii][j][r] = adadelta(wm[ii][j][r], gw[ii][j][r] * hp.gscale, g1[ii][j][r], g2[ii][j][r], hp);
           W1[((2 * w + ii) * 16 + fq * 4 + r) * W1S + j * 16 + fr] = f2bf(wm[ii][j][r]);
         }
+    if (s + 1 < a.nsteps) draw_keep(s + 1);  // KEEP is next read after the D wait's barrier
     stamp(a, s, 9);
     // ---- D: the updated conv parameters for the next step ----
     if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok)) return;
     stamp(a, s, 10);
     {
-      const auto R = rsrc(a.slabD + (long)par * NSLICE * SLICE);
-      constexpr int NK = (NCONV / 4 + 255) / 256;
-      f32x4 dv[NK];
+      const auto R = rsrc((const unsigned char*)a.slabD + (long)par * D_BYTES);
+      constexpr int NB = OFF_B2 * 2 / 16;        // 1024 16-B chunks of bf16 conv2 weights
+      constexpr int NF = (NCONV - OFF_B2) / 4;   // 56 16-B chunks of fp32
+      f32x4 dv[NB / 256 + 1];
 #pragma unroll
-      for (int k = 0; k < NK; ++k) {
-        const int idx = tid + 256 * k;
-        dv[k] = idx < NCONV / 4 ? ld_sc1(R, idx * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < NB / 256; ++k) dv[k] = ld_sc1(R, (tid + 256 * k) * 16);
+      dv[NB / 256] = tid < NF ? ld_sc1(R, D_F32 + tid * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NB / 256; ++k) {
+        const int c = tid + 256 * k;  // chunk c: conv2 row c >> 4, 8 values from column (c & 15) * 8
+        *(f32x4*)(W2 + (c >> 4) * W2S + (c & 15) * 8) = dv[k];
       }
-#pragma unroll
-      for (int k = 0; k < NK; ++k) {
-        const int idx = tid + 256 * k;
-        if (idx >= NCONV / 4) break;
-        const f32x4 v = dv[k];
-        const int j = idx * 4;  // 4 params never straddle a region (8192, 8256, 8384 are multiples of 4)
-        if (j < OFF_B2) {
-          *(bf16x4*)(W2 + (j >> 7) * W2S + (j & 127)) =
-              (bf16x4){(short)f2bf(v[0]), (short)f2bf(v[1]), (short)f2bf(v[2]), (short)f2bf(v[3])};
-        } else {
-          float* dst = j < OFF_W1 ? CB2 + (j - OFF_B2) : (j < OFF_B1 ? CW1 + (j - OFF_W1) : CB1 + (j - OFF_B1));
-          *(f32x4*)dst = v;
-        }
+      if (tid < NF) {
+        const int j = OFF_B2 + tid * 4;  // 4 params never straddle a region (8256, 8384 are multiples of 4)
+        float* dst = j < OFF_W1 ? CB2 + (j - OFF_B2) : (j < OFF_B1 ? CW1 + (j - OFF_W1) : CB1 + (j - OFF_B1));
+        *(f32x4*)dst = dv[NB / 256];
       }
     }
     __syncthreads();
@@ -961,4 +994,5 @@ extern "C" void hopsx_mnist_persist_geom(long* g) {
   g[7] = PAY;
   g[8] = FL_WORDS;
   g[9] = LDS_BYTES;
+  g[10] = D_BYTES;
 }

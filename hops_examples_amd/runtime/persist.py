@@ -39,7 +39,7 @@ def geometry() -> dict:
     if _GEOM is None:
         g = _ext().mnist_persist_geom()
         _GEOM = dict(zip(["batch", "npos", "nhead", "grid", "nconv", "nslice", "slice", "pay", "flag_words",
-                          "lds_bytes"], g))
+                          "lds_bytes", "d_bytes"], g))
     return _GEOM
 
 
@@ -82,7 +82,7 @@ class PersistentMnistStep:
         self.slabA = torch.empty(2 * npos * B * 128, **f32)
         self.slabB = torch.empty(2 * nh * g["pay"], **f32)
         self.slabC = torch.empty(2 * npos * g["nconv"], **f32)
-        self.slabD = torch.empty(2 * g["nslice"] * g["slice"], **f32)
+        self.slabD = torch.empty(2 * g["d_bytes"] // 4, **f32)
         self.flags = torch.zeros(g["flag_words"], device=dev, dtype=torch.int32)
         self.err = torch.zeros(4, device=dev, dtype=torch.int32)
         self.out = torch.zeros(2 * self.spl, **f32)
