@@ -107,6 +107,24 @@ __device__ __forceinline__ void wd_mark(const WideDeepArgs& A, int slot) {
   if (A.dbg && threadIdx.x == 0) A.dbg[slot] = wall_clock64();
 }
 
+// Adagrad / FTRL-proximal (optim_core.h upd<5> / upd<6>) with the hardware square root and reciprocal
+// (1 ulp) instead of the correctly rounded sqrt + division sequences: the update phase runs ~16 deep
+// parameters a lane and the touched wide rows every step, on the step's critical path
+__device__ __forceinline__ float adagrad_fast(float w, float g, float& s1, const OptHP& h) {
+  g = fmaf(h.wd, w, g);
+  s1 = fmaf(g, g, s1);
+  return w - h.lr * g * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(s1) + h.a);
+}
+__device__ __forceinline__ float ftrl_fast(float w, float g, float& z, float& n, const OptHP& h) {
+  const float nn = fmaf(g, g, n);
+  const float rs = __builtin_amdgcn_sqrtf(nn);
+  const float sigma = (rs - __builtin_amdgcn_sqrtf(n)) * __builtin_amdgcn_rcpf(h.lr);
+  z += g - sigma * w;
+  n = nn;
+  const float den = (h.c + rs) * __builtin_amdgcn_rcpf(h.lr) + 2.f * h.b;
+  return (fabsf(z) <= h.a) ? 0.f : -(z - copysignf(h.a, z)) * __builtin_amdgcn_rcpf(den);
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -187,10 +205,15 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     const bool relu = l + 1 < L;
     for (int t = wave; t < tm * tn; t += WD_WAVES) {
       const int m0 = (t / tn) * 16, n0 = (t % tn) * 16;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      // two independent accumulator chains (even / odd k): a dependent 16x16x4 f32 MFMA chain waits
+      // out each MFMA's latency; ks is a multiple of 4 (dpad pads to 16)
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-      for (int k = 0; k < ks; ++k)
+      for (int k = 0; k < ks; k += 2) {
         acc = mfma4(Ap[(m0 + fr) * sa + 4 * k + fq], Wp[(n0 + fr) * sw + 4 * k + fq], acc);
+        acc1 = mfma4(Ap[(m0 + fr) * sa + 4 * k + 4 + fq], Wp[(n0 + fr) * sw + 4 * k + 4 + fq], acc1);
+      }
+      acc += acc1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = m0 + 4 * fq + r, o = n0 + fr;
@@ -257,19 +280,27 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     for (int j = 0; j < WD_MAXT; ++j) {
       const int t = wave + j * WD_WAVES;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (t < tdw) {  // dW[o][i] = sum_b G[b][o] A[b][i]
+      if (t < tdw) {  // dW[o][i] = sum_b G[b][o] A[b][i]  (Bp / 4 is a multiple of 4)
         const int o0 = (t / tni) * 16, i0 = (t % tni) * 16;
+        f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int k = 0; k < Bp / 4; ++k)
+        for (int k = 0; k < Bp / 4; k += 2) {
           acc = mfma4(Gp[(4 * k + fq) * sg + o0 + fr], Ap[(4 * k + fq) * sa + i0 + fr], acc);
+          acc1 = mfma4(Gp[(4 * k + 4 + fq) * sg + o0 + fr], Ap[(4 * k + 4 + fq) * sa + i0 + fr], acc1);
+        }
+        acc += acc1;
       }
       hw[j] = acc;
       f32x4 acx = {0.f, 0.f, 0.f, 0.f};
       if (t < tdx) {  // dX[b][i] = sum_o G[b][o] W[o][i]
         const int b0 = (t / tni) * 16, i0 = (t % tni) * 16;
+        f32x4 acx1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int k = 0; k < dpad(out) / 4; ++k)
+        for (int k = 0; k < dpad(out) / 4; k += 2) {
           acx = mfma4(Gp[(b0 + fr) * sg + 4 * k + fq], Wp[(4 * k + fq) * sw + i0 + fr], acx);
+          acx1 = mfma4(Gp[(b0 + fr) * sg + 4 * k + 4 + fq], Wp[(4 * k + 4 + fq) * sw + i0 + fr], acx1);
+        }
+        acx += acx1;
       }
       hx[j] = acx;
     }
@@ -305,8 +336,8 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       if (sl >= 0) {
         const float g = wd_lds[sl];
         if (A.apply_opt) {
-          float s1 = ps[k], s2 = 0.f, s3 = 0.f;
-          const float w = upd<5>(pw[k], g * A.ada.gscale, s1, s2, s3, A.ada, 1.f, 1.f);
+          float s1 = ps[k];
+          const float w = adagrad_fast(pw[k], g * A.ada.gscale, s1, A.ada);
           pw[k] = w;  // the next step of this launch starts from the updated weight
           ps[k] = s1;
           if (last) {
@@ -325,8 +356,8 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     // was prefetched at the start (no other thread touches the row before the claim)
     const float g = atomicExch(A.grad + wrow, 0.f);
     if (g != 0.f) {
-      float z = wz, n = wn, s3 = 0.f;
-      const float w = upd<6>(wv, g * A.ftrl.gscale, z, n, s3, A.ftrl, 1.f, 1.f);
+      float z = wz, n = wn;
+      const float w = ftrl_fast(wv, g * A.ftrl.gscale, z, n, A.ftrl);
       A.master[wrow] = w;
       A.ftrl_z[wrow] = z;
       A.ftrl_n[wrow] = n;
