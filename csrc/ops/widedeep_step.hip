@@ -205,15 +205,10 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     const bool relu = l + 1 < L;
     for (int t = wave; t < tm * tn; t += WD_WAVES) {
       const int m0 = (t / tn) * 16, n0 = (t % tn) * 16;
-      // two independent accumulator chains (even / odd k): a dependent 16x16x4 f32 MFMA chain waits
-      // out each MFMA's latency; ks is a multiple of 4 (dpad pads to 16)
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-      for (int k = 0; k < ks; k += 2) {
+      for (int k = 0; k < ks; ++k)
         acc = mfma4(Ap[(m0 + fr) * sa + 4 * k + fq], Wp[(n0 + fr) * sw + 4 * k + fq], acc);
-        acc1 = mfma4(Ap[(m0 + fr) * sa + 4 * k + 4 + fq], Wp[(n0 + fr) * sw + 4 * k + 4 + fq], acc1);
-      }
-      acc += acc1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = m0 + 4 * fq + r, o = n0 + fr;
@@ -280,27 +275,19 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     for (int j = 0; j < WD_MAXT; ++j) {
       const int t = wave + j * WD_WAVES;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      if (t < tdw) {  // dW[o][i] = sum_b G[b][o] A[b][i]  (Bp / 4 is a multiple of 4)
+      if (t < tdw) {  // dW[o][i] = sum_b G[b][o] A[b][i]
         const int o0 = (t / tni) * 16, i0 = (t % tni) * 16;
-        f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int k = 0; k < Bp / 4; k += 2) {
+        for (int k = 0; k < Bp / 4; ++k)
           acc = mfma4(Gp[(4 * k + fq) * sg + o0 + fr], Ap[(4 * k + fq) * sa + i0 + fr], acc);
-          acc1 = mfma4(Gp[(4 * k + 4 + fq) * sg + o0 + fr], Ap[(4 * k + 4 + fq) * sa + i0 + fr], acc1);
-        }
-        acc += acc1;
       }
       hw[j] = acc;
       f32x4 acx = {0.f, 0.f, 0.f, 0.f};
       if (t < tdx) {  // dX[b][i] = sum_o G[b][o] W[o][i]
         const int b0 = (t / tni) * 16, i0 = (t % tni) * 16;
-        f32x4 acx1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int k = 0; k < dpad(out) / 4; k += 2) {
+        for (int k = 0; k < dpad(out) / 4; ++k)
           acx = mfma4(Gp[(b0 + fr) * sg + 4 * k + fq], Wp[(4 * k + fq) * sw + i0 + fr], acx);
-          acx1 = mfma4(Gp[(b0 + fr) * sg + 4 * k + 4 + fq], Wp[(4 * k + 4 + fq) * sw + i0 + fr], acx1);
-        }
-        acx += acx1;
       }
       hx[j] = acx;
     }
