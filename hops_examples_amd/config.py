@@ -26,8 +26,8 @@ Performance / communication knobs read where they act:
                         next smaller tile (csrc/ops/gemm_core.h plan_gemm; defaults 2 x CUs / CUs)
   HOPSX_GEMM_SPLIT_CFG, HOPSX_GEMM_SPLIT_TARGET  split-K GEMM tile (1 = 64x64) / workgroups per CU
   HOPSX_WGRAD_MFMA_MAXK  largest KH*KW*C on the direct MFMA weight gradient (default 640)
-  HOPSX_BNSTATS_MAX_1X1_FLOP  1x1 convs above this keep the library GEMM + a BN statistics pass
-                        (default 1e8); HOPSX_PLAIN_MIN_PX fewest output pixels for that library path (256)
+  HOPSX_BNSTATS_MAX_1X1_FLOP  1x1 convs above this run as plain GEMMs (gg engine) + a BN statistics
+                        pass (default 1e8); HOPSX_PLAIN_MIN_PX fewest output pixels for that path (256)
   HOPSX_BN_COOP         1 = one-launch BN backward with a grid barrier (measured slower; off)
   HOPSX_DGRAD_XCD       1 = XCD-aware block order in the direct MFMA dgrad (measured neutral; off)
   HOPSX_DISABLE         comma list of fast paths to turn off for A/B checks, e.g. bnstats, bn_defer,

@@ -681,8 +681,9 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
 
 
 def _bnstats_conv(g) -> bool:
-    """Conv shapes whose BN statistics ride on the conv epilogue: everything the hopsx kernels run,
-    except 1x1 convs big enough that the library GEMM (hipBLASLt) + a statistics pass beats them."""
+    """Conv shapes whose BN statistics ride on the conv epilogue: everything except 1x1 convs above
+    HOPSX_BNSTATS_MAX_1X1_FLOP, which run as plain GEMMs (_plain_gemm_conv: the hopsx gg engine, or
+    hipBLASLt only under HOPSX_PLAIN_GEMM=blaslt) followed by a separate statistics pass."""
     if "bnstats" in _disabled() or not K.bn_prestats_ok(g[6]):
         return False
     B, H, W, C, OH, OW, CO, KH, KW = g[:9]
@@ -691,11 +692,12 @@ def _bnstats_conv(g) -> bool:
     return C % 8 == 0
 
 
-# 1x1 routing (profiles/r2s7_plain_1x1_ab.txt): above 1e8 FLOP a 1x1 conv takes the library GEMM + a
-# BN statistics pass from 256 output pixels up (ResNet-50 B=8 +5.8 %, B=64 +1.3 % vs 1e9 / 4096; the
-# hand-written GEMM's 32x32 tiles are short of work on those long-K skinny shapes)
+# 1x1 routing: above 1e8 FLOP a 1x1 conv from 256 output pixels up leaves the stats-epilogue conv
+# kernel for the plain-GEMM path + a BN statistics pass (the thresholds were tuned in round 2 when that
+# path was hipBLASLt, profiles/r2s7_plain_1x1_ab.txt; since round 3 it is the hopsx gg engine, and the
+# library is only used under HOPSX_PLAIN_GEMM=blaslt)
 _BNSTATS_MAX_1X1_FLOP = float(os.environ.get("HOPSX_BNSTATS_MAX_1X1_FLOP", 1e8))
-# fewest output pixels for which a plain 1x1 conv goes to the library GEMM (hipBLASLt)
+# fewest output pixels for which a plain 1x1 conv takes the plain-GEMM path
 _PLAIN_MIN_PX = int(os.environ.get("HOPSX_PLAIN_MIN_PX", 256))
 
 

@@ -1,0 +1,96 @@
+#!/bin/bash
+# One-MI355X job runner (through gpurun, from the repo root): every job writes under
+# gpurun_out/<tag>/, runs each GPU step under its own time limit and stops at the first GPU failure.
+#
+#   tools/gpu.sh verify  <tag> [quick]   GPU test suite, smoke(), bench.py; + ResNet benches unless quick
+#   tools/gpu.sh persist <tag>           persistent flagship: numerics + phase timing, its tests, bench 20/200
+#   tools/gpu.sh taxi    <tag>           fused taxi step: tests, phase stamps, 200-step bench, bench.py
+#   tools/gpu.sh data    <tag>           50M-row Parquet -> HBM ingest, Titanic config 4, 2/4-rank rehearsals
+#   tools/gpu.sh configs <tag>           every BASELINE config once (benchmarks/run.py) -> all.jsonl
+#   tools/gpu.sh resnet  <tag>           CIFAR ResNet-20/56 + ResNet-50 B=64/256 benches and kernel tables
+#   tools/gpu.sh prof    <tag>           rocprofv3 kernel table of bench.py (flagship only)
+#   tools/gpu.sh pmc     <tag>           PMC passes over bench.py (one counter group per run)
+#   tools/gpu.sh knobs   <tag> "ENV=.." ...   flagship bench.py --steps 20 per env setting ("" = default)
+set -o pipefail
+job=${1:?job}; tag=${2:-$1}; shift 2
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+R=$(pwd)
+
+fail() { tail -30 "$1"; exit 1; }
+# pytest: 1 = an assertion failed (the GPU is fine, keep measuring); anything else stops the job
+pyt() { local log=$1; shift; timeout -k 10 ${T:-300} python -u -m pytest -x -v --timeout 120 --timeout-method thread "$@" > $log 2>&1
+        local rc=$?; tail -6 $log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
+bench() { local name=$1; shift; timeout -k 10 ${T:-300} python -u "$@" > $out/$name.json 2> $out/$name.err || fail $out/$name.err
+          tail -1 $out/$name.json | cut -c1-400; }
+ktable() { local d=$1 name=$2; shift 2
+           timeout -k 10 ${T:-300} rocprofv3 --kernel-trace --stats -d $out/$d -o run -- python3 "$@" > $out/$d.log 2>&1 || fail $out/$d.log
+           python tools/profdb.py $out/$d/run_results.db > $out/$name 2>/dev/null || true
+           f=$(find $out/$d -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" $out/${name%.txt}_stats.csv
+           rm -rf $out/$d; head -25 $out/$name; }
+
+case $job in
+verify)
+  T=900 pyt $out/pytest_gpu.log tests -m gpu
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || fail $out/smoke.log
+  bench bench bench.py --steps 20 --warmup 5
+  [ "$1" = quick ] && exit 0
+  bench cifar20 benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 100 --warmup 10
+  bench r50_b64 benchmarks/run.py resnet50 --batch 64 --steps 30 --warmup 5
+  bench r50_b256 benchmarks/run.py resnet50 --batch 256 --steps 10 --warmup 3 ;;
+persist)
+  timeout -k 10 240 python -u tools/persist_check.py --steps 8 --timing 32 > $out/check.log 2>&1 || fail $out/check.log
+  tail -40 $out/check.log
+  pyt $out/pytest.log tests/test_persist_gpu.py
+  bench bench20 bench.py --steps 20 --warmup 5 --no-taxi
+  bench bench200 bench.py --steps 200 --warmup 20 --no-taxi ;;
+taxi)
+  pyt $out/pytest.log tests/test_widedeep_fused_gpu.py tests/test_tfx_gpu.py
+  timeout -k 10 180 python -u tools/dbg_widedeep.py > $out/phases.txt 2>&1 || fail $out/phases.txt
+  cat $out/phases.txt
+  bench taxi benchmarks/run.py taxi --steps 200 --warmup 20
+  bench bench bench.py --steps 20 --warmup 5 ;;
+data)
+  T=400 bench ingest benchmarks/run.py titanic_ingest --rows 50000000
+  bench titanic benchmarks/run.py titanic --rows 891000 --steps 300 --warmup 20
+  for n in 2 4; do
+    HOPSX_RANK_FAST_EXIT=0 PYTHONFAULTHANDLER=1 timeout -k 10 240 python -u bench.py --gpus $n --rehearse --steps 5 --warmup 2 --no-taxi > $out/rh$n.json 2> $out/rh$n.err
+    rc=$?; echo "rehearsal $n ranks rc=$rc"; tail -3 $out/rh$n.json
+    grep -n -i "terminate\|abort\|Fatal Python\|Segmentation" $out/rh$n.err | head -20
+    [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+  done ;;
+configs)
+  : > $out/all.jsonl
+  run() { timeout -k 10 300 python benchmarks/run.py "$@" 2>>$out/err.log | tail -1 >> $out/all.jsonl || fail $out/err.log; }
+  run mnist_mirrored --steps 200 --warmup 20
+  run taxi --steps 200 --warmup 20
+  run taxi --steps 200 --warmup 20 --from-transform
+  run titanic --steps 200 --warmup 20
+  run cifar_resnet --depth 20 --batch 128 --steps 100 --warmup 10
+  run cifar_resnet --depth 56 --batch 128 --steps 50 --warmup 10
+  run resnet50 --batch 8 --steps 30 --warmup 5
+  cut -c1-300 $out/all.jsonl ;;
+resnet)
+  bench cifar20 benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 100 --warmup 10
+  bench cifar56 benchmarks/run.py cifar_resnet --depth 56 --batch 128 --steps 50 --warmup 10
+  bench r50_b64 benchmarks/run.py resnet50 --batch 64 --steps 30 --warmup 5
+  bench r50_b256 benchmarks/run.py resnet50 --batch 256 --steps 10 --warmup 3
+  ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10
+  ktable p50 r50_b64_kernels.txt benchmarks/run.py resnet50 --batch 64 --steps 20 --warmup 5 ;;
+prof)
+  ktable pf flagship_kernels.txt bench.py --steps 200 --warmup 20 --no-taxi ;;
+pmc)
+  cd /tmp
+  P="python3 $R/bench.py --steps 40 --warmup 10 --no-taxi"
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES -d "$R/$out/a" -o run --output-format csv -- $P > "$R/$out/a.log" 2>&1 && \
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES FETCH_SIZE -d "$R/$out/b" -o run --output-format csv -- $P > "$R/$out/b.log" 2>&1 && \
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES WRITE_SIZE -d "$R/$out/c" -o run --output-format csv -- $P > "$R/$out/c.log" 2>&1 ;;
+knobs)
+  for s in "$@"; do
+    r=$(env $s timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi 2>>$out/err.log) || { echo "FAIL [$s]"; fail $out/err.log; }
+    echo "[$s] $(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')" | tee -a $out/ab.txt
+  done ;;
+*) echo "unknown job $job"; exit 2 ;;
+esac
+exit 0
