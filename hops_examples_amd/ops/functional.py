@@ -801,7 +801,13 @@ def rng_state(device) -> torch.Tensor:
 
 
 def seed_device_rng(seed: int, device) -> None:
-    rng_state(device).copy_(torch.tensor([seed, 0], dtype=torch.int64))
+    """Pin the device RNG.  Does not draw from torch's global generator (rng_state's lazy default
+    does), so seeding before ``torch.manual_seed``-dependent init leaves that init unchanged."""
+    key = str(device)
+    if key in _RNG:
+        _RNG[key].copy_(torch.tensor([seed, 0], dtype=torch.int64))
+    else:
+        _RNG[key] = torch.tensor([seed, 0], dtype=torch.int64, device=device)
 
 
 def advance_rng(device) -> None:

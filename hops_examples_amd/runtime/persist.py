@@ -225,7 +225,8 @@ class _RoundGrad(torch.autograd.Function):
 
 def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torch.Tensor, cursor: int, n: int,
                     seed: int, ctr: int, salt: int, drop_p: float, lr: float, rho: float, eps: float,
-                    xscale: float = 1.0 / 255.0, xshift: float = -0.5, emulate_bf16: bool = False):
+                    xscale: float = 1.0 / 255.0, xshift: float = -0.5, emulate_bf16: bool = False,
+                    margins: list | None = None):
     """``n`` fp64 training steps of MirroredMnistCNN with the kernel's data order, dropout masks,
     loss (mean sparse CE) and Adadelta.  params / s1 / s2: name -> tensor (hopsx layouts: conv OHWI,
     dense [out, in]).  Returns fp64 (params, s1, s2, losses).
@@ -234,7 +235,11 @@ def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torc
     conv1 output, conv2 weight, the relu'd conv2 output (before the max-pool, as the kernel ties it),
     the pooled+dropout activations, the fc1 weight, dh (fc1 output gradient, not its bias gradient) and
     the conv2 output gradient — and nothing else, so the kernel differs from it only by fp32 vs fp64
-    accumulation (and the rare relu / max-pool tie that rounding flips)."""
+    accumulation (and the rare relu / max-pool tie that rounding flips).
+
+    ``margins``: a list that receives, per step, the smallest |pre-activation| of each ReLU (conv1,
+    conv2, fc1) — how close the step came to a tie that fp32-vs-fp64 accumulation can flip.  A flip
+    at fc1 moves a whole fc1 row's gradient and, through dh, every conv gradient."""
     import torch.nn.functional as F
 
     rf = _RoundFwd.apply if emulate_bf16 else (lambda t: t)
@@ -251,13 +256,18 @@ def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torc
         y = ys[bt]
         for v in P.values():
             v.requires_grad_(True)
-        h = rf(F.relu(F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"])))
-        h = rg(rf(F.relu(F.conv2d(h, rf(P["conv2.weight"]).permute(0, 3, 1, 2), P["conv2.bias"]))))
+        z1 = F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"])
+        h = rf(F.relu(z1))
+        z2 = F.conv2d(h, rf(P["conv2.weight"]).permute(0, 3, 1, 2), P["conv2.bias"])
+        h = rg(rf(F.relu(z2)))
         h = F.max_pool2d(h, 2).permute(0, 2, 3, 1).reshape(B, -1)  # NHWC flatten
         if drop_p > 0:
             keep = dropout_keep(seed, ctr + s, salt, po, drop_p).reshape(B, -1)
             h = h * keep.to(h.dtype) / (1.0 - drop_p)
-        h = F.relu(rg(F.linear(rf(h), rf(P["fc1.weight"]))) + P["fc1.bias"])
+        z3 = rg(F.linear(rf(h), rf(P["fc1.weight"]))) + P["fc1.bias"]
+        h = F.relu(z3)
+        if margins is not None:
+            margins.append({k: float(z.detach().abs().min()) for k, z in (("conv1", z1), ("conv2", z2), ("fc1", z3))})
         logits = F.linear(h, P["fc2.weight"], P["fc2.bias"])
         loss = F.cross_entropy(logits, y)
         grads = torch.autograd.grad(loss, list(P.values()))

@@ -46,7 +46,7 @@ def _snapshot(m, eng):
     return P, S1, S2, a.master.clone()
 
 
-def _run_and_reference(n, seed=0, emulate_bf16=False):
+def _run_and_reference(n, seed=0, emulate_bf16=False, margins=None):
     m, opt, eng, xs, ys = _setup(seed)
     P0, S10, S20, _ = _snapshot(m, eng)
     rng0 = eng.rng.clone().cpu()
@@ -57,7 +57,7 @@ def _run_and_reference(n, seed=0, emulate_bf16=False):
     P1, S11, S21, _ = _snapshot(m, eng)
     Pr, S1r, S2r, lr_ = persist.reference_steps(P0, S10, S20, xs, ys, 0, n, int(rng0[0]) & ((1 << 64) - 1),
                                                 int(rng0[1]), int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95,
-                                                1e-7, emulate_bf16=emulate_bf16)
+                                                1e-7, emulate_bf16=emulate_bf16, margins=margins)
     return m, opt, eng, P0, P1, Pr, S11, S1r, losses, torch.tensor(lr_, dtype=torch.float64)
 
 
@@ -72,8 +72,17 @@ def _delta_stats(P0, P1, Pr, k):
 def test_persistent_one_step_matches_bf16_emulation():
     """One step against the fp64 reference that rounds exactly the operands the kernel stores as bf16:
     what is left is fp32-vs-fp64 accumulation, so every parameter update must agree to ~1e-6 of the
-    Adadelta step (1.41e-3 = sqrt(eps / (1 - rho)) for |g| >> sqrt(eps))."""
-    m, opt, eng, P0, P1, Pr, S1k, S1r, lk, lr_ = _run_and_reference(1, emulate_bf16=True)
+    Adadelta step (1.41e-3 = sqrt(eps / (1 - rho)) for |g| >> sqrt(eps)).
+
+    The comparison is only this tight away from ReLU ties: with seed 0 one sample's fc1 unit 50 sits
+    so close to 0 that fp32-vs-fp64 accumulation flips it, which moves fc1 row 50's gradient and,
+    through dh, every conv gradient (tools/persist_diag.py; seeds 1-3 agree to cos 1.000000 on every
+    parameter).  The test pins seed 1 (smallest |fc1 pre-activation| 1.8e-5) and checks that it stays
+    clear of fp32 accumulation error (~1e-6 over K = 10816), so a change of setup that lands on a tie
+    says so instead of failing on the symptom."""
+    mg = []
+    m, opt, eng, P0, P1, Pr, S1k, S1r, lk, lr_ = _run_and_reference(1, seed=1, emulate_bf16=True, margins=mg)
+    assert mg[0]["fc1"] > 5e-6, f"setup sits on an fc1 ReLU tie: {mg[0]}"
     assert abs(float(lk[0]) - float(lr_[0])) < 1e-5 * float(lr_[0]), (lk, lr_)
     for k in eng.PARAMS:
         cos, err, dr = _delta_stats(P0, P1, Pr, k)

@@ -29,12 +29,14 @@ def one(seed):
     eng.check()
     P1, S11, _, _ = T._snapshot(m, eng)
     lk = float(eng.losses(1)[0, 0])
-    refs = {}
+    refs, mg = {}, []
     for emu in (True, False):
         refs[emu] = persist.reference_steps(P0, S10, S20, xs, ys, 0, 1, int(rng0[0]) & ((1 << 64) - 1), int(rng0[1]),
                                             int(m.pool.salt), float(m.pool.dropout), 1.0, 0.95, 1e-7,
-                                            emulate_bf16=emu)
-    print(f"seed {seed}: loss kernel {lk:.7f} emu {refs[True][3][0]:.7f} fp64 {refs[False][3][0]:.7f}")
+                                            emulate_bf16=emu, margins=mg if emu else None)
+    print(f"seed {seed}: loss kernel {lk:.7f} emu {refs[True][3][0]:.7f} fp64 {refs[False][3][0]:.7f} "
+          f"relu margins {mg[0]} | rng {rng0.tolist()} salt {int(m.pool.salt)} "
+          f"sum(P0) {sum(float(v.double().sum()) for v in P0.values()):.9f} sum(x) {int(xs.long().sum())}")
     for k in eng.PARAMS:
         dk = (P1[k] - P0[k]).double().flatten()
         de = (refs[True][0][k] - P0[k].double()).flatten()
