@@ -109,14 +109,30 @@ def main():
     nparams = param_count(model)
     ParamArena.from_module(model, dev)
     opt = optim.Adadelta(model, lr=1.0)
-    dp = DataParallel(model) if world > 1 else None
     from hops_examples_amd.runtime.persist import PersistentMnistStep
 
-    if dp is None and not a.no_graph and dev.type == "cuda" and PersistentMnistStep.supported(model, opt, B, world):
-        # one GPU: the whole step (fwd, loss, bwd, Adadelta) runs inside ONE persistent launch per 32
-        # steps, fc1 weights + optimizer state resident on chip (runtime/persist.py; HOPSX_PERSIST=0 off)
-        step = PersistentMnistStep(model, opt, steps_per_launch=32)
-    else:
+    step, dp, persist_note = None, None, None
+    if not a.no_graph and dev.type == "cuda" and PersistentMnistStep.supported(model, opt, B, world):
+        # the whole step (fwd, loss, bwd, Adadelta) runs inside ONE persistent launch per 32 steps, fc1
+        # weights + optimizer state resident on chip (runtime/persist.py; HOPSX_PERSIST=0 off); with N
+        # ranks (one per GPU) the replicas exchange activations / gradients over xGMI inside the launch
+        from hops_examples_amd.parallel import oneshot
+
+        if world == 1 or oneshot._colocation(dev) == 1:
+            try:
+                eng = PersistentMnistStep(model, opt, steps_per_launch=32)
+            except RuntimeError as e:  # raised on every rank alike (the setup agrees collectively)
+                eng, persist_note = None, f"setup failed: {e}"[:300]
+            if eng is not None and (world == 1 or eng.selftest()):
+                step = eng
+            elif eng is not None:
+                eng.close()
+                persist_note = "selftest failed: fell back to TrainStep + DataParallel"
+        else:
+            persist_note = "ranks share a GPU: persistent step needs one GPU per rank"
+    if step is None and world > 1:
+        dp = DataParallel(model)
+    if step is None:
         # 32 steps per replayed graph (Keras steps_per_execution; HOPSX_STEPS_PER_EXEC overrides): vs 8,
         # +1.5 % at the driver's 20-step run and +1 % at 200 steps (profiles/r2s7_spe_ab.txt)
         step = TrainStep(model, opt, "sparse_ce", dp=dp, graph=not a.no_graph, steps_per_execution=32)
@@ -149,6 +165,11 @@ def main():
     replicas = None
     dp_path = dp.path if dp is not None else None
     ranks = None
+    if isinstance(step, PersistentMnistStep) and world > 1:
+        replicas = step.verify_replicas()
+        dp_path = "persistent in-kernel xGMI exchange"
+        ranks = launch.gather_rank_info(dev, {"persistent_dp": True})
+        step.close()
     if dp is not None:
         replicas = dp.verify_replicas()  # outside the timed region
         ranks = launch.gather_rank_info(dev, {"p2p_world": dp.p2p_world})
@@ -190,6 +211,7 @@ def main():
                 "steps_per_execution": step.steps_per_execution if getattr(step, "_gU", True) is not None else 1,
                 "allreduce": dp_path,
                 "wire_bytes_per_param": None if dp is None else dp.wire_bytes_per_param,
+                "persistent_note": persist_note,
                 "ranks": ranks,
             },
             "replicas_identical": None if replicas is None else replicas["identical"],

@@ -58,7 +58,7 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                                S(st));
   });
   m.def("mnist_persist_geom", []() {
-    std::vector<long> g(11);
+    std::vector<long> g(14);
     hopsx_mnist_persist_geom(g.data());
     return g;
   });

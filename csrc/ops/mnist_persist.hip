@@ -93,7 +93,25 @@ constexpr int H_LOG = H_H + HID * 4;          // f32 [16]
 constexpr int H_PAY = H_LOG + 16 * 4;         // f32 [PAY]
 constexpr int H_ALL = H_PAY + PAY * 4;        // f32 [32][PAY]
 constexpr int H_END = H_ALL + NHEAD * PAY * 4;
-static_assert(H_END <= LDS_BYTES, "head LDS map must fit the position map");
+constexpr int H_DHS = H_END;                  // bf16 [32][DHS] dh staging (head 0, data-parallel)
+static_assert(H_DHS + B * DHS * 2 <= LDS_BYTES, "head LDS map must fit the position map");
+
+// ---- data-parallel exchange (DP instantiation, world > 1) ----
+// Each rank owns one uncached (UC) exchange buffer and one UC flag page, IPC-mapped by every peer.
+// A producer PUSHES its payload into every peer's buffer at slot [its rank] (system-scope write-through
+// stores), drains, and raises its flag word in every peer's page; a consumer polls its OWN page and
+// reads its OWN buffer (local memory, no L2 copies to go stale).  Flags carry a global step epoch that
+// grows across launches (never reset), payloads are double-buffered by step parity.
+constexpr int XMAX = 8;                                         // ranks (one node)
+constexpr long XS_POOL = (long)NPOS * 4 * 64 * 16;              // fc1-wgrad B fragments of all positions
+constexpr long XS_DHT = 8L * 64 * 16;                           // fc1-wgrad A fragments (dh^T), 8 n-blocks
+constexpr int NFC2 = NCLS * HID + HID + NCLS, NFC2P = 1424;     // [fc2 w | fc1 b | fc2 b] gradient
+constexpr long XS_FC2 = NFC2P * 4;
+constexpr long XS_CONV = (long)NSLICE * SLICE * 4;              // conv slice gradient sums
+constexpr long XO_POOL = 0, XO_DHT = XO_POOL + 2L * XMAX * XS_POOL, XO_FC2 = XO_DHT + 2L * XMAX * XS_DHT,
+               XO_CONV = XO_FC2 + 2L * XMAX * XS_FC2, X_BYTES = XO_CONV + 2L * XMAX * XS_CONV;
+constexpr int XF_POOL = 0, XF_H = XMAX * NPOS, XF_CONV = XF_H + XMAX, XF_WORDS = XF_CONV + XMAX * NSLICE;
+static_assert(NFC2 <= NFC2P && NFC2P % 4 == 0 && X_BYTES < 0x7fffffffL, "exchange geometry");
 static_assert(LDS_BYTES <= 160 * 1024, "one workgroup per CU: 160 KiB LDS");
 static_assert(L_RED + NRED * SLICE * 4 <= L_SL && 2 * 32 * 5 * 4 <= 1024 * 4, "reduce scratch");
 static_assert(NRED * 13 <= 256 && NSLICE * SLICE >= NCONV && NSLICE <= NPOS, "slice geometry");
@@ -127,6 +145,14 @@ struct Args {
   unsigned salt;
   int nsteps;
   int acquire;  // 1: agent-scope acquire after every poll (diagnostic; the sc1 form needs none)
+  long long tmo;  // wall-clock ticks a poll waits before it declares the producer lost
+  float inv_gb;   // 1 / global batch (world * B): the loss is the mean over every replica's images
+  // data parallel (DP instantiation)
+  int world, rank;
+  int loopback;                 // 1: one process plays every rank (peers = this rank's own buffers)
+  long long* xstep;             // global step counter (epoch base of the exchange flags)
+  unsigned char* xbuf[XMAX];    // exchange buffers of ranks 0..world-1 (own at [rank])
+  unsigned* xflag[XMAX];        // flag pages of ranks 0..world-1
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
@@ -147,13 +173,33 @@ __device__ __forceinline__ unsigned flag_load(const unsigned* f) {
   return __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr long long kTimeoutTicks = 200000000ll;  // 2 s at the 100 MHz wall clock: a hang guard only
+// system-scope (sc0 sc1) 16-B / 4-B buffer store and load: the cross-rank exchange path
+__device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, int byte_off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, byte_off, 0, 17);
+}
+__device__ __forceinline__ void st_sys1(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, byte_off, 0, 17);
+}
+__device__ __forceinline__ f32x4 ld_sys(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 17));
+}
+__device__ __forceinline__ float ld_sys1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 17));
+}
+__device__ __forceinline__ void xflag_store(unsigned* f, unsigned v) {
+  __hip_atomic_store((gu32*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned xflag_load(const unsigned* f) {
+  return __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// slot a push lands in: the producer's rank (loopback: the simulated peer's, so every slot fills)
+__device__ __forceinline__ int xslot(const Args& a, int peer) { return a.loopback ? peer : a.rank; }
 
 // Wave 0 polls flags[0..n) until every word equals `epoch` (relaxed sc1 loads + s_sleep); gives up
-// on the sticky error word or after kTimeoutTicks (recording `code`).  Returns the verdict to the
+// on the sticky error word or after a.tmo ticks (recording `code`).  Returns the verdict to the
 // whole workgroup (uniform).
 __device__ __forceinline__ bool wait_all(const unsigned* flags, int n, unsigned epoch, unsigned* err, unsigned code,
-                                      int acquire, int* s_ok) {
+                                      int acquire, int* s_ok, long long tmo) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     int good = 1;
@@ -166,7 +212,7 @@ __device__ __forceinline__ bool wait_all(const unsigned* flags, int n, unsigned 
         good = 0;
         break;
       }
-      if ((spins & 15u) == 15u && wall_clock64() - t0 > kTimeoutTicks) {
+      if ((spins & 15u) == 15u && wall_clock64() - t0 > tmo) {
         if (lane == 0) atomicCAS(err, 0u, code);
         good = 0;
         break;
@@ -180,6 +226,44 @@ __device__ __forceinline__ bool wait_all(const unsigned* flags, int n, unsigned 
   __syncthreads();
   const int g = *s_ok;
   return g != 0;
+}
+
+// Wave 0 polls this rank's flag page until word base + r * stride has reached `epoch` for every peer
+// r != rank (the epoch grows across launches: "reached" is a wrap-safe >=).  Same failure handling
+// and uniform verdict as wait_all.
+__device__ __forceinline__ bool wait_peers(const Args& a, int base, int stride, unsigned epoch, unsigned code,
+                                        int* s_ok) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned* page = a.xflag[a.rank];
+    int good = 1;
+    const long long t0 = wall_clock64();
+    for (unsigned spins = 0;; ++spins) {
+      const bool mine = lane < a.world && lane != a.rank;
+      const int ok = !mine || (int)(xflag_load(page + base + lane * stride) - epoch) >= 0;
+      if (__all(ok)) break;
+      if (__builtin_amdgcn_readfirstlane(flag_load(a.err)) != 0u) {
+        good = 0;
+        break;
+      }
+      if ((spins & 15u) == 15u && wall_clock64() - t0 > a.tmo) {
+        if (lane == 0) atomicCAS(a.err, 0u, code);
+        good = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    drain();
+    if (lane == 0) *s_ok = good;
+  }
+  __syncthreads();
+  const int g = *s_ok;
+  return g != 0;
+}
+// raise this rank's flag word base + slot * stride in every peer's page (after the payload drained)
+__device__ __forceinline__ void raise_peers(const Args& a, int base, int stride, unsigned epoch) {
+  const int r = threadIdx.x & 63;
+  if (r < a.world && r != a.rank) xflag_store(a.xflag[r] + base + xslot(a, r) * stride, epoch);
 }
 
 // Adadelta (optim_core.h upd<3>, rho = a, eps = b) with the hardware square root / reciprocal square
@@ -228,8 +312,10 @@ __device__ __forceinline__ void stamp(const Args& a, int s, int ph) {
 // position workgroup p: conv1 -> conv2 -> pool -> fc1 partial; backward of all of it; fc1 slice
 // Adadelta; conv-parameter slice owner
 // ------------------------------------------------------------------------------------------------
+template <bool DP>
 __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, int* s_ok, const OptHP& hp,
-                                            long long cur0, unsigned long long seed, unsigned long long ctr0) {
+                                            long long cur0, unsigned long long seed, unsigned long long ctr0,
+                                            long long xs0) {
   const int p = blockIdx.x, ph = p / PH, pw = p - ph * PH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int tq = fr >> 2, tp = fr & 3;
@@ -302,7 +388,8 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
                           ((uint64_t)ctr * 0x8CB92BA72F3D8DD7ull);
     for (int e = threadIdx.x; e < B * C2; e += 256) {
       const int b = e >> 6, co = e & 63;
-      KEEP[e] = P > 0.f ? (unsigned char)(uniform01(dkey, (uint64_t)((long)(b * NPOS + p) * C2 + co)) >= P) : 1;
+      const long gb = (long)a.rank * B + b;  // global image index: every replica draws its own masks
+      KEEP[e] = P > 0.f ? (unsigned char)(uniform01(dkey, (uint64_t)((gb * NPOS + p) * C2 + co)) >= P) : 1;
     }
   };
   draw_keep(0);
@@ -435,10 +522,25 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       __syncthreads();
       if (tid == 0) flag_store(a.flags + FL_A + p, ep);
     }
+    const unsigned gep = (unsigned)(xs0 + s + 1);  // cross-rank epoch (grows across launches)
+    if constexpr (DP) {
+      // push this position's pooled activations to every peer, already in the fc1-wgrad B-fragment
+      // layout (wave w: column block j = w; k = image), for the peers' fc1 weight gradient at the end
+      // of the step; off the critical path (the peers read them after their conv backward)
+      const int c0 = w * 16 + 4 * tp;
+      const f32x4 f = __builtin_bit_cast(f32x4, lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0));
+      for (int r = 0; r < a.world; ++r) {
+        if (r == a.rank) continue;
+        st_sys(rsrc(a.xbuf[r] + XO_POOL + (par * XMAX + xslot(a, r)) * XS_POOL + (long)p * 4096), (w * 64 + lane) * 16, f);
+      }
+      drain();
+      __syncthreads();
+      if (tid < 64) raise_peers(a, XF_POOL + p, NPOS, gep);
+    }
     if (s + 1 < a.nsteps) xv = xload(s + 1);  // next step's patch, consumed next iteration
     stamp(a, s, 2);
     // ---- B: dh of all 32 images ----
-    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(2, s), a.acquire, s_ok)) return;
+    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(2, s), a.acquire, s_ok, a.tmo)) return;
     stamp(a, s, 3);
     {
       const auto R = rsrc(a.slabB + (long)par * NHEAD * PAY);
@@ -454,6 +556,9 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     // ---- fc1 weight gradient (lane-owned layout) and input gradient ----
     f32x4 gw[2][4], dp[2];
     {
+      // data parallel: the weight gradient sums every replica's images in rank order at the end of
+      // the step (below); here only the input gradient
+      if constexpr (!DP) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {  // A = dh^T (row n, k = b)
         const int n0 = (2 * w + ii) * 16 + 4 * tp;
@@ -464,6 +569,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
           const bf16x8 bfr = lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0);
           gw[ii][j] = mfma(af, bfr, (f32x4){0.f, 0.f, 0.f, 0.f});
         }
+      }
       }
       dp[0] = dp[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -610,7 +716,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     stamp(a, s, 6);
     // ---- slice owners: fixed-order reduce of 52 params over the 169 partials, Adadelta, publish D ----
     if (owner) {
-      if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok)) return;
+      if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok, a.tmo)) return;
       stamp(a, s, 7);
       const int e0 = p * SLICE;
       if (tid < 13 * NRED) {
@@ -631,10 +737,33 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         *(f32x4*)(RED + g * SLICE + 4 * j) = acc;
       }
       __syncthreads();
-      if (tid < SLICE) {  // wave 0
-        const int e = e0 + tid;
-        float gs = 0.f;
+      const int e = e0 + tid;
+      float gs = 0.f;
+      if (tid < SLICE) {
         for (int g = 0; g < NRED; ++g) gs += RED[g * SLICE + tid];
+      }
+      if constexpr (DP) {
+        // this rank's slice sum to every peer, then every replica's, summed in rank order (identical
+        // on every rank, so the replicas stay bit-identical)
+        if (tid < 64) {
+          if (tid < SLICE) {
+            for (int r = 0; r < a.world; ++r) {
+              if (r == a.rank) continue;
+              st_sys1(rsrc(a.xbuf[r] + XO_CONV + (par * XMAX + xslot(a, r)) * XS_CONV), e * 4, gs);
+            }
+          }
+          drain();
+          raise_peers(a, XF_CONV + p, NSLICE, gep);
+        }
+        if (!wait_peers(a, XF_CONV + p, NSLICE, gep, ecode(6, s), s_ok)) return;
+        if (tid < SLICE) {
+          const auto X = rsrc(a.xbuf[a.rank] + XO_CONV + (long)par * XMAX * XS_CONV);
+          float t = 0.f;
+          for (int r = 0; r < a.world; ++r) t += r == a.rank ? gs : ld_sys1(X, (int)(r * XS_CONV) + e * 4);
+          gs = t;
+        }
+      }
+      if (tid < SLICE) {  // wave 0
         float wn = 0.f;
         if (e < NCONV) {
           SLm[tid] = adadelta(SLm[tid], gs * hp.gscale, SL1[tid], SL2[tid], hp);
@@ -659,6 +788,44 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       }
       stamp(a, s, 8);
     }
+    if constexpr (DP) {
+      // ---- fc1 weight gradient over every replica's images: dh^T fragments (each rank's head 0) and
+      // pooled fragments (each rank's position p), accumulated in rank order on one MFMA chain ----
+      if (!wait_peers(a, XF_H, 1, gep, ecode(7, s), s_ok)) return;
+      if (!wait_peers(a, XF_POOL + p, NPOS, gep, ecode(8, s), s_ok)) return;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gw[ii][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const auto XP = rsrc(a.xbuf[a.rank] + XO_POOL + (long)par * XMAX * XS_POOL + (long)p * 4096);
+      const auto XD = rsrc(a.xbuf[a.rank] + XO_DHT + (long)par * XMAX * XS_DHT);
+      for (int r = 0; r < a.world; ++r) {
+        bf16x8 af[2], bfr[4];
+        if (r == a.rank) {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            const int n0 = (2 * w + ii) * 16 + 4 * tp;
+            af[ii] = lds_tr(DH + (8 * fq + tq) * DHS + n0, DH + (8 * fq + tq + 4) * DHS + n0);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c0 = j * 16 + 4 * tp;
+            bfr[j] = lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0);
+          }
+        } else {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+            af[ii] = __builtin_bit_cast(bf16x8, ld_sys(XD, (int)(r * XS_DHT) + ((2 * w + ii) * 64 + lane) * 16));
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            bfr[j] = __builtin_bit_cast(bf16x8, ld_sys(XP, (int)(r * XS_POOL) + (j * 64 + lane) * 16));
+        }
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) gw[ii][j] = mfma(af[ii], bfr[j], gw[ii][j]);
+      }
+    }
     // ---- Adadelta on the fc1 slice (registers) and the new bf16 weights for the next forward: off the
     // critical path, while this workgroup waits for the D hand-off (W1 is next read after it) ----
 #pragma unroll
@@ -673,7 +840,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     if (s + 1 < a.nsteps) draw_keep(s + 1);  // KEEP is next read after the D wait's barrier
     stamp(a, s, 9);
     // ---- D: the updated conv parameters for the next step ----
-    if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok)) return;
+    if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok, a.tmo)) return;
     stamp(a, s, 10);
     {
       const auto R = rsrc((const unsigned char*)a.slabD + (long)par * D_BYTES);
@@ -725,6 +892,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
   // every workgroup has started (D of the last step needs C of every position, which needs B of
   // every head): the run-state words can advance
   if (p == 0 && tid == 0) {
+    if constexpr (DP) a.xstep[0] = xs0 + a.nsteps;
     a.cursor[0] = (cur0 + a.nsteps) % a.nbatch;
     a.rng[1] = ctr0 + (unsigned long long)a.nsteps;
     if (a.step_dev) a.step_dev[0] += (float)a.nsteps;
@@ -735,8 +903,9 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
 // head workgroup i (image i): fc1 reduce + bias + relu, Dense10, softmax CE, dh; replicated
 // fc2 / fc1-bias Adadelta from all 32 payloads
 // ------------------------------------------------------------------------------------------------
+template <bool DP>
 __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int* s_ok, const OptHP& hp,
-                                        long long cur0) {
+                                        long long cur0, long long xs0) {
   const int i = blockIdx.x - NPOS;
   const int tid = threadIdx.x, lane = tid & 63;
   float* HW = (float*)(smem + H_W2);
@@ -777,7 +946,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     const int par = s & 1;
     const int y = (int)a.ys[((cur0 + s) % a.nbatch) * B + i];
     // ---- A: reduce the 169 fc1 partial rows of image i (fixed order) ----
-    if (!wait_all(a.flags + FL_A, NPOS, ep, a.err, ecode(1, s), a.acquire, s_ok)) return;
+    if (!wait_all(a.flags + FL_A, NPOS, ep, a.err, ecode(1, s), a.acquire, s_ok, a.tmo)) return;
     stamp(a, s, 0);
     {
       const int n4 = tid & 31, g = tid >> 5;
@@ -821,7 +990,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
       const float se = wave_sum(e);
       const unsigned long long hit = __ballot(lane < NCLS && z == m);
       const int am = __ffsll((long long)hit) - 1;
-      if (lane < NCLS) PAYL[PAY_DL + lane] = (e / se - (lane == y ? 1.f : 0.f)) * (1.f / B);
+      if (lane < NCLS) PAYL[PAY_DL + lane] = (e / se - (lane == y ? 1.f : 0.f)) * a.inv_gb;
       if (lane == 0) {
         PAYL[PAY_LOSS] = __logf(se) + m - LOG[y];
         PAYL[PAY_COR] = am == y ? 1.f : 0.f;
@@ -846,7 +1015,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     }
     stamp(a, s, 1);
     // ---- replicated fc2 / fc1-bias update from every image's payload ----
-    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(5, s), a.acquire, s_ok)) return;
+    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(5, s), a.acquire, s_ok, a.tmo)) return;
     {
       const auto R = rsrc(a.slabB + (long)par * NHEAD * PAY);
       constexpr int NK = (NHEAD * PAY / 4 + 255) / 256;
@@ -863,24 +1032,86 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
       }
     }
     __syncthreads();
-    for (int j = tid; j < NCLS * HID; j += 256) {
-      const int c = j / HID, n = j - c * HID;
+    // this replica's fc2 / fc1-bias / fc2-bias gradients: element tid + 256 k of fc2.weight (k < 5),
+    // fc1.bias[tid], fc2.bias[tid]
+    constexpr int NW = NCLS * HID / 256;
+    static_assert(NCLS * HID == NW * 256, "fc2 weight split");
+    float gl[NW + 2];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int j = tid + 256 * k, c = j / HID, n = j - c * HID;
       float g = 0.f;
 #pragma unroll 8
       for (int b = 0; b < B; ++b) g = fmaf(ALL[b * PAY + PAY_DL + c], ALL[b * PAY + PAY_H + n], g);
-      HW[j] = adadelta(HW[j], g * hp.gscale, HW1[j], HW2[j], hp);
+      gl[k] = g;
     }
+    gl[NW] = gl[NW + 1] = 0.f;
     if (tid < HID) {
-      float g = 0.f;
 #pragma unroll 8
-      for (int b = 0; b < B; ++b) g += ALL[b * PAY + PAY_DH + tid];
-      HB1[tid] = adadelta(HB1[tid], g * hp.gscale, HB1[128 + tid], HB1[256 + tid], hp);
+      for (int b = 0; b < B; ++b) gl[NW] += ALL[b * PAY + PAY_DH + tid];
     }
     if (tid < NCLS) {
-      float g = 0.f;
-      for (int b = 0; b < B; ++b) g += ALL[b * PAY + PAY_DL + tid];
-      HB2[tid] = adadelta(HB2[tid], g * hp.gscale, HB2[16 + tid], HB2[32 + tid], hp);
+      for (int b = 0; b < B; ++b) gl[NW + 1] += ALL[b * PAY + PAY_DL + tid];
     }
+    if constexpr (DP) {
+      const unsigned gep = (unsigned)(xs0 + s + 1);
+      if (i == 0) {
+        // head 0 pushes this replica's head gradients and dh^T (fc1-wgrad A fragments, bf16, the layout
+        // the position workgroups read from their own LDS) to every peer
+        bf16_raw* DS = (bf16_raw*)(smem + H_DHS);
+        for (int e = tid; e < B * HID; e += 256) DS[(e >> 7) * DHS + (e & 127)] = f2bf(ALL[(e >> 7) * PAY + PAY_DH + (e & 127)]);
+        __syncthreads();
+        const int w = tid >> 6, fr = lane & 15, fq = lane >> 4, tq = fr >> 2, tp = fr & 3;
+        f32x4 fd[2];
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int n0 = (2 * w + ii) * 16 + 4 * tp;
+          fd[ii] = __builtin_bit_cast(f32x4, lds_tr(DS + (8 * fq + tq) * DHS + n0, DS + (8 * fq + tq + 4) * DHS + n0));
+        }
+        for (int r = 0; r < a.world; ++r) {
+          if (r == a.rank) continue;
+          const int sl = xslot(a, r);
+          const auto XG = rsrc(a.xbuf[r] + XO_FC2 + (par * XMAX + sl) * XS_FC2);
+#pragma unroll
+          for (int k = 0; k < NW; ++k) st_sys1(XG, (tid + 256 * k) * 4, gl[k]);
+          if (tid < HID) st_sys1(XG, (NCLS * HID + tid) * 4, gl[NW]);
+          if (tid < NCLS) st_sys1(XG, (NCLS * HID + HID + tid) * 4, gl[NW + 1]);
+          const auto XD = rsrc(a.xbuf[r] + XO_DHT + (par * XMAX + sl) * XS_DHT);
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) st_sys(XD, ((2 * w + ii) * 64 + lane) * 16, fd[ii]);
+        }
+        drain();
+        __syncthreads();
+        if (tid < 64) raise_peers(a, XF_H, 1, gep);
+      }
+      if (!wait_peers(a, XF_H, 1, gep, ecode(9, s), s_ok)) return;
+      // every replica's gradient, summed in rank order
+      const auto X = rsrc(a.xbuf[a.rank] + XO_FC2 + (long)par * XMAX * XS_FC2);
+      float t[NW + 2];
+#pragma unroll
+      for (int k = 0; k < NW + 2; ++k) t[k] = 0.f;
+      for (int r = 0; r < a.world; ++r) {
+        if (r == a.rank) {
+#pragma unroll
+          for (int k = 0; k < NW + 2; ++k) t[k] += gl[k];
+        } else {
+          const int o = (int)(r * XS_FC2);
+#pragma unroll
+          for (int k = 0; k < NW; ++k) t[k] += ld_sys1(X, o + (tid + 256 * k) * 4);
+          if (tid < HID) t[NW] += ld_sys1(X, o + (NCLS * HID + tid) * 4);
+          if (tid < NCLS) t[NW + 1] += ld_sys1(X, o + (NCLS * HID + HID + tid) * 4);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NW + 2; ++k) gl[k] = t[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int j = tid + 256 * k;
+      HW[j] = adadelta(HW[j], gl[k] * hp.gscale, HW1[j], HW2[j], hp);
+    }
+    if (tid < HID) HB1[tid] = adadelta(HB1[tid], gl[NW] * hp.gscale, HB1[128 + tid], HB1[256 + tid], hp);
+    if (tid < NCLS) HB2[tid] = adadelta(HB2[tid], gl[NW + 1] * hp.gscale, HB2[16 + tid], HB2[32 + tid], hp);
     if (i == 0 && tid == 255) {
       float l = 0.f, cc = 0.f;
       for (int b = 0; b < B; ++b) {
@@ -918,28 +1149,35 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
   }
 }
 
+template <bool DP>
 __global__ __launch_bounds__(256, 1) void mnist_persist_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_ok;
   const OptHP hp = load_hp(a.hp, a.hp_dev);
   const long long cur0 = a.cursor[0];
+  const long long xs0 = DP ? a.xstep[0] : 0;
   if (blockIdx.x < NPOS) {
-    position_wg(a, smem, &s_ok, hp, cur0, a.rng[0], a.rng[1]);
+    position_wg<DP>(a, smem, &s_ok, hp, cur0, a.rng[0], a.rng[1], xs0);
   } else {
-    head_wg(a, smem, &s_ok, hp, cur0);
+    head_wg<DP>(a, smem, &s_ok, hp, cur0, xs0);
   }
 }
 
 }  // namespace mnistp
 
-// ptrs: master shadow s1 s2 xs ys cursor rng step_dev hp_dev slabA slabB slabC slabD flags err out [dbg]
-// iv:   off[8] nbatch salt nsteps batch acquire
+// ptrs: master shadow s1 s2 xs ys cursor rng step_dev hp_dev slabA slabB slabC slabD flags err out dbg(0 = none)
+//       [xstep xbuf[world] xflag[world]]   (world > 1: the data-parallel instantiation)
+// iv:   off[8] nbatch salt nsteps batch acquire world rank loopback timeout_ms
 // fv:   drop_p xscale xshift lr gscale wd rho eps
 extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, int ni, const float* fv, int nf,
                                    hipStream_t st) {
   using namespace mnistp;
-  if (np < 17 || ni < 13 || nf < 8) return (int)hipErrorInvalidValue;
+  if (np < 18 || ni < 17 || nf < 8) return (int)hipErrorInvalidValue;
   if (iv[11] != B || iv[10] < 1 || iv[8] < 1) return (int)hipErrorInvalidValue;
+  const int world = (int)iv[13], rank = (int)iv[14];
+  if (world < 1 || world > XMAX || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
+  const bool dp = world > 1;
+  if (dp && np < 19 + 2 * world) return (int)hipErrorInvalidValue;
   Args a{};
   a.master = (float*)p[0];
   a.shadow = (bf16_raw*)p[1];
@@ -958,26 +1196,42 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.flags = (unsigned*)p[14];
   a.err = (unsigned*)p[15];
   a.out = (float*)p[16];
-  a.dbg = np > 17 ? (unsigned long long*)p[17] : nullptr;
+  a.dbg = (unsigned long long*)p[17];
   for (int k = 0; k < 8; ++k) a.off[k] = iv[k];
   a.nbatch = iv[8];
   a.salt = (unsigned)iv[9];
   a.nsteps = (int)iv[10];
   a.acquire = (int)iv[12];
+  a.world = world;
+  a.rank = rank;
+  a.loopback = (int)iv[15];
+  a.tmo = (long long)iv[16] * 100000ll;  // ms -> 100 MHz ticks
+  a.inv_gb = 1.f / (float)(world * B);
+  if (dp) {
+    a.xstep = (long long*)p[18];
+    for (int r = 0; r < world; ++r) {
+      a.xbuf[r] = (unsigned char*)p[19 + r];
+      a.xflag[r] = (unsigned*)p[19 + world + r];
+      if (!a.xbuf[r] || !a.xflag[r] || ((uint64_t)a.xbuf[r] & 15)) return (int)hipErrorInvalidValue;
+    }
+  }
   a.drop_p = fv[0];
   a.xscale = fv[1];
   a.xshift = fv[2];
   a.hp = OptHP{fv[3], fv[4], fv[5], fv[6], fv[7], 0.f, 0.f, 0.f};
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)mnist_persist_k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             LDS_BYTES);
+  static bool attr[2] = {false, false};
+  const void* fn = dp ? (const void*)mnist_persist_k<true> : (const void*)mnist_persist_k<false>;
+  if (!attr[dp]) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return (int)e;
-    attr = true;
+    attr[dp] = true;
   }
   hipError_t e = hipMemsetAsync(a.flags, 0, FL_WORDS * sizeof(unsigned), st);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mnist_persist_k, dim3(GRID), dim3(256), LDS_BYTES, st, a);
+  if (dp)
+    hipLaunchKernelGGL(mnist_persist_k<true>, dim3(GRID), dim3(256), LDS_BYTES, st, a);
+  else
+    hipLaunchKernelGGL(mnist_persist_k<false>, dim3(GRID), dim3(256), LDS_BYTES, st, a);
   return (int)hipGetLastError();
 }
 
@@ -995,4 +1249,7 @@ extern "C" void hopsx_mnist_persist_geom(long* g) {
   g[8] = FL_WORDS;
   g[9] = LDS_BYTES;
   g[10] = D_BYTES;
+  g[11] = X_BYTES;
+  g[12] = XF_WORDS;
+  g[13] = XMAX;
 }

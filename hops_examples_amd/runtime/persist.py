@@ -15,8 +15,20 @@ batch of ``xs``/``ys`` (cycling), with dropout masks keyed on the device RNG cou
 the batch cursor are up to date in HBM when a launch returns.  The result is deterministic: no float
 atomics, every cross-workgroup sum is a fixed-order loop.
 
-Limits: one GPU (data-parallel runs use TrainStep + the fused P2P step), batch 32, Adadelta, the
-MirroredMnistCNN architecture.  ``PersistentMnistStep.supported(...)`` says whether it applies.
+Data parallel (world 2..8, one rank per GPU of one node): every rank runs the same persistent
+kernel on its own 32 images and the replicas exchange, inside the launch, exactly what the update
+needs over xGMI — each position's pooled activations and each rank's dh (the fc1 weight gradient is
+their product, so 1.38 M gradient floats never cross the wire), the 1,418 head gradients and the
+8,416 conv-gradient slice sums.  Producers push into the peers' uncached exchange buffers and raise a
+flag word in the peers' flag pages; consumers poll their own page (csrc/ops/mnist_persist.hip,
+"data-parallel exchange").  Every cross-rank sum runs in rank order, so the replicas stay
+bit-identical; the loss is the mean over the global batch (MirroredStrategy semantics,
+mirroredstrategy_mnist_example.ipynb:128-131).  ``loopback=world`` lets ONE process play every rank
+(the peers' buffers are its own): the same code paths on one GPU, for tests.
+
+Limits: batch 32 per replica, Adadelta, the MirroredMnistCNN architecture, ranks on distinct GPUs
+(two kernels of 201 one-per-CU workgroups cannot be co-resident on one GPU).
+``PersistentMnistStep.supported(...)`` says whether it applies.
 """
 from __future__ import annotations
 
@@ -39,7 +51,7 @@ def geometry() -> dict:
     if _GEOM is None:
         g = _ext().mnist_persist_geom()
         _GEOM = dict(zip(["batch", "npos", "nhead", "grid", "nconv", "nslice", "slice", "pay", "flag_words",
-                          "lds_bytes", "d_bytes"], g))
+                          "lds_bytes", "d_bytes", "x_bytes", "xflag_words", "max_ranks"], g))
     return _GEOM
 
 
@@ -53,18 +65,29 @@ class PersistentMnistStep:
 
     @staticmethod
     def supported(model, opt, batch: int, world: int = 1) -> bool:
+        """Local checks (model, optimizer, batch, world size).  For world > 1 the caller also needs
+        every rank on its own GPU of one node (``parallel.oneshot._colocation``) and a passing
+        ``selftest()``; ``HOPSX_PERSIST_DP=0`` keeps data-parallel runs on TrainStep."""
         from ..models.mnist import MirroredMnistCNN
         from ..optim import Adadelta
 
         if os.environ.get("HOPSX_PERSIST", "1") != "1":
             return False
+        if world > 1 and (os.environ.get("HOPSX_PERSIST_DP", "1") != "1" or world > geometry()["max_ranks"]):
+            return False
         a = getattr(opt, "arena", None)
-        return (isinstance(model, MirroredMnistCNN) and isinstance(opt, Adadelta) and world == 1 and batch == 32
+        return (isinstance(model, MirroredMnistCNN) and isinstance(opt, Adadelta) and batch == 32
                 and a is not None and a.device.type == "cuda" and a.shadow is not None
                 and opt._sl.start == 0 and opt._sl.stop >= a.numel and model.training)
 
-    def __init__(self, model, opt, steps_per_launch: int = 32, debug_stamps: bool = False):
+    def __init__(self, model, opt, steps_per_launch: int = 32, debug_stamps: bool = False, world: int | None = None,
+                 loopback: int = 0, timeout_s: float | None = None):
+        """``world``: replicas (default: the process group's size; 1 without one).  ``loopback``: play
+        that many ranks in this one process (tests).  ``timeout_s``: how long a hand-off waits before
+        the launch is declared failed (default 2 s on one GPU, ``HOPSX_PERSIST_TIMEOUT_S`` or 60 s
+        across ranks, whose launches can start far apart)."""
         from ..ops.functional import rng_state
+        from ..parallel import dist as hdist
 
         a = opt.arena
         self.model, self.opt, self.arena = model, opt, a
@@ -90,10 +113,147 @@ class PersistentMnistStep:
         self.rng = rng_state(dev)
         self.dbg = torch.zeros(g["grid"] * self.spl * 16, device=dev, dtype=torch.int64) if debug_stamps else None
         self.acquire = int(os.environ.get("HOPSX_PERSIST_ACQUIRE", "0"))
+        self.loopback = int(loopback)
+        if self.loopback > 1:
+            self.world, self.rank = self.loopback, 0
+        else:
+            self.world = int(world) if world is not None else hdist.world_size()
+            self.rank = hdist.rank() if self.world > 1 else 0
+        if self.world > g["max_ranks"]:
+            raise ValueError(f"the persistent step supports <= {g['max_ranks']} ranks")
+        default_t = "60" if self.world > 1 else "2"
+        self.timeout_ms = int(1000 * float(timeout_s or os.environ.get("HOPSX_PERSIST_TIMEOUT_S", default_t)))
+        self._xptrs: list[int] = []
+        self._owned: list[int] = []
+        self._opened: list[int] = []
+        if self.world > 1:
+            self._setup_exchange()
         self.use_graph = False
         self.steps_per_execution = self.spl
         self._last = None
         self._n = 0
+
+    # ------------------------------------------------------------------ data parallel
+    def _setup_exchange(self) -> None:
+        """Allocate this rank's uncached exchange buffer + flag page, map every peer's (IPC handles
+        through the default process group), make the replicas identical (rank 0's weights)."""
+        import torch.distributed as dist
+
+        from ..parallel import oneshot
+
+        C = oneshot.ext()
+        g = self.geom
+        local = self.loopback > 1
+        err = None
+        try:
+            buf, hb = C.alloc(int(g["x_bytes"]), True)
+            self._owned.append(buf)
+            flg, hf = C.alloc(int(g["xflag_words"]) * 4, True)
+            self._owned.append(flg)
+        except Exception as e:  # every rank must learn of it before the handle exchange
+            err, hb, hf = repr(e), None, None
+        self.xstep = torch.zeros(1, device=self.device, dtype=torch.int64)
+        if local:
+            if err:
+                raise RuntimeError(f"persistent DP exchange setup failed: {err}")
+            bufs, flags = [buf] * self.world, [flg] * self.world
+        else:
+            objs = [None] * self.world
+            dist.all_gather_object(objs, (self.rank, None if err else bytes(hb), None if err else bytes(hf), err))
+            bad = [(o[0], o[3]) for o in objs if o[3]]
+            if bad:
+                self.close()
+                raise RuntimeError(f"persistent DP exchange setup failed on ranks {bad}")
+            bufs, flags = [0] * self.world, [0] * self.world
+            try:
+                for r, b, f, _ in objs:
+                    if r == self.rank:
+                        bufs[r], flags[r] = buf, flg
+                    else:
+                        bufs[r] = C.open(b)
+                        self._opened.append(bufs[r])
+                        flags[r] = C.open(f)
+                        self._opened.append(flags[r])
+            except Exception as e:
+                err = repr(e)
+            oks = [None] * self.world
+            dist.all_gather_object(oks, err)
+            if any(oks):
+                self.close()
+                raise RuntimeError(f"persistent DP: mapping a peer's exchange buffer failed: {oks}")
+            # replicas start from rank 0's parameters and optimizer state
+            a = self.arena
+            for t in (a.master, self.s1, self.s2):
+                dist.broadcast(t, 0)
+            a.shadow.copy_(a.master.to(a.shadow.dtype))
+            dist.broadcast(self.opt.step_count, 0)
+            torch.cuda.synchronize(self.device)
+            dist.barrier()
+        self._xptrs = [self.xstep.data_ptr()] + bufs + flags
+
+    def close(self) -> None:
+        """Unmap the peers' buffers and free this rank's (collective in spirit: call on every rank
+        after the last launch has finished)."""
+        if not self._owned:
+            return
+        from ..parallel import oneshot
+
+        C = oneshot.ext()
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            C.close(p)
+        for p in self._owned:
+            C.free(p)
+        self._opened, self._owned, self._xptrs = [], [], []
+
+    def param_digest(self) -> tuple[float, int]:
+        """(sum, integer bit-sum) of the fp32 master: equal on every replica iff the replicas agree."""
+        m = self.arena.master
+        return float(m.double().sum()), int(m.view(torch.int32).long().sum())
+
+    def verify_replicas(self) -> dict:
+        """Collective: do all replicas hold bit-identical parameters?"""
+        import torch.distributed as dist
+
+        d = self.param_digest()
+        if self.world <= 1 or self.loopback > 1:
+            return {"identical": True, "digests": [d]}
+        objs = [None] * self.world
+        dist.all_gather_object(objs, d)
+        return {"identical": all(o == objs[0] for o in objs), "digests": objs}
+
+    def selftest(self, steps: int = 3) -> bool:
+        """Collective pre-flight of the cross-rank exchange on a scratch copy of the model state: a few
+        launches on this rank's own random batch, then every rank must report no hand-off error and
+        bit-identical scratch parameters.  The real state (arena, optimizer, RNG counter, cursor)
+        is untouched.  Returns the verdict every rank agrees on."""
+        import torch.distributed as dist
+
+        a = self.arena
+        B = self.geom["batch"]
+        saved = [t.clone() for t in (a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor)]
+        ok = True
+        try:
+            xs = torch.randint(0, 256, (2, B, 28, 28, 1), dtype=torch.uint8, device=self.device)
+            ys = torch.randint(0, 10, (2, B), dtype=torch.int64, device=self.device)
+            for k in (steps, 1):
+                self._launch(xs, ys, 2, k)
+            torch.cuda.synchronize(self.device)
+            ok = int(self.err[0].item()) == 0
+            dig = self.param_digest()
+        except Exception:
+            ok, dig = False, None
+        finally:
+            for t, s in zip((a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor), saved):
+                t.copy_(s)
+            torch.cuda.synchronize(self.device)
+        if self.world > 1 and self.loopback <= 1:
+            objs = [None] * self.world
+            dist.all_gather_object(objs, (ok, dig))
+            ok = all(o[0] for o in objs) and all(o[1] == objs[0][1] for o in objs)
+        if ok:
+            self.err.zero_()
+        return ok
 
     # ------------------------------------------------------------------ launch
     def _check_data(self, xs, ys):
@@ -117,13 +277,13 @@ class PersistentMnistStep:
                 ys.data_ptr(), self.cursor.data_ptr(), self.rng.data_ptr(), opt.step_count.data_ptr(),
                 opt._hp_dev.data_ptr() if opt._hp_dev is not None else 0, self.slabA.data_ptr(),
                 self.slabB.data_ptr(), self.slabC.data_ptr(), self.slabD.data_ptr(), self.flags.data_ptr(),
-                self.err.data_ptr(), self.out.data_ptr()]
-        if self.dbg is not None:
-            ptrs.append(self.dbg.data_ptr())
+                self.err.data_ptr(), self.out.data_ptr(), self.dbg.data_ptr() if self.dbg is not None else 0]
+        ptrs += self._xptrs
         pool = m.pool
         drop = float(pool.dropout) if pool.training else 0.0
         scale, shift = m.conv1.in_affine
-        iv = self.offs + [nb, int(pool.salt), int(k), self.geom["batch"], self.acquire]
+        iv = self.offs + [nb, int(pool.salt), int(k), self.geom["batch"], self.acquire, self.world, self.rank,
+                          1 if self.loopback > 1 else 0, self.timeout_ms]
         fv = [drop, float(scale), float(shift)] + (hp + [0.0] * 5)[:5]
         _C.check(self._ext.mnist_persist(ptrs, iv, fv, _C.stream()), "mnist_persist")
 

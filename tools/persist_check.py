@@ -21,7 +21,7 @@ from hops_examples_amd.runtime import persist  # noqa: E402
 from hops_examples_amd.runtime.arena import ParamArena  # noqa: E402
 
 
-def setup(seed, spl, stamps=False, nb=8):
+def setup(seed, spl, stamps=False, nb=8, loopback=0):
     torch.manual_seed(seed)
     dev = torch.device("cuda", 0)
     m = MirroredMnistCNN().to(dev)
@@ -29,7 +29,8 @@ def setup(seed, spl, stamps=False, nb=8):
     opt = optim.Adadelta(m, lr=1.0)
     xs = torch.randint(0, 256, (nb, 32, 28, 28, 1), dtype=torch.uint8, device=dev)
     ys = torch.randint(0, 10, (nb, 32), dtype=torch.int64, device=dev)
-    return m, opt, persist.PersistentMnistStep(m, opt, steps_per_launch=spl, debug_stamps=stamps), xs, ys
+    return m, opt, persist.PersistentMnistStep(m, opt, steps_per_launch=spl, debug_stamps=stamps,
+                                                                  loopback=loopback), xs, ys
 
 
 def numerics(n):
@@ -63,8 +64,8 @@ def numerics(n):
                   f"|dref|max {dr.abs().max().item():.3e} s1 rel {srel:.6f}")
 
 
-def timing(n, reps=5):
-    m, opt, eng, xs, ys = setup(1, n, stamps=True, nb=64)
+def timing(n, reps=5, loopback=0):
+    m, opt, eng, xs, ys = setup(1, n, stamps=True, nb=64, loopback=loopback)
     eng.run_resident(xs, ys, n)  # warm
     torch.cuda.synchronize()
     ts = []
@@ -78,7 +79,7 @@ def timing(n, reps=5):
     pos, head = st[:169], st[169:]
     own = pos[:162]
     step_us = (pos[:, 2:, 0] - pos[:, 1:-1, 0]).median().item()
-    print(f"host wall {min(ts):.2f} us/step (best of {reps}), in-kernel step {step_us:.2f} us")
+    print(f"[loopback {loopback}] host wall {min(ts):.2f} us/step (best of {reps}), in-kernel step {step_us:.2f} us")
 
     def med(t, a, b):
         return (t[:, 1:, b] - t[:, 1:, a]).median().item()
@@ -105,7 +106,13 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--timing", type=int, default=32)
+    ap.add_argument("--loopback", type=int, nargs="*", default=[],
+                    help="also time the data-parallel instantiation playing these world sizes in-process")
+    ap.add_argument("--timing-only", action="store_true")
     a = ap.parse_args()
-    numerics(1)
-    numerics(a.steps)
+    if not a.timing_only:
+        numerics(1)
+        numerics(a.steps)
     timing(a.timing)
+    for w in a.loopback:
+        timing(a.timing, loopback=w)
