@@ -28,6 +28,26 @@ static inline T* P(u p) {
 }
 static inline hipStream_t S(u s) { return reinterpret_cast<hipStream_t>(s); }
 
+// deterministic mode: one flag per kernel translation unit (common.h HOPSX_DET_TU)
+extern "C" int hopsx_det_set_conv_mfma(int);
+extern "C" unsigned hopsx_det_lost_conv_mfma();
+extern "C" int hopsx_det_set_loss(int);
+extern "C" unsigned hopsx_det_lost_loss();
+extern "C" int hopsx_det_set_gemm(int);
+extern "C" unsigned hopsx_det_lost_gemm();
+extern "C" int hopsx_det_set_norm(int);
+extern "C" unsigned hopsx_det_lost_norm();
+extern "C" int hopsx_det_set_pool(int);
+extern "C" unsigned hopsx_det_lost_pool();
+extern "C" int hopsx_det_set_conv(int);
+extern "C" unsigned hopsx_det_lost_conv();
+extern "C" int hopsx_det_set_elementwise(int);
+extern "C" unsigned hopsx_det_lost_elementwise();
+extern "C" int hopsx_det_set_rowreduce(int);
+extern "C" unsigned hopsx_det_lost_rowreduce();
+extern "C" int hopsx_det_set_wgrad_glds(int);
+extern "C" unsigned hopsx_det_lost_wgrad_glds();
+
 PYBIND11_MODULE(_hopsx_ops, m) {
   m.doc() = "hopsx CDNA4 (gfx950) HIP kernel library";
   m.attr("ARCH") = "gfx950";
@@ -53,6 +73,32 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     return hopsx_widedeep_slots(iv.data(), (int)iv.size(), P<int>(out), n);
   });
   m.def("widedeep_step_lds", [](std::vector<long> iv) { return hopsx_widedeep_step_lds(iv.data(), (int)iv.size()); });
+  m.def("set_deterministic", [](int on) {
+    int e = 0;
+    if (!e) e = hopsx_det_set_conv_mfma(on);
+    if (!e) e = hopsx_det_set_loss(on);
+    if (!e) e = hopsx_det_set_gemm(on);
+    if (!e) e = hopsx_det_set_norm(on);
+    if (!e) e = hopsx_det_set_pool(on);
+    if (!e) e = hopsx_det_set_conv(on);
+    if (!e) e = hopsx_det_set_elementwise(on);
+    if (!e) e = hopsx_det_set_rowreduce(on);
+    if (!e) e = hopsx_det_set_wgrad_glds(on);
+    return e;
+  });
+  m.def("det_lost", []() {
+    unsigned n = 0;
+    n += hopsx_det_lost_conv_mfma();
+    n += hopsx_det_lost_loss();
+    n += hopsx_det_lost_gemm();
+    n += hopsx_det_lost_norm();
+    n += hopsx_det_lost_pool();
+    n += hopsx_det_lost_conv();
+    n += hopsx_det_lost_elementwise();
+    n += hopsx_det_lost_rowreduce();
+    n += hopsx_det_lost_wgrad_glds();
+    return n;
+  });
   m.def("mnist_persist", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, u st) {
     return hopsx_mnist_persist(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),
                                S(st));

@@ -153,3 +153,70 @@ static inline long hopsx_env_int(const char* name, long dflt) {
   const char* e = std::getenv(name);
   return e && *e ? std::atol(e) : dflt;
 }
+
+// ---- deterministic mode (HOPSX_DETERMINISTIC=1) ----
+// Every float reduction that crosses workgroups is made order-fixed, so a replay from the same state
+// is bit-identical:
+//  * host side: no split-K (plan_gemm / want_splitk / the gg engine plan one K slice per tile), so an
+//    output element of a GEMM has exactly one producer;
+//  * device side: the sites where several workgroups add into the same floats (bias-gradient column
+//    sums, weight-gradient partials over pixel chunks, split-K head workspaces, BatchNorm statistics)
+//    take turns in workgroup order: workgroup `my` waits until the site's counter reads `my`, adds,
+//    drains its atomics and hands the turn on (the last one resets the counter to zero).  Workgroups
+//    are dispatched in id order per XCD, so the lowest waiting one's predecessor is always running
+//    or done: no deadlock; a wait that still exceeds ~1 s gives up (correct, no longer ordered) and
+//    counts in hx_det_lost.  Deterministic mode assumes one stream (concurrent launches of the same
+//    site would interleave their turns).
+// The flag and the counters are per translation unit (static device symbols, zero at load);
+// HOPSX_DET_TU(tag) in a .hip file defines the host setter hopsx_det_set_<tag>.
+static inline bool hopsx_deterministic() {
+  static const bool on = [] {
+    const char* e = std::getenv("HOPSX_DETERMINISTIC");
+    return e && *e == '1';
+  }();
+  return on;
+}
+constexpr int HX_DET_SITES = 16;
+static __device__ int hx_det_on;
+static __device__ unsigned hx_det_ctr[HX_DET_SITES * 32];  // one 128-B line per site
+static __device__ unsigned hx_det_lost;
+// site ids (distinct per kernel that may run in the same launch)
+enum HxDetSite : int { DET_GEMM_COLSUM = 0, DET_DGRAD_COLSUM = 1, DET_WGRAD = 2, DET_MLP_WS = 3, DET_BN_FWD = 4,
+                       DET_BN_STATS = 5, DET_POOL_COLSUM = 6, DET_GG_COLSUM = 7, DET_COLSUM = 8, DET_BN_BWD = 9 };
+
+__device__ __forceinline__ bool det_on() { return __builtin_amdgcn_readfirstlane(hx_det_on) != 0; }
+// workgroup-uniform: wait for this workgroup's turn at `site` (all threads call it)
+__device__ inline void det_turn_begin(int site, unsigned my) {
+  if (threadIdx.x == 0) {
+    unsigned* c = hx_det_ctr + site * 32;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != my) {
+      if (wall_clock64() - t0 > 100000000ll) {
+        atomicAdd(&hx_det_lost, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+// hand the turn on once this workgroup's atomics have completed (all threads call it)
+__device__ inline void det_turn_end(int site, unsigned my, unsigned total) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(hx_det_ctr + site * 32, my + 1u == total ? 0u : my + 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+#define HOPSX_DET_TU(tag)                                                                          \
+  extern "C" int hopsx_det_set_##tag(int on) {                                                     \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(hx_det_on), &on, sizeof(int), 0, hipMemcpyHostToDevice); \
+  }                                                                                                \
+  extern "C" unsigned hopsx_det_lost_##tag() {                                                     \
+    unsigned v = 0;                                                                                \
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(hx_det_lost), sizeof(unsigned), 0, hipMemcpyDeviceToHost); \
+    return v;                                                                                      \
+  }

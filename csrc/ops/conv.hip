@@ -8,6 +8,8 @@
 #include "gemm_glds.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(conv)
+
 using namespace hopsx;
 
 static ConvGeom make_geom(const int* g) {
@@ -132,6 +134,8 @@ __global__ __launch_bounds__(1024) void conv_direct_wgrad_k(const bf16_raw* __re
     if (k == 0) red[rep * (KC + g.CO) + KC + co] = b0 + b1;
   }
   __syncthreads();
+  const bool det = !slab && det_on();  // deterministic mode: the atomic path adds in workgroup order
+  if (det) det_turn_begin(DET_WGRAD, blockIdx.x);
   if (rep == 0) {
     float s = 0.f, sb = 0.f;
     for (int q = 0; q < R; ++q) {
@@ -146,6 +150,7 @@ __global__ __launch_bounds__(1024) void conv_direct_wgrad_k(const bf16_raw* __re
       if (dbias && k == 0 && sb != 0.f) atomicAdd(dbias + co, sb);
     }
   }
+  if (det) det_turn_end(DET_WGRAD, blockIdx.x, gridDim.x);
 }
 
 // Small-K weight gradient (K = KH*KW*C <= 16, CO % 8 == 0): the input layers of the MNIST

@@ -17,6 +17,8 @@
 #include "ops_api.h"
 #include "optim_slice.h"
 
+HOPSX_DET_TU(conv_mfma)
+
 using namespace hopsx;
 
 namespace {
@@ -318,6 +320,8 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
     }
     __syncthreads();
     float* dst = bnacc + (long)(blockIdx.x % HOPSX_BN_NREP) * 2 * CO;
+    const bool det = det_on();
+    if (det) det_turn_begin(DET_BN_FWD, blockIdx.x);
     for (int e = threadIdx.x; e < 2 * CO; e += 256) {
       const int which = e / CO, c = e - which * CO;
       float t = 0.f;
@@ -325,6 +329,7 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
       for (int wv = 0; wv < CM_WAVES; ++wv) t += red[(wv * 2 + which) * CO + c];
       atomicAdd(dst + e, t);
     }
+    if (det) det_turn_end(DET_BN_FWD, blockIdx.x, gridDim.x);
   }
   if (pe.dbg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -637,6 +642,8 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
       }
     }
     __syncthreads();
+    const bool det = det_on();
+    if (det) det_turn_begin(DET_DGRAD_COLSUM, (unsigned)bid);
     for (int i = threadIdx.x; i < CI; i += blockDim.x) {
       float v = 0.f;
 #pragma unroll
@@ -652,6 +659,7 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
         if (v != 0.f) atomicAdd(dw0 + i, v);
       }
     }
+    if (det) det_turn_end(DET_DGRAD_COLSUM, (unsigned)bid, (unsigned)nblk);
   }
   if (dbg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -693,7 +701,7 @@ struct WgradArgs {
 
 // (bx, by): pixel-group and column-block coordinates of this workgroup
 template <int NFC, int NFKW>
-__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& A, int bx, int by) {
+__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& A, int bx, int by, int nbx, int nby) {
   const bf16_raw* __restrict__ dy = A.dy;
   const bf16_raw* __restrict__ x = A.x;
   const bf16_raw* __restrict__ y = A.y;
@@ -835,6 +843,10 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& A, int bx, int 
   }
   __syncthreads();
   phase_mark(dbg, 2);
+  // deterministic mode: the pixel-chunk groups (bx) of every column block add in workgroup order
+  const bool det = det_on();
+  const unsigned dmy = (unsigned)(by * nbx + bx);
+  if (det) det_turn_begin(DET_WGRAD, dmy);
   for (int e = threadIdx.x; e < CO * KB; e += 256) {
     const int co = e / KB, col = e - co * KB;
     const float v = rowm[e];
@@ -845,6 +857,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& A, int bx, int 
       const float v = bsum[e] + bsum[CO + e] + bsum[2 * CO + e] + bsum[3 * CO + e];
       if (v != 0.f) atomicAdd(dbias + e, v);
     }
+  if (det) det_turn_end(DET_WGRAD, dmy, (unsigned)(nbx * nby));
   if (dbg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     phase_mark(dbg, 3);
@@ -853,7 +866,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& A, int bx, int 
 
 template <int NFC, int NFKW>
 __global__ __launch_bounds__(256) void conv_wgrad_mfma_k(WgradArgs A) {
-  conv_wgrad_body<NFC, NFKW>(A, blockIdx.x, blockIdx.y);
+  conv_wgrad_body<NFC, NFKW>(A, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
 }
 
 // Horizontal fusion of one conv layer's backward: the input-gradient workgroups (first nA) and
@@ -885,7 +898,7 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs
     conv_dgrad_body<NF, KS, K0, 2>(A, bid, nA);
   } else {
     const int j = bid - nA;
-    conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx);
+    conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx, nBx, ((int)gridDim.x - (OPT ? os.nblk : 0) - nA) / nBx);
   }
 }
 
@@ -901,7 +914,7 @@ __global__ __launch_bounds__(256) void conv_bwd_pair_gemm_k(ConvDgradALoader al,
     mfma_gemm_body<BM, BM, 2, true, false>(al, bl, ep, M, N, K, kps, nullptr, blockIdx.x, nA, 0, 1);
   } else {
     const int j = blockIdx.x - nA;
-    conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx);
+    conv_wgrad_body<NFC, 2>(B, j % nBx, j / nBx, nBx, ((int)gridDim.x - nA) / nBx);
   }
 }
 

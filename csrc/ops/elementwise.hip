@@ -5,6 +5,8 @@
 #include "common.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(elementwise)
+
 static inline int ew_grid(long n, int per_thread = 1) {
   long g = (n / per_thread + 255) / 256;
   if (g > 8192) g = 8192;
@@ -79,10 +81,14 @@ __global__ __launch_bounds__(256) void colsum_k(const bf16_raw* __restrict__ x, 
   __shared__ float red[4][64];
   red[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
+  const bool det = det_on();
+  const unsigned dmy = blockIdx.y * gridDim.x + blockIdx.x;
+  if (det) det_turn_begin(DET_COLSUM, dmy);
   if (threadIdx.x < 64 && n < N) {
     const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     atomicAdd(out + n, t);
   }
+  if (det) det_turn_end(DET_COLSUM, dmy, gridDim.x * gridDim.y);
 }
 
 __global__ void act_bwd_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ y, bf16_raw* __restrict__ dx,
@@ -111,8 +117,12 @@ __global__ __launch_bounds__(256) void act_bwd_colsum_k(const bf16_raw* __restri
   __shared__ float red[4][64];
   red[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
+  const bool det = det_on();
+  const unsigned dmy = blockIdx.y * gridDim.x + blockIdx.x;
+  if (det) det_turn_begin(DET_COLSUM, dmy);
   if (threadIdx.x < 64 && n < N)
     atomicAdd(colsum + n, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+  if (det) det_turn_end(DET_COLSUM, dmy, gridDim.x * gridDim.y);
 }
 
 __global__ void add_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ b, bf16_raw* __restrict__ o,

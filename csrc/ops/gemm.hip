@@ -2,6 +2,8 @@
 #include "gemm_core.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(gemm)
+
 using namespace hopsx;
 
 // Finishing pass of a split-K GEMM whose partial sums were atomically

@@ -623,6 +623,11 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
   }
   if constexpr (!has_ticket<EP>::value) {
     if (ep.colsum) {
+      // deterministic mode: the column-sum atomics of this launch's tiles in workgroup order (no
+      // split-K there, so every tile of the launch reaches this point exactly once)
+      const bool det = det_on();
+      const unsigned dmy = (unsigned)(by * gx + bx), dtot = (unsigned)(gx * gy);
+      if (det) det_turn_begin(DET_GEMM_COLSUM, dmy);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         float v = cs[j];
@@ -642,6 +647,7 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
           if (fq == 0 && n < N) atomicAdd(ep.colsum + n, v);
         }
       }
+      if (det) det_turn_end(DET_GEMM_COLSUM, dmy, dtot);
     }
   } else {
     // ---- in-launch split-K finish (agent-scope release per slice, acquire in the last one)
@@ -717,6 +723,7 @@ struct GemmPlan {
 
 inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu = 256) {
   GemmPlan p;
+  if (hopsx_deterministic()) allow_split = false;  // one producer per output element
   const long t128 = ((M + 127) / 128) * ((N + 127) / 128);
   const long t64 = ((M + 63) / 64) * ((N + 63) / 64);
   // A/B knobs (host side, read once): HOPSX_GEMM_T64_MIN / _T128_MIN = the tile count below which a

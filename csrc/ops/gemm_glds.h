@@ -595,7 +595,8 @@ inline bool gg_plan(long M, long N, long K, bool allow_split, GgPlan& p, long mi
 template <bool A_KC, bool B_KC, class AS, class BS, class EP>
 inline bool launch_gg(const AS& as, const BS& bs, const EP& ep, int M, int N, int K, bool allow_split,
                       hipStream_t st, long min_wg_override = -1) {
-  if (M <= 0 || N <= 0 || K <= 0 || hopsx_disabled("gg")) return false;
+  // deterministic mode keeps gemm_core.h's engine (one K slice per tile, turn-ordered column sums)
+  if (M <= 0 || N <= 0 || K <= 0 || hopsx_disabled("gg") || hopsx_deterministic()) return false;
   GgPlan p;
   if (!gg_plan(M, N, K, allow_split, p, min_wg_override)) return false;
   static const int diag = (int)hopsx_env_int("HOPSX_GG_DIAG", 0);

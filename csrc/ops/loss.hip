@@ -18,6 +18,8 @@
 #include "common.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(loss)
+
 __device__ __forceinline__ float ld_logit(const void* p, int f32, long i) {
   return f32 ? ((const float*)p)[i] : bf2f(((const bf16_raw*)p)[i]);
 }
@@ -201,6 +203,8 @@ __global__ __launch_bounds__(1024) void loss_k(int kind, const void* __restrict_
     sc[wave] = cacc;
   }
   __syncthreads();
+  const bool det = gridDim.x > 1 && det_on();  // deterministic mode: the loss partials in block order
+  if (det) det_turn_begin(DET_COLSUM, blockIdx.x);
   if (threadIdx.x == 0) {
     float l = 0.f;
     int c = 0;
@@ -217,6 +221,7 @@ __global__ __launch_bounds__(1024) void loss_k(int kind, const void* __restrict_
       if (correct) atomicAdd(correct, c);
     }
   }
+  if (det) det_turn_end(DET_COLSUM, blockIdx.x, gridDim.x);
 }
 
 extern "C" int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
@@ -331,6 +336,10 @@ __device__ inline void head_ce_body(int kind, const void* __restrict__ logits, i
     sc[wave] = cacc;
   }
   __syncthreads();
+  // deterministic mode: the loss and head weight-gradient atomics of the row blocks in block order
+  const bool det = gx > 1 && det_on();
+  const unsigned dmy = (unsigned)(by * gx + bx);
+  if (det) det_turn_begin(DET_COLSUM, dmy);
   if (threadIdx.x == 0 && by == 0) {
     float l = 0.f;
     int c = 0;
@@ -378,6 +387,7 @@ __device__ inline void head_ce_body(int kind, const void* __restrict__ logits, i
       for (int r = 0; r < nr; ++r) s += sdl[r * C + n];
       if (s != 0.f) atomicAdd(db + n, s);
     }
+  if (det) det_turn_end(DET_COLSUM, dmy, (unsigned)(gx * gy));
   // input gradient of the head (the previous layer applies its own act' mask)
   for (int e = threadIdx.x; e < nr * kn; e += blockDim.x) {
     const int r = e / kn, k = k0 + (e - r * kn);
@@ -904,6 +914,9 @@ __global__ __launch_bounds__(1024) void mlp_head_k(MlpHeadArgs a) {
   // line (a.rot != 0) so the memory-side atomics of concurrent workgroups hit different addresses
   // instead of all queueing on the same line in the same order
   const int tot = a.B * a.N1;
+  // deterministic mode: the split-K partial tiles are added in workgroup order
+  const bool det = det_on();
+  if (det) det_turn_begin(DET_MLP_WS, blockIdx.x);
   const int rot = a.rot ? (int)(((unsigned)blockIdx.x * 64u) % (unsigned)tot) & ~63 : 0;
   for (int i0 = threadIdx.x; i0 < tot; i0 += blockDim.x) {
     int i = i0 + rot;
@@ -911,6 +924,7 @@ __global__ __launch_bounds__(1024) void mlp_head_k(MlpHeadArgs a) {
     const int row = i / a.N1, col = i - row * a.N1;
     atomicAdd(a.ws + i, st[row * SR + col]);
   }
+  if (det) det_turn_end(DET_MLP_WS, blockIdx.x, gridDim.x);
   __shared__ int s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics are done
   __syncthreads();

@@ -150,6 +150,7 @@ struct Args {
   // data parallel (DP instantiation)
   int world, rank;
   int loopback;                 // 1: one process plays every rank (peers = this rank's own buffers)
+  int xfence;                   // 1: system-scope release fence before raising peer flags
   long long* xstep;             // global step counter (epoch base of the exchange flags)
   unsigned char* xbuf[XMAX];    // exchange buffers of ranks 0..world-1 (own at [rank])
   unsigned* xflag[XMAX];        // flag pages of ranks 0..world-1
@@ -261,7 +262,10 @@ __device__ __forceinline__ bool wait_peers(const Args& a, int base, int stride, 
   return g != 0;
 }
 // raise this rank's flag word base + slot * stride in every peer's page (after the payload drained)
+// The payload stores are system-scope write-through and drained (vmcnt 0) by every storing wave before
+// this; the release fence (default on) additionally orders them before the flag on the fabric.
 __device__ __forceinline__ void raise_peers(const Args& a, int base, int stride, unsigned epoch) {
+  if (a.xfence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: buffer_wbl2 sc0 sc1 + drain
   const int r = threadIdx.x & 63;
   if (r < a.world && r != a.rank) xflag_store(a.xflag[r] + base + xslot(a, r) * stride, epoch);
 }
@@ -1167,12 +1171,12 @@ __global__ __launch_bounds__(256, 1) void mnist_persist_k(const Args a) {
 
 // ptrs: master shadow s1 s2 xs ys cursor rng step_dev hp_dev slabA slabB slabC slabD flags err out dbg(0 = none)
 //       [xstep xbuf[world] xflag[world]]   (world > 1: the data-parallel instantiation)
-// iv:   off[8] nbatch salt nsteps batch acquire world rank loopback timeout_ms
+// iv:   off[8] nbatch salt nsteps batch acquire world rank loopback timeout_ms xfence
 // fv:   drop_p xscale xshift lr gscale wd rho eps
 extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, int ni, const float* fv, int nf,
                                    hipStream_t st) {
   using namespace mnistp;
-  if (np < 18 || ni < 17 || nf < 8) return (int)hipErrorInvalidValue;
+  if (np < 18 || ni < 18 || nf < 8) return (int)hipErrorInvalidValue;
   if (iv[11] != B || iv[10] < 1 || iv[8] < 1) return (int)hipErrorInvalidValue;
   const int world = (int)iv[13], rank = (int)iv[14];
   if (world < 1 || world > XMAX || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
@@ -1205,6 +1209,7 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.world = world;
   a.rank = rank;
   a.loopback = (int)iv[15];
+  a.xfence = (int)iv[17];
   a.tmo = (long long)iv[16] * 100000ll;  // ms -> 100 MHz ticks
   a.inv_gb = 1.f / (float)(world * B);
   if (dp) {

@@ -7,6 +7,8 @@
 #include "common.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(norm)
+
 // column sums of x and x^2 (stats) -- one workgroup per (64-column strip, row slab)
 __global__ __launch_bounds__(256) void bn_stats_k(const bf16_raw* __restrict__ x, float* __restrict__ s1,
                                                   float* __restrict__ s2, int M, int C, int rpb) {
@@ -23,11 +25,15 @@ __global__ __launch_bounds__(256) void bn_stats_k(const bf16_raw* __restrict__ x
   ra[threadIdx.x >> 6][threadIdx.x & 63] = a;
   rb[threadIdx.x >> 6][threadIdx.x & 63] = b;
   __syncthreads();
+  const bool det = det_on();
+  const unsigned dmy = blockIdx.y * gridDim.x + blockIdx.x;
+  if (det) det_turn_begin(DET_BN_STATS, dmy);
   if (threadIdx.x < 64 && c < C) {
     const int t = threadIdx.x;
     atomicAdd(s1 + c, ra[0][t] + ra[1][t] + ra[2][t] + ra[3][t]);
     atomicAdd(s2 + c, rb[0][t] + rb[1][t] + rb[2][t] + rb[3][t]);
   }
+  if (det) det_turn_end(DET_BN_STATS, dmy, gridDim.x * gridDim.y);
 }
 
 // turn (sum, sumsq) into (mean, rstd) in place; update running stats (unbiased var)
@@ -82,11 +88,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_raw* __restric
   ra[threadIdx.x >> 6][threadIdx.x & 63] = a;
   rb[threadIdx.x >> 6][threadIdx.x & 63] = b;
   __syncthreads();
+  const bool det = det_on();
+  const unsigned dmy = blockIdx.y * gridDim.x + blockIdx.x;
+  if (det) det_turn_begin(DET_BN_BWD, dmy);
   if (threadIdx.x < 64 && c < C) {
     const int t = threadIdx.x;
     atomicAdd(ws + c, ra[0][t] + ra[1][t] + ra[2][t] + ra[3][t]);
     atomicAdd(ws + C + c, rb[0][t] + rb[1][t] + rb[2][t] + rb[3][t]);
   }
+  if (det) det_turn_end(DET_BN_BWD, dmy, gridDim.x * gridDim.y);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(const bf16_raw* __restrict__ dy, const bf16_raw* __restrict__ x,
@@ -157,8 +167,18 @@ struct BnFin {
 
 // Fold a workgroup's per-lane column partials (8 channels c0..c0+7 of channel group threadIdx % CG,
 // sums s1 / s2) and add them to this workgroup's replica row dst[0:2C] (red: >= 256*16 floats LDS).
+__device__ __forceinline__ void bn_block_colsum_body(float* s1, float* s2, float* red, float* dst, int C, int CG,
+                                                     int RPI);
+// deterministic mode: the workgroups add their partials in workgroup order (common.h det_turn_*)
 __device__ __forceinline__ void bn_block_colsum(float* s1, float* s2, float* red, float* dst, int C, int CG,
                                                 int RPI) {
+  const bool det = det_on();
+  if (det) det_turn_begin(DET_BN_STATS, blockIdx.x);
+  bn_block_colsum_body(s1, s2, red, dst, C, CG, RPI);
+  if (det) det_turn_end(DET_BN_STATS, blockIdx.x, gridDim.x);
+}
+__device__ __forceinline__ void bn_block_colsum_body(float* s1, float* s2, float* red, float* dst, int C, int CG,
+                                                     int RPI) {
   if (CG < 64) {
     // lanes of a wave with the same channel group (lane % CG) fold with xor shuffles, log2(64/CG)
     // steps; then 4 wave partials per channel meet in LDS.  (A serial walk over the RPI row

@@ -5,6 +5,8 @@
 #include "common.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(pool)
+
 static inline int grid_for(long n, int block = 256) {
   long g = (n + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -429,6 +431,13 @@ extern "C" int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, 
                                    int W, int C, int OH, int OW, int KH, int KW, int sh, int sw, int ph, int pw,
                                    int act, float* colsum, float p, const unsigned long long* rng, unsigned salt,
                                    hipStream_t st) {
+  if (colsum && hopsx_deterministic()) {
+    // the fused column sum adds through LDS float atomics (unordered even within a workgroup):
+    // deterministic mode sums the stored input gradient in a second, turn-ordered pass instead
+    const int e = hopsx_maxpool2d_bwd(dy, argmax, x, dx, B, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, act, nullptr, p,
+                                      rng, salt, st);
+    return e ? e : hopsx_colsum_bf16(dx, colsum, B * H * W, C, st);
+  }
   const size_t shm = colsum ? (size_t)C * sizeof(float) : 0;
   if (pool_fast(C, KH, KW, sh, sw, ph, pw, dy, dx, argmax, x)) {
     const long n8 = (long)B * OH * OW * (C / 8);

@@ -10,6 +10,8 @@
 #include "common.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(rowreduce)
+
 extern "C" int hopsx_colsum_bf16_scalar(const void* x, float* out, int M, int N, hipStream_t st);
 extern "C" int hopsx_act_bwd_colsum_scalar(const void* dy, const void* y, void* dx, int M, int N, int act,
                                            float* colsum, hipStream_t st);
@@ -47,11 +49,14 @@ __global__ __launch_bounds__(256) void rowreduce8_k(const bf16_raw* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[rl * N + cg * 8 + j] = s[j];
   __syncthreads();
+  const bool det = det_on();
+  if (det) det_turn_begin(DET_COLSUM, blockIdx.x);
   for (int c = tid; c < N; c += blockDim.x) {
     float t = 0.f;
     for (int r = 0; r < rpp; ++r) t += red[r * N + c];
     if (t != 0.f) atomicAdd(colsum + c, t);
   }
+  if (det) det_turn_end(DET_COLSUM, blockIdx.x, gridDim.x);
 }
 
 static int launch_rowreduce(const void* dy, const void* y, void* dx, int M, int N, int act, float* colsum,

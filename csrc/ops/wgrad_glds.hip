@@ -9,6 +9,8 @@
 #include "gemm_glds.h"
 #include "ops_api.h"
 
+HOPSX_DET_TU(wgrad_glds)
+
 using namespace hopsx;
 
 extern "C" int hopsx_conv_wgrad_glds_ok(const int* geom) {

@@ -38,14 +38,32 @@ def _load():
     return _ext
 
 
+_det_done = False
+
+
+def deterministic() -> bool:
+    """``HOPSX_DETERMINISTIC=1``: order-fixed cross-workgroup float reductions (common.h
+    "deterministic mode"): replays from the same state are bit-identical, at some speed cost."""
+    return os.environ.get("HOPSX_DETERMINISTIC", "0") == "1"
+
+
 def ext():
     """The kernel module; raises if it is unavailable."""
+    global _det_done
     m = _load()
     if m is None:
         raise RuntimeError(
             "hopsx HIP kernel library _hopsx_ops is not built/importable "
             f"({_err!r}); run `python -m hops_examples_amd._build`"
         )
+    if not _det_done:
+        _det_done = True
+        if deterministic() and torch.cuda.is_available():
+            # the device-side flag of every kernel translation unit (host-side planning reads the
+            # environment itself); set before the first launch, outside any graph capture
+            e = m.set_deterministic(1)
+            if e:
+                raise RuntimeError(f"hopsx: enabling deterministic mode failed (hip error {e})")
     return m
 
 

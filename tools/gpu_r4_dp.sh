@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4: persistent data-parallel step (loopback) + deterministic mode evidence on one MI355X.
+set -o pipefail
+out=gpurun_out/${1:-dp}; mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_persist_gpu.py tests/test_persist_dp_gpu.py -x -v --timeout 120 --timeout-method thread > $out/pytest.log 2>&1
+rc=$?; tail -12 $out/pytest.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python -u tools/persist_check.py --timing-only --timing 32 --loopback 2 8 > $out/timing.log 2>&1 || { tail -20 $out/timing.log; exit 1; }
+cat $out/timing.log
+HOPSX_DETERMINISTIC=1 timeout -k 10 200 python -u tools/det_check.py > $out/det.json 2> $out/det.err || { tail -30 $out/det.err; exit 1; }
+cat $out/det.json
+timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi > $out/bench.json 2> $out/bench.err || { tail $out/bench.err; exit 1; }
+cat $out/bench.json
