@@ -537,14 +537,17 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         if (r == a.rank) continue;
         st_sys(rsrc(a.xbuf[r] + XO_POOL + (par * XMAX + xslot(a, r)) * XS_POOL + (long)p * 4096), (w * 64 + lane) * 16, f);
       }
-      drain();
-      __syncthreads();
-      if (tid < 64) raise_peers(a, XF_POOL + p, NPOS, gep);
+      // (flags raised after the B wait: by then the stores have long completed, so the drain is free)
     }
     if (s + 1 < a.nsteps) xv = xload(s + 1);  // next step's patch, consumed next iteration
     stamp(a, s, 2);
     // ---- B: dh of all 32 images ----
     if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(2, s), a.acquire, s_ok, a.tmo)) return;
+    if constexpr (DP) {
+      drain();
+      __syncthreads();
+      if (tid < 64) raise_peers(a, XF_POOL + p, NPOS, gep);
+    }
     stamp(a, s, 3);
     {
       const auto R = rsrc(a.slabB + (long)par * NHEAD * PAY);
@@ -718,6 +721,59 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       if (tid == 0) flag_store(a.flags + FL_C + p, ep);
     }
     stamp(a, s, 6);
+    if constexpr (DP) {
+      // ---- fc1 weight gradient over every replica's images: dh^T fragments (each rank's head 0) and
+      // pooled fragments (each rank's position p); one MFMA product per replica, summed in rank order
+      // (the per-replica gradients, added exactly as an all-reduce in rank order would).  It runs
+      // before the slice owners' C wait, whose idle time hides the exchange-buffer loads ----
+      if (!wait_peers(a, XF_H, 1, gep, ecode(7, s), s_ok)) return;
+      if (!wait_peers(a, XF_POOL + p, NPOS, gep, ecode(8, s), s_ok)) return;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gw[ii][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const auto XP = rsrc(a.xbuf[a.rank] + XO_POOL + (long)par * XMAX * XS_POOL + (long)p * 4096);
+      const auto XD = rsrc(a.xbuf[a.rank] + XO_DHT + (long)par * XMAX * XS_DHT);
+      // rank r's fragments: own from LDS, a peer's from this rank's exchange buffer; loaded two ranks
+      // ahead of the MFMAs that consume them (three register sets, indices fixed by the unrolled loop)
+      constexpr int PF = 3;
+      bf16x8 af[PF][2], bfr[PF][4];
+      auto fetch = [&](int r, int b) {
+        if (r == a.rank) {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            const int n0 = (2 * w + ii) * 16 + 4 * tp;
+            af[b][ii] = lds_tr(DH + (8 * fq + tq) * DHS + n0, DH + (8 * fq + tq + 4) * DHS + n0);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c0 = j * 16 + 4 * tp;
+            bfr[b][j] = lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0);
+          }
+        } else {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+            af[b][ii] = __builtin_bit_cast(bf16x8, ld_sys(XD, (int)(r * XS_DHT) + ((2 * w + ii) * 64 + lane) * 16));
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            bfr[b][j] = __builtin_bit_cast(bf16x8, ld_sys(XP, (int)(r * XS_POOL) + (j * 64 + lane) * 16));
+        }
+      };
+#pragma unroll
+      for (int r = 0; r < PF - 1; ++r)
+        if (r < a.world) fetch(r, r);
+#pragma unroll
+      for (int r = 0; r < XMAX; ++r) {
+        if (r < a.world) {
+          if (r + PF - 1 < XMAX && r + PF - 1 < a.world) fetch(r + PF - 1, (r + PF - 1) % PF);
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              gw[ii][j] += mfma(af[r % PF][ii], bfr[r % PF][j], (f32x4){0.f, 0.f, 0.f, 0.f});
+        }
+      }
+    }
     // ---- slice owners: fixed-order reduce of 52 params over the 169 partials, Adadelta, publish D ----
     if (owner) {
       if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok, a.tmo)) return;
@@ -762,8 +818,13 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         if (!wait_peers(a, XF_CONV + p, NSLICE, gep, ecode(6, s), s_ok)) return;
         if (tid < SLICE) {
           const auto X = rsrc(a.xbuf[a.rank] + XO_CONV + (long)par * XMAX * XS_CONV);
+          float v[XMAX];  // every peer's value in flight before the rank-order sum
+#pragma unroll
+          for (int r = 0; r < XMAX; ++r) v[r] = r < a.world && r != a.rank ? ld_sys1(X, (int)(r * XS_CONV) + e * 4) : gs;
           float t = 0.f;
-          for (int r = 0; r < a.world; ++r) t += r == a.rank ? gs : ld_sys1(X, (int)(r * XS_CONV) + e * 4);
+#pragma unroll
+          for (int r = 0; r < XMAX; ++r)
+            if (r < a.world) t += v[r];
           gs = t;
         }
       }
@@ -791,44 +852,6 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         if (lane == 0) flag_store(a.flags + FL_D + p, ep);
       }
       stamp(a, s, 8);
-    }
-    if constexpr (DP) {
-      // ---- fc1 weight gradient over every replica's images: dh^T fragments (each rank's head 0) and
-      // pooled fragments (each rank's position p), accumulated in rank order on one MFMA chain ----
-      if (!wait_peers(a, XF_H, 1, gep, ecode(7, s), s_ok)) return;
-      if (!wait_peers(a, XF_POOL + p, NPOS, gep, ecode(8, s), s_ok)) return;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gw[ii][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      const auto XP = rsrc(a.xbuf[a.rank] + XO_POOL + (long)par * XMAX * XS_POOL + (long)p * 4096);
-      const auto XD = rsrc(a.xbuf[a.rank] + XO_DHT + (long)par * XMAX * XS_DHT);
-      for (int r = 0; r < a.world; ++r) {
-        bf16x8 af[2], bfr[4];
-        if (r == a.rank) {
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii) {
-            const int n0 = (2 * w + ii) * 16 + 4 * tp;
-            af[ii] = lds_tr(DH + (8 * fq + tq) * DHS + n0, DH + (8 * fq + tq + 4) * DHS + n0);
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int c0 = j * 16 + 4 * tp;
-            bfr[j] = lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0);
-          }
-        } else {
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii)
-            af[ii] = __builtin_bit_cast(bf16x8, ld_sys(XD, (int)(r * XS_DHT) + ((2 * w + ii) * 64 + lane) * 16));
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            bfr[j] = __builtin_bit_cast(bf16x8, ld_sys(XP, (int)(r * XS_POOL) + (j * 64 + lane) * 16));
-        }
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) gw[ii][j] = mfma(af[ii], bfr[j], gw[ii][j]);
-      }
     }
     // ---- Adadelta on the fc1 slice (registers) and the new bf16 weights for the next forward: off the
     // critical path, while this workgroup waits for the D hand-off (W1 is next read after it) ----
@@ -1094,18 +1117,22 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
       float t[NW + 2];
 #pragma unroll
       for (int k = 0; k < NW + 2; ++k) t[k] = 0.f;
-      for (int r = 0; r < a.world; ++r) {
-        if (r == a.rank) {
+      float v[XMAX][NW + 2];  // every peer's gradients in flight before the rank-order sums
 #pragma unroll
-          for (int k = 0; k < NW + 2; ++k) t[k] += gl[k];
-        } else {
-          const int o = (int)(r * XS_FC2);
+      for (int r = 0; r < XMAX; ++r) {
+        const bool peer = r < a.world && r != a.rank;
+        const int o = (int)(r * XS_FC2);
 #pragma unroll
-          for (int k = 0; k < NW; ++k) t[k] += ld_sys1(X, o + (tid + 256 * k) * 4);
-          if (tid < HID) t[NW] += ld_sys1(X, o + (NCLS * HID + tid) * 4);
-          if (tid < NCLS) t[NW + 1] += ld_sys1(X, o + (NCLS * HID + HID + tid) * 4);
-        }
+        for (int k = 0; k < NW; ++k) v[r][k] = peer ? ld_sys1(X, o + (tid + 256 * k) * 4) : gl[k];
+        v[r][NW] = peer && tid < HID ? ld_sys1(X, o + (NCLS * HID + tid) * 4) : gl[NW];
+        v[r][NW + 1] = peer && tid < NCLS ? ld_sys1(X, o + (NCLS * HID + HID + tid) * 4) : gl[NW + 1];
       }
+#pragma unroll
+      for (int r = 0; r < XMAX; ++r)
+        if (r < a.world) {
+#pragma unroll
+          for (int k = 0; k < NW + 2; ++k) t[k] += v[r][k];
+        }
 #pragma unroll
       for (int k = 0; k < NW + 2; ++k) gl[k] = t[k];
     }

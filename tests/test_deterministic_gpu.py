@@ -39,9 +39,12 @@ def test_replays_are_bit_identical(det):
     assert det["det_turns_lost"] == 0, det
 
 
-def test_engine_variants_agree_exactly(det):
-    """The steps_per_execution graph vs one-step replays and the optimizer co-launch vs the separate
-    optimizer kernel run the same arithmetic in the same order: in deterministic mode they agree
-    bit-for-bit (the default-mode tests allow the atomic-order drift instead)."""
+def test_engine_variants_agree(det):
+    """The steps_per_execution graph vs one-step replays (and eager vs graph) run the same kernels in
+    the same order: bit-for-bit equal in deterministic mode.  The optimizer co-launched into the conv
+    backward is the same update compiled into another kernel (hipcc's contraction choices differ in
+    the last bit: measured rel 4.8e-8 after 6 steps), so it is bounded at fp32 noise — instead of the
+    12 % that the default-mode test must allow for atomic-order drift."""
     assert det["mnist_ugraph_vs_1step_bitwise"], det
-    assert det["adadelta_colaunch_vs_unfused_bitwise"], det
+    assert det["mnist_eager_vs_graph_bitwise"], det
+    assert det["adadelta_colaunch_vs_unfused_rel"] <= 1e-6, det

@@ -90,7 +90,10 @@ def test_persistent_one_step_matches_bf16_emulation():
         # element's update by up to ~5 % of a step (measured max 6.5e-5); more than 7 % of a step (1e-4)
         # is allowed for at most 1 element in 1000 (a gradient within noise of 0), bounded by 2 steps
         nbad = int((err > 1e-4).sum())
-        assert cos > 0.99999 and nbad <= max(0, err.numel() // 1000) and float(err.max()) <= 2 * 1.42e-3, \
+        # (the cosine of a 32-element bias update is one element's 6 % error: the element bounds
+        # carry those; measured conv1.bias cos 0.99993 with every element within 9.1e-5)
+        cmin = 0.99999 if err.numel() >= 1024 else 0.9999
+        assert cos > cmin and nbad <= max(0, err.numel() // 1000) and float(err.max()) <= 2 * 1.42e-3, \
             f"{k}: cos {cos:.7f} off {nbad}/{err.numel()} max {float(err.max()):.3e}"
         # E[g^2] = 0.05 g^2: the conv gradients are sums of ~50k terms with cancellation, where fp32
         # vs fp64 order moves the smallest entries by up to ~1 % (measured rel-L2 <= 3.2e-3)

@@ -7,7 +7,11 @@ timeout -k 10 300 python -u -m pytest tests/test_persist_gpu.py tests/test_persi
 rc=$?; tail -12 $out/pytest.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -u tools/persist_check.py --timing-only --timing 32 --loopback 2 8 > $out/timing.log 2>&1 || { tail -20 $out/timing.log; exit 1; }
 cat $out/timing.log
+HOPSX_PERSIST_XFENCE=0 timeout -k 10 200 python -u tools/persist_check.py --timing-only --timing 32 --loopback 8 > $out/timing_nofence.log 2>&1 || { tail -20 $out/timing_nofence.log; exit 1; }
+grep "loopback 8" -A14 $out/timing_nofence.log
 HOPSX_DETERMINISTIC=1 timeout -k 10 200 python -u tools/det_check.py > $out/det.json 2> $out/det.err || { tail -30 $out/det.err; exit 1; }
 cat $out/det.json
 timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi > $out/bench.json 2> $out/bench.err || { tail $out/bench.err; exit 1; }
 cat $out/bench.json
+HOPSX_DETERMINISTIC=1 timeout -k 10 200 python -u tools/bn_gap.py > $out/bn_gap.txt 2>&1 || { tail -30 $out/bn_gap.txt; exit 1; }
+head -80 $out/bn_gap.txt
