@@ -316,10 +316,79 @@ static bool gg_conv_fwd(const void* x, const void* w, const ConvGeom& g, const E
   return launch_gg<true, true>(GgIm2col{(const bf16_raw*)x, g, M, K}, ws, e, M, N, K, false, st);
 }
 
+// The pixels of parity classes that no tap reaches (a 1x1 / stride-2 conv: all but the (0, 0)
+// class) get dX = 0, or the added gradient: 16-B chunks, `live` = bitmask of the classes with taps.
+__global__ __launch_bounds__(256) void dgrad_par_fill_k(bf16_raw* __restrict__ out, const bf16_raw* __restrict__ add,
+                                                        long nch, int C8, int W, int H, int sh, int sw, unsigned live) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nch; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / C8;
+    const int iw = (int)(pix % W), ih = (int)((pix / W) % H);
+    if ((live >> ((ih % sh) * sw + iw % sw)) & 1u) continue;
+    *(bf16x8*)(out + i * 8) = add ? *(const bf16x8*)(add + i * 8) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+// Strided dgrad as sh*sw dense parity-class GEMMs (gemm_glds.h GgDgradParA); classes without taps
+// are filled (dgrad_par_fill_k).  All class plans are checked before anything is launched.
+static bool gg_dgrad_par(const void* dy, const void* w, const ConvGeom& g, const EpiDActBF16& e, hipStream_t st) {
+  if ((g.sh == 1 && g.sw == 1) || g.dh != 1 || g.dw != 1 || g.sh > 4 || g.sw > 4 || hopsx_disabled("dgrad_par"))
+    return false;
+  if ((uintptr_t)e.out % 16 || (uintptr_t)e.add % 16) return false;
+  GgParGeom cls[16];
+  int n = 0;
+  unsigned live = 0;
+  for (int py = 0; py < g.sh; ++py)
+    for (int px = 0; px < g.sw; ++px) {
+      GgParGeom c{};
+      c.py = py;
+      c.px = px;
+      c.kh0 = (py + g.ph) % g.sh;
+      c.kw0 = (px + g.pw) % g.sw;
+      c.nkh = c.kh0 < g.KH ? (g.KH - c.kh0 + g.sh - 1) / g.sh : 0;
+      c.nkw = c.kw0 < g.KW ? (g.KW - c.kw0 + g.sw - 1) / g.sw : 0;
+      c.Hp = (g.H - py + g.sh - 1) / g.sh;
+      c.Wp = (g.W - px + g.sw - 1) / g.sw;
+      if (c.Hp <= 0 || c.Wp <= 0) return false;
+      if (c.nkh <= 0 || c.nkw <= 0) continue;  // no tap reaches this class: filled below
+      c.fWp.init(c.Wp);
+      c.fHWp.init(c.Hp * c.Wp);
+      c.fNKW.init(c.nkw);
+      GgPlan p;
+      if (!gg_plan((long)g.B * c.Hp * c.Wp, g.C, (long)c.nkh * c.nkw * g.CO, false, p, 1)) return false;
+      live |= 1u << (py * g.sw + px);
+      cls[n++] = c;
+    }
+  if (n == 0) return false;
+  if (n < g.sh * g.sw) {
+    const long nch = (long)g.B * g.H * g.W * (g.C / 8);
+    long blocks = (nch + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(dgrad_par_fill_k, dim3((unsigned)blocks), dim3(256), 0, st, e.out, e.add, nch, g.C / 8, g.W,
+                       g.H, g.sh, g.sw, live);
+  }
+  for (int i = 0; i < n; ++i) {
+    const GgParGeom& c = cls[i];
+    const int M = g.B * c.Hp * c.Wp, K = c.nkh * c.nkw * g.CO;
+    const GgDgradParA as{(const bf16_raw*)dy, g, c, M, K};
+    const GgWeightTPar bs{(const bf16_raw*)w, g, c, K, g.C};
+    const EpiDgradParBF16 ep{e.out, e.y, e.act, e.colsum, e.add, g.C, g.H, g.W, c.Wp, c.Hp * c.Wp,
+                             c.py, c.px, g.sh, g.sw, c.fWp, c.fHWp};
+    if (!launch_gg<true, false>(as, bs, ep, M, g.C, K, false, st, 1)) return false;  // (plans checked above)
+  }
+  return true;
+}
+
 static bool gg_conv_dgrad(const void* dy, const void* w, const ConvGeom& g, const EpiDActBF16& e, hipStream_t st) {
   const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
   if (g.C % 8 || g.CO % 8 || ((uintptr_t)dy | (uintptr_t)w) % 16 || hopsx_disabled("gg_dgrad") || gg_narrow(g, N))
     return false;
+  // stride > 1: the dense parity-class GEMMs instead of the zero-inserting gather (when the whole
+  // shape would take gg; the class GEMMs are launched however few workgroups each gives)
+  {
+    GgPlan p;
+    if (e.ldo == g.C && (!e.y || e.ldy == g.C) && gg_plan(M, N, K, false, p) && gg_dgrad_par(dy, w, g, e, st))
+      return true;
+  }
   const GgWeightT ws{(const bf16_raw*)w, g, K, N};
   if (g.KH == 1 && g.KW == 1 && g.ph == 0 && g.pw == 0 && (g.sh > 1 || g.sw > 1) && g.H == g.OH * g.sh &&
       g.W == g.OW * g.sw && !e.colsum && !hopsx_disabled("dgrad_scatter")) {

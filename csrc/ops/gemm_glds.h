@@ -188,6 +188,88 @@ struct GgWeightT {
   }
 };
 
+// ---- strided dgrad by input-pixel parity class (stride s > 1, dilation 1) ----
+// dX[ih] gathers dY[oh] W[kh] over ih + ph - kh = s * oh: an input pixel with ih mod s = py only
+// ever meets the taps kh = (py + ph) mod s (+ s, + 2s, ...).  So each of the s_h * s_w classes is a
+// DENSE implicit GEMM over 1/(s_h s_w) of the pixels with ~1/(s_h s_w) of the taps, where the
+// zero-inserting GgDgradA stages and multiplies the whole KH x KW window for every pixel (3 of 4
+// taps of a 3x3 / stride-2 dgrad are zeros: the 2.5-3.2x gap to PyTorch in
+// profiles/r3s7_conv_gemm_vs_torch.txt).
+struct GgParGeom {
+  int py, px;      // the class: ih mod sh, iw mod sw
+  int kh0, kw0;    // first tap of the class per axis; taps kh0 + sh * t
+  int nkh, nkw;    // taps per axis
+  int Hp, Wp;      // input rows / columns of the class
+  FastDiv fWp, fHWp, fNKW;
+};
+
+// A (KC): (o = class pixel (b, ihh, iww), i = k = (th, tw, co)) -> dY[b, oh, ow, co]
+struct GgDgradParA {
+  const bf16_raw* dy;
+  ConvGeom g;
+  GgParGeom c;
+  int olim, ilim;  // B*Hp*Wp, nkh*nkw*CO
+  __device__ __forceinline__ GgSlot kc(int m, int k, int kend) const {
+    const bool ok = m < olim;
+    const int mc = ok ? m : 0;
+    const int b = c.fHWp.div(mc), rem = mc - b * (c.Hp * c.Wp);
+    const int ihh = c.fWp.div(rem), iww = rem - ihh * c.Wp;
+    return GgSlot{dy + (long)b * g.OH * g.OW * g.CO, g.sh * ihh + c.py + g.ph, g.sw * iww + c.px + g.pw, 0, k,
+                  min(ilim, kend) - k, ok};
+  }
+  __device__ __forceinline__ const void* kc_at(const GgSlot& s, int dk) const {
+    const int k = s.k0 + dk;
+    const int kc = k < ilim ? k : 0;
+    const int t = g.fCO.div(kc), co = kc - t * g.CO;
+    const int th = c.fNKW.div(t), tw = t - th * c.nkw;
+    const int hn = s.a - (c.kh0 + g.sh * th), wn = s.b - (c.kw0 + g.sw * tw);  // multiples of s
+    const int oh = g.fSH.div(hn > 0 ? hn : 0), ow = g.fSW.div(wn > 0 ? wn : 0);
+    const bool ok = s.ok && dk < s.rem && hn >= 0 && wn >= 0 && oh < g.OH && ow < g.OW;
+    return ok ? (const void*)(s.q + (oh * g.OW + ow) * g.CO + co) : (const void*)g_gg_zero;
+  }
+};
+
+// B (RC): the class's taps of W[co][kh][kw][ci] as (o = k = (th, tw, co), i = ci)
+struct GgWeightTPar {
+  const bf16_raw* w;
+  ConvGeom g;
+  GgParGeom c;
+  int olim, ilim;  // nkh*nkw*CO, C
+  __device__ __forceinline__ GgSlot rc(int k, int col, int kend) const {
+    const bool ok = col < ilim;
+    return GgSlot{w + (ok ? col : 0), 0, 0, 0, k, min(olim, kend) - k, ok};
+  }
+  __device__ __forceinline__ const void* rc_at(const GgSlot& s, int dk) const {
+    const int k = s.k0 + dk;
+    const int kc = k < olim ? k : 0;
+    const int t = g.fCO.div(kc), co = kc - t * g.CO;
+    const int th = c.fNKW.div(t), tw = t - th * c.nkw;
+    const int kh = c.kh0 + g.sh * th, kw = c.kw0 + g.sw * tw;
+    const bool ok = s.ok && dk < s.rem;
+    return ok ? (const void*)(s.q + ((co * g.KH + kh) * g.KW + kw) * g.C) : (const void*)g_gg_zero;
+  }
+};
+
+// the class's rows land on their own pixels of dX: EpiDActBF16's act' / added gradient / column sum
+struct EpiDgradParBF16 {
+  bf16_raw* out;
+  const bf16_raw* yprev;
+  int act;
+  float* colsum;
+  const bf16_raw* add;
+  int C, H, W, Wp, HWp, py, px, sh, sw;
+  FastDiv fWp, fHWp;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    const int b = fHWp.div(m), r = m - b * HWp;
+    const int ihh = fWp.div(r), iww = r - ihh * Wp;
+    const long pos = (((long)b * H + sh * ihh + py) * W + sw * iww + px) * C + n;
+    if (yprev) v *= act_grad_from_out(bf2f(yprev[pos]), act);
+    if (add) v += bf2f(add[pos]);
+    out[pos] = f2bf(v);
+    return v;
+  }
+};
+
 // dW^T orientation of a weight gradient: the GEMM computes D[m = k][n = co], stored to out[n][m]
 struct EpiAtomicF32T {
   float* out;

@@ -15,3 +15,12 @@ timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi > $out/bench.j
 cat $out/bench.json
 HOPSX_DETERMINISTIC=1 timeout -k 10 200 python -u tools/bn_gap.py > $out/bn_gap.txt 2>&1 || { tail -30 $out/bn_gap.txt; exit 1; }
 head -80 $out/bn_gap.txt
+timeout -k 10 120 python -u tools/dbg_widedeep.py > $out/taxi_phases.txt 2>&1 || { tail -20 $out/taxi_phases.txt; exit 1; }
+cat $out/taxi_phases.txt
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/p20 -o run -- python3 benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 30 --warmup 10 > $out/p20.log 2>&1 || { tail -20 $out/p20.log; exit 1; }
+python tools/profdb.py $out/p20/run_results.db > $out/r20_kernels.txt 2>&1; rm -rf $out/p20
+head -40 $out/r20_kernels.txt
+timeout -k 10 240 python -u -m pytest tests/test_dgrad_par_gpu.py -x -v --timeout 120 --timeout-method thread > $out/dgrad_par.log 2>&1
+rc=$?; tail -10 $out/dgrad_par.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u tools/bench_conv_gemm.py --batch 64 --torch > $out/conv_gemm_b64.txt 2>&1 || { tail -20 $out/conv_gemm_b64.txt; exit 1; }
+tail -30 $out/conv_gemm_b64.txt
