@@ -262,8 +262,9 @@ __device__ __forceinline__ bool wait_peers(const Args& a, int base, int stride, 
   return g != 0;
 }
 // raise this rank's flag word base + slot * stride in every peer's page (after the payload drained)
-// The payload stores are system-scope write-through and drained (vmcnt 0) by every storing wave before
-// this; the release fence (default on) additionally orders them before the flag on the fabric.
+// The payload stores are system-scope write-through (sc0 sc1) and drained (vmcnt 0) by every storing
+// wave before this: that completes them at the system coherence point, the release for exactly these
+// stores.  The optional fence (HOPSX_PERSIST_XFENCE=1) also writes back other dirty L2 lines.
 __device__ __forceinline__ void raise_peers(const Args& a, int base, int stride, unsigned epoch) {
   if (a.xfence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: buffer_wbl2 sc0 sc1 + drain
   const int r = threadIdx.x & 63;
@@ -721,59 +722,6 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       if (tid == 0) flag_store(a.flags + FL_C + p, ep);
     }
     stamp(a, s, 6);
-    if constexpr (DP) {
-      // ---- fc1 weight gradient over every replica's images: dh^T fragments (each rank's head 0) and
-      // pooled fragments (each rank's position p); one MFMA product per replica, summed in rank order
-      // (the per-replica gradients, added exactly as an all-reduce in rank order would).  It runs
-      // before the slice owners' C wait, whose idle time hides the exchange-buffer loads ----
-      if (!wait_peers(a, XF_H, 1, gep, ecode(7, s), s_ok)) return;
-      if (!wait_peers(a, XF_POOL + p, NPOS, gep, ecode(8, s), s_ok)) return;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gw[ii][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      const auto XP = rsrc(a.xbuf[a.rank] + XO_POOL + (long)par * XMAX * XS_POOL + (long)p * 4096);
-      const auto XD = rsrc(a.xbuf[a.rank] + XO_DHT + (long)par * XMAX * XS_DHT);
-      // rank r's fragments: own from LDS, a peer's from this rank's exchange buffer; loaded two ranks
-      // ahead of the MFMAs that consume them (three register sets, indices fixed by the unrolled loop)
-      constexpr int PF = 3;
-      bf16x8 af[PF][2], bfr[PF][4];
-      auto fetch = [&](int r, int b) {
-        if (r == a.rank) {
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii) {
-            const int n0 = (2 * w + ii) * 16 + 4 * tp;
-            af[b][ii] = lds_tr(DH + (8 * fq + tq) * DHS + n0, DH + (8 * fq + tq + 4) * DHS + n0);
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int c0 = j * 16 + 4 * tp;
-            bfr[b][j] = lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0);
-          }
-        } else {
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii)
-            af[b][ii] = __builtin_bit_cast(bf16x8, ld_sys(XD, (int)(r * XS_DHT) + ((2 * w + ii) * 64 + lane) * 16));
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            bfr[b][j] = __builtin_bit_cast(bf16x8, ld_sys(XP, (int)(r * XS_POOL) + (j * 64 + lane) * 16));
-        }
-      };
-#pragma unroll
-      for (int r = 0; r < PF - 1; ++r)
-        if (r < a.world) fetch(r, r);
-#pragma unroll
-      for (int r = 0; r < XMAX; ++r) {
-        if (r < a.world) {
-          if (r + PF - 1 < XMAX && r + PF - 1 < a.world) fetch(r + PF - 1, (r + PF - 1) % PF);
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              gw[ii][j] += mfma(af[r % PF][ii], bfr[r % PF][j], (f32x4){0.f, 0.f, 0.f, 0.f});
-        }
-      }
-    }
     // ---- slice owners: fixed-order reduce of 52 params over the 169 partials, Adadelta, publish D ----
     if (owner) {
       if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok, a.tmo)) return;
@@ -852,6 +800,60 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
         if (lane == 0) flag_store(a.flags + FL_D + p, ep);
       }
       stamp(a, s, 8);
+    }
+    if constexpr (DP) {
+      // ---- fc1 weight gradient over every replica's images: dh^T fragments (each rank's head 0) and
+      // pooled fragments (each rank's position p); one MFMA product per replica, summed in rank order
+      // (the per-replica gradients, added exactly as an all-reduce in rank order would).  After the
+      // owner phase: placed before the owners' C wait it delayed the D publish (measured +2 us at 8
+      // loopback ranks: the exchange-buffer loads take longer than that wait) ----
+      if (!wait_peers(a, XF_H, 1, gep, ecode(7, s), s_ok)) return;
+      if (!wait_peers(a, XF_POOL + p, NPOS, gep, ecode(8, s), s_ok)) return;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gw[ii][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const auto XP = rsrc(a.xbuf[a.rank] + XO_POOL + (long)par * XMAX * XS_POOL + (long)p * 4096);
+      const auto XD = rsrc(a.xbuf[a.rank] + XO_DHT + (long)par * XMAX * XS_DHT);
+      // rank r's fragments: own from LDS, a peer's from this rank's exchange buffer; loaded two ranks
+      // ahead of the MFMAs that consume them (three register sets, indices fixed by the unrolled loop)
+      constexpr int PF = 3;
+      bf16x8 af[PF][2], bfr[PF][4];
+      auto fetch = [&](int r, int b) {
+        if (r == a.rank) {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            const int n0 = (2 * w + ii) * 16 + 4 * tp;
+            af[b][ii] = lds_tr(DH + (8 * fq + tq) * DHS + n0, DH + (8 * fq + tq + 4) * DHS + n0);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c0 = j * 16 + 4 * tp;
+            bfr[b][j] = lds_tr(POOL + (8 * fq + tq) * PLS + c0, POOL + (8 * fq + tq + 4) * PLS + c0);
+          }
+        } else {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+            af[b][ii] = __builtin_bit_cast(bf16x8, ld_sys(XD, (int)(r * XS_DHT) + ((2 * w + ii) * 64 + lane) * 16));
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            bfr[b][j] = __builtin_bit_cast(bf16x8, ld_sys(XP, (int)(r * XS_POOL) + (j * 64 + lane) * 16));
+        }
+      };
+#pragma unroll
+      for (int r = 0; r < PF - 1; ++r)
+        if (r < a.world) fetch(r, r);
+#pragma unroll
+      for (int r = 0; r < XMAX; ++r) {
+        if (r < a.world) {
+          if (r + PF - 1 < XMAX && r + PF - 1 < a.world) fetch(r + PF - 1, (r + PF - 1) % PF);
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              gw[ii][j] += mfma(af[r % PF][ii], bfr[r % PF][j], (f32x4){0.f, 0.f, 0.f, 0.f});
+        }
+      }
     }
     // ---- Adadelta on the fc1 slice (registers) and the new bf16 weights for the next forward: off the
     // critical path, while this workgroup waits for the D hand-off (W1 is next read after it) ----

@@ -83,9 +83,16 @@ def _resnet_step(disable: str):
 
 
 def test_resnet20_step_bnstats_matches_unfused():
-    """Same logits / running statistics; the gradients agree as well as two runs of the unfused
-    path agree with each other (float-atomic summation order makes both nondeterministic, and a
-    last-bit change of a BN statistic flips bf16 roundings that 20 layers of backward amplify)."""
+    """Same logits / running statistics; the one-step gradients agree to cos > 0.97.
+
+    Why not tighter (profiles/r4_bn_gap_resnet20.txt, tools/bn_gap.py, deterministic mode so both
+    paths are bit-reproducible): the two paths sum the BN statistics in a different order (conv
+    epilogue per-tile partials vs the statistics pass), so a mean / rstd differs in the last bit.
+    The stem and block-0 convs/BNs come out bit-identical; the first difference is 6e-6 at
+    blocks.0.b.bn, and this random-init ResNet-20 then roughly doubles it every layer (1.5e-2 at
+    the last block) and the backward takes the gradient to ~0.19 relative (cos 0.989).  Any equally
+    valid reordering (another GEMM tiling) does the same: it is the network's sensitivity at init,
+    not a defect of either path — the single ConvBN layer test below is the tight comparison."""
     l0, g0, b0 = _resnet_step("bnstats")
     _, g0b, _ = _resnet_step("bnstats")
     l1, g1, b1 = _resnet_step("")

@@ -26,7 +26,7 @@ bench() { local name=$1; shift; timeout -k 10 ${T:-300} python -u "$@" > $out/$n
           tail -1 $out/$name.json | cut -c1-400; }
 ktable() { local d=$1 name=$2; shift 2
            timeout -k 10 ${T:-300} rocprofv3 --kernel-trace --stats -d $out/$d -o run -- python3 "$@" > $out/$d.log 2>&1 || fail $out/$d.log
-           python tools/profdb.py $out/$d/run_results.db > $out/$name 2>/dev/null || true
+           db=$(find $out/$d -name '*.db' | head -1); [ -n "$db" ] && python tools/profdb.py "$db" > $out/$name 2>&1
            f=$(find $out/$d -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" $out/${name%.txt}_stats.csv
            rm -rf $out/$d; head -25 $out/$name; }
 

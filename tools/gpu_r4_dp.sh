@@ -18,7 +18,8 @@ head -80 $out/bn_gap.txt
 timeout -k 10 120 python -u tools/dbg_widedeep.py > $out/taxi_phases.txt 2>&1 || { tail -20 $out/taxi_phases.txt; exit 1; }
 cat $out/taxi_phases.txt
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/p20 -o run -- python3 benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 30 --warmup 10 > $out/p20.log 2>&1 || { tail -20 $out/p20.log; exit 1; }
-python tools/profdb.py $out/p20/run_results.db > $out/r20_kernels.txt 2>&1; rm -rf $out/p20
+db=$(find $out/p20 -name '*.db' | head -1); f=$(find $out/p20 -name '*kernel_stats.csv' | head -1)
+[ -n "$f" ] && cp "$f" $out/r20_kernel_stats.csv; [ -n "$db" ] && python tools/profdb.py "$db" > $out/r20_kernels.txt 2>&1; rm -rf $out/p20
 head -40 $out/r20_kernels.txt
 timeout -k 10 240 python -u -m pytest tests/test_dgrad_par_gpu.py -x -v --timeout 120 --timeout-method thread > $out/dgrad_par.log 2>&1
 rc=$?; tail -10 $out/dgrad_par.log; [ $rc -le 1 ] || exit $rc
