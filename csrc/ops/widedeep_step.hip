@@ -37,6 +37,7 @@ constexpr int WD_THREADS = 1024;
 constexpr int WD_WAVES = WD_THREADS / 64;
 constexpr int WD_MAXT = 4;      // dW / dX tiles a wave holds in registers across the in-place barrier
 constexpr int WD_PF = 16;       // deep parameters per thread prefetched into registers (span <= 16 K)
+constexpr int WD_DX = 1;        // dense-input image elements per thread (Bp * (dpad(d0) + 1) <= 1 K: taxi 48 x 17)
 constexpr int WD_LDS_MAX = 160 * 1024;
 
 struct WideDeepArgs {
@@ -125,6 +126,11 @@ __device__ __forceinline__ float ftrl_fast(float w, float g, float& z, float& n,
   return (fabsf(z) <= h.a) ? 0.f : -(z - copysignf(h.a, z)) * __builtin_amdgcn_rcpf(den);
 }
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for every outstanding global
+// access (vmcnt 0), which would put the wide rows' gradient atomics and the next batch's prefetch
+// loads on the critical path of every layer's barrier
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -158,27 +164,40 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     ps[k] = A.apply_opt ? A.ada_s[xc] : 0.f;
     psl[k] = x < deep_hi ? A.slot[xc - deep_lo] : -1;
   }
+  // the batch of step s in registers: this thread's wide id, label and dense-image elements; step
+  // s + 1's are loaded during step s's backward (they do not depend on its updates)
+  const bool wide_t = tid < B * A.nwide;
+  const int d0 = A.dims[0], s0 = dpad(d0) + 1;
+  long long cid = 0;
+  float yv = 0.f, dxv[WD_DX];
+  auto prefetch = [&](int s) {
+    const long long bi = (bi0 + s) % A.nbatch;
+    cid = wide_t ? A.cat[bi * (long long)B * A.nwide + tid] : 0;
+    yv = tid < B ? A.label[bi * (long long)B + tid] : 0.f;
+    const float* xb = A.dense + bi * (long long)B * d0;
+#pragma unroll
+    for (int j = 0; j < WD_DX; ++j) {
+      const int e = tid + j * WD_THREADS, b = e / s0, i = e - b * s0;
+      dxv[j] = e < Bp * s0 && b < B && i < d0 ? xb[(long)b * d0 + i] : 0.f;
+    }
+  };
+  prefetch(0);
   for (int step = 0; step < A.nsteps; ++step) {
   const bool last = step + 1 == A.nsteps;
-  const long long bi = (bi0 + step) % A.nbatch;
   if (step) __syncthreads();  // the previous step's wide-row updates (same CU) are visible after this
-  const long long* cb = A.cat + bi * (long long)B * A.nwide;
-  const bool wide_t = tid < B * A.nwide;
-  const long wrow = A.wide_off + (wide_t ? cb[tid] : 0);
+  const long wrow = A.wide_off + cid;
   const float wv = A.master[wrow];
   float wz = 0.f, wn = 0.f;
   if (A.apply_opt) {
     wz = A.ftrl_z[wrow];
     wn = A.ftrl_n[wrow];
   }
-  const float* yb = A.label + bi * (long long)B;
-  const float yv = tid < B ? yb[tid] : 0.f;
+  const float ylab = yv;
   {
-    const int d0 = A.dims[0], s0 = dpad(d0) + 1;
-    const float* xb = A.dense + bi * (long long)B * d0;
-    for (int e = tid; e < Bp * s0; e += WD_THREADS) {
-      const int b = e / s0, i = e - b * s0;
-      wd_lds[Ly.act[0] + e] = b < B ? (i < d0 ? xb[(long)b * d0 + i] : (i == d0 ? 1.f : 0.f)) : 0.f;
+#pragma unroll
+    for (int j = 0; j < WD_DX; ++j) {
+      const int e = tid + j * WD_THREADS, b = e / s0, i = e - b * s0;
+      if (e < Bp * s0) wd_lds[Ly.act[0] + e] = b < B && i == d0 ? 1.f : dxv[j];
     }
     // zero the weight / bias images (their padding must read 0) and the wide sums
     for (int e = Ly.w[0] + tid; e < Ly.wsum + Bp; e += WD_THREADS) wd_lds[e] = 0.f;
@@ -231,9 +250,9 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       const int b = tid;
       const float z = Zp[b * sz] + wd_lds[Ly.wsum + b];
       const float p = 1.f / (1.f + __expf(-z));
-      lsum = fmaxf(z, 0.f) - z * yv + __logf(1.f + __expf(-fabsf(z)));
-      csum = ((p > 0.5f) == (yv > 0.5f));
-      Zp[b * sz] = (p - yv) / (float)B;  // G_L in place of the logits
+      lsum = fmaxf(z, 0.f) - z * ylab + __logf(1.f + __expf(-fabsf(z)));
+      csum = ((p > 0.5f) == (ylab > 0.5f));
+      Zp[b * sz] = (p - ylab) / (float)B;  // G_L in place of the logits
     }
     lsum = wave_sum(lsum);
 #pragma unroll
@@ -244,6 +263,7 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
     }
     __syncthreads();
     if (wide_t) atomicAdd(A.grad + wrow, Zp[(tid / A.nwide) * sz]);  // wide gradient (summed per row)
+    if (step + 1 < A.nsteps) prefetch(step + 1);  // in flight during the backward (LDS-only barriers)
     if (tid == 0) {
       float l = 0.f, c = 0.f;
       for (int w = 0; w < WD_WAVES; ++w) {
@@ -291,7 +311,7 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       }
       hx[j] = acx;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < WD_MAXT; ++j) {
       const int t = wave + j * WD_WAVES;
@@ -309,7 +329,7 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     wd_mark(A, 11 + l);
   }
 
@@ -338,6 +358,9 @@ __global__ __launch_bounds__(WD_THREADS) void widedeep_step_k(WideDeepArgs A) {
       }
     }
   }
+  // every wave's wide-gradient atomics complete before any claim reads a row
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (A.apply_opt && wide_t) {
     // the summed gradient of this row, claimed by exactly one thread (and left zero); its state
     // was prefetched at the start (no other thread touches the row before the claim)
@@ -418,6 +441,7 @@ extern "C" long hopsx_widedeep_step_lds(const long* iv, int ni) {
   const float f[16] = {};
   if (wd_fill(a, p, 17, iv, ni, f, 16)) return -1;
   if (a.dims[a.L] != 1 || (long)a.B * a.nwide > WD_THREADS || a.B > WD_THREADS) return -1;
+  if ((long)a.Bp * (dpad(a.dims[0]) + 1) > (long)WD_DX * WD_THREADS) return -1;
   if (a.boff[a.L - 1] + a.dims[a.L] - a.woff[0] > (long)WD_PF * WD_THREADS) return -1;
   for (int l = 0; l < a.L; ++l) {
     const int tn = dpad(a.dims[l]) / 16;
