@@ -218,6 +218,7 @@ struct ConvWeightTLoader {
 // value that should enter the optional column sum.
 // ----------------------------------------------------------------------------
 struct EpiStoreBF16 {  // out = act(alpha*acc + bias[n])
+  static constexpr bool kVec8 = true;
   bf16_raw* out;
   long ldo;
   const float* bias;
@@ -229,6 +230,14 @@ struct EpiStoreBF16 {  // out = act(alpha*acc + bias[n])
     v = apply_act(v, act);
     out[(long)m * ldo + n] = f2bf(v);
     return v;
+  }
+  // the vectorized epilogue (gemm_glds.h): 8 consecutive columns n..n+7 of row m, one 16-B store
+  __host__ __device__ bool vec8_ok() const { return ldo % 8 == 0 && (uintptr_t)out % 16 == 0 && !colsum; }
+  __device__ __forceinline__ void store8(int m, int n, const float* v) const {
+    bf16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = (short)f2bf(apply_act(v[j] * alpha + (bias ? bias[n + j] : 0.f), act));
+    *(bf16x8*)(out + (long)m * ldo + n) = q;
   }
 };
 
@@ -309,6 +318,11 @@ struct EpiAtomicTicket {
 };
 
 template <class EP, class = void>
+struct has_vec8 { static constexpr bool value = false; };
+template <class EP>
+struct has_vec8<EP, decltype((void)EP::kVec8)> { static constexpr bool value = EP::kVec8; };
+
+template <class EP, class = void>
 struct has_ticket { static constexpr bool value = false; };
 template <class EP>
 struct has_ticket<EP, decltype((void)EP::kTicket)> { static constexpr bool value = EP::kTicket; };
@@ -323,6 +337,7 @@ struct has_pre<EP, decltype((void)EP::kPre)> { static constexpr bool value = EP:
 
 // out = acc * act'(y[m,n])  (backprop through the activation whose OUTPUT is y)
 struct EpiDActBF16 {
+  static constexpr bool kVec8 = true;
   bf16_raw* out;
   long ldo;
   const bf16_raw* y;
@@ -335,6 +350,23 @@ struct EpiDActBF16 {
     if (add) v += bf2f(add[(long)m * ldo + n]);
     out[(long)m * ldo + n] = f2bf(v);
     return v;
+  }
+  __host__ __device__ bool vec8_ok() const {
+    return ldo % 8 == 0 && (uintptr_t)out % 16 == 0 && (!y || (ldy % 8 == 0 && (uintptr_t)y % 16 == 0)) &&
+           (uintptr_t)add % 16 == 0 && !colsum;
+  }
+  __device__ __forceinline__ void store8(int m, int n, const float* v) const {
+    const bf16x8 yv = y ? *(const bf16x8*)(y + (long)m * ldy + n) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16x8 av = add ? *(const bf16x8*)(add + (long)m * ldo + n) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    bf16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j];
+      if (y) t *= act_grad_from_out(bf2f((uint16_t)yv[j]), act);
+      if (add) t += bf2f((uint16_t)av[j]);
+      q[j] = (short)f2bf(t);
+    }
+    *(bf16x8*)(out + (long)m * ldo + n) = q;
   }
 };
 

@@ -252,6 +252,7 @@ struct GgWeightTPar {
 
 // the class's rows land on their own pixels of dX: EpiDActBF16's act' / added gradient / column sum
 struct EpiDgradParBF16 {
+  static constexpr bool kVec8 = true;
   bf16_raw* out;
   const bf16_raw* yprev;
   int act;
@@ -267,6 +268,25 @@ struct EpiDgradParBF16 {
     if (add) v += bf2f(add[pos]);
     out[pos] = f2bf(v);
     return v;
+  }
+  __host__ __device__ bool vec8_ok() const {
+    return C % 8 == 0 && (uintptr_t)out % 16 == 0 && (uintptr_t)yprev % 16 == 0 && (uintptr_t)add % 16 == 0 && !colsum;
+  }
+  __device__ __forceinline__ void store8(int m, int n, const float* v) const {
+    const int b = fHWp.div(m), r = m - b * HWp;
+    const int ihh = fWp.div(r), iww = r - ihh * Wp;
+    const long pos = (((long)b * H + sh * ihh + py) * W + sw * iww + px) * C + n;
+    const bf16x8 yv = yprev ? *(const bf16x8*)(yprev + pos) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16x8 av = add ? *(const bf16x8*)(add + pos) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    bf16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j];
+      if (yprev) t *= act_grad_from_out(bf2f((uint16_t)yv[j]), act);
+      if (add) t += bf2f((uint16_t)av[j]);
+      q[j] = (short)f2bf(t);
+    }
+    *(bf16x8*)(out + pos) = q;
   }
 };
 
@@ -578,6 +598,37 @@ __global__ __launch_bounds__(512) void gg_kernel(const AS as, const BS bs, const
       for (int j = 0; j < FN; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (s == 1.2345e-30f) atomicAdd(&g_gg_sink, s);
     return;
+  }
+  // vectorized epilogue (epilogues with store8, no column sum, N % 8 == 0): the tile goes through LDS
+  // as fp32 rows and leaves as 16-B stores of 8 consecutive columns (the fragment layout stores 2-B
+  // values, four 32-B pieces per wave instruction) — also 16-B loads of the act' / addend operands
+  if constexpr (has_vec8<EP>::value) {
+    constexpr int SR = BN + 4;  // fp32 row stride (bank offset 4 between the fragment's 4 rows)
+    static_assert(BM * SR * 4 <= C::LDS, "vector epilogue staging must fit the tile's LDS");
+    if (N % 8 == 0 && ep.vec8_ok()) {
+      float* st = (float*)smem;
+      __syncthreads();  // every wave's last fragment reads of the main loop are done
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[(wm * C::WTM + i * 16 + fq * 4 + r) * SR + wn * C::WTN + j * 16 + fr] = acc[i][j][r];
+      __syncthreads();
+      constexpr int CPR = BN / 8;  // 8-column chunks per row
+#pragma unroll 4
+      for (int c = tid; c < BM * CPR; c += 512) {
+        const int row = c / CPR, col = (c - row * CPR) * 8;
+        const int m = m0 + row, n = n0 + col;
+        if (m < M && n < N) {
+          const f32x4 v0 = *(const f32x4*)(st + row * SR + col), v1 = *(const f32x4*)(st + row * SR + col + 4);
+          const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          ep.store8(m, n, v);
+        }
+      }
+      return;
+    }
   }
   // epilogue: lane holds D[row = 16 i + 4 fq + r][col = 16 j + fr] of its wave tile
   float cs[FN], cs2[FN];

@@ -68,6 +68,12 @@ class Bottleneck(nn.Module):
         self.short = ConvBN(cin, cout, 1, stride, act=None) if (stride != 1 or cin != cout) else None
 
     def forward(self, x):
+        if self.short is None and self.training and x.is_cuda and torch.is_grad_enabled() and \
+                "res_addend" not in os.environ.get("HOPSX_DISABLE", ""):
+            # identity shortcut: c's BN backward hands the residual's gradient to a's (1x1) dgrad,
+            # whose vectorized epilogue adds it (gemm_glds.h store8) — no autograd add launch
+            slot = {}
+            return self.c(self.b(self.a(x, gslot=slot)), residual=x, res_gslot=slot)
         s = x if self.short is None else self.short(x)
         return self.c(self.b(self.a(x)), residual=s)
 
