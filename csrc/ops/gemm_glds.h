@@ -685,7 +685,9 @@ struct GgPlan {
 inline bool gg_plan(long M, long N, long K, bool allow_split, GgPlan& p, long min_wg_override = -1,
                     int num_cu = 256) {
   static const long force = hopsx_env_int("HOPSX_GG_CFG", -1);
-  static const long min_wg_env = hopsx_env_int("HOPSX_GG_MIN_WG", 128);
+  // 64: the stage-4 ResNet-50 shapes (7x7, 100 tiles of 128x128) run 1.5-2.2x faster on gg than on
+  // gemm_core.h even at 0.4 workgroups per CU (profiles/r4_gg_min_wg_ab.txt)
+  static const long min_wg_env = hopsx_env_int("HOPSX_GG_MIN_WG", 64);
   const long min_wg = min_wg_override >= 0 ? min_wg_override : min_wg_env;
   static const long split_target = hopsx_env_int("HOPSX_GG_SPLIT_TARGET", 1);
   static const long min_ks = hopsx_env_int("HOPSX_GG_SPLIT_MINKT", 8);
