@@ -144,9 +144,11 @@ __device__ __forceinline__ float act_grad_from_out(float y, int act) {
 #include <cstring>
 // Host-side kill switch for specialised fast paths, for A/B checks:
 // HOPSX_DISABLE=direct_conv,pool8,rowreduce,loss_thread,splitk
+// (read on every call: a cached getenv pointer dangles once the process changes the variable — the
+// A/B tests toggle it between runs — and then decided launches from freed memory)
 static inline bool hopsx_disabled(const char* name) {
-  static const char* env = std::getenv("HOPSX_DISABLE");
-  return env && std::strstr(env, name) != nullptr;
+  const char* env = std::getenv("HOPSX_DISABLE");
+  return env && *env && std::strstr(env, name) != nullptr;
 }
 // integer tuning knob from the environment (read on every call: host-side launch sizing only)
 static inline long hopsx_env_int(const char* name, long dflt) {
