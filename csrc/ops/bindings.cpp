@@ -6,7 +6,17 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <utility>
 #include <vector>
+
+#if defined(HOPSX_DEBUG) && HOPSX_DEBUG
+#define HOPSX_DEBUG_BUILD 1
+#else
+#define HOPSX_DEBUG_BUILD 0
+#endif
 
 #include "ops_api.h"
 
@@ -48,7 +58,23 @@ extern "C" unsigned hopsx_det_lost_rowreduce();
 extern "C" int hopsx_det_set_wgrad_glds(int);
 extern "C" unsigned hopsx_det_lost_wgrad_glds();
 
-PYBIND11_MODULE(_hopsx_ops, m) {
+extern "C" int hopsx_dbg_read_conv_mfma(unsigned* out);
+extern "C" int hopsx_dbg_read_loss(unsigned* out);
+extern "C" int hopsx_dbg_read_gemm(unsigned* out);
+extern "C" int hopsx_dbg_read_norm(unsigned* out);
+extern "C" int hopsx_dbg_read_pool(unsigned* out);
+extern "C" int hopsx_dbg_read_conv(unsigned* out);
+extern "C" int hopsx_dbg_read_elementwise(unsigned* out);
+extern "C" int hopsx_dbg_read_rowreduce(unsigned* out);
+extern "C" int hopsx_dbg_read_wgrad_glds(unsigned* out);
+extern "C" int hopsx_dbg_read_embedding(unsigned* out);
+
+// the debug build (-DHOPSX_DEBUG=1) is the module _hopsx_ops_dbg (same sources, hx_check compiled in)
+#ifndef HOPSX_MODNAME
+#define HOPSX_MODNAME _hopsx_ops
+#endif
+#define HX_PYMOD(name) PYBIND11_MODULE(name, m)
+HX_PYMOD(HOPSX_MODNAME) {
   m.doc() = "hopsx CDNA4 (gfx950) HIP kernel library";
   m.attr("ARCH") = "gfx950";
 
@@ -85,6 +111,30 @@ PYBIND11_MODULE(_hopsx_ops, m) {
     if (!e) e = hopsx_det_set_rowreduce(on);
     if (!e) e = hopsx_det_set_wgrad_glds(on);
     return e;
+  });
+  m.attr("DEBUG") = HOPSX_DEBUG_BUILD;
+  // device-side check records per translation unit: [(tag, failures, line, workgroup, thread)], cleared
+  m.def("dbg_read", []() {
+    static const std::pair<const char*, int (*)(unsigned*)> tus[] = {
+    {"conv_mfma", hopsx_dbg_read_conv_mfma},
+    {"loss", hopsx_dbg_read_loss},
+    {"gemm", hopsx_dbg_read_gemm},
+    {"norm", hopsx_dbg_read_norm},
+    {"pool", hopsx_dbg_read_pool},
+    {"conv", hopsx_dbg_read_conv},
+    {"elementwise", hopsx_dbg_read_elementwise},
+    {"rowreduce", hopsx_dbg_read_rowreduce},
+    {"wgrad_glds", hopsx_dbg_read_wgrad_glds},
+    {"embedding", hopsx_dbg_read_embedding},
+    };
+    std::vector<std::tuple<std::string, unsigned, unsigned, unsigned, unsigned>> out;
+    for (const auto& t : tus) {
+      unsigned v[4] = {0u, 0u, 0u, 0u};
+      const int e = t.second(v);
+      if (e) throw std::runtime_error(std::string("hopsx dbg_read: hip error ") + std::to_string(e));
+      if (v[0]) out.emplace_back(t.first, v[0], v[1], v[2], v[3]);
+    }
+    return out;
   });
   m.def("det_lost", []() {
     unsigned n = 0;
@@ -295,14 +345,14 @@ PYBIND11_MODULE(_hopsx_ops, m) {
                         P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), P<float>(acc), S(st));
   });
   m.def("embedding_bag_fwd", [](u table, u idx, u offs, int nbags, int dim, long nidx, int bag_len, int mode, u out,
-                                int of32, long ldo, u st) {
+                                int of32, long ldo, long rows, u st) {
     return hopsx_embedding_bag_fwd(P<float>(table), P<long>(idx), P<long>(offs), nbags, dim, nidx, bag_len, mode,
-                                   P<void>(out), of32, ldo, S(st));
+                                   P<void>(out), of32, ldo, rows, S(st));
   });
   m.def("embedding_bag_bwd", [](u dout, int df32, long ldo, u idx, u offs, int nbags, int dim, long nidx,
-                                int bag_len, int mode, u dtable, u st) {
+                                int bag_len, int mode, u dtable, long rows, u st) {
     return hopsx_embedding_bag_bwd(P<void>(dout), df32, ldo, P<long>(idx), P<long>(offs), nbags, dim, nidx, bag_len,
-                                   mode, P<float>(dtable), S(st));
+                                   mode, P<float>(dtable), rows, S(st));
   });
   m.def("column_stats", [](u x, int rows, int cols, u out, u st) {
     return hopsx_column_stats(P<float>(x), rows, cols, P<float>(out), S(st));

@@ -213,7 +213,43 @@ __device__ inline void det_turn_end(int site, unsigned my, unsigned total) {
                        __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+// ---- device-side bound checks.  hx_check(c) compiles to `true` in a release build; in the debug build
+// (-DHOPSX_DEBUG=1: module _hopsx_ops_dbg, loaded when HOPSX_DEBUG=1) it evaluates c, and a failure records
+// the translation unit's first failing site (source line, workgroup, thread) plus a failure count in
+// hx_dbg_err and yields false, so the caller skips the access instead of faulting.  hx_guard(c) is the
+// same check kept in release builds too: for user-supplied indices (embedding ids, class labels), where
+// an out-of-range value must not become an out-of-bounds access.  kernels.debug_errors() reads and
+// clears the records (HOPSX_DBG_TU below); the debug build's kernels.check() raises on one after every
+// launch outside graph capture.
+#ifndef HOPSX_DEBUG
+#define HOPSX_DEBUG 0
+#endif
+static __device__ unsigned hx_dbg_err[4];  // failures, line of the first, its workgroup, its thread
+__device__ __forceinline__ bool hx_fail_at(int line) {
+  if (atomicAdd(&hx_dbg_err[0], 1u) == 0u) {
+    atomicExch(&hx_dbg_err[1], (unsigned)line);
+    atomicExch(&hx_dbg_err[2], blockIdx.x + gridDim.x * blockIdx.y);
+    atomicExch(&hx_dbg_err[3], threadIdx.x);
+  }
+  return false;
+}
+#define hx_guard(c) ((c) ? true : hx_fail_at(__LINE__))
+#if HOPSX_DEBUG
+#define hx_check(c) hx_guard(c)
+#else
+#define hx_check(c) true
+#endif
+// host reader of the translation unit's records: out[4] as above; clears them
+#define HOPSX_DBG_TU(tag)                                                                            \
+  extern "C" int hopsx_dbg_read_##tag(unsigned* out) {                                              \
+    int e = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hx_dbg_err), 4 * sizeof(unsigned), 0,          \
+                                     hipMemcpyDeviceToHost);                                        \
+    const unsigned z[4] = {0u, 0u, 0u, 0u};                                                         \
+    if (!e && out[0]) e = (int)hipMemcpyToSymbol(HIP_SYMBOL(hx_dbg_err), z, sizeof(z), 0, hipMemcpyHostToDevice); \
+    return e;                                                                                       \
+  }
 #define HOPSX_DET_TU(tag)                                                                          \
+  HOPSX_DBG_TU(tag)                                                                                \
   extern "C" int hopsx_det_set_##tag(int on) {                                                     \
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(hx_det_on), &on, sizeof(int), 0, hipMemcpyHostToDevice); \
   }                                                                                                \

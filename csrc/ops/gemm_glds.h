@@ -112,7 +112,8 @@ struct GgIm2col {
     const int mc = ok ? m : 0;
     const int b = g.fOHW.div(mc), rem = mc - b * (g.OH * g.OW);
     const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
-    return GgSlot{x + (long)b * g.H * g.W * g.C, oh * g.sh - g.ph, ow * g.sw - g.pw, 0, k, min(ilim, kend) - k, ok};
+    const bool in = ok && hx_check(b < g.B && oh < g.OH && ow < g.OW);  // (the fast divisions)
+    return GgSlot{x + (long)b * g.H * g.W * g.C, oh * g.sh - g.ph, ow * g.sw - g.pw, 0, k, min(ilim, kend) - k, in};
   }
   __device__ __forceinline__ const void* kc_at(const GgSlot& s, int dk) const {
     const int k = s.k0 + dk;
@@ -120,7 +121,8 @@ struct GgIm2col {
     const int t = g.fC.div(kc), ci = kc - t * g.C;
     const int kh = g.fKW.div(t), kw = t - kh * g.KW;
     const int ih = s.a + kh * g.dh, iw = s.b + kw * g.dw;
-    const bool ok = s.ok && dk < s.rem && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+    const bool ok = s.ok && dk < s.rem && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W &&
+                    hx_check(kh < g.KH && ci < g.C);
     return ok ? (const void*)(s.q + (ih * g.W + iw) * g.C + ci) : (const void*)g_gg_zero;
   }
   // RC (weight-gradient B): the column k = (kh, kw, ci) is fixed -> channel and tap offsets
@@ -137,7 +139,8 @@ struct GgIm2col {
     const int b = g.fOHW.div(mc), rem = mc - b * (g.OH * g.OW);
     const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
     const int ih = oh * g.sh + s.a, iw = ow * g.sw + s.b;
-    const bool ok = s.ok && dk < s.rem && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+    const bool ok = s.ok && dk < s.rem && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W &&
+                    hx_check(b < g.B);
     return ok ? (const void*)(s.q + (((long)b * g.H + ih) * g.W + iw) * g.C) : (const void*)g_gg_zero;
   }
 };
@@ -153,7 +156,8 @@ struct GgDgradA {
     const int mc = ok ? m : 0;
     const int b = g.fHW.div(mc), rem = mc - b * (g.H * g.W);
     const int ih = g.fW.div(rem), iw = rem - ih * g.W;
-    return GgSlot{dy + (long)b * g.OH * g.OW * g.CO, ih + g.ph, iw + g.pw, 0, k, min(ilim, kend) - k, ok};
+    const bool in = ok && hx_check(b < g.B && ih < g.H && iw < g.W);
+    return GgSlot{dy + (long)b * g.OH * g.OW * g.CO, ih + g.ph, iw + g.pw, 0, k, min(ilim, kend) - k, in};
   }
   __device__ __forceinline__ const void* kc_at(const GgSlot& s, int dk) const {
     const int k = s.k0 + dk;
@@ -164,7 +168,7 @@ struct GgDgradA {
     const int hc = hn > 0 ? hn : 0, wc = wn > 0 ? wn : 0;
     const int oh = g.sh == 1 ? hc : g.fSH.div(hc), ow = g.sw == 1 ? wc : g.fSW.div(wc);
     const bool ok = s.ok && dk < s.rem && hn >= 0 && wn >= 0 && oh * g.sh == hn && ow * g.sw == wn && oh < g.OH &&
-                    ow < g.OW;
+                    ow < g.OW && hx_check(kh < g.KH && co < g.CO);
     return ok ? (const void*)(s.q + (oh * g.OW + ow) * g.CO + co) : (const void*)g_gg_zero;
   }
 };
@@ -183,7 +187,7 @@ struct GgWeightT {
     const int kc = k < olim ? k : 0;
     const int t = g.fCO.div(kc), co = kc - t * g.CO;
     const int kh = g.fKW.div(t), kw = t - kh * g.KW;
-    const bool ok = s.ok && dk < s.rem;
+    const bool ok = s.ok && dk < s.rem && hx_check(kh < g.KH && co < g.CO);
     return ok ? (const void*)(s.q + ((co * g.KH + kh) * g.KW + kw) * g.C) : (const void*)g_gg_zero;
   }
 };
@@ -214,8 +218,9 @@ struct GgDgradParA {
     const int mc = ok ? m : 0;
     const int b = c.fHWp.div(mc), rem = mc - b * (c.Hp * c.Wp);
     const int ihh = c.fWp.div(rem), iww = rem - ihh * c.Wp;
+    const bool in = ok && hx_check(b < g.B && ihh < c.Hp && iww < c.Wp);
     return GgSlot{dy + (long)b * g.OH * g.OW * g.CO, g.sh * ihh + c.py + g.ph, g.sw * iww + c.px + g.pw, 0, k,
-                  min(ilim, kend) - k, ok};
+                  min(ilim, kend) - k, in};
   }
   __device__ __forceinline__ const void* kc_at(const GgSlot& s, int dk) const {
     const int k = s.k0 + dk;
@@ -224,7 +229,8 @@ struct GgDgradParA {
     const int th = c.fNKW.div(t), tw = t - th * c.nkw;
     const int hn = s.a - (c.kh0 + g.sh * th), wn = s.b - (c.kw0 + g.sw * tw);  // multiples of s
     const int oh = g.fSH.div(hn > 0 ? hn : 0), ow = g.fSW.div(wn > 0 ? wn : 0);
-    const bool ok = s.ok && dk < s.rem && hn >= 0 && wn >= 0 && oh < g.OH && ow < g.OW;
+    const bool ok = s.ok && dk < s.rem && hn >= 0 && wn >= 0 && oh < g.OH && ow < g.OW &&
+                    hx_check(oh * g.sh == hn && ow * g.sw == wn && co < g.CO);  // (the class's taps only)
     return ok ? (const void*)(s.q + (oh * g.OW + ow) * g.CO + co) : (const void*)g_gg_zero;
   }
 };
@@ -245,7 +251,7 @@ struct GgWeightTPar {
     const int t = g.fCO.div(kc), co = kc - t * g.CO;
     const int th = c.fNKW.div(t), tw = t - th * c.nkw;
     const int kh = c.kh0 + g.sh * th, kw = c.kw0 + g.sw * tw;
-    const bool ok = s.ok && dk < s.rem;
+    const bool ok = s.ok && dk < s.rem && hx_check(kh < g.KH && kw < g.KW && co < g.CO);
     return ok ? (const void*)(s.q + ((co * g.KH + kh) * g.KW + kw) * g.C) : (const void*)g_gg_zero;
   }
 };

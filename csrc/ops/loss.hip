@@ -65,7 +65,8 @@ __device__ __forceinline__ void row_thread(int kind, const void* logits, int lf3
     const float lse = mx + __logf(se);
     if (kind == 0) {
       const long lab = ((const long*)target)[row];
-      const float zl = ld_logit(logits, lf32, base + lab);
+      // a label outside [0, C) (kernels.debug_errors names it) reads no logit: it contributes lse
+      const float zl = hx_guard((unsigned long)lab < (unsigned long)C) ? ld_logit(logits, lf32, base + lab) : 0.f;
       if (dl)
         for (int c = 0; c < C; ++c)
           st_grad(dl, df32, base + c, (__expf(ld_logit(logits, lf32, base + c) - lse) - (c == lab ? 1.f : 0.f)) * gs);
@@ -127,7 +128,7 @@ __device__ __forceinline__ void row_wave(int kind, const void* logits, int lf32,
         for (int c = lane; c < C; c += 64)
           st_grad(dl, df32, base + c, (__expf(ld_logit(logits, lf32, base + c) - lse) - (c == lab ? 1.f : 0.f)) * gs);
       if (lane == 0) {
-        lacc += lse - ld_logit(logits, lf32, base + lab);
+        lacc += lse - (hx_guard((unsigned long)lab < (unsigned long)C) ? ld_logit(logits, lf32, base + lab) : 0.f);
         cacc += (amx == lab);
       }
     } else {
@@ -549,7 +550,8 @@ __device__ inline void mlp_loss16(int kind, const float* slog, const void* targe
       const float lse = mx + __logf(se);
       const float p = ok ? __expf(z - lse) : 0.f;
       if (kind == 0) {
-        const long lab = r < B ? ((const long*)target)[r] : -1;
+        long lab = r < B ? ((const long*)target)[r] : -1;
+        if (r < B && c == 0 && !hx_guard((unsigned long)lab < (unsigned long)C)) lab = -1;
         if (ok) {
           sdl[r * C + c] = (p - (c == lab ? 1.f : 0.f)) * gs;
           if (c == lab) lacc += lse - z;

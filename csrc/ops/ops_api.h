@@ -165,9 +165,11 @@ int hopsx_nonfinite(const void* x, long n, int is_bf16, unsigned* out, hipStream
 
 // ---- embedding bag (embedding.hip) ----
 int hopsx_embedding_bag_fwd(const float* table, const long* idx, const long* offsets, int nbags, int dim,
-                            long nidx, int bag_len, int mode, void* out, int out_f32, long ldo, hipStream_t st);
+                            long nidx, int bag_len, int mode, void* out, int out_f32, long ldo, long rows,
+                            hipStream_t st);
 int hopsx_embedding_bag_bwd(const void* dout, int dout_f32, long ldo, const long* idx, const long* offsets,
-                            int nbags, int dim, long nidx, int bag_len, int mode, float* dtable, hipStream_t st);
+                            int nbags, int dim, long nidx, int bag_len, int mode, float* dtable, long rows,
+                            hipStream_t st);
 
 // ---- column statistics for the feature store (stats.hip) ----
 int hopsx_column_stats(const float* x, int rows, int cols, float* out_stats, hipStream_t st);

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k(const bf16_raw* __restrict_
         const int kw = iw - (ow * sw - pw);
         if (kw < 0 || kw >= KW) continue;
         const long o = (((long)b * OH + oh) * OW + ow) * C + c;
-        if (am[o] == kh * KW + kw) {
+        const unsigned a = am[o];
+        if (hx_check(a < (unsigned)(KH * KW)) && a == (unsigned)(kh * KW + kw)) {
           float d = bf2f(dy[o]);
           if (p > 0.f) d = uniform01(key, o) >= p ? d * dscale : 0.f;
           g += d;

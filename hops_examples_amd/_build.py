@@ -115,9 +115,10 @@ HIP_FLAGS = [
 
 
 def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra_link: list[str],
-               extra_headers: list[Path] | None = None) -> Path:
+               extra_headers: list[Path] | None = None, defines: list[str] | None = None) -> Path:
     """kind: 'hip' compiles every source with hipcc for gfx950, 'cpp' with g++.  ``extra_headers``:
-    headers outside ``srcdir`` the sources include (part of the rebuild digest)."""
+    headers outside ``srcdir`` the sources include (part of the rebuild digest).  ``defines``: extra
+    -D flags of the HIP compiles (the debug variant)."""
     out = PKG / f"{name}{EXT}"
     objdir = BUILD / name
     objdir.mkdir(parents=True, exist_ok=True)
@@ -127,7 +128,7 @@ def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra
     for s in srcs:
         o = objdir / (s.name + ".o")
         if kind == "hip" or s.suffix == ".hip":
-            cmd = [HIPCC, *HIP_FLAGS, *_py_includes(), f"-I{srcdir}", "-c", str(s), "-o", str(o)]
+            cmd = [HIPCC, *HIP_FLAGS, *(defines or []), *_py_includes(), f"-I{srcdir}", "-c", str(s), "-o", str(o)]
             if s.suffix == ".cpp":
                 cmd.insert(1, "-x")
                 cmd.insert(2, "hip")
@@ -160,10 +161,15 @@ def _build_lib(name: str, srcdir: Path, kind: str, force: bool, jobs: int, extra
     return out
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> list[Path]:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True, debug: bool = False) -> list[Path]:
+    """The three in-tree extensions; ``debug=True`` also builds ``_hopsx_ops_dbg``, the kernel library
+    with the device-side bound checks compiled in (common.h hx_check; loaded when HOPSX_DEBUG=1)."""
     jobs = jobs or min(8, os.cpu_count() or 4)
     outs = []
     outs.append(_build_lib("_hopsx_ops", ROOT / "csrc" / "ops", "hip", force, jobs, []))
+    if debug:
+        outs.append(_build_lib("_hopsx_ops_dbg", ROOT / "csrc" / "ops", "hip", force, jobs, [],
+                               defines=["-DHOPSX_DEBUG=1", "-DHOPSX_MODNAME=_hopsx_ops_dbg"]))
     if (ROOT / "csrc" / "io").exists() and any((ROOT / "csrc" / "io").glob("*.cpp")):
         outs.append(_build_lib("_hopsx_io", ROOT / "csrc" / "io", "cpp", force, jobs,
                                []))
@@ -181,9 +187,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--debug", action="store_true", help="also build _hopsx_ops_dbg (device bound checks)")
     a = ap.parse_args()
     try:
-        build(force=a.force, jobs=a.j)
+        build(force=a.force, jobs=a.j, debug=a.debug)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

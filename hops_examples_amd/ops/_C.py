@@ -21,6 +21,13 @@ def _load():
     global _ext, _err
     if _ext is not None or _err is not None:
         return _ext
+    if debug():
+        # the debug build (python -m hops_examples_amd._build --debug): no autobuild, no fallback
+        try:
+            _ext = importlib.import_module("hops_examples_amd._hopsx_ops_dbg")
+        except Exception as e:
+            _err = e
+        return _ext
     try:
         _ext = importlib.import_module("hops_examples_amd._hopsx_ops")
     except Exception as e:  # pragma: no cover - depends on build state
@@ -39,6 +46,23 @@ def _load():
 
 
 _det_done = False
+
+
+def debug() -> bool:
+    """``HOPSX_DEBUG=1``: load ``_hopsx_ops_dbg`` (device-side bound checks, common.h hx_check); every
+    checked launch outside graph capture is followed by a synchronize and a read of the records."""
+    return os.environ.get("HOPSX_DEBUG", "0") == "1"
+
+
+def debug_errors(clear: bool = True) -> list:
+    """Device-side check records since the last read: [(translation unit, failures, source line,
+    workgroup, thread)].  Release builds record the always-on guards (hx_guard: embedding ids, class
+    labels) too.  Reading clears them."""
+    m = _load()
+    if m is None or not torch.cuda.is_available() or not hasattr(m, "dbg_read"):
+        return []
+    torch.cuda.synchronize()
+    return [tuple(r) for r in m.dbg_read()]
 
 
 def deterministic() -> bool:
@@ -89,6 +113,14 @@ def stream() -> int:
 def check(rc: int, what: str) -> None:
     if rc != 0:
         raise RuntimeError(f"hopsx kernel {what} failed with hipError {rc}")
+    if _DEBUG and not torch.cuda.is_current_stream_capturing():
+        errs = debug_errors()
+        if errs:
+            raise RuntimeError(f"hopsx kernel {what}: device-side check failed: " + "; ".join(
+                f"{tu}.hip line {ln} (workgroup {wg}, thread {th}; {n} failure(s))" for tu, n, ln, wg, th in errs))
+
+
+_DEBUG = debug()
 
 
 # mirror of csrc/ops/ops_api.h

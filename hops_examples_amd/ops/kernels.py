@@ -12,7 +12,7 @@ import os
 import torch
 
 from . import _C
-from ._C import ACT, EPI_ATOMIC_F32, EPI_DACT_BF16, EPI_STORE_BF16, EPI_STORE_F32, check, ptr, stream
+from ._C import ACT, EPI_ATOMIC_F32, EPI_DACT_BF16, EPI_STORE_BF16, EPI_STORE_F32, check, debug_errors, ptr, stream  # noqa: F401
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -621,7 +621,8 @@ def embedding_bag_fwd(table, idx, offsets, mode, out, ldo=None, bag_len=1):
     dim = table.shape[1]
     assert offsets is not None or idx.numel() == nb * bag_len, "idx / bag_len / out shape mismatch"
     check(_C.ext().embedding_bag_fwd(ptr(table), ptr(idx), ptr(offsets), nb, dim, idx.numel(), bag_len, mode, ptr(out),
-                                     int(out.dtype == F32), ldo if ldo is not None else out.stride(0), stream()),
+                                     int(out.dtype == F32), ldo if ldo is not None else out.stride(0), table.shape[0],
+                                     stream()),
           "embedding_bag_fwd")
     return out
 
@@ -631,7 +632,7 @@ def embedding_bag_bwd(dout, idx, offsets, mode, dtable, nbags, ldo=None, bag_len
     assert offsets is not None or idx.numel() == nbags * bag_len, "idx / bag_len mismatch"
     check(_C.ext().embedding_bag_bwd(ptr(dout), int(dout.dtype == F32), ldo if ldo is not None else dout.stride(0),
                                      ptr(idx), ptr(offsets), nbags, dim, idx.numel(), bag_len, mode, ptr(dtable),
-                                     stream()),
+                                     dtable.shape[0], stream()),
           "embedding_bag_bwd")
     return dtable
 

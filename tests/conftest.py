@@ -25,3 +25,16 @@ def project_root(tmp_path, monkeypatch):
     _cfg.reset()
     yield root
     _cfg.reset()
+
+
+@pytest.fixture(autouse=True)
+def _hopsx_device_checks(request):
+    """HOPSX_DEBUG=1 (the _hopsx_ops_dbg build): every GPU test ends with no device-side check record
+    (common.h hx_check); without it this fixture does nothing."""
+    yield
+    if os.environ.get("HOPSX_DEBUG", "0") != "1" or request.node.get_closest_marker("gpu") is None:
+        return
+    from hops_examples_amd.ops import _C
+
+    errs = _C.debug_errors()
+    assert not errs, f"device-side bound checks failed: {errs}"

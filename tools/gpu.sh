@@ -11,6 +11,7 @@
 #   tools/gpu.sh prof    <tag>           rocprofv3 kernel table of bench.py (flagship only)
 #   tools/gpu.sh pmc     <tag>           PMC passes over bench.py (one counter group per run)
 #   tools/gpu.sh knobs   <tag> "ENV=.." ...   flagship bench.py --steps 20 per env setting ("" = default)
+#   tools/gpu.sh debug   <tag>           kernel suites on the debug build (_hopsx_ops_dbg, HOPSX_DEBUG=1)
 set -o pipefail
 job=${1:?job}; tag=${2:-$1}; shift 2
 out=gpurun_out/$tag
@@ -86,6 +87,9 @@ pmc)
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES -d "$R/$out/a" -o run --output-format csv -- $P > "$R/$out/a.log" 2>&1 && \
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES FETCH_SIZE -d "$R/$out/b" -o run --output-format csv -- $P > "$R/$out/b.log" 2>&1 && \
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES WRITE_SIZE -d "$R/$out/c" -o run --output-format csv -- $P > "$R/$out/c.log" 2>&1 ;;
+debug)
+  export HOPSX_DEBUG=1; T=600 pyt $out/pytest_debug.log tests/test_debug_checks_gpu.py tests/test_kernels_gpu.py tests/test_kernels_v2_gpu.py \
+    tests/test_dgrad_par_gpu.py tests/test_wgrad_glds_gpu.py tests/test_bnstats_gpu.py tests/test_models_gpu.py ;;
 knobs)
   for s in "$@"; do
     r=$(env $s timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi 2>>$out/err.log) || { echo "FAIL [$s]"; fail $out/err.log; }
