@@ -380,8 +380,9 @@ HX_PYMOD(HOPSX_MODNAME) {
     return hopsx_column_stats64(P<double>(x), rows, cols, P<double>(out), S(st));
   });
   m.def("u8_normalize_chan", [](u x, u y, long pixels, int C, std::vector<float> scale, std::vector<float> shift,
-                                int rev, u st) {
+                                int rev, int cout, u st) {
     if ((int)scale.size() < C || (int)shift.size() < C) return -2;
-    return hopsx_u8_normalize_chan(P<unsigned char>(x), P<void>(y), pixels, C, scale.data(), shift.data(), rev, S(st));
+    return hopsx_u8_normalize_chan(P<unsigned char>(x), P<void>(y), pixels, C, scale.data(), shift.data(), rev, cout,
+                                   S(st));
   });
 }

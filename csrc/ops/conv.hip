@@ -509,8 +509,12 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
   // LDS-DMA 128x128 kernel (wgrad_glds.hip) for the conv -> BN layers (no dY mask, no bias grad);
   // the small-CO direct-MFMA kernel keeps its shapes unless HOPSX_WGRAD_GLDS_FIRST=1 (A/B knob)
   static const int glds_first = hopsx_env_int("HOPSX_WGRAD_GLDS_FIRST", 0);
-  const bool mfma_ok =
-      hopsx_conv_wgrad_mfma_ok(geom) && (uintptr_t)dy % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0;
+  // ... up to a size: past ~32M pixel-columns (ResNet-50 at B=64: the stage-1 3x3, the 8-channel stem)
+  // the LDS-DMA engine wins even at CO = 64 (profiles/r4_stem_wgrad_ab.txt: +1.7 % per step); the CIFAR
+  // ResNets' convs (<= 19M) keep the short-conv kernel
+  static const long mfma_max_mk = hopsx_env_int("HOPSX_WGRAD_MFMA_MAX_MK", 32L << 20);
+  const bool mfma_ok = hopsx_conv_wgrad_mfma_ok(geom) && (long)K * N < mfma_max_mk && (uintptr_t)dy % 16 == 0 &&
+                       (uintptr_t)y % 16 == 0 && (uintptr_t)x % 16 == 0;
   if (!y && !dbias && (glds_first || !mfma_ok) && hopsx_conv_wgrad_glds_ok(geom) &&
       hopsx_conv2d_wgrad_glds(dy, x, geom, dw, 0, st) == 0)
     return 0;

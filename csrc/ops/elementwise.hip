@@ -69,6 +69,20 @@ __global__ void u8_norm_chan_k(const unsigned char* __restrict__ x, bf16_raw* __
   }
 }
 
+// C <= 4 channels in, 8 out (channels C..7 zero): the layout of a stem conv whose input channels are
+// zero-padded to 8 so it runs on the C % 8 == 0 MFMA conv paths; one 16-B store per pixel
+__global__ void u8_norm_chan8_k(const unsigned char* __restrict__ x, bf16_raw* __restrict__ y, long pixels, int C,
+                                ChanAffine a, int rev) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < pixels; p += (long)gridDim.x * blockDim.x) {
+    const unsigned char* px = x + p * C;
+    bf16x8 q = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < C) q[c] = (short)f2bf(px[rev ? C - 1 - c : c] * a.scale[c] + a.shift[c]);
+    *(bf16x8*)(y + p * 8) = q;
+  }
+}
+
 // out[n] += sum_m x[m][n]; one workgroup owns a column strip, rows split over gridDim.y
 __global__ __launch_bounds__(256) void colsum_k(const bf16_raw* __restrict__ x, float* __restrict__ out, int M,
                                                 int N, int rows_per_block) {
@@ -155,8 +169,8 @@ extern "C" int hopsx_cast_bf16_f32(const void* x, float* y, long n, hipStream_t 
   return (int)hipGetLastError();
 }
 extern "C" int hopsx_u8_normalize_chan(const unsigned char* x, void* y, long pixels, int C, const float* scale,
-                                       const float* shift, int rev, hipStream_t st) {
-  if (C < 1 || C > 4 || pixels < 0) return -2;
+                                       const float* shift, int rev, int cout, hipStream_t st) {
+  if (C < 1 || C > 4 || pixels < 0 || (cout != C && cout != 8) || (cout == 8 && (uintptr_t)y % 16)) return -2;
   ChanAffine a{};
   for (int c = 0; c < C; ++c) {
     a.scale[c] = scale[c];
@@ -165,7 +179,10 @@ extern "C" int hopsx_u8_normalize_chan(const unsigned char* x, void* y, long pix
   long g = (pixels + 255) / 256;
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(u8_norm_chan_k, dim3((unsigned)g), dim3(256), 0, st, x, (bf16_raw*)y, pixels, C, a, rev);
+  if (cout == 8)
+    hipLaunchKernelGGL(u8_norm_chan8_k, dim3((unsigned)g), dim3(256), 0, st, x, (bf16_raw*)y, pixels, C, a, rev);
+  else
+    hipLaunchKernelGGL(u8_norm_chan_k, dim3((unsigned)g), dim3(256), 0, st, x, (bf16_raw*)y, pixels, C, a, rev);
   return (int)hipGetLastError();
 }
 extern "C" int hopsx_u8_normalize(const unsigned char* x, void* y, long n, float scale, float shift, hipStream_t st) {

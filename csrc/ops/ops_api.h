@@ -195,7 +195,7 @@ int hopsx_range_window(const long* ts, const int* seg, const long* seg_off, cons
 int hopsx_column_stats64(const double* x, int rows, int cols, double* out_stats, hipStream_t st);
 // per-channel uint8 NHWC -> bf16 image normalisation (C <= 4, optional channel reversal)
 int hopsx_u8_normalize_chan(const unsigned char* x, void* y, long pixels, int C, const float* scale,
-                            const float* shift, int rev, hipStream_t st);
+                            const float* shift, int rev, int cout, hipStream_t st);
 // columnar chunk -> row-major fp32 [rows][ld] (columns.hip); dtypes: 0 f32 1 f64 2 i64 3 i32 4 i16 5 i8
 // 6 u8 7 f16; k <= 16
 int hopsx_cols_to_f32(const void* const* cols, const int* dtypes, int k, long rows, float* out, long ld,

@@ -93,7 +93,12 @@ class Conv2d(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, x, bnstats: bool = False, gslot=None):
-        return HF.conv2d(x, self.weight, self.bias, act=self.activation, in_affine=self.in_affine, bnstats=bnstats,
+        w = self.weight
+        if x.shape[-1] > self.in_channels:
+            # an input laid out with zero channels beyond in_channels (models/resnet.py image stems: the
+            # normalisation kernel writes 8 channels): the weight is zero-padded to match
+            w = HF.pad_input_channels(w, x.shape[-1])
+        return HF.conv2d(x, w, self.bias, act=self.activation, in_affine=self.in_affine, bnstats=bnstats,
                          gslot=gslot, **self.cfg)
 
     def extra_repr(self):

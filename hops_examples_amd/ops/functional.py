@@ -632,6 +632,35 @@ def _conv_apply(x, w, b, st, pd, dl, a, in_affine, pool=None, bnstats=False, gsl
     return y
 
 
+class _PadCinFn(torch.autograd.Function):
+    """A conv weight [CO, KH, KW, C] zero-padded to ``cp`` input channels, for an input whose channels
+    C..cp-1 are zero (a 3-channel image stem laid out as 8 channels by kernels.u8_normalize_chan, so the
+    conv takes the C % 8 == 0 MFMA paths instead of the generic narrow-channel gather).  The padded
+    taps meet zeros, so the conv is unchanged; backward hands the first C channels of the padded
+    weight's gradient to the parameter (into its arena gradient directly when it has one)."""
+
+    @staticmethod
+    def forward(ctx, w, cp):
+        ctx.w = w
+        return torch.nn.functional.pad(w.detach(), (0, cp - w.shape[-1]))
+
+    @staticmethod
+    def backward(ctx, g):
+        w = ctx.w
+        gs = g[..., :w.shape[-1]]
+        tgt = _arena.grad_target(w)
+        hooks.grad_ready(w)
+        if tgt is not None:
+            tgt.add_(gs)
+            return None, None
+        return gs.contiguous(), None
+
+
+def pad_input_channels(w, cp: int):
+    """``w`` padded with zero input channels to ``cp`` (autograd-aware, see _PadCinFn)."""
+    return _PadCinFn.apply(w, int(cp))
+
+
 def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=None, bnstats=False, gslot=None):
     """NHWC conv. x [B,H,W,C], w [CO,KH,KW,C]. padding: int, tuple, 'valid' or 'same' (stride 1).
 

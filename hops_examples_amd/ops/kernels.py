@@ -479,14 +479,17 @@ def cols_to_f32(cols, out):
     return out
 
 
-def u8_normalize_chan(x, scale, shift, reverse=False, out=None):
+def u8_normalize_chan(x, scale, shift, reverse=False, out=None, cout=None):
     """uint8 NHWC [..., C] -> bf16, per channel x * scale[c] + shift[c] (channel order reversed first
-    with ``reverse``: RGB -> BGR)."""
+    with ``reverse``: RGB -> BGR).  ``cout=8``: the output has 8 channels, C..7 zero (a stem conv's
+    input padded for the C % 8 == 0 MFMA paths, nn.Conv2d)."""
     C = x.shape[-1]
+    cout = C if cout is None else int(cout)
     if out is None:
-        out = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((*x.shape[:-1], cout), device=x.device, dtype=torch.bfloat16)
     check(_C.ext().u8_normalize_chan(ptr(x), ptr(out), x.numel() // C, C, [float(v) for v in scale],
-                                     [float(v) for v in shift], int(bool(reverse)), stream()), "u8_normalize_chan")
+                                     [float(v) for v in shift], int(bool(reverse)), cout, stream()),
+          "u8_normalize_chan")
     return out
 
 
