@@ -712,13 +712,22 @@ static bool bn_vec_ok(int C, std::initializer_list<const void*> ptrs) {
   return true;
 }
 
+// Deferred fold (the apply kernel folds the replicas, no arrival round trips in the reduction) costs
+// every apply workgroup a read of BN_NREP x 2C floats: cheap at narrow C, a large share of the apply's
+// traffic at C = 1024 / 2048.  Above HOPSX_BN_DEFER_MAXC the reduction's last workgroup folds instead.
+static int bn_defer(int C) {
+  static const long maxc = hopsx_env_int("HOPSX_BN_DEFER_MAXC", 1L << 30);
+  return hopsx_disabled("bn_defer") || C > maxc ? 0 : 1;
+}
+
 static int colred_grid(int M, int C, int& rpb) {
   const int RPI = 256 / (C / 8);
   // ~BN_UNR rows per thread: one trip of loads in flight per lane and >= 256 workgroups on the
   // ResNet-20 stage-1 shapes (8 rows per thread left half the CUs idle there)
   const long rpt = hopsx_env_int("HOPSX_BN_RPT", BN_UNR);
   long g = (M + (long)RPI * rpt - 1) / ((long)RPI * rpt);
-  if (g > 1024) g = 1024;
+  static const long maxg = hopsx_env_int("HOPSX_BN_MAXG", 1024);
+  if (g > maxg) g = maxg;
   if (g < 1) g = 1;
   rpb = (int)((M + g - 1) / g);
   return (int)((M + rpb - 1) / rpb);
@@ -727,7 +736,8 @@ static int colred_grid(int M, int C, int& rpb) {
 static int apply_grid(long nch, int C) {
   const int CG = C >> 3;
   long g = (nch + 511) / 512;  // two chunks per thread per trip
-  if (g > 4096) g = 4096;
+  static const long maxg = hopsx_env_int("HOPSX_BN_APPLY_MAXG", 4096);
+  if (g > maxg) g = maxg;
   if (g < 1) g = 1;
   // gridDim*256 must be a multiple of CG (per-thread channel group); CG divides 256
   (void)CG;
@@ -806,7 +816,7 @@ extern "C" int hopsx_bn_fwd_train(const void* x, void* y, const float* gamma, co
   if (acc && bn_vec_ok(C, {x, y, residual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
     const int g = colred_grid(M, C, rpb);
-    const int defer = hopsx_disabled("bn_defer") ? 0 : 1;
+    const int defer = bn_defer(C);
     const BnFin fin{mean_out, rstd_out, running_mean, running_var, momentum, eps, nullptr, nullptr, nullptr, defer};
     hipLaunchKernelGGL(bn_colred8_k<0>, dim3(g), dim3(256), 0, st, (const bf16_raw*)x, nullptr, nullptr, nullptr,
                        nullptr, acc, M, C, rpb, 0, fin);
@@ -870,7 +880,7 @@ extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const 
     const int g = colred_grid(M, C, rpb);
     if (bn_bwd_coop(dy, x, y, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, C, act, dresidual, acc, st))
       return (int)hipGetLastError();
-    const int defer = hopsx_disabled("bn_defer") ? 0 : 1;
+    const int defer = bn_defer(C);
     const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, defer};
     hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
                        (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act, fin);
