@@ -480,11 +480,13 @@ def main():
     ap.add_argument("--rehearse", action="store_true", help="allow more ranks than GPUs (shared devices, gloo)")
     ap.add_argument("--from-transform", action="store_true",
                     help="taxi: train on the TFX Transform stage's output (raw trips analyzed + transformed on the GPU)")
+    ap.add_argument("--inline", action="store_true",
+                    help="cifar_resnet on one GPU in this process (no experiment worker: profilers see the kernels)")
     a = ap.parse_args()
     from hops_examples_amd.parallel import launch
 
     if not launch.is_rank_process():
-        if a.config == "cifar_resnet":
+        if a.config == "cifar_resnet" and not (a.inline and a.gpus == 1):
             sys.exit(cifar_via_experiment(a))
         if a.config == "titanic" and a.gpus > 1:
             sys.exit(titanic_via_experiment(a))

@@ -1153,7 +1153,7 @@ static void pair_wgrad_plan(const ConvGeom& g, long slots, int& cpw, long& nBx, 
 // dgrad on the implicit GEMM + wgrad on the direct MFMA kernel in one launch (conv_bwd_pair_gemm_k)
 static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                               int act_prev, float* colsum, const void* y, int yact, const void* x, float* dw,
-                              float* dbias, hipStream_t st) {
+                              float* dbias, const void* addend, hipStream_t st) {
   if (hopsx_disabled("bwd_pair_gemm")) return -2;
   ConvGeom g = cm_geom(geom);
   if (g.C % 8 != 0 || g.CO % 8 != 0 || ((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)w) % 16 != 0)
@@ -1180,7 +1180,8 @@ static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, vo
                      g.KH * g.KW * g.C, cpw, dbg};
   ConvDgradALoader al{(const bf16_raw*)dy, g, 1, (const bf16_raw*)y, yact};
   ConvWeightTLoader bl{(const bf16_raw*)w, g, 1};
-  EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act_prev, colsum};
+  // addend: another consumer's gradient of x, added after the dgrad (no act' of a producing layer here)
+  EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act_prev, colsum, (const bf16_raw*)addend};
 #define HOPSX_PG(BMv, NFCv)                                                                                   \
   if (BM == BMv && g.CO / 16 == NFCv) {                                                                     \
     hipLaunchKernelGGL((conv_bwd_pair_gemm_k<BMv, NFCv>), dim3((unsigned)total), dim3(256), shm, st, al, bl, e, M, \
@@ -1251,9 +1252,11 @@ static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, 
   if (fused && addend) return -2;
   if ((uintptr_t)addend % 16 != 0) return -3;
   if (!hopsx_conv_dgrad_mfma_ok(geom)) {
-    if (addend) return -3;  // the GEMM variant has no addend: call again without it and add afterwards
+    // the GEMM variant adds an addend in its epilogue after the dgrad; with an act' of the producing
+    // layer (yprev) the sum would have to come first: call again without it and add afterwards
+    if (addend && yprev) return -3;
     if (os.kind >= 0) return -2;
-    return fused ? -2 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, st);
+    return fused ? -2 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, addend, st);
   }
   if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
   if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)yprev) % 16 != 0) return -2;

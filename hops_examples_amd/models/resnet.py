@@ -21,6 +21,7 @@ import torch
 from torch import nn
 
 from .. import nn as hnn
+from ..ops import functional as HF
 
 
 class ConvBN(nn.Module):
@@ -34,6 +35,11 @@ class ConvBN(nn.Module):
         # the BN is one apply launch instead of a statistics pass + an apply.  gslot / res_gslot:
         # see BasicBlock.forward
         return self.bn(self.conv(x, bnstats=self.bn.training, gslot=gslot), residual, gslot=res_gslot)
+
+
+def _fuse_proj(block, x) -> bool:
+    return (block.training and x.is_cuda and torch.is_grad_enabled() and x.requires_grad
+            and "proj_addend" not in os.environ.get("HOPSX_DISABLE", ""))
 
 
 class BasicBlock(nn.Module):
@@ -52,6 +58,12 @@ class BasicBlock(nn.Module):
             # first) is handed to a's conv backward, whose dgrad epilogue adds it — no autograd add
             slot = {}
             return self.b(self.a(x, gslot=slot), residual=x, res_gslot=slot)
+        if self.short is not None and _fuse_proj(self, x):
+            # projection shortcut: conv a's dX goes to the short conv's dgrad epilogue (backpropagated
+            # after a's: created first), not to an autograd add (ops.functional.GiveGrad)
+            slot = {}
+            s = self.short(x, gslot=slot)
+            return self.b(self.a(x, gslot=HF.GiveGrad(slot)), residual=s)
         s = x if self.short is None else self.short(x)
         return self.b(self.a(x), residual=s)
 
@@ -74,6 +86,10 @@ class Bottleneck(nn.Module):
             # whose vectorized epilogue adds it (gemm_glds.h store8) — no autograd add launch
             slot = {}
             return self.c(self.b(self.a(x, gslot=slot)), residual=x, res_gslot=slot)
+        if self.short is not None and _fuse_proj(self, x):  # (see BasicBlock.forward)
+            slot = {}
+            s = self.short(x, gslot=slot)
+            return self.c(self.b(self.a(x, gslot=HF.GiveGrad(slot))), residual=s)
         s = x if self.short is None else self.short(x)
         return self.c(self.b(self.a(x)), residual=s)
 

@@ -322,6 +322,9 @@ class _Conv2dFn(torch.autograd.Function):
                 gslot=None):
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
         ctx.pool = None
+        ctx.give = None
+        if isinstance(gslot, GiveGrad):
+            ctx.give, gslot = gslot.slot, None
         # gslot: a dict through which a later-backpropagated consumer of x (a ResNet block's identity
         # shortcut, _BNFn) hands over its gradient of x; this dgrad adds it (in the epilogue where
         # the kernel has one) instead of autograd launching an add
@@ -379,6 +382,15 @@ class _Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        grads = _Conv2dFn._backward(ctx, dy)
+        give = getattr(ctx, "give", None)
+        if give is not None and grads[0] is not None and not give.pop("late", False):
+            give["g"] = grads[0]  # the other consumer of x adds it in its dgrad epilogue (GiveGrad)
+            grads = (None,) + tuple(grads[1:])
+        return grads
+
+    @staticmethod
+    def _backward(ctx, dy):
         if dy is None:
             return (None,) * 12
         if ctx.plain:  # 1x1 conv as library GEMMs: dX = dY W, dW += dY^T X (fp32 out, bf16 in)
@@ -482,8 +494,24 @@ class _Conv2dFn(torch.autograd.Function):
                 None, None, None, None)
 
 
+class GiveGrad:
+    """``gslot=GiveGrad(slot)`` on a conv: its input gradient is handed to the slot instead of autograd,
+    for the OTHER conv consuming the same input (``gslot=slot``, backpropagated later) to add in its
+    dgrad epilogue — a projection-shortcut block's two convs of x, no autograd add.  Order-safe: a taker
+    that runs first marks the slot "late" and the giver then returns its gradient normally."""
+    __slots__ = ("slot",)
+
+    def __init__(self, slot: dict):
+        self.slot = slot
+
+
 def _take_addend(ctx):
-    return ctx.gslot.pop("g", None) if ctx.gslot is not None else None
+    if ctx.gslot is None:
+        return None
+    a = ctx.gslot.pop("g", None)
+    if a is None:
+        ctx.gslot["late"] = True  # (a giver that has not run yet returns its gradient to autograd itself)
+    return a
 
 
 def _add_addend(ctx, dx):

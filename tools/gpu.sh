@@ -77,7 +77,7 @@ resnet)
   bench cifar56 benchmarks/run.py cifar_resnet --depth 56 --batch 128 --steps 50 --warmup 10
   bench r50_b64 benchmarks/run.py resnet50 --batch 64 --steps 30 --warmup 5
   bench r50_b256 benchmarks/run.py resnet50 --batch 256 --steps 10 --warmup 3
-  ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10
+  ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10 --inline
   ktable p50 r50_b64_kernels.txt benchmarks/run.py resnet50 --batch 64 --steps 20 --warmup 5 ;;
 prof)
   ktable pf flagship_kernels.txt bench.py --steps 200 --warmup 20 --no-taxi ;;
