@@ -340,9 +340,10 @@ HX_PYMOD(HOPSX_MODNAME) {
                               P<void>(res), act, S(st));
   });
   m.def("bn_bwd", [](u dy, u x, u y, u g, u mean, u rstd, u dx, u dg, u db, u ws, int M, int C, int act, u dres,
-                     u acc, u st) {
+                     u acc, u zbeta, u st) {
     return hopsx_bn_bwd(P<void>(dy), P<void>(x), P<void>(y), P<float>(g), P<float>(mean), P<float>(rstd), P<void>(dx),
-                        P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), P<float>(acc), S(st));
+                        P<float>(dg), P<float>(db), P<float>(ws), M, C, act, P<void>(dres), P<float>(acc),
+                        P<float>(zbeta), S(st));
   });
   m.def("embedding_bag_fwd", [](u table, u idx, u offs, int nbags, int dim, long nidx, int bag_len, int mode, u out,
                                 int of32, long ldo, long rows, u st) {

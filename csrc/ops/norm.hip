@@ -134,6 +134,11 @@ __global__ void bn_grad_acc_k(const float* __restrict__ ws, float* __restrict__ 
 constexpr int BN_NREP = HOPSX_BN_NREP;
 constexpr int BN_UNR = 4;
 
+// The forward's per-channel shift, one explicit fma: the backward recomputes it bit-identically, so a
+// ReLU BN without residual takes its act' mask from z (t = z * sc + sh > 0, exactly the forward's test)
+// instead of reading y back (zmask: one tensor less in both backward passes).
+__device__ __forceinline__ float bn_shift(float beta, float mu, float sc) { return fmaf(-mu, sc, beta); }
+
 __device__ __forceinline__ void ld8f(const bf16_raw* p, float* v) {
   const bf16x8 q = *(const bf16x8*)p;
 #pragma unroll
@@ -227,17 +232,26 @@ template <int MODE>
 __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__ a, const bf16_raw* __restrict__ x,
                                                     const bf16_raw* __restrict__ y, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, float* __restrict__ acc, int M,
-                                                    int C, int rpb, int act, BnFin fin) {
+                                                    int C, int rpb, int act, BnFin fin,
+                                                    const float* __restrict__ gamma = nullptr,
+                                                    const float* __restrict__ zbeta = nullptr) {
   const int CG = C >> 3, RPI = 256 / CG;
   const int cg = threadIdx.x % CG, rsub = threadIdx.x / CG;
   const int c0 = cg * 8;
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  float s1[8], s2[8], mu[8], rs[8];
+  float s1[8], s2[8], mu[8], rs[8], zs[8], zh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; mu[j] = 0.f; rs[j] = 0.f; }
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; mu[j] = 0.f; rs[j] = 0.f; zs[j] = 0.f; zh[j] = 0.f; }
+  const bool zmask = MODE == 1 && zbeta != nullptr && act == ACT_RELU;  // act' from z (bn_shift)
   if (MODE == 1) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; rs[j] = rstd[c0 + j]; }
+    if (zmask)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        zs[j] = rs[j] * (gamma ? gamma[c0 + j] : 1.f);
+        zh[j] = bn_shift(zbeta[c0 + j], mu[j], zs[j]);
+      }
   }
   for (int r = r0 + rsub; r < r1; r += BN_UNR * RPI) {
     float va[BN_UNR][8], vx[BN_UNR][8], vy[BN_UNR][8];
@@ -248,7 +262,7 @@ __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__
       ld8f(a + o, va[u]);
       if (MODE == 1) {
         ld8f(x + o, vx[u]);
-        if (act != ACT_NONE) ld8f(y + o, vy[u]);
+        if (act != ACT_NONE && !zmask) ld8f(y + o, vy[u]);
       }
     }
 #pragma unroll
@@ -261,7 +275,8 @@ __global__ __launch_bounds__(256) void bn_colred8_k(const bf16_raw* __restrict__
           s2[j] = fmaf(va[u][j], va[u][j], s2[j]);
         } else {
           float dz = va[u][j];
-          if (act != ACT_NONE) dz *= act_grad_from_out(vy[u][j], act);
+          if (zmask) dz = fmaf(vx[u][j], zs[j], zh[j]) > 0.f ? dz : 0.f;
+          else if (act != ACT_NONE) dz *= act_grad_from_out(vy[u][j], act);
           s1[j] += dz;
           s2[j] = fmaf(dz, (vx[u][j] - mu[j]) * rs[j], s2[j]);
         }
@@ -323,7 +338,7 @@ __global__ __launch_bounds__(256) void bn_apply8_k(const bf16_raw* __restrict__ 
   for (int j = 0; j < 8; ++j) {
     const float rs = var_mode ? rsqrtf(rstd[c0 + j] + eps) : rstd[c0 + j];
     sc[j] = rs * (gamma ? gamma[c0 + j] : 1.f);
-    sh[j] = (beta ? beta[c0 + j] : 0.f) - mean[c0 + j] * sc[j];
+    sh[j] = bn_shift(beta ? beta[c0 + j] : 0.f, mean[c0 + j], sc[j]);
   }
   for (long i = i0; i < nch; i += 2 * stride) {
     float v[2][8], rv[2][8];
@@ -388,7 +403,7 @@ __global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restric
     const float rs = rsqrtf(var + fin.eps);
     const float sc = rs * (gamma ? gamma[c] : 1.f);
     ssc[c] = sc;
-    ssh[c] = (beta ? beta[c] : 0.f) - mu * sc;
+    ssh[c] = bn_shift(beta ? beta[c] : 0.f, mu, sc);
     if (blockIdx.x == 0) {
       fin.mean_out[c] = mu;
       fin.rstd_out[c] = rs;
@@ -490,8 +505,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, float* __restrict__ acc,
                                                            bf16_raw* __restrict__ dx, bf16_raw* __restrict__ dres,
-                                                           long nch, int M, int C, int act, BnFin fin) {
+                                                           long nch, int M, int C, int act, BnFin fin,
+                                                           const float* __restrict__ zbeta = nullptr) {
   __shared__ float sk1[2048], sk2[2048], smd[2048], smu[2048], srs[2048];  // C <= 2048 (bn_vec_ok)
+  const bool zmask = zbeta != nullptr && act == ACT_RELU;  // act' from z (bn_shift), y not read
   __shared__ int last;
   const float invM = 1.f / M;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -505,7 +522,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
     pd[1] = *(const bf16x8*)(dy + i1 * 8);
     px[0] = *(const bf16x8*)(x + i0 * 8);
     px[1] = *(const bf16x8*)(x + i1 * 8);
-    if (act != ACT_NONE) {
+    if (act != ACT_NONE && !zmask) {
       py[0] = *(const bf16x8*)(y + i0 * 8);
       py[1] = *(const bf16x8*)(y + i1 * 8);
     }
@@ -534,7 +551,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
   if (threadIdx.x == 0) last = grid_arrive_last((unsigned*)(acc + (long)BN_NREP * 2 * C)) ? 1 : 0;
   const int CG = C >> 3;
   const int c0 = (int)(i0 % CG) * 8;
-  float k1[8], k2[8], md[8], mu[8], rs[8];
+  float k1[8], k2[8], md[8], mu[8], rs[8], zs[8], zh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     k1[j] = sk1[c0 + j];
@@ -542,6 +559,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
     md[j] = smd[c0 + j];
     mu[j] = smu[c0 + j];
     rs[j] = srs[c0 + j];
+    zs[j] = zh[j] = 0.f;
+    if (zmask) {
+      zs[j] = rs[j] * (gamma ? gamma[c0 + j] : 1.f);  // = k1, the forward's scale
+      zh[j] = bn_shift(zbeta[c0 + j], mu[j], zs[j]);
+    }
   }
   for (long i = i0; i < nch; i += 2 * stride) {
     const long ib = i + stride < nch ? i + stride : i;
@@ -550,7 +572,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
       pd[1] = *(const bf16x8*)(dy + ib * 8);
       px[0] = *(const bf16x8*)(x + i * 8);
       px[1] = *(const bf16x8*)(x + ib * 8);
-      if (act != ACT_NONE) {
+      if (act != ACT_NONE && !zmask) {
         py[0] = *(const bf16x8*)(y + i * 8);
         py[1] = *(const bf16x8*)(y + ib * 8);
       }
@@ -563,7 +585,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         d[j] = bf2f((uint16_t)pd[u][j]);
-        if (act != ACT_NONE) d[j] *= act_grad_from_out(bf2f((uint16_t)py[u][j]), act);
+        if (zmask) d[j] = fmaf(bf2f((uint16_t)px[u][j]), zs[j], zh[j]) > 0.f ? d[j] : 0.f;
+        else if (act != ACT_NONE) d[j] *= act_grad_from_out(bf2f((uint16_t)py[u][j]), act);
       }
       if (dres) st8f(dres + o, d);
 #pragma unroll
@@ -871,9 +894,11 @@ extern "C" int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, co
   return (int)hipGetLastError();
 }
 
+// zbeta: the BN's beta when its forward had no residual (ReLU: act' taken from x, see bn_shift); else null
 extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                             const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C,
-                            int act, void* dresidual, float* acc, hipStream_t st) {
+                            int act, void* dresidual, float* acc, const float* zbeta, hipStream_t st) {
+  if (hopsx_disabled("bn_zmask")) zbeta = nullptr;
   const long n = (long)M * C;
   if (acc && bn_vec_ok(C, {dy, x, y, dx, dresidual})) {  // acc: BN_NREP x 2C floats + arrival words, zero at rest
     int rpb;
@@ -883,11 +908,11 @@ extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const 
     const int defer = bn_defer(C);
     const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, defer};
     hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
-                       (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act, fin);
+                       (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act, fin, gamma, zbeta);
     if (defer) {
       hipLaunchKernelGGL(bn_bwd_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
                          (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, acc, (bf16_raw*)dx,
-                         (bf16_raw*)dresidual, n / 8, M, C, act, fin);
+                         (bf16_raw*)dresidual, n / 8, M, C, act, fin, zbeta);
       return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(bn_bwd_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,

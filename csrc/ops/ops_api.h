@@ -99,7 +99,7 @@ int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, const float* 
                        hipStream_t st);
 int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                  const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, int act,
-                 void* dresidual, float* acc, hipStream_t st);
+                 void* dresidual, float* acc, const float* zbeta, hipStream_t st);
 
 // ---- direct MFMA convs for short reductions (conv_mfma.hip) ----
 // ---- whole wide&deep training step in one workgroup (widedeep_step.hip) ----

@@ -922,7 +922,9 @@ class _BNFn(torch.autograd.Function):
         gg, gb = _wgrad_buf(gamma), _wgrad_buf(beta)
         ws = torch.empty(2 * C, device=dy.device)
         dres = torch.empty_like(dy2) if has_res else None
-        dx = K.bn_bwd(dy2, x2, y, gamma, mean, rstd, gg, gb, ws, act=act, dresidual=dres)
+        # no residual + ReLU: the backward recomputes the act' mask from x (no read of y; K.bn_bwd zbeta)
+        zb = beta.detach() if (beta is not None and not has_res and K.act_id(act) == 1) else None
+        dx = K.bn_bwd(dy2, x2, y, gamma, mean, rstd, gg, gb, ws, act=act, dresidual=dres, zbeta=zb)
         if has_res and ctx.gslot is not None:
             ctx.gslot["g"] = dres.view(shape)
             dres = None

@@ -607,13 +607,15 @@ def bn_fwd_infer(x2d, gamma, beta, rmean, rvar, eps, residual=None, act=0, out=N
     return out
 
 
-def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None, out=None):
+def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None, out=None, zbeta=None):
+    """``zbeta``: the BN's beta when its forward had NO residual: a ReLU's act' is then recomputed from
+    x (the forward's exact z * scale + shift > 0 test) instead of reading y (norm.hip bn_shift)."""
     M, C = x.shape
     if out is None:
         out = torch.empty_like(x)
     check(_C.ext().bn_bwd(ptr(dy), ptr(x), ptr(y), ptr(gamma), ptr(mean), ptr(rstd), ptr(out), ptr(dgamma),
                           ptr(dbeta), ptr(ws), M, C, act_id(act), ptr(dresidual), ptr(bn_acc(dy.device, C)),
-                          stream()), "bn_bwd")
+                          ptr(zbeta), stream()), "bn_bwd")
     return out
 
 

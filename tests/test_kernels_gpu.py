@@ -287,6 +287,36 @@ def test_batchnorm(M, C):
         assert K.bn_coop_timeouts(torch.device(dev), C) == 0
 
 
+@pytest.mark.parametrize("M,C", [(4096, 64), (2048, 256), (512, 2048)])
+def test_batchnorm_bwd_zmask(M, C):
+    """ReLU BN without residual: the backward's act' mask recomputed from x (zbeta, norm.hip bn_shift)
+    gives the y-read path's result, and matches PyTorch."""
+    torch.manual_seed(9)
+    x = bf(torch.randn(M, C, device=dev) * 2 + 0.3)
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    mean, rstd = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    y = K.bn_fwd_train(x, gamma, beta, mean, rstd, rm, rv, 0.1, 1e-5, act="relu")
+    dy = bf(torch.randn(M, C, device=dev))
+    outs = []
+    for zb in (None, beta):
+        dg, db, ws = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.empty(2 * C, device=dev)
+        dx = K.bn_bwd(dy, x, y, gamma, mean, rstd, dg, db, ws, act="relu", zbeta=zb)
+        outs.append((dx, dg, db))
+    (dx0, dg0, db0), (dx1, dg1, db1) = outs
+    close(dx1, dx0, rtol=1e-2, atol=1e-2)  # the same mask; the column sums differ by float-atomic order only
+    torch.testing.assert_close(dg1, dg0, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db1, db0, rtol=1e-5, atol=1e-4)
+    xr = x.float().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    yr = F.batch_norm(xr, None, None, gr, br, True, 0.1, 1e-5).relu()
+    gx, gg, gb = torch.autograd.grad(yr, (xr, gr, br), dy.float())
+    close(dx1, gx, rtol=3e-2, atol=3e-2)
+    close(dg1, gg, rtol=3e-2, atol=3e-2)
+    close(db1, gb, rtol=3e-2, atol=3e-2)
+
+
 def test_embedding_bag():
     torch.manual_seed(8)
     V, D = 1000, 24
