@@ -36,12 +36,14 @@ def is_rank_process() -> bool:
 
 
 def rank_exit(code: int = 0) -> None:
-    """End a rank of OUR self-launch (``launch``) after its work and process-group teardown: flush the
-    streams and ``os._exit``, skipping interpreter teardown — a native thread / static destructor
-    racing at exit once turned a finished rehearsal rank into an abort (``terminate called without
-    an active exception``, exit -6).  A no-op for ranks of other launchers (torchrun) and for
-    single-process runs, which exit normally."""
-    if os.environ.get("HOPSX_SELF_LAUNCHED") != "1" or os.environ.get("HOPSX_RANK_FAST_EXIT", "1") == "0":
+    """End a rank of OUR self-launch (``launch``).  By default the rank returns and exits through normal
+    interpreter teardown.  Round 3 once saw a finished rehearsal rank abort in teardown ("terminate
+    called without an active exception", exit -6) and made ``os._exit`` the default; the round-4
+    rehearsals at 2 and 4 ranks through normal teardown exit 0 with no abort
+    (profiles/r4_rehearsal_teardown.txt), so the fast exit is now opt-in: ``HOPSX_RANK_FAST_EXIT=1``
+    flushes the streams and ``os._exit``s.  A no-op for ranks of other launchers (torchrun) and for
+    single-process runs."""
+    if os.environ.get("HOPSX_SELF_LAUNCHED") != "1" or os.environ.get("HOPSX_RANK_FAST_EXIT", "0") != "1":
         return
     try:
         sys.stdout.flush()
