@@ -12,6 +12,10 @@
 #   tools/gpu.sh pmc     <tag>           PMC passes over bench.py (one counter group per run)
 #   tools/gpu.sh knobs   <tag> "ENV=.." ...   flagship bench.py --steps 20 per env setting ("" = default)
 #   tools/gpu.sh debug   <tag>           kernel suites on the debug build (_hopsx_ops_dbg, HOPSX_DEBUG=1)
+#   tools/gpu.sh ab      <tag> <reps> "<benchmarks/run.py args>" "ENV=.." ...   A/B of one benchmark config per
+#                                        env setting ("" = default), <reps> rounds -> <tag>/ab.txt (the round-4
+#                                        A/Bs in profiles/r4_*_ab.txt were run this way)
+#   tools/gpu.sh tables  <tag>           rocprofv3 kernel tables of ResNet-20 (in-process) and ResNet-50 B=64
 set -o pipefail
 job=${1:?job}; tag=${2:-$1}; shift 2
 out=gpurun_out/$tag
@@ -90,6 +94,15 @@ pmc)
 debug)
   export HOPSX_DEBUG=1; T=600 pyt $out/pytest_debug.log tests/test_debug_checks_gpu.py tests/test_kernels_gpu.py tests/test_kernels_v2_gpu.py \
     tests/test_dgrad_par_gpu.py tests/test_wgrad_glds_gpu.py tests/test_bnstats_gpu.py tests/test_models_gpu.py ;;
+ab)
+  reps=$1; args=$2; shift 2
+  for rep in $(seq $reps); do for s in "" "$@"; do
+    r=$(env $s timeout -k 10 300 python benchmarks/run.py $args 2>>$out/err.log | tail -1) || { echo "FAIL [$s]"; fail $out/err.log; }
+    echo "[$s] $args -> $(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" | tee -a $out/ab.txt
+  done; done ;;
+tables)
+  ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10 --inline
+  ktable p50 r50_b64_kernels.txt benchmarks/run.py resnet50 --batch 64 --steps 20 --warmup 5 ;;
 knobs)
   for s in "$@"; do
     r=$(env $s timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi 2>>$out/err.log) || { echo "FAIL [$s]"; fail $out/err.log; }
