@@ -131,7 +131,7 @@ class FusedWideDeepStep:
         self.loss = torch.zeros(1, device=dev)
         self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
         self.cursor = torch.zeros(1, device=dev, dtype=torch.int64)
-        # HOPSX_PHASE_DBG=1: the kernel stamps its phase boundaries here (tools/dbg_widedeep.py)
+        # HOPSX_PHASE_DBG=1: the kernel stamps its phase boundaries here (tools/taxi_phases.py)
         self.dbg = (torch.zeros(20, device=dev, dtype=torch.int64)
                     if os.environ.get("HOPSX_PHASE_DBG") == "1" else None)
 

@@ -128,7 +128,7 @@ def test_steps_per_execution_matches_single_step_replays():
     optimizer prefetches the next batch) trains like U one-step replays: same device cursor, the
     next batch staged in the static inputs, same loss, and a weight trajectory that differs from the
     one-step replays no more than two one-step runs differ from each other (split-K fp32 atomics
-    + bf16 shadow rounding make repeated runs diverge by a few %; tools/dbg_spe.py measures it)."""
+    + bf16 shadow rounding make repeated runs diverge by a few %; tools/spe_drift.py measures it)."""
     from hops_examples_amd import optim
     from hops_examples_amd.runtime.step import TrainStep
 

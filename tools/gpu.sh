@@ -52,7 +52,7 @@ persist)
   bench bench200 bench.py --steps 200 --warmup 20 --no-taxi ;;
 taxi)
   pyt $out/pytest.log tests/test_widedeep_fused_gpu.py tests/test_tfx_gpu.py
-  timeout -k 10 180 python -u tools/dbg_widedeep.py > $out/phases.txt 2>&1 || fail $out/phases.txt
+  timeout -k 10 180 python -u tools/taxi_phases.py > $out/phases.txt 2>&1 || fail $out/phases.txt
   cat $out/phases.txt
   bench taxi benchmarks/run.py taxi --steps 200 --warmup 20
   bench bench bench.py --steps 20 --warmup 5 ;;
