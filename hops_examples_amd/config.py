@@ -27,7 +27,10 @@ Performance / communication knobs read where they act:
   HOPSX_GEMM_SPLIT_CFG, HOPSX_GEMM_SPLIT_TARGET  split-K GEMM tile (1 = 64x64) / workgroups per CU
   HOPSX_WGRAD_MFMA_MAXK  largest KH*KW*C on the direct MFMA weight gradient (default 640)
   HOPSX_BNSTATS_MAX_1X1_FLOP  1x1 convs above this run as plain GEMMs (gg engine) + a BN statistics
-                        pass (default 1e8); HOPSX_PLAIN_MIN_PX fewest output pixels for that path (256)
+                        pass (default: no limit); HOPSX_PLAIN_MIN_PX fewest output pixels for that path (256)
+  HOPSX_WGRAD_MFMA_MAX_MK  short-conv weight gradients from this many pixel-columns on go to the
+                        LDS-DMA engine (default 32M)
+  HOPSX_BN_DEFER_MAXC, HOPSX_BN_MAXG, HOPSX_BN_APPLY_MAXG, HOPSX_BN_RPT  BN launch geometry (A/B only)
   HOPSX_BN_COOP         1 = one-launch BN backward with a grid barrier (measured slower; off)
   HOPSX_DGRAD_XCD       1 = XCD-aware block order in the direct MFMA dgrad (measured neutral; off)
   HOPSX_DISABLE         comma list of fast paths to turn off for A/B checks, e.g. bnstats, bn_defer,

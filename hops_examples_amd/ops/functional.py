@@ -749,11 +749,12 @@ def _bnstats_conv(g) -> bool:
     return C % 8 == 0
 
 
-# 1x1 routing: above 1e8 FLOP a 1x1 conv from 256 output pixels up leaves the stats-epilogue conv
-# kernel for the plain-GEMM path + a BN statistics pass (the thresholds were tuned in round 2 when that
-# path was hipBLASLt, profiles/r2s7_plain_1x1_ab.txt; since round 3 it is the hopsx gg engine, and the
-# library is only used under HOPSX_PLAIN_GEMM=blaslt)
-_BNSTATS_MAX_1X1_FLOP = float(os.environ.get("HOPSX_BNSTATS_MAX_1X1_FLOP", 1e8))
+# 1x1 routing: above HOPSX_BNSTATS_MAX_1X1_FLOP a 1x1 conv leaves the stats-epilogue conv kernel for the
+# plain-GEMM path + a BN statistics pass.  Round 2 set 1e8 when that path was hipBLASLt
+# (profiles/r2s7_plain_1x1_ab.txt); with both paths on the gg engine the stats epilogue wins at every
+# size (ResNet-50 B=8 / 64 / 256: +4.7 / +3-4 / +3.5 %, CIFAR flat; profiles/r4_launch_knobs_ab.txt),
+# so the default is no limit
+_BNSTATS_MAX_1X1_FLOP = float(os.environ.get("HOPSX_BNSTATS_MAX_1X1_FLOP", 1e30))
 # fewest output pixels for which a plain 1x1 conv takes the plain-GEMM path
 _PLAIN_MIN_PX = int(os.environ.get("HOPSX_PLAIN_MIN_PX", 256))
 
