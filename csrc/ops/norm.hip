@@ -743,6 +743,43 @@ static int bn_defer(int C) {
   return hopsx_disabled("bn_defer") || C > maxc ? 0 : 1;
 }
 
+// Wide channels: one small launch folds the replicas once (thread per channel; re-zeroes them) and the
+// plain apply kernels read the folded per-channel values, instead of every apply workgroup reading
+// BN_NREP x 2C floats.  A/B knob HOPSX_BN_FOLD_MINC (channels from which it applies; default off).
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_fold_k(float* __restrict__ acc, int M, int C, BnFin fin) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int r = 0; r < BN_NREP; ++r) {
+    s += acc[(long)r * 2 * C + c];
+    q += acc[(long)r * 2 * C + C + c];
+    acc[(long)r * 2 * C + c] = 0.f;
+    acc[(long)r * 2 * C + C + c] = 0.f;
+  }
+  if (MODE == 0) {  // as bn_apply_fin8_k
+    const float mu = s / M;
+    const float var = fmaxf(q / M - mu * mu, 0.f);
+    fin.mean_out[c] = mu;
+    fin.rstd_out[c] = rsqrtf(var + fin.eps);
+    if (fin.rmean) {
+      const float unb = M > 1 ? var * M / (M - 1) : var;
+      fin.rmean[c] = (1.f - fin.momentum) * fin.rmean[c] + fin.momentum * mu;
+      fin.rvar[c] = (1.f - fin.momentum) * fin.rvar[c] + fin.momentum * unb;
+    }
+  } else {  // as bn_bwd_apply_fin8_k's workgroup 0
+    fin.ws[c] = s;
+    fin.ws[C + c] = q;
+    if (fin.dbeta) fin.dbeta[c] += s;
+    if (fin.dgamma) fin.dgamma[c] += q;
+  }
+}
+static bool bn_fold_first(int C) {
+  static const long minc = hopsx_env_int("HOPSX_BN_FOLD_MINC", 1L << 30);
+  return C >= minc;
+}
+
 static int colred_grid(int M, int C, int& rpb) {
   const int RPI = 256 / (C / 8);
   // ~BN_UNR rows per thread: one trip of loads in flight per lane and >= 256 workgroups on the
@@ -873,6 +910,12 @@ extern "C" int hopsx_bn_fwd_apply_fin(const void* x, void* y, const float* gamma
   if (!acc || !bn_vec_ok(C, {x, y, residual})) return -2;
   const long n = (long)M * C;
   const BnFin fin{mean_out, rstd_out, running_mean, running_var, momentum, eps, nullptr, nullptr, nullptr};
+  if (bn_fold_first(C)) {
+    hipLaunchKernelGGL(bn_fold_k<0>, dim3((C + 255) / 256), dim3(256), 0, st, acc, M, C, fin);
+    hipLaunchKernelGGL(bn_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x, (bf16_raw*)y,
+                       gamma, beta, mean_out, rstd_out, 0, eps, n / 8, C, (const bf16_raw*)residual, act);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)x,
                      (bf16_raw*)y, gamma, beta, acc, n / 8, M, C, (const bf16_raw*)residual, act, fin);
   return (int)hipGetLastError();
@@ -909,6 +952,13 @@ extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const 
     const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, defer};
     hipLaunchKernelGGL(bn_colred8_k<1>, dim3(g), dim3(256), 0, st, (const bf16_raw*)dy, (const bf16_raw*)x,
                        (const bf16_raw*)y, mean, rstd, acc, M, C, rpb, act, fin, gamma, zbeta);
+    if (defer && bn_fold_first(C)) {  // (wide channels: y is read, the plain apply has no zmask)
+      hipLaunchKernelGGL(bn_fold_k<1>, dim3((C + 255) / 256), dim3(256), 0, st, acc, M, C, fin);
+      hipLaunchKernelGGL(bn_bwd_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
+                         (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, ws, (bf16_raw*)dx,
+                         (bf16_raw*)dresidual, n / 8, M, C, act);
+      return (int)hipGetLastError();
+    }
     if (defer) {
       hipLaunchKernelGGL(bn_bwd_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
                          (const bf16_raw*)x, (const bf16_raw*)y, gamma, mean, rstd, acc, (bf16_raw*)dx,
