@@ -100,9 +100,7 @@ def main():
 
     from hops_examples_amd import optim
     from hops_examples_amd.models.mnist import MirroredMnistCNN, param_count
-    from hops_examples_amd.parallel.dp import DataParallel
     from hops_examples_amd.runtime.arena import ParamArena
-    from hops_examples_amd.runtime.step import TrainStep
 
     B = a.batch_per_gpu
     model = MirroredMnistCNN().to(dev)
@@ -110,32 +108,16 @@ def main():
     ParamArena.from_module(model, dev)
     opt = optim.Adadelta(model, lr=1.0)
     from hops_examples_amd.runtime.persist import PersistentMnistStep
+    from hops_examples_amd.runtime.step import make_step
 
-    step, dp, persist_note = None, None, None
-    if not a.no_graph and dev.type == "cuda" and PersistentMnistStep.supported(model, opt, B, world):
-        # the whole step (fwd, loss, bwd, Adadelta) runs inside ONE persistent launch per 32 steps, fc1
-        # weights + optimizer state resident on chip (runtime/persist.py; HOPSX_PERSIST=0 off); with N
-        # ranks (one per GPU) the replicas exchange activations / gradients over xGMI inside the launch
-        from hops_examples_amd.parallel import oneshot
-
-        if world == 1 or oneshot._colocation(dev) == 1:
-            try:
-                eng = PersistentMnistStep(model, opt, steps_per_launch=32)
-            except RuntimeError as e:  # raised on every rank alike (the setup agrees collectively)
-                eng, persist_note = None, f"setup failed: {e}"[:300]
-            if eng is not None and (world == 1 or eng.selftest()):
-                step = eng
-            elif eng is not None:
-                eng.close()
-                persist_note = "selftest failed: fell back to TrainStep + DataParallel"
-        else:
-            persist_note = "ranks share a GPU: persistent step needs one GPU per rank"
-    if step is None and world > 1:
-        dp = DataParallel(model)
-    if step is None:
-        # 32 steps per replayed graph (Keras steps_per_execution; HOPSX_STEPS_PER_EXEC overrides): vs 8,
-        # +1.5 % at the driver's 20-step run and +1 % at 200 steps (profiles/r2s7_spe_ab.txt)
-        step = TrainStep(model, opt, "sparse_ce", dp=dp, graph=not a.no_graph, steps_per_execution=32)
+    # the framework's step factory (runtime/step.py make_step): the persistent whole-step kernel (fwd, loss,
+    # bwd, Adadelta of 32 steps in ONE launch; with N ranks, one per GPU, the replicas exchange inside
+    # the launch over xGMI after a collective selftest) whenever it applies, else TrainStep + DataParallel
+    # with 32 steps per replayed graph (Keras steps_per_execution; HOPSX_STEPS_PER_EXEC overrides)
+    step = make_step(model, opt, "sparse_ce", dp="auto", batch=B, graph=not a.no_graph and dev.type == "cuda",
+                     steps_per_execution=32)
+    dp = getattr(step, "dp", None) if step.kind == "trainstep" else None
+    persist_note = step.note
 
     # an MNIST-sized synthetic epoch (>= 60k images) resident in HBM, so the random
     # labels are not memorised within the timed window

@@ -392,12 +392,13 @@ class PqFile {
       throw std::runtime_error("cannot mmap " + path);
     }
     data_ = (const uint8_t*)p;
+    ::close(fd_);  // the mapping outlives the descriptor: no fd held per cached file
+    fd_ = -1;
     madvise(p, size_, MADV_SEQUENTIAL);
     try {
       meta_ = hopsx_io::parse_footer(data_, size_);
     } catch (...) {
       munmap(p, size_);
-      ::close(fd_);
       throw;
     }
   }
@@ -409,7 +410,7 @@ class PqFile {
     py::dict d;
     d["num_rows"] = meta_.num_rows;
     py::list cols, rgs;
-    for (const auto& c : meta_.columns) cols.append(py::make_tuple(c.name, c.type, c.repetition));
+    for (const auto& c : meta_.columns) cols.append(py::make_tuple(c.name, c.type, c.repetition, c.plain));
     for (const auto& rg : meta_.row_groups) {
       py::list ch;
       for (const auto& c : rg.chunks) ch.append(py::make_tuple(c.type, c.codec, c.num_values, c.total_compressed));

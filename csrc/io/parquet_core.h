@@ -144,6 +144,10 @@ struct PqColumn {  // a leaf of a flat schema
   std::string name;
   int type = -1;
   int repetition = 0;  // 0 required, 1 optional, 2 repeated
+  // false when a converted type / logical type changes what the physical values mean (DECIMAL scale,
+  // unsigned, DATE/TIME/TIMESTAMP units, strings...): the raw values are then not the column's values,
+  // and the reader must take the Arrow path.  Plain: no annotation, or a signed INT_8..INT_64.
+  bool plain = true;
 };
 struct PqChunk {
   int type = -1, codec = 0;
@@ -207,7 +211,31 @@ inline PqMeta parse_footer(const uint8_t* data, size_t size) {
           else if (fid == 3 && fty == 5) c.repetition = (int)t.zigzag();
           else if (fid == 4 && fty == 8) c.name = t.binary();
           else if (fid == 5 && fty == 5) nchild = (int)t.zigzag();
-          else t.skip(fty);
+          else if (fid == 6 && fty == 5) {  // converted_type: INT_8..INT_64 (15..18) keep plain values
+            const int64_t ct = t.zigzag();
+            if (ct < 15 || ct > 18) c.plain = false;
+          } else if (fid == 7 && fty == 5) {  // scale (DECIMAL)
+            if (t.zigzag() != 0) c.plain = false;
+          } else if (fid == 10 && fty == 12) {  // logicalType union: only a signed INTEGER stays plain
+            int lid, lty, llast = 0;
+            while (t.field(lid, lty, llast)) {
+              if (lid == 10 && lty == 12) {  // IntType {1: bitWidth i8, 2: isSigned bool}
+                int iid, ity, ilast = 0;
+                while (t.field(iid, ity, ilast)) {
+                  if (iid == 2 && (ity == 1 || ity == 2)) {
+                    if (ity == 2) c.plain = false;  // compact-protocol bool false
+                  } else {
+                    t.skip(ity);
+                  }
+                }
+              } else {
+                c.plain = false;
+                t.skip(lty);
+              }
+            }
+          } else {
+            t.skip(fty);
+          }
         }
         if (i == 0) continue;  // the root
         if (nchild > 0) throw Unsupported("parquet: nested schema");

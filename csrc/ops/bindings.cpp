@@ -19,6 +19,7 @@
 #endif
 
 #include "ops_api.h"
+extern "C" int hopsx_mnist_persist_occupancy(int dp);  // mnist_persist.hip
 
 namespace py = pybind11;
 extern "C" void hopsx_mlp_head_debug(void* p);
@@ -98,6 +99,10 @@ HX_PYMOD(HOPSX_MODNAME) {
   m.def("widedeep_slots", [](std::vector<long> iv, u out, long n) {
     return hopsx_widedeep_slots(iv.data(), (int)iv.size(), P<int>(out), n);
   });
+  m.def("taxi_step2_ok", [](std::vector<long> iv, long rows) { return hopsx_taxi_step2_ok(iv.data(), (int)iv.size(), rows); });
+  m.def("taxi_step2", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, long rows, u st) {
+    return hopsx_taxi_step2(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(), rows, S(st));
+  });
   m.def("widedeep_step_lds", [](std::vector<long> iv) { return hopsx_widedeep_step_lds(iv.data(), (int)iv.size()); });
   m.def("set_deterministic", [](int on) {
     int e = 0;
@@ -153,6 +158,7 @@ HX_PYMOD(HOPSX_MODNAME) {
     return hopsx_mnist_persist(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),
                                S(st));
   });
+  m.def("mnist_persist_occupancy", [](int dp) { return hopsx_mnist_persist_occupancy(dp); });
   m.def("mnist_persist_geom", []() {
     std::vector<long> g(14);
     hopsx_mnist_persist_geom(g.data());

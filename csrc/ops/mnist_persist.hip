@@ -1269,6 +1269,18 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   return (int)hipGetLastError();
 }
 
+// Workgroups of the persistent kernel one CU can hold at once (registers, LDS, wave slots): the
+// launch hands data between workgroups, so all GRID of them must be co-resident — the host requires
+// this >= 1 and CUs >= GRID before it picks the persistent engine (runtime/persist.py launchable()).
+extern "C" int hopsx_mnist_persist_occupancy(int dp) {
+  using namespace mnistp;
+  const void* fn = dp ? (const void*)mnist_persist_k<true> : (const void*)mnist_persist_k<false>;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess) return -1;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, LDS_BYTES) != hipSuccess) return -1;
+  return n;
+}
+
 // geometry for the host wrapper (buffer sizes) and the tests
 extern "C" void hopsx_mnist_persist_geom(long* g) {
   using namespace mnistp;

@@ -107,6 +107,10 @@ long hopsx_widedeep_step_lds(const long* iv, int ni);
 int hopsx_widedeep_slots(const long* iv, int ni, int* out, long n);
 int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
                         hipStream_t st);
+// ---- taxi step v2: bf16 MFMA, LDS-resident model + wide table, optimizer state in registers (taxi_step.hip) ----
+long hopsx_taxi_step2_ok(const long* iv, int ni, long rows);
+int hopsx_taxi_step2(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf, long rows,
+                     hipStream_t st);
 // ---- flagship MNIST CNN: nsteps whole training steps in one persistent launch (mnist_persist.hip) ----
 int hopsx_mnist_persist(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf,
                         hipStream_t st);

@@ -1,0 +1,990 @@
+// The Chicago-taxi wide & deep training step, v2: bf16 MFMA on an LDS-resident model, with the
+// wide table and every optimizer state on chip for the whole launch.
+//
+// Why v2 (widedeep_step.hip is v1, kept for data-parallel gradients and non-default shapes): v1 runs
+// the deep GEMMs on the f32-input MFMA, which on gfx950 issues at 1/16 of the bf16 rate, so one
+// CU needs ~9 us of pure MFMA time a step; its wide rows make four L2 round trips a step (gradient
+// atomics, a claiming exchange, the FTRL stores, the next step's gather); and its 1024-thread
+// layout spills ~600 B a lane.  The step is a dependent chain (4 forward layers, loss, 3 dX layers,
+// the W0 update, the next step) of ~2.7 M MACs: spreading it over CUs would put a cross-CU
+// hand-off (~1 us) on each link, so v2 keeps ONE workgroup and shortens the chain:
+//
+//   * mixed precision like the rest of the framework (bf16 operands, fp32 accumulation, fp32
+//     master weights, fp32 optimizer state): activations, gradients and weights are bf16 images
+//     in LDS, read as `v_mfma_f32_16x16x32_bf16` / `16x16x16` operands — row reads for the forward
+//     and dX products, `ds_read_b64_tr_b16` transposed reads for dX's W operand and both dW
+//     operands, so each tensor has ONE image.  Row strides are odd multiples of 16 elements: the
+//     transposed reads of 8 rows land on 8 distinct bank groups.
+//   * the forward pass and the dX chain of 16 examples depend only on those 16 rows: "tile waves"
+//     0..2 each own one 16-row batch tile and run its whole forward (4 layers, logits, loss, the
+//     logit gradient) with no barrier at all, then one dX layer per backward phase.  The weight
+//     gradients sum over all rows, so "gradient waves" 3..7 compute them one phase behind the G
+//     they read.  Five barriers a step: FWD, B3, B2, B1, B0.
+//   * every deep parameter (weight or bias) is owned by the gradient-wave lane whose dW
+//     accumulator holds its gradient (static tile -> wave map): fp32 weight + Adagrad state live in
+//     that lane's registers for the whole launch and the update happens as the gradient leaves the
+//     MFMA; the new bf16 image entry is written one phase later, once that layer's dX has read the
+//     old weight.  Biases ride the GEMMs as a ones column of A (db = that column of dW) but are
+//     applied in fp32 in the forward epilogue.  The logits layer (34 -> 1) is the dot product of
+//     the last hidden tile with w4 in the forward wave; its backward is G4 = g w4 relu'.
+//   * the wide (linear) part: the 6,287-row weight table lives in LDS (fp32), its FTRL state in the
+//     registers of the owning threads (row r -> thread r % 512).  Per step: the tile waves gather
+//     their examples' 13 rows (FWD), zero + mark the touched rows (B3) and add the example gradients
+//     with LDS float atomics (B2: each of a wave's instructions covers one column, whose id range no
+//     other column shares, so the summation order is fixed); owners apply FTRL to the marked rows
+//     and write the new weights back (B1, B0) — branch-free.
+//   * the launch loads / stores the deep parameters through an LDS staging copy of their arena span
+//     (coalesced), so per-launch overhead stays small next to the 20-32 steps it runs.
+//
+// Numerics = a bf16 layer-by-layer training step with fp32 accumulation (the layerwise TrainStep
+// path of this framework); tests/test_taxi_v2_gpu.py checks it against a bf16-emulating fp64
+// reference of the same step.  HOPSX_TAXI_KERNEL=v1 selects the fp32 v1 kernel.
+// Parity: the reference's TFX taxi trainer (README.md:99-112): DNNLinearCombinedClassifier,
+// hidden [100, 70, 48, 34], FTRL on the wide part, Adagrad on the deep part, batch 40.
+#include <cstdint>
+#include <type_traits>
+
+#include "common.h"
+#include "optim_core.h"
+
+namespace taxi2 {
+
+constexpr int NT = 512;  // 8 waves: 2 per SIMD, 256 registers a lane for the owned optimizer state
+constexpr int NW = NT / 64;
+constexpr int NTW = 3;   // tile waves (batch tiles of 16 rows)
+constexpr int BP = 48;   // batch rows (B <= 48)
+constexpr int NWIDE = 13;
+constexpr int WJ = 13;  // wide rows per thread
+constexpr int MAXROWS = NT * WJ;
+constexpr int D0 = 3, D1 = 100, D2 = 70, D3 = 48, D4 = 34;  // dense input + hidden widths (logits: 1)
+
+constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
+constexpr int pad32(int x) { return (x + 31) & ~31; }
+
+// ---- LDS images (bf16 element offsets); strides are odd multiples of 16 elements
+constexpr int SA0 = 16, SA1 = 144, SA2 = 112, SA3 = 80, SA4 = 48, SG = 112;
+constexpr int OFF_A0 = 0;                        // [2][BP][SA0] (double-buffered input)
+constexpr int OFF_A1 = OFF_A0 + 2 * BP * SA0;    // [BP][SA1]
+constexpr int OFF_A2 = OFF_A1 + BP * SA1;
+constexpr int OFF_A3 = OFF_A2 + BP * SA2;
+constexpr int OFF_A4 = OFF_A3 + BP * SA3;
+constexpr int OFF_GX = OFF_A4 + BP * SA4;        // G4, G2
+constexpr int OFF_GY = OFF_GX + BP * SG;         // G3, G1
+constexpr int W0R = 16 * cdiv(D1, 16);           // W0 rows (no dX for layer 0)
+constexpr int W1R = pad32(D2), W2R = pad32(D3), W3R = pad32(D4);  // K of dX = rows
+constexpr int OFF_W0 = OFF_GY + BP * SG;
+constexpr int OFF_W1 = OFF_W0 + W0R * SA0;
+constexpr int OFF_W2 = OFF_W1 + W1R * SA1;
+constexpr int OFF_W3 = OFF_W2 + W2R * SA2;
+constexpr int BF_END = OFF_W3 + W3R * SA3;
+constexpr int BF_BYTES = BF_END * 2;
+// ---- fp32 region (float offsets from BF_BYTES)
+constexpr int F_B0 = 0, F_B1 = F_B0 + 16 * cdiv(D1, 16), F_B2 = F_B1 + 16 * cdiv(D2, 16),
+              F_B3 = F_B2 + 16 * cdiv(D3, 16), F_W4 = F_B3 + 16 * cdiv(D4, 16), F_MISC = F_W4 + 48,
+              F_RED = F_MISC + 16, F_DW4 = F_RED + 16, F_WTAB = F_DW4 + 3 * 48, F_BITS = F_WTAB + MAXROWS, F_END = F_BITS + MAXROWS / 32;
+constexpr int LDS_BYTES = BF_BYTES + F_END * 4;
+constexpr int STAGE_MAX = LDS_BYTES / 4;  // floats of the deep arena span staged through LDS
+static_assert(BF_BYTES % 16 == 0 && LDS_BYTES <= 160 * 1024, "taxi2 LDS budget");
+
+struct Args {
+  float* master;
+  bf16_raw* shadow;
+  float* ada_s;
+  float* ftrl_z;
+  float* ftrl_n;
+  const float* dense;     // [nbatch][B][3]
+  const long long* cat;   // [nbatch][B][13] global one-hot ids
+  const float* label;     // [nbatch][B]
+  long long* cursor;      // batch of the first step (advanced by nsteps), or null
+  float* loss;
+  int* correct;
+  float* step_ada;
+  float* step_ftrl;
+  unsigned long long* rng;
+  unsigned long long* dbg;  // phase stamps or null
+  float2* zn;               // [rows] FTRL (z, n) interleaved: kernel-private copy, one access per touched row
+  int B, nbatch, nsteps, rows, rng_bumps;
+  int ada_rsq;  // Adagrad as w -= lr g rsq(s): wd == 0 and eps below fp32 resolution of sqrt(s) (host-checked)
+  long wide_off, deep_lo, deep_hi;
+  long woff[5], boff[5];
+  int rw[5], rb[5];  // woff / boff relative to deep_lo (staging-copy offsets)
+  OptHP ada, ftrl;
+};
+
+typedef __attribute__((address_space(3))) bf16x4* lds4_t;
+
+__device__ __forceinline__ bf16_raw f2b(float f) { return __builtin_bit_cast(bf16_raw, (__bf16)f); }
+__device__ __forceinline__ float b2f(short v) { return __uint_as_float(((uint32_t)(uint16_t)v) << 16); }
+__device__ __forceinline__ float rbf(float f) { return b2f((short)f2b(f)); }  // round to bf16
+__device__ __forceinline__ f32x4 mma32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma16(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// operand with K along the row: lane l takes row r0 + (l & 15), 8 (or 4) consecutive k
+__device__ __forceinline__ bf16x8 rd8(const bf16_raw* img, int S, int r0, int k0, int lane) {
+  return *(const bf16x8*)(img + (r0 + (lane & 15)) * S + k0 + 8 * (lane >> 4));
+}
+__device__ __forceinline__ bf16x4 rd4(const bf16_raw* img, int S, int r0, int k0, int lane) {
+  return *(const bf16x4*)(img + (r0 + (lane & 15)) * S + k0 + 4 * (lane >> 4));
+}
+// operand with K down the rows (T10 transposed read): lane l gets column c0 + (l & 15) of rows
+// k0 + 4 (l >> 4) + j (x16) or k0 + 8 (l >> 4) + j (x32).  EXEC must be full: never call under a
+// lane-dependent branch.
+__device__ __forceinline__ bf16x4 tr4(const bf16_raw* img, int S, int k0, int c0, int lane) {
+  const int i = lane & 15;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)(img + (k0 + 4 * (lane >> 4) + (i >> 2)) * S + c0 + 4 * (i & 3)));
+}
+__device__ __forceinline__ bf16x8 tr8(const bf16_raw* img, int S, int k0, int c0, int lane) {
+  const int i = lane & 15;
+  const bf16_raw* p = img + (k0 + 8 * (lane >> 4) + (i >> 2)) * S + c0 + 4 * (i & 3);
+  const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)p);
+  const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)(p + 4 * S));
+  return (bf16x8){v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+}
+__device__ __forceinline__ void st4(bf16_raw* p, float a, float b, float c, float d) {
+  *(bf16x4*)p = (bf16x4){(short)f2b(a), (short)f2b(b), (short)f2b(c), (short)f2b(d)};
+}
+__device__ __forceinline__ float sel(bool c, float a, float b) { return c ? a : b; }
+
+// Workgroup barrier that waits only for LDS traffic: the next batch's loads stay in flight across
+// it (a __syncthreads() would drain them at every phase)
+__device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// keeps the compiler from moving LDS accesses across it (this wave's own write -> read order)
+__device__ __forceinline__ void fence_c() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ float adagrad(float w, float g, float& s, const OptHP& h) {
+  g = fmaf(h.wd, w, g);
+  s = fmaf(g, g, s);
+  return w - h.lr * g * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(s) + h.a);
+}
+// the same update when wd == 0 and eps is below the fp32 resolution of sqrt(s) (the accumulator never
+// drops below its initial value): one transcendental instead of two, 5 VALU an element
+__device__ __forceinline__ float adagrad_rsq(float w, float g, float& s, float nlr) {
+  s = fmaf(g, g, s);
+  return fmaf(nlr * g, __builtin_amdgcn_rsqf(s), w);
+}
+
+// An opaque copy of x: the LDS addresses of a phase's tasks derive from it, so the compiler recomputes
+// them in the phase instead of hoisting ~200 loop-invariant addresses out of the step loop (which
+// spilled them to scratch)
+__device__ __forceinline__ int fresh(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ int fresh_s(int x) {  // (the same for wave-uniform values, in SGPRs)
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+__device__ __forceinline__ void stamp(const Args& a, int slot) {
+  if (a.dbg && threadIdx.x == 0) a.dbg[slot] = wall_clock64();
+}
+// (HOPSX_PHASE_DBG) a stamp from lane 0 of wave w: tile wave 0 / gradient wave 3 inside a phase
+__device__ __forceinline__ void stampw(const Args& a, int slot, int w) {
+  if (a.dbg && threadIdx.x == 64 * w) a.dbg[slot] = wall_clock64();
+}
+
+// ------------------------------------------------------------------------------- layer geometry
+// layer l: IN -> OUT, A_l image (OFFA, SA), W_l image (OFFW, stride SA), output image (OFFZ, SZ),
+// fp32 bias at FB.  KF = forward K (x16 for layer 0).
+template <int L_, int IN_, int OUT_, int OFFA_, int SA_, int OFFW_, int OFFZ_, int SZ_, int FB_>
+struct Layer {
+  static constexpr int L = L_, IN = IN_, OUT = OUT_, OFFA = OFFA_, SA = SA_, OFFW = OFFW_, OFFZ = OFFZ_,
+                       SZ = SZ_, FB = FB_;
+  static constexpr bool X16 = IN_ < 16;
+  static constexpr int KF = X16 ? 16 : pad32(IN_ + 1);
+  static constexpr int OT = cdiv(OUT_, 16);       // output-feature tiles
+  static constexpr int ITW = cdiv(IN_ + 1, 16);   // dW input tiles (bias column included)
+  static constexpr int ITX = cdiv(IN_, 16);       // dX input tiles
+  static constexpr int KX = pad32(OUT_);          // dX K (= W image rows)
+  static constexpr int NDW = OT * ITW;
+  static_assert(KF <= SA_ && 16 * ITW <= SA_, "layer image width");
+};
+using L0 = Layer<0, D0, D1, OFF_A0, SA0, OFF_W0, OFF_A1, SA1, F_B0>;
+using L1 = Layer<1, D1, D2, OFF_A1, SA1, OFF_W1, OFF_A2, SA2, F_B1>;
+using L2 = Layer<2, D2, D3, OFF_A2, SA2, OFF_W2, OFF_A3, SA3, F_B2>;
+using L3 = Layer<3, D3, D4, OFF_A3, SA3, OFF_W3, OFF_A4, SA4, F_B3>;
+static_assert(L1::KX <= W1R && L2::KX <= W2R && L3::KX <= W3R && 16 * L0::OT <= W0R, "W image rows");
+constexpr int NDW4 = cdiv(D4 + 1, 16);  // logits layer dW tiles (output column 0)
+
+// dW tiles -> waves: tile t of a phase goes to the wave w with (w + 5) % 8 == t % 8, round t / 8, so the
+// tile waves (busy with dX) get the lighter share of each phase; dW0 (7 tiles): waves 0..6, one each.
+// The logits layer's 35 gradients are VALU row sums in the tile waves (FWD), owned by wave 7's lanes.
+constexpr int R3 = cdiv(L3::NDW, NW), R2 = cdiv(L2::NDW, NW), R1 = cdiv(L1::NDW, NW);
+static_assert(L0::NDW < NW && NW == 8, "tile map");
+constexpr int S3 = 0, S2 = S3 + R3, S1 = S2 + R2, S0 = S1 + R1, NSLOT = S0 + 1;
+__device__ __forceinline__ int perm8(int wave) { return (wave + 5) & 7; }
+
+struct Own {
+  float w[NSLOT][4], s[NSLOT][4];
+  float w4, s4;  // (wave 7, lanes 0..34) logits weight / bias and its Adagrad state
+};
+
+// dW tile t of layer Ly: i-tile t / OT, o-tile t % OT (element r: i = i0 + 4 (lane >> 4) + r, o = o0 + lane & 15)
+template <class Ly>
+__device__ __forceinline__ void dw_coords(int t, int lane, int& i, int& o) {
+  i = (t / Ly::OT) * 16 + 4 * (lane >> 4);
+  o = (t % Ly::OT) * 16 + (lane & 15);
+}
+
+// staging-copy offset (arena index - deep_lo) of element (i, o) of layer Ly's dW tile, or -1 (padding)
+template <class Ly, class AR>
+__device__ __forceinline__ int pidx(const AR& a, int i, int o) {
+  if (o >= Ly::OUT || i > Ly::IN) return -1;
+  return i == Ly::IN ? a.rb[Ly::L] + o : a.rw[Ly::L] + o * Ly::IN + i;
+}
+template <class AR>
+__device__ __forceinline__ int pidx4(const AR& a, int i, int o) {  // logits layer
+  if (o != 0 || i > D4) return -1;
+  return i == D4 ? a.rb[4] : a.rw[4] + i;
+}
+
+// owned values <-> the LDS staging copy of the deep arena span (write: w or s of the slot)
+template <class Ly, class AR>
+__device__ __forceinline__ void own_get(const AR& a, const float* stage, int t, int lane, float (&v)[4]) {
+  int i, o;
+  dw_coords<Ly>(t, lane, i, o);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int x = pidx<Ly, AR>(a, i + r, o);
+    v[r] = x >= 0 ? stage[x] : 0.f;
+  }
+}
+template <class Ly, class AR>
+__device__ __forceinline__ void own_put(const AR& a, float* stage, int t, int lane, const float (&v)[4]) {
+  int i, o;
+  dw_coords<Ly>(t, lane, i, o);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int x = pidx<Ly, AR>(a, i + r, o);
+    if (x >= 0) stage[x] = v[r];
+  }
+}
+// put owned elements into the bf16 W image (4 consecutive i of row o) and the fp32 bias array
+template <class Ly>
+__device__ __forceinline__ void put_w(bf16_raw* Lb, float* LF, int t, int lane, const float (&w)[4]) {
+  int i, o;
+  dw_coords<Ly>(t, lane, i, o);
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = sel((o < Ly::OUT) & (i + r < Ly::IN), w[r], 0.f);
+  st4(Lb + Ly::OFFW + o * Ly::SA + i, v[0], v[1], v[2], v[3]);
+  // the bias element (i + r == IN) can only be register IN % 4 (i is a multiple of 4)
+  constexpr int rb = Ly::IN % 4;
+  if ((o < Ly::OUT) & (i + rb == Ly::IN)) LF[Ly::FB + o] = w[rb];
+}
+// ---- dW: the R rounds of this wave in a phase, tiles t = p + 8 j (p = perm8(wave)), x16 MFMAs over the 48
+// batch rows, Adagrad on the owned elements as the gradient leaves the accumulator (branch-free; a round
+// past the layer's tile count runs a clamped dummy tile whose update is discarded).  Operands are
+// double-buffered: the next round's transposed reads are in flight during this round's MFMAs (fence_c
+// keeps the compiler from hoisting every round's reads at once, which would not fit the registers).
+struct DwOps {
+  bf16x4 a[BP / 16], g[BP / 16];
+};
+template <class Ly>
+__device__ __forceinline__ DwOps dw_load(const bf16_raw* Aimg, const bf16_raw* G, int t, int lane) {
+  t = t < Ly::NDW ? t : Ly::NDW - 1;
+  const int i0 = (t / Ly::OT) * 16, o0 = (t % Ly::OT) * 16;
+  DwOps d;
+#pragma unroll
+  for (int k = 0; k < BP / 16; ++k) {
+    d.a[k] = tr4(Aimg, Ly::SA, 16 * k, i0, lane);
+    d.g[k] = tr4(G, SG, 16 * k, o0, lane);
+  }
+  return d;
+}
+template <class Ly, int R, bool RSQ>
+__device__ __forceinline__ void dw_seq(const bf16_raw* Aimg, const bf16_raw* G, int p, int lane, float (*w)[4],
+                                       float (*s)[4], const OptHP& h) {
+  // padding elements (o >= OUT, i > IN) and a dummy round update registers nothing ever reads (put_w and
+  // the write-back skip them), so no validity selects here
+  DwOps cur = dw_load<Ly>(Aimg, G, p, lane);
+  const float nlr = -h.lr;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int t = p + 8 * j;
+    DwOps nxt = cur;
+    if (j + 1 < R) nxt = dw_load<Ly>(Aimg, G, t + 8, lane);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < BP / 16; ++k) acc = mma16(cur.a[k], cur.g[k], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (RSQ) w[j][r] = adagrad_rsq(w[j][r], acc[r] * h.gscale, s[j][r], nlr);
+      else w[j][r] = adagrad(w[j][r], acc[r] * h.gscale, s[j][r], h);
+    }
+    cur = nxt;
+    fence_c();
+  }
+}
+// the R rounds' images (a uniform branch per round: an out-of-range round owns nothing)
+template <class Ly, int R>
+__device__ __forceinline__ void put_seq(bf16_raw* Lb, float* LF, int p, int lane, float (*w)[4]) {
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+    if (p + 8 * j < Ly::NDW) put_w<Ly>(Lb, LF, p + 8 * j, lane, w[j]);
+}
+
+// ---- dX for batch tile b0 of layer Ly: dX^T[i][b] = sum_o W[o][i] G[b][o]; G_l[b][i] = dX relu'(A_l[b][i])
+template <class Ly>
+__device__ __forceinline__ void dx_tile(bf16_raw* Lb, const bf16_raw* G, bf16_raw* Gout, int b0, int lane) {
+  constexpr int NK = Ly::KX / 32;
+  bf16x8 gop[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) gop[k] = rd8(G, SG, b0, 32 * k, lane);
+  const int b = b0 + (lane & 15);
+  bf16x8 cur[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) cur[k] = tr8(Lb + Ly::OFFW, Ly::SA, 32 * k, 0, lane);
+#pragma unroll
+  for (int it = 0; it < Ly::ITX; ++it) {
+    bf16x8 nxt[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) nxt[k] = it + 1 < Ly::ITX ? tr8(Lb + Ly::OFFW, Ly::SA, 32 * k, 16 * (it + 1), lane) : cur[k];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NK; ++k) acc = mma32(cur[k], gop[k], acc);
+    const int i = 16 * it + 4 * (lane >> 4);
+    const bf16x4 av = *(const bf16x4*)(Lb + Ly::OFFA + b * Ly::SA + i);
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = sel(b2f(av[r]) > 0.f, acc[r], 0.f);  // (cols >= IN: A is 0 or the
+    // ones column, whose dX is 0 since W's column IN is 0 in the image)
+    st4(Gout + b * SG + i, v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) cur[k] = nxt[k];
+    fence_c();
+  }
+}
+
+// ---- forward of layer Ly for batch tile b0: Z^T[o][b] = sum_k W[o][k] A[b][k] + bias[o], relu ->
+// A_{l+1} rows b0...  No masks: W rows >= OUT are 0 and the fp32 bias array holds 1 at OUT (the ones
+// column the next layer's db needs) and -1e30 beyond (relu -> 0); rows >= B hold finite garbage that
+// only ever meets zero gradient rows (g_b = 0 for b >= B).  KEEP: also returns the activations.
+template <class Ly, bool KEEP>
+__device__ __forceinline__ void fwd_tile(bf16_raw* Lb, const float* LF, const bf16_raw* Ain, int b0, int lane, int B,
+                                         float (*out)[4]) {
+  constexpr int NK = Ly::X16 ? 1 : Ly::KF / 32;
+  const int b = b0 + (lane & 15);
+  if constexpr (Ly::X16) {
+    const bf16x4 aop = rd4(Ain, Ly::SA, b0, 0, lane);
+    bf16x4 w[Ly::OT];
+#pragma unroll
+    for (int ot = 0; ot < Ly::OT; ++ot) w[ot] = rd4(Lb + Ly::OFFW, Ly::SA, 16 * ot, 0, lane);
+#pragma unroll
+    for (int ot = 0; ot < Ly::OT; ++ot) {
+      const f32x4 acc = mma16(w[ot], aop, (f32x4){0.f, 0.f, 0.f, 0.f});
+      const int o = 16 * ot + 4 * (lane >> 4);
+      const f32x4 bias = *(const f32x4*)(LF + Ly::FB + o);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[r] + bias[r], 0.f);
+      st4(Lb + Ly::OFFZ + b * Ly::SZ + o, v[0], v[1], v[2], v[3]);
+    }
+  } else {
+    bf16x8 aop[NK], cur[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      aop[k] = rd8(Ain, Ly::SA, b0, 32 * k, lane);
+      cur[k] = rd8(Lb + Ly::OFFW, Ly::SA, 0, 32 * k, lane);
+    }
+#pragma unroll
+    for (int ot = 0; ot < Ly::OT; ++ot) {
+      bf16x8 nxt[NK];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) nxt[k] = ot + 1 < Ly::OT ? rd8(Lb + Ly::OFFW, Ly::SA, 16 * (ot + 1), 32 * k, lane) : cur[k];
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NK; ++k) acc = mma32(cur[k], aop[k], acc);
+      const int o = 16 * ot + 4 * (lane >> 4);
+      const f32x4 bias = *(const f32x4*)(LF + Ly::FB + o);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[r] + bias[r], 0.f);
+      st4(Lb + Ly::OFFZ + b * Ly::SZ + o, v[0], v[1], v[2], v[3]);
+      if constexpr (KEEP) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[ot][r] = v[r];
+      }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) cur[k] = nxt[k];
+      fence_c();
+    }
+  }
+}
+
+// the kernel's arguments read where used, through an opaque copy of the kernarg pointer (held in
+// SGPRs across the step loop they spilled).  The pointer stays in the constant address space: the
+// reads are scalar loads (a generic pointer made them flat vector loads, each a memory round trip
+// that also waited for every outstanding store)
+typedef const __attribute__((address_space(4))) Args* kargs_t;
+__device__ __forceinline__ kargs_t cold_p() {
+  kargs_t p = (kargs_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+#define COLD (*cold_p())
+
+template <bool GET, bool PASS_S>
+__device__ __forceinline__ void own_stage(float* stage, Own& own, int wave, int lane) {
+  const auto& C = COLD;
+  auto& v = PASS_S ? own.s : own.w;
+  const int p = perm8(wave);
+#pragma unroll
+  for (int j = 0; j < R3; ++j)
+    if (p + 8 * j < L3::NDW) {
+      if (GET) own_get<L3>(C, stage, p + 8 * j, lane, v[S3 + j]);
+      else own_put<L3>(C, stage, p + 8 * j, lane, v[S3 + j]);
+    }
+#pragma unroll
+  for (int j = 0; j < R2; ++j)
+    if (p + 8 * j < L2::NDW) {
+      if (GET) own_get<L2>(C, stage, p + 8 * j, lane, v[S2 + j]);
+      else own_put<L2>(C, stage, p + 8 * j, lane, v[S2 + j]);
+    }
+#pragma unroll
+  for (int j = 0; j < R1; ++j)
+    if (p + 8 * j < L1::NDW) {
+      if (GET) own_get<L1>(C, stage, p + 8 * j, lane, v[S1 + j]);
+      else own_put<L1>(C, stage, p + 8 * j, lane, v[S1 + j]);
+    }
+  if (wave < L0::NDW) {
+    if (GET) own_get<L0>(C, stage, wave, lane, v[S0]);
+    else own_put<L0>(C, stage, wave, lane, v[S0]);
+  }
+  if (wave == NW - 1 && lane <= D4) {  // logits layer: lane i < 34 weight i, lane 34 the bias
+    const int x = lane < D4 ? C.rw[4] + lane : C.rb[4];
+    float& o = PASS_S ? own.s4 : own.w4;
+    if (GET) o = stage[x];
+    else stage[x] = o;
+  }
+}
+
+// dst[0..n) = src[0..n) into LDS, 8 loads of a thread in flight at once (a plain strided loop waits
+// for each load before the next: ~25 round trips for the deep span); 16-byte loads when src is aligned
+__device__ __forceinline__ void gather_in(float* dst, const float* src, int n, int tid) {
+  constexpr int PER = 8;
+  if (((uintptr_t)src & 15) == 0) {
+    const int n4 = n >> 2;
+    for (int base = 0; base < n4; base += NT * PER) {
+      f32x4 v[PER];  // (native vectors: an array of HIP's float4 struct stays in scratch)
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int e = base + tid + NT * k;
+        v[k] = ((const f32x4*)src)[e < n4 ? e : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (base + tid + NT * k < n4) ((f32x4*)dst)[base + tid + NT * k] = v[k];
+    }
+    for (int e = 4 * n4 + tid; e < n; e += NT) dst[e] = src[e];
+    return;
+  }
+  for (int base = 0; base < n; base += NT * PER) {
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = base + tid + NT * k;
+      v[k] = e < n ? src[e] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (base + tid + NT * k < n) dst[base + tid + NT * k] = v[k];
+  }
+}
+constexpr unsigned SENT = 0xFFFFFFFFu;  // staging sentinel (a NaN no owner writes): "not owned, keep"
+
+template <bool RSQ>
+__global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  bf16_raw* const Lb = (bf16_raw*)lds;
+  float* const LF = (float*)(lds + BF_BYTES);
+  float* const stage = (float*)lds;
+  unsigned* const bits = (unsigned*)(LF + F_BITS);
+  const int tid = threadIdx.x;
+  int lane = tid & 63;
+  const int wave0 = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int wave = wave0, b0 = 16 * wave0;  // b0: (tile waves) batch tile
+  const bool tw = wave0 < NTW;  // tile wave
+  const int B = A.B;
+  const OptHP ha = A.ada;
+  stamp(A, 0);
+
+  // ------------------------------------------------------------------ launch prologue
+  Own own;
+  {
+    const auto& C = COLD;
+    const int span = (int)(C.deep_hi - C.deep_lo);
+    // deep parameters and their Adagrad state, each through a coalesced LDS staging copy of the span
+    gather_in(stage, C.master + C.deep_lo, span, tid);
+    __syncthreads();
+    own_stage<true, false>(stage, own, wave, lane);
+    __syncthreads();
+    gather_in(stage, C.ada_s + C.deep_lo, span, tid);
+    __syncthreads();
+    own_stage<true, true>(stage, own, wave, lane);
+    __syncthreads();
+    // the kernel-private (z, n) copy of the FTRL state (leaders read / write one float2 per row a step);
+    // 8 rows of a thread in flight at once
+    for (int base = 0; base < C.rows; base += NT * 8) {
+      float zv[8], nv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = base + tid + NT * k, rc = r < C.rows ? r : 0;
+        zv[k] = C.ftrl_z[C.wide_off + rc];
+        nv[k] = C.ftrl_n[C.wide_off + rc];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (base + tid + NT * k < C.rows) C.zn[base + tid + NT * k] = make_float2(zv[k], nv[k]);
+    }
+  }
+  // the batch (tile waves): lane -> example b = b0 + (lane & 15), columns c = (lane >> 4) + 4 m
+  const int eb = b0 + (lane & 15), eg = lane >> 4;
+  const bool evb = tw && eb < B;
+  const long long bi0 = A.cursor ? A.cursor[0] : 0;
+  int cid[4], nid[4];
+  float yv = 0.f, ny = 0.f, nd = 0.f;
+  int bnx = (int)(bi0 % A.nbatch);  // the batch the "next" registers hold (advanced by fetch, no modulo)
+  auto fetch = [&](bool advance) {  // the next batch -> the "next" registers
+    const auto& C = COLD;
+    if (advance) bnx = bnx + 1 == C.nbatch ? 0 : bnx + 1;
+    const long long bi = bnx;
+    const long long* cb = C.cat + (bi * B + (evb ? eb : 0)) * NWIDE;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) nid[m] = evb && eg + 4 * m < NWIDE ? (int)cb[eg + 4 * m] : -1;
+    ny = evb ? C.label[bi * B + eb] : 0.f;
+    nd = evb && eg < D0 ? C.dense[(bi * B + eb) * D0 + eg] : 0.f;
+  };
+  if (tw) {
+    fetch(false);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) cid[m] = nid[m];
+    yv = ny;
+  }
+  {
+    uint4* z = (uint4*)lds;
+    for (int e = tid; e < LDS_BYTES / 16; e += NT) z[e] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  // the input's ones column (db0); the fp32 bias arrays' constant tail: 1 at OUT makes the forward
+  // epilogue write the next layer's ones column, -1e30 beyond makes it write zeros
+  if (tid < B) {
+    Lb[OFF_A0 + tid * SA0 + D0] = f2b(1.f);
+    Lb[OFF_A0 + BP * SA0 + tid * SA0 + D0] = f2b(1.f);
+  }
+  if (tid < 16) {
+    if (D1 + tid < 16 * L0::OT) LF[F_B0 + D1 + tid] = tid ? -1e30f : 1.f;
+    if (D2 + tid < 16 * L1::OT) LF[F_B1 + D2 + tid] = tid ? -1e30f : 1.f;
+    if (D3 + tid < 16 * L2::OT) LF[F_B2 + D3 + tid] = tid ? -1e30f : 1.f;
+    if (D4 + tid < 16 * L3::OT) LF[F_B3 + D4 + tid] = tid ? -1e30f : 1.f;
+  }
+  // OUT a multiple of 16: no epilogue tile reaches the ones column, which is then constant
+  if (tid < B) {
+    if (D1 % 16 == 0) Lb[OFF_A1 + tid * SA1 + D1] = f2b(1.f);
+    if (D2 % 16 == 0) Lb[OFF_A2 + tid * SA2 + D2] = f2b(1.f);
+    if (D3 % 16 == 0) Lb[OFF_A3 + tid * SA3 + D3] = f2b(1.f);
+    if (D4 % 16 == 0) Lb[OFF_A4 + tid * SA4 + D4] = f2b(1.f);
+  }
+  if (evb && eg < D0) Lb[OFF_A0 + eb * SA0 + eg] = f2b(nd);
+  {
+    const int p = perm8(wave);
+    put_seq<L3, R3>(Lb, LF, p, lane, own.w + S3);
+    put_seq<L2, R2>(Lb, LF, p, lane, own.w + S2);
+    put_seq<L1, R1>(Lb, LF, p, lane, own.w + S1);
+    if (wave == NW - 1 && lane <= D4) LF[lane < D4 ? F_W4 + lane : F_MISC] = own.w4;
+  }
+  if (wave < L0::NDW) put_w<L0>(Lb, LF, wave, lane, own.w[S0]);
+  gather_in(LF + F_WTAB, A.master + A.wide_off, A.rows, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the zn copy has landed before any leader reads it)
+  __syncthreads();
+  stamp(A, 1);
+
+  float lsum = 0.f, csum = 0.f, gb = 0.f;
+  const float invB = 1.f / (float)B;
+  float wv[4], zl[4], nl[4];  // (tile waves) gathered wide weights; FTRL state of the rows this lane leads
+  unsigned lead = 0u;
+  for (int step = 0; step < A.nsteps; ++step) {
+    const bool last = step + 1 == A.nsteps;
+    const bf16_raw* A0 = Lb + OFF_A0 + (step & 1) * BP * SA0;
+    if (last) stamp(A, 7);
+    // ============================================================ FWD: tile waves, no barrier inside
+    lane = fresh(tid & 63);
+    wave = fresh_s(wave0);
+    b0 = 16 * wave;
+    if (tw) {
+      // this lane's wide rows (kept: the FTRL of the rows it leads needs the old weight), their sum
+      // folded over the 4 lane groups in a fixed order
+      float ws = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        wv[m] = cid[m] >= 0 ? LF[F_WTAB + cid[m]] : 0.f;
+        ws += wv[m];
+      }
+      fwd_tile<L0, false>(Lb, LF, A0, b0, lane, B, nullptr);
+      fence_c();
+      if (last) stampw(A, 8, 0);
+      fwd_tile<L1, false>(Lb, LF, Lb + L1::OFFA, b0, lane, B, nullptr);
+      fence_c();
+      if (last) stampw(A, 9, 0);
+      fwd_tile<L2, false>(Lb, LF, Lb + L2::OFFA, b0, lane, B, nullptr);
+      fence_c();
+      if (last) stampw(A, 10, 0);
+      float a4[L3::OT][4];
+      fwd_tile<L3, true>(Lb, LF, Lb + L3::OFFA, b0, lane, B, a4);
+      if (last) stampw(A, 11, 0);
+      // logits = a4 . w4 + b4 (a4 as the bf16 image holds it), + the wide sum
+      float zd = 0.f;
+#pragma unroll
+      for (int ot = 0; ot < L3::OT; ++ot) {
+        const f32x4 w4 = *(const f32x4*)(LF + F_W4 + 16 * ot + 4 * eg);  // zero beyond D4 (ones column too)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zd = fmaf(rbf(a4[ot][r]), w4[r], zd);
+      }
+      zd += __shfl_xor(zd, 16, 64);
+      zd += __shfl_xor(zd, 32, 64);
+      ws += __shfl_xor(ws, 16, 64);
+      ws += __shfl_xor(ws, 32, 64);
+      const bool vb = eb < B;
+      const float z = zd + LF[F_MISC] + ws;
+      const float e = __expf(-fabsf(z));
+      const float re = __builtin_amdgcn_rcpf(1.f + e);
+      const float p = z >= 0.f ? re : e * re;
+      gb = vb ? (p - yv) * invB : 0.f;
+      // G4[b][o] = g w4[o] relu'(a4[b][o]) (K columns 0..47 of dX3; 48..63 meet zero W3 rows)
+#pragma unroll
+      for (int ot = 0; ot < L3::OT; ++ot) {
+        const f32x4 w4 = *(const f32x4*)(LF + F_W4 + 16 * ot + 4 * eg);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = sel(a4[ot][r] > 0.f, gb * w4[r], 0.f);
+        st4(Lb + OFF_GX + eb * SG + 16 * ot + 4 * eg, v[0], v[1], v[2], v[3]);
+      }
+      // logits-layer gradient partials over this tile's 16 examples: sum_b g_b a4[b][o] (the ones
+      // column o = 34 gives db4), a fixed-order DPP row sum, one row-leader lane per 4 columns
+#pragma unroll
+      for (int ot = 0; ot < L3::OT; ++ot) {
+        float q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = row_fold<1>(gb * rbf(a4[ot][r]));
+        if ((lane & 15) == 0) *(f32x4*)(LF + F_DW4 + wave * 48 + 16 * ot + 4 * eg) = (f32x4){q[0], q[1], q[2], q[3]};
+      }
+      if (last && eg == 0 && vb) {
+        lsum = fmaxf(z, 0.f) - z * yv + __logf(1.f + e);
+        csum = (float)((p > 0.5f) == (yv > 0.5f));
+      }
+      if (last) stampw(A, 12, 0);
+    }
+    bar();
+    if (last) stamp(A, 2);
+    // ============================================================ B3: dX3 ; mark wide rows | dW3, dW4
+    lane = fresh(tid & 63);
+    wave = fresh_s(wave0);
+    b0 = 16 * wave;
+    if (tw) {
+      dx_tile<L3>(Lb, Lb + OFF_GX, Lb + OFF_GY, b0, lane);
+      if (last) stampw(A, 13, 0);
+      // mark the touched rows and zero their table slots (the gradient sums land there); the entry whose
+      // atomicOr sets a row's bit leads that row's FTRL and fetches its state now (used in B0).  The
+      // previous step's FTRL stores (same CU) have completed first: by now this wait costs nothing.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned old[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {  // (invalid entries or their bit 0: no-op atomics, no branch)
+        const int r = cid[m] >= 0 ? cid[m] : 0;
+        old[m] = atomicOr(bits + (r >> 5), cid[m] >= 0 ? 1u << (r & 31) : 0u);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (cid[m] >= 0) LF[F_WTAB + cid[m]] = 0.f;
+      lead = 0u;
+      {
+        const auto& C = COLD;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int r = cid[m];
+          if (r >= 0 && !((old[m] >> (r & 31)) & 1u)) {
+            lead |= 1u << m;
+            const float2 q = C.zn[r];
+            zl[m] = q.x;
+            nl[m] = q.y;
+          }
+        }
+      }
+      if (last) stampw(A, 14, 0);
+      if (step + 1 < A.nsteps) fetch(true);  // the next batch, in flight during the backward
+    }
+    dw_seq<L3, R3, RSQ>(Lb + L3::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S3, own.s + S3, ha);
+    if (last) stampw(A, 15, 3);
+    if (wave == NW - 1) {  // the logits layer: sum the tiles' partials in order, Adagrad, new w4 / b4 now
+      const int i = lane <= D4 ? lane : 0;
+      const float g = (LF[F_DW4 + i] + LF[F_DW4 + 48 + i]) + LF[F_DW4 + 96 + i];
+      float s1 = own.s4;
+      const float wn = RSQ ? adagrad_rsq(own.w4, g * ha.gscale, s1, -ha.lr) : adagrad(own.w4, g * ha.gscale, s1, ha);
+      if (lane <= D4) {
+        own.w4 = wn;
+        own.s4 = s1;
+        LF[lane < D4 ? F_W4 + lane : F_MISC] = wn;
+      }
+    }
+    bar();
+    if (last) stamp(A, 3);
+    // ============================================================ B2: dX2 ; wide gradients | W3 image, dW2
+    lane = fresh(tid & 63);
+    wave = fresh_s(wave0);
+    b0 = 16 * wave;
+    if (tw) {
+      dx_tile<L2>(Lb, Lb + OFF_GY, Lb + OFF_GX, b0, lane);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (cid[m] >= 0) atomicAdd(LF + F_WTAB + cid[m], gb);
+    }
+    put_seq<L3, R3>(Lb, LF, perm8(wave), lane, own.w + S3);
+    dw_seq<L2, R2, RSQ>(Lb + L2::OFFA, Lb + OFF_GY, perm8(wave), lane, own.w + S2, own.s + S2, ha);
+    bar();
+    if (last) stamp(A, 4);
+    // ============================================================ B1: dX1 | W2 image, dW1
+    lane = fresh(tid & 63);
+    wave = fresh_s(wave0);
+    b0 = 16 * wave;
+    if (tw) dx_tile<L1>(Lb, Lb + OFF_GX, Lb + OFF_GY, b0, lane);
+    if (last) stampw(A, 16, 0);
+    put_seq<L2, R2>(Lb, LF, perm8(wave), lane, own.w + S2);
+    dw_seq<L1, R1, RSQ>(Lb + L1::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S1, own.s + S1, ha);
+    if (last) stampw(A, 17, 3);
+    bar();
+    if (last) stamp(A, 5);
+    // ============================================================ B0: dW0 (+ image) ; FTRL ; next A0 | W1 image
+    lane = fresh(tid & 63);
+    wave = fresh_s(wave0);
+    b0 = 16 * wave;
+    if (wave < L0::NDW) {
+      dw_seq<L0, 1, RSQ>(A0, Lb + OFF_GY, wave, lane, own.w + S0, own.s + S0, ha);
+      put_w<L0>(Lb, LF, wave, lane, own.w[S0]);
+    }
+    put_seq<L1, R1>(Lb, LF, perm8(wave), lane, own.w + S1);
+    if (tw) {
+      // FTRL-proximal on the rows this lane leads: the summed gradient is in the table slot, the old
+      // weight in wv; the new weight goes back to the table, weight / z / n / shadow to memory
+      const auto& C = COLD;
+      const OptHP hf = {C.ftrl.lr, C.ftrl.gscale, C.ftrl.wd, C.ftrl.a, C.ftrl.b, C.ftrl.c, C.ftrl.d, C.ftrl.e};
+      float w1[4], z1[4], n1[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int r = cid[m] >= 0 ? cid[m] : 0;
+        const float g = LF[F_WTAB + r] * hf.gscale;
+        const float nn = fmaf(g, g, nl[m]);
+        const float rs = __builtin_amdgcn_sqrtf(nn);
+        const float ilr = __builtin_amdgcn_rcpf(hf.lr);
+        const float zz = zl[m] + g - (rs - __builtin_amdgcn_sqrtf(nl[m])) * ilr * wv[m];
+        const float den = (hf.c + rs) * ilr + 2.f * hf.b;
+        w1[m] = (fabsf(zz) <= hf.a) ? 0.f : -(zz - copysignf(hf.a, zz)) * __builtin_amdgcn_rcpf(den);
+        z1[m] = zz;
+        n1[m] = nn;
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (lead & (1u << m)) {
+          LF[F_WTAB + cid[m]] = w1[m];
+          atomicAnd(bits + (cid[m] >> 5), ~(1u << (cid[m] & 31)));
+        }
+      // the next batch (loaded during B3) into registers / the other A0 image BEFORE the (z, n) stores:
+      // a wait for these loads must not include those stores (conditional: the compiler would wait
+      // for every outstanding access)
+      int cn[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) cn[m] = nid[m];
+      const float yn = ny;
+      if (!last && evb && eg < D0) Lb[OFF_A0 + ((step + 1) & 1) * BP * SA0 + eb * SA0 + eg] = f2b(nd);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (lead & (1u << m)) C.zn[cid[m]] = make_float2(z1[m], n1[m]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) cid[m] = cn[m];
+      yv = yn;
+      if (last) stampw(A, 18, 0);
+    }
+    bar();
+    if (last) stamp(A, 6);
+  }
+
+  // ------------------------------------------------------------------ write-back
+  if (tw) {
+    lsum = wave_sum(lsum);
+    csum = wave_sum(csum);
+    if (lane == 0) {
+      LF[F_RED + wave] = lsum;
+      LF[F_RED + 8 + wave] = csum;
+    }
+  }
+  __syncthreads();
+  {
+    const auto& C = COLD;
+    if (tid == 0) {
+      float l = 0.f, c = 0.f;
+      for (int w = 0; w < NTW; ++w) {
+        l += LF[F_RED + w];
+        c += LF[F_RED + 8 + w];
+      }
+      if (C.loss) C.loss[0] = l / (float)B;
+      if (C.correct) C.correct[0] = (int)c;
+    }
+    // deep parameters and state through the staging copy: sentinel-filled, the owners' values written,
+    // then copied out coalesced where not the sentinel (the span's alignment gaps keep their values)
+    const int span = (int)(C.deep_hi - C.deep_lo);
+    unsigned* su = (unsigned*)stage;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      float* dst = (pass ? C.ada_s : C.master) + C.deep_lo;
+      for (int e = tid; e < span; e += NT) su[e] = SENT;
+      __syncthreads();
+      if (pass) own_stage<false, true>(stage, own, wave, lane);
+      else own_stage<false, false>(stage, own, wave, lane);
+      __syncthreads();
+      // 4 elements a lane: one 16-byte store (+ 8-byte shadow) where all 4 are owned (the alignment gaps
+      // between tensors are the only exceptions)
+      const bool al = ((uintptr_t)dst & 15) == 0;
+      for (int e4 = tid; 4 * e4 < span; e4 += NT) {
+        const int e = 4 * e4;
+        bool all = al && e + 3 < span;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) all = all && su[e + k] != SENT;
+        if (all) {
+          const f32x4 v = *(const f32x4*)(stage + e);
+          *(f32x4*)(dst + e) = v;
+          if (!pass && C.shadow) st4(C.shadow + C.deep_lo + e, v[0], v[1], v[2], v[3]);
+        } else {
+          for (int k = 0; k < 4 && e + k < span; ++k)
+            if (su[e + k] != SENT) {
+              dst[e + k] = stage[e + k];
+              if (!pass && C.shadow) C.shadow[C.deep_lo + e + k] = f2b(stage[e + k]);
+            }
+        }
+      }
+      __syncthreads();
+    }
+    // the wide part: weights from the table, (z, n) from the private copy (8 rows of a thread in flight)
+    for (int base = 0; base < C.rows; base += NT * 8) {
+      float qz[8], qn[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = base + tid + NT * k;
+        const float2 t = C.zn[r < C.rows ? r : 0];
+        qz[k] = t.x;
+        qn[k] = t.y;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = base + tid + NT * k;
+        if (r < C.rows) {
+          const long x = C.wide_off + r;
+          const float w = LF[F_WTAB + r];
+          C.master[x] = w;
+          if (C.shadow) C.shadow[x] = f2b(w);
+          C.ftrl_z[x] = qz[k];
+          C.ftrl_n[x] = qn[k];
+        }
+      }
+    }
+    if (tid == 0) {
+      if (C.step_ada) C.step_ada[0] += (float)C.nsteps;
+      if (C.step_ftrl) C.step_ftrl[0] += (float)C.nsteps;
+      if (C.rng) C.rng[1] += (unsigned long long)C.rng_bumps * (unsigned long long)C.nsteps;
+      if (C.cursor) C.cursor[0] = (bi0 + C.nsteps) % C.nbatch;
+    }
+  }
+  stamp(A, 19);
+}
+
+// iv: L B nbatch nwide wide_off apply_opt rng_bumps dims[L+1] woff[L] boff[L] [nsteps] (widedeep_step.hip's
+// contract); fv: ada(8) ftrl(8).  0 = this kernel takes the configuration.
+int fill(Args& a, const long* iv, int ni, const float* fv, int nf, long rows) {
+  if (ni < 7 || nf != 16 || rows < 1 || rows > MAXROWS) return -1;
+  const int L = (int)iv[0];
+  const int nbase = 7 + (L + 1) + 2 * L;
+  if (L != 5 || (ni != nbase && ni != nbase + 1)) return -1;
+  const int dims[6] = {D0, D1, D2, D3, D4, 1};
+  for (int i = 0; i <= L; ++i)
+    if (iv[7 + i] != dims[i]) return -1;
+  a.B = (int)iv[1];
+  a.nbatch = (int)iv[2];
+  if (iv[3] != NWIDE || iv[5] != 1 || a.B < 1 || a.B > BP || a.nbatch < 1) return -1;
+  a.wide_off = iv[4];
+  a.rng_bumps = (int)iv[6];
+  a.deep_lo = iv[8 + L];
+  a.deep_hi = a.deep_lo;
+  for (int i = 0; i < L; ++i) {
+    a.woff[i] = iv[8 + L + i];
+    a.boff[i] = iv[8 + 2 * L + i];
+    const long dims_in = dims[i], dims_out = dims[i + 1];
+    a.deep_lo = a.woff[i] < a.deep_lo ? a.woff[i] : a.deep_lo;
+    a.deep_lo = a.boff[i] < a.deep_lo ? a.boff[i] : a.deep_lo;
+    const long we = a.woff[i] + dims_in * dims_out, be = a.boff[i] + dims_out;
+    a.deep_hi = we > a.deep_hi ? we : a.deep_hi;
+    a.deep_hi = be > a.deep_hi ? be : a.deep_hi;
+  }
+  if (a.deep_hi - a.deep_lo > STAGE_MAX || a.deep_lo < 0) return -1;
+  for (int i = 0; i < L; ++i) {
+    a.rw[i] = (int)(a.woff[i] - a.deep_lo);
+    a.rb[i] = (int)(a.boff[i] - a.deep_lo);
+  }
+  // the wide slice must not overlap the deep span (the owners write both)
+  if (a.wide_off < a.deep_hi && a.wide_off + rows > a.deep_lo) return -1;
+  a.nsteps = ni == nbase + 1 ? (int)iv[nbase] : 1;
+  if (a.nsteps < 1) return -1;
+  a.rows = (int)rows;
+  a.ada = OptHP{fv[0], fv[1], fv[2], fv[3], fv[4], fv[5], fv[6], fv[7]};
+  a.ftrl = OptHP{fv[8], fv[9], fv[10], fv[11], fv[12], fv[13], fv[14], fv[15]};
+  return 0;
+}
+
+}  // namespace taxi2
+
+// rows = wide table rows.  Returns the LDS bytes if the v2 kernel takes this configuration, else -1.
+extern "C" long hopsx_taxi_step2_ok(const long* iv, int ni, long rows) {
+  taxi2::Args a{};
+  const float f[16] = {};
+  if (taxi2::fill(a, iv, ni, f, 16, rows)) return -1;
+  return taxi2::LDS_BYTES;
+}
+
+// ptrs: master grad shadow ada_s ftrl_z ftrl_n dense cat label cursor loss correct step_ada step_ftrl rng dbg
+// (widedeep_step.hip's order; grad is unused: the gradients never leave the kernel), zn ([rows] float2
+// scratch), rsq (nonzero: the host checked wd == 0 and eps < 1e-7 sqrt(initial Adagrad accumulator))
+extern "C" int hopsx_taxi_step2(const uint64_t* p, int np, const long* iv, int ni, const float* fv, int nf, long rows,
+                                hipStream_t st) {
+  taxi2::Args a{};
+  if (np != 18 || taxi2::fill(a, iv, ni, fv, nf, rows)) return -2;
+  a.master = (float*)p[0];
+  a.shadow = (bf16_raw*)p[2];
+  a.ada_s = (float*)p[3];
+  a.ftrl_z = (float*)p[4];
+  a.ftrl_n = (float*)p[5];
+  a.dense = (const float*)p[6];
+  a.cat = (const long long*)p[7];
+  a.label = (const float*)p[8];
+  a.cursor = (long long*)p[9];
+  a.loss = (float*)p[10];
+  a.correct = (int*)p[11];
+  a.step_ada = (float*)p[12];
+  a.step_ftrl = (float*)p[13];
+  a.rng = (unsigned long long*)p[14];
+  a.dbg = (unsigned long long*)p[15];
+  a.zn = (float2*)p[16];
+  a.ada_rsq = p[17] ? 1 : 0;
+  if (!a.master || !a.ada_s || !a.ftrl_z || !a.ftrl_n || !a.dense || !a.cat || !a.label || !a.zn) return -2;
+  if (a.ada_rsq && a.ada.wd != 0.f) return -2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)taxi2::taxi_step_k<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              taxi2::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)taxi2::taxi_step_k<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              taxi2::LDS_BYTES);
+    attr = true;
+  }
+  if (a.ada_rsq) hipLaunchKernelGGL(taxi2::taxi_step_k<true>, dim3(1), dim3(taxi2::NT), (size_t)taxi2::LDS_BYTES, st, a);
+  else hipLaunchKernelGGL(taxi2::taxi_step_k<false>, dim3(1), dim3(taxi2::NT), (size_t)taxi2::LDS_BYTES, st, a);
+  return (int)hipGetLastError();
+}

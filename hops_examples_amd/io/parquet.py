@@ -76,7 +76,8 @@ def _staging(device: torch.device) -> _Staging:
     return st
 
 
-_NATIVE: dict = {}  # (path, size, mtime_ns) -> _hopsx_io.ParquetFile (footer parsed once, mmapped)
+_NATIVE: dict = {}  # (path, size, mtime_ns) -> _hopsx_io.ParquetFile (footer parsed once, mmapped; LRU)
+_NATIVE_MAX = 256  # mapped files kept (each holds its mapping, not a descriptor)
 _NP = {0: np.dtype(np.uint8), 1: np.dtype(np.int32), 2: np.dtype(np.int64), 4: np.dtype(np.float32),
        5: np.dtype(np.float64)}  # Parquet physical type -> raw value dtype in the staging slot
 
@@ -91,15 +92,19 @@ def _native_file(path: str):
     except OSError:
         return None
     key = (path, st.st_size, st.st_mtime_ns)
-    f = _NATIVE.get(key, False)
+    f = _NATIVE.pop(key, False)
     if f is False:
+        for k in [k for k in _NATIVE if k[0] == path]:  # an older version of this file: drop its mapping
+            del _NATIVE[k]
         try:
             from .. import _hopsx_io as io
 
             f = io.ParquetFile(path)
         except Exception:  # noqa: BLE001 - not built, not Parquet, or unsupported layout: Arrow reads it
             f = None
-        _NATIVE[key] = f
+    _NATIVE[key] = f  # (re)inserted last: the dict is in LRU order
+    while len(_NATIVE) > _NATIVE_MAX:
+        del _NATIVE[next(iter(_NATIVE))]
     return f
 
 
@@ -165,13 +170,15 @@ class ParquetDeviceReader:
     # ---------------------------------------------------------------- host side
     def _native_plan(self, nf):
         """(handle, leaf indices, raw dtypes) of the requested columns, or None if any is outside
-        the native decoder's scope (missing, nested, string / INT96 / fixed-length, repeated)."""
+        the native decoder's scope (missing, nested, string / INT96 / fixed-length, repeated, or a
+        converted / logical type that changes the meaning of the raw values: DECIMAL, unsigned,
+        DATE / TIME / TIMESTAMP — Arrow converts those)."""
         md = nf.meta()
-        by_name = {name: (i, t, rep) for i, (name, t, rep) in enumerate(md["columns"])}
+        by_name = {col[0]: (i, *col[1:]) for i, col in enumerate(md["columns"])}
         idx, dts = [], []
         for c in self.columns:
             e = by_name.get(c)
-            if e is None or e[1] not in _NP or e[2] == 2:
+            if e is None or e[1] not in _NP or e[2] == 2 or (len(e) > 3 and not e[3]):
                 return None
             idx.append(e[0])
             dts.append(_NP[e[1]])

@@ -171,7 +171,10 @@ def _as_nhwc_image(x, m):
         # 8 output channels (3..7 zero): the stem conv then runs on the C % 8 == 0 MFMA paths with its
         # weight zero-padded to match (nn.Conv2d), instead of the generic narrow-channel gather
         cout = 8 if "stem_pad" not in os.environ.get("HOPSX_DISABLE", "") else None
-        return K.u8_normalize_chan(x.contiguous(), m.img_scale_c, m.img_shift_c, reverse=m.img_reverse, cout=cout)
+        y = K.u8_normalize_chan(x.contiguous(), m.img_scale_c, m.img_shift_c, reverse=m.img_reverse, cout=cout)
+        if cout:
+            y._hx_chpad = x.shape[-1]  # channels beyond this are zero (nn.Conv2d pads its weight only then)
+        return y
     y = x.float()
     if m.img_reverse:
         y = y.flip(-1)

@@ -127,6 +127,9 @@ class FusedWideDeepStep:
                                                              os.environ.get("HOPSX_STEPS_PER_EXEC", "32"))))
         self._slot_cache = {}
         self._n = 0
+        self._B = None
+        self._v2: dict = {}
+        self._zn = None
         dev = self.arena.device
         self.loss = torch.zeros(1, device=dev)
         self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -146,7 +149,24 @@ class FusedWideDeepStep:
 
         dev = self.arena.device
         return (dev.type == "cuda" and self.acts_ok and self.dims[-1] == 1
-                and _C.ext().widedeep_step_lds(self._ints(B, 1)) > 0)
+                and (self.v2(B) or _C.ext().widedeep_step_lds(self._ints(B, 1)) > 0))
+
+    def v2(self, B: int) -> bool:
+        """The v2 kernel (csrc/ops/taxi_step.hip: bf16 MFMA, wide table + optimizer state on chip) takes
+        the default taxi shape on one GPU; HOPSX_TAXI_KERNEL=v1 forces the fp32 v1 kernel."""
+        from ..ops import _C
+
+        key = (B, self.dp is None, os.environ.get("HOPSX_TAXI_KERNEL", "v2"))
+        r = self._v2.get(key)
+        if r is None:
+            r = (self.dp is None and key[2] != "v1" and self.acts_ok and self.arena.device.type == "cuda"
+                 and _C.ext().taxi_step2_ok(self._ints(B, 1), int(self.model.wide.weight.shape[0])) > 0)
+            self._v2[key] = r
+        return r
+
+    @property
+    def kernel(self) -> str:
+        return "v2" if self.v2(self._B or TRAIN_BATCH_SIZE) else "v1"
 
     def _slots(self, B: int):
         """Host-built table: LDS slot of every deep arena element for batch size B (cached)."""
@@ -177,12 +197,26 @@ class FusedWideDeepStep:
         from ..ops.kernels import check, stream
 
         a = self.arena
+        B = dense.shape[-2]
+        self._B = B
         ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
         ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")), ptr(a.state("ftrl_s0")),
                 ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label), ptr(cursor), ptr(self.loss),
                 ptr(self.correct), ptr(self.ada.step_count), ptr(self.ftrl.step_count), ptr(rng_state(a.device)),
-                ptr(self.dbg), ptr(self._slots(dense.shape[-2]))]
-        check(_C.ext().widedeep_step(ptrs, self._ints(dense.shape[-2], nbatch, nsteps), self._floats(), stream()),
+                ptr(self.dbg)]
+        if self.v2(B):
+            rows = int(self.model.wide.weight.shape[0])
+            if self._zn is None:
+                self._zn = torch.empty(rows, 2, device=a.device)  # the kernel's (z, n) scratch
+            # Adagrad as w -= lr g rsq(s) (one transcendental): exact to fp32 when wd == 0 and eps is below
+            # the resolution of sqrt(s), whose floor is the initial accumulator
+            floor = float(getattr(self.ada, "initial_accumulator_value", 0.0))
+            rsq = int(self.ada.weight_decay == 0 and floor > 0 and self.ada.hp["eps"] < 1e-7 * math.sqrt(floor))
+            check(_C.ext().taxi_step2(ptrs + [ptr(self._zn), rsq], self._ints(B, nbatch, nsteps), self._floats(),
+                                      rows, stream()), "taxi_step2")
+            return
+        ptrs.append(ptr(self._slots(B)))
+        check(_C.ext().widedeep_step(ptrs, self._ints(B, nbatch, nsteps), self._floats(), stream()),
               "widedeep_step")
 
     def _finish(self):
@@ -217,7 +251,8 @@ class FusedWideDeepStep:
             self._finish()
         else:
             if self._key != key:  # new data or hyper-parameters (e.g. an lr schedule): recapture
-                self._slots(dense.shape[-2])  # host->device copy of the slot table must precede capture
+                if not self.v2(dense.shape[-2]):
+                    self._slots(dense.shape[-2])  # host->device copy of the slot table must precede capture
                 self._sync_hp()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
@@ -243,7 +278,8 @@ class FusedWideDeepStep:
     def _capture_u(self, dense, cat, ys, U: int):
         """U consecutive steps in one graph: ONE launch running U steps in-kernel on one GPU (the
         weights stay on chip between them); U launches + gradient exchanges when data-parallel."""
-        self._slots(dense.shape[-2])
+        if not self.v2(dense.shape[-2]):
+            self._slots(dense.shape[-2])
         self._sync_hp()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -368,7 +404,7 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
     fused = FusedWideDeepStep(model, opt, dp=dp) if os.environ.get("HOPSX_TAXI_FUSED", "1") == "1" else None
     if fused is not None and fused.ok(batch):
         dense = dense.view(nb, batch, -1)
-        path = "fused"
+        path = f"fused-{fused.kernel}"
 
         def run(i):
             # one launch: the kernel reads batch `cursor` of the resident epoch and advances it

@@ -94,9 +94,13 @@ class Conv2d(nn.Module):
 
     def forward(self, x, bnstats: bool = False, gslot=None):
         w = self.weight
-        if x.shape[-1] > self.in_channels:
+        if x.shape[-1] != self.in_channels:
             # an input laid out with zero channels beyond in_channels (models/resnet.py image stems: the
-            # normalisation kernel writes 8 channels): the weight is zero-padded to match
+            # normalisation kernel writes 8 channels and tags the tensor): the weight is zero-padded to
+            # match.  Any other channel mismatch (an RGBA image, a wrong layout) is an error, not data to drop.
+            if getattr(x, "_hx_chpad", None) != self.in_channels or x.shape[-1] < self.in_channels:
+                raise ValueError(f"Conv2d expects {self.in_channels} input channels (NHWC), got input of shape "
+                                 f"{tuple(x.shape)}")
             w = HF.pad_input_channels(w, x.shape[-1])
         return HF.conv2d(x, w, self.bias, act=self.activation, in_affine=self.in_affine, bnstats=bnstats,
                          gslot=gslot, **self.cfg)

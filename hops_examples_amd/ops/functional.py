@@ -677,10 +677,13 @@ class _PadCinFn(torch.autograd.Function):
         w = ctx.w
         gs = g[..., :w.shape[-1]]
         tgt = _arena.grad_target(w)
-        hooks.grad_ready(w)
         if tgt is not None:
+            # accumulate BEFORE announcing: the DP overlap hook may launch this bucket's all-reduce
+            # (stream-ordered) the moment the stem weight — the last gradient of backward — is ready
             tgt.add_(gs)
+            hooks.grad_ready(w)
             return None, None
+        hooks.grad_ready(w)
         return gs.contiguous(), None
 
 

@@ -259,6 +259,7 @@ class Adagrad(FusedOptimizer):
 
     def __init__(self, params, lr=0.01, eps=1e-10, initial_accumulator_value=0.0, weight_decay=0.0):
         super().__init__(params, lr, weight_decay, eps=eps)
+        self.initial_accumulator_value = float(initial_accumulator_value)  # the accumulator's floor
         if initial_accumulator_value:
             self._states[0].fill_(initial_accumulator_value)
 

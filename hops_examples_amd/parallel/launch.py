@@ -90,15 +90,27 @@ def _raise_terminated(signum, frame):  # noqa: ARG001
     raise _Terminated(signum)
 
 
-def _child_setup() -> None:
-    """In each rank before exec: die with the launcher (PR_SET_PDEATHSIG = SIGTERM), so a launcher
-    killed by SIGKILL leaves no rank spinning on the GPU in its own session."""
+def _pdeathsig_setup():
+    """A preexec function for each rank: die with the launcher (PR_SET_PDEATHSIG = SIGTERM), so a
+    launcher killed by SIGKILL leaves no rank spinning on the GPU in its own session.  libc and prctl are
+    resolved HERE, in the parent: the forked child (before exec) only calls the bound function — an
+    import in the child could deadlock on a lock another parent thread (torch, a pool) held at fork.
+    The child also checks that the launcher did not die before prctl took effect."""
     try:
         import ctypes
 
-        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+        prctl = ctypes.CDLL("libc.so.6", use_errno=True).prctl
+        getppid, kill, parent = os.getppid, os.kill, os.getpid()
+        sigterm, sigkill = int(signal.SIGTERM), signal.SIGKILL
     except Exception:  # noqa: BLE001
-        pass
+        return None
+
+    def setup():
+        prctl(1, sigterm, 0, 0, 0)
+        if getppid() != parent:  # the launcher is already gone
+            kill(os.getpid(), sigkill)
+
+    return setup
 
 
 def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float | None = None,
@@ -114,24 +126,31 @@ def launch(nproc: int, argv: list[str], rehearse: bool = False, timeout_s: float
         return 2
     port = free_port()
     procs = []
-    # a driver timeout / job manager stops the launcher with SIGTERM or SIGHUP: turn both into an
-    # exception so the finally block below kills every rank (they run in sessions of their own)
-    prev = {sig: signal.signal(sig, _raise_terminated) for sig in (signal.SIGTERM, signal.SIGHUP)}
-    for r in range(nproc):
-        env = dict(os.environ)
-        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc),
-                    "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
-                    "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1",
-                    "HOPSX_SELF_LAUNCHED": "1"})
-        if rehearse and ngpu < nproc:
-            env.setdefault("HOPSX_DIST_BACKEND", "gloo")
-        if extra_env:
-            env.update({k: str(v) for k, v in extra_env.items()})
-        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env, start_new_session=True,
-                                      preexec_fn=_child_setup))
+    preexec = _pdeathsig_setup()
     t0 = time.time()
     rc = 0
+    # a driver timeout / job manager stops the launcher with SIGTERM or SIGHUP: turn both into an
+    # exception so the finally block below kills every rank (they run in sessions of their own).  Signal
+    # handlers can only be installed from the main thread; elsewhere the caller's handling stands.
+    import threading
+
+    prev = {}
     try:
+        if threading.current_thread() is threading.main_thread():
+            prev = {sig: signal.signal(sig, _raise_terminated) for sig in (signal.SIGTERM, signal.SIGHUP)}
+        for r in range(nproc):
+            env = dict(os.environ)
+            env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc),
+                        "LOCAL_WORLD_SIZE": str(nproc), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                        "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0", "PYTHONUNBUFFERED": "1",
+                        "HOPSX_SELF_LAUNCHED": "1"})
+            if rehearse and ngpu < nproc:
+                env.setdefault("HOPSX_DIST_BACKEND", "gloo")
+            if extra_env:
+                env.update({k: str(v) for k, v in extra_env.items()})
+            procs.append(subprocess.Popen([sys.executable] + list(argv), env=env, start_new_session=True,
+                                          preexec_fn=preexec))
+        t0 = time.time()
         while True:
             codes = [p.poll() for p in procs]
             bad = [c for c in codes if c not in (None, 0)]

@@ -59,16 +59,71 @@ class PersistentError(RuntimeError):
     pass
 
 
+def flagship_layers(model):
+    """The (conv1, conv2, pool, fc1, fc2) layers when ``model`` has the structure of the reference's
+    MirroredStrategy MNIST CNN (mirroredstrategy_mnist_example.ipynb:189-207) — Conv 1->32 k2 relu,
+    Conv 32->64 k2 relu, MaxPool 2 (+ fused dropout), Dense 10816->128 relu, Dense 128->10, uint8 input
+    affine on conv1 — matched on the layers, not on the class; else None."""
+    from .. import nn as hnn
+    from ..models.mnist import MirroredMnistCNN
+
+    names = ("conv1", "conv2", "pool", "fc1", "fc2")
+    L = [getattr(model, n, None) for n in names]
+    if any(x is None for x in L):
+        return None
+    c1, c2, pool, f1, f2 = L
+
+    def conv_ok(c, cin, cout):
+        return (isinstance(c, hnn.Conv2d) and c.in_channels == cin and c.out_channels == cout
+                and tuple(c.kernel_size) == (2, 2) and c.activation == "relu" and c.bias is not None
+                and c.cfg.get("stride", 1) in (1, (1, 1)) and c.cfg.get("padding", 0) in (0, "valid", (0, 0))
+                and c.cfg.get("dilation", 1) in (1, (1, 1)))
+
+    def dense_ok(d, fin, fout, act):
+        return (isinstance(d, hnn.Linear) and tuple(d.weight.shape) == (fout, fin) and d.activation == act
+                and d.bias is not None)
+
+    ok = (conv_ok(c1, 1, 32) and conv_ok(c2, 32, 64) and c1.in_affine is not None
+          and isinstance(pool, hnn.MaxPool2d) and pool.k == 2 and pool.s in (None, 2) and not pool.p
+          and 0.0 <= float(pool.dropout) < 1.0
+          and dense_ok(f1, 13 * 13 * 64, 128, "relu") and dense_ok(f2, 128, 10, None))
+    # the forward must be exactly that chain: the reference model class (or a subclass keeping its forward)
+    return L if ok and type(model).forward is MirroredMnistCNN.forward else None
+
+
+def _device_cus(dev) -> int:
+    return int(torch.cuda.get_device_properties(dev).multi_processor_count)
+
+
+def _occupancy(dp: bool) -> int:
+    return int(_ext().mnist_persist_occupancy(int(dp)))
+
+
+def launchable(dev, world: int = 1) -> tuple[bool, str]:
+    """Can all of the persistent kernel's workgroups be resident at once on ``dev``?  Its workgroups
+    hand data to each other inside the launch, so a partitioned GPU (fewer CUs than the grid) or a
+    kernel too big for one workgroup per CU would spin until the hand-off timeout: refuse instead."""
+    g = geometry()
+    cus = _device_cus(dev)
+    if cus < g["grid"]:
+        return False, f"{cus} CUs < the persistent grid of {g['grid']} workgroups"
+    occ = _occupancy(world > 1)
+    if occ < 1:
+        return False, f"occupancy {occ} workgroups per CU"
+    return True, "ok"
+
+
 class PersistentMnistStep:
     PARAMS = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "fc1.weight", "fc1.bias",
               "fc2.weight", "fc2.bias")
 
     @staticmethod
     def supported(model, opt, batch: int, world: int = 1) -> bool:
-        """Local checks (model, optimizer, batch, world size).  For world > 1 the caller also needs
-        every rank on its own GPU of one node (``parallel.oneshot._colocation``) and a passing
-        ``selftest()``; ``HOPSX_PERSIST_DP=0`` keeps data-parallel runs on TrainStep."""
-        from ..models.mnist import MirroredMnistCNN
+        """Local checks: the model's structure (``flagship_layers``), Adadelta over the whole arena, batch
+        32 per replica, training mode, and a device that can hold every workgroup at once
+        (``launchable``).  For world > 1 the caller also needs every rank on its own GPU of one node
+        (``parallel.oneshot._colocation``) and a passing ``selftest()``; ``HOPSX_PERSIST=0`` /
+        ``HOPSX_PERSIST_DP=0`` keep runs on TrainStep."""
         from ..optim import Adadelta
 
         if os.environ.get("HOPSX_PERSIST", "1") != "1":
@@ -76,9 +131,11 @@ class PersistentMnistStep:
         if world > 1 and (os.environ.get("HOPSX_PERSIST_DP", "1") != "1" or world > geometry()["max_ranks"]):
             return False
         a = getattr(opt, "arena", None)
-        return (isinstance(model, MirroredMnistCNN) and isinstance(opt, Adadelta) and batch == 32
-                and a is not None and a.device.type == "cuda" and a.shadow is not None
-                and opt._sl.start == 0 and opt._sl.stop >= a.numel and model.training)
+        if not (isinstance(opt, Adadelta) and batch == 32 and a is not None and a.device.type == "cuda"
+                and a.shadow is not None and opt._sl.start == 0 and opt._sl.stop >= a.numel and model.training
+                and flagship_layers(model) is not None):
+            return False
+        return launchable(a.device, world)[0]
 
     def __init__(self, model, opt, steps_per_launch: int = 32, debug_stamps: bool = False, world: int | None = None,
                  loopback: int = 0, timeout_s: float | None = None):
@@ -312,6 +369,16 @@ class PersistentMnistStep:
 
     def step_resident(self, xs, ys):
         return self.run_resident(xs, ys, 1)
+
+    def __call__(self, x, y):
+        """One step on an explicit batch (TrainStep API): x uint8 [32, 28, 28(, 1)], y int64 [32] — a
+        resident epoch of one batch.  Prefer ``run_resident`` on a device-resident epoch: one launch
+        then runs ``steps_per_launch`` steps."""
+        xs = x.reshape(1, *x.shape) if x.is_contiguous() else x.contiguous().reshape(1, *x.shape)
+        return self.run_resident(xs, y.reshape(1, -1).contiguous(), 1)
+
+    def eager(self, x, y):
+        return self(x, y)
 
     def prepare_resident(self, xs, ys, n=None) -> None:  # TrainStep API parity: nothing to capture
         self._check_data(xs, ys)

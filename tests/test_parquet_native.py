@@ -88,3 +88,35 @@ def test_reader_uses_native_and_falls_back(tmp_path):
     r2 = ParquetDeviceReader(s, ["x"], device="cpu")
     assert s in r2.native  # only numeric columns requested: native
     np.testing.assert_array_equal(r2.read().numpy()[:, 0], np.arange(10.0, dtype=np.float32))
+
+
+def test_annotated_columns_take_the_arrow_path(tmp_path):
+    """DECIMAL (INT32/INT64 physical, scaled), unsigned, DATE and TIMESTAMP columns carry raw values that
+    are not the column's values: the native plan refuses them and Arrow converts (no unscaled decimals,
+    no negative uint32); signed small ints (INT_8 / INT_16 annotations) stay native."""
+    import decimal
+
+    n = 64
+    rng = np.random.default_rng(1)
+    dec = [decimal.Decimal(int(v)).scaleb(-2) for v in rng.integers(-10**6, 10**6, n)]
+    tbl = pa.table({"d": pa.array(dec, type=pa.decimal128(9, 2)),
+                    "u": pa.array(rng.integers(2**31, 2**32 - 1, n, dtype=np.uint32)),
+                    "day": pa.array(rng.integers(0, 20000, n).astype("datetime64[D]").astype("datetime64[D]")),
+                    "ts": pa.array(rng.integers(0, 10**9, n).astype("datetime64[s]")),
+                    "i8": pa.array(rng.integers(-100, 100, n).astype(np.int8)),
+                    "x": pa.array(rng.random(n))})
+    p = str(tmp_path / "a.parquet")
+    pq.write_table(tbl, p, store_decimal_as_integer=True)
+    f = io.ParquetFile(p)
+    plain = {c[0]: c[3] for c in f.meta()["columns"]}
+    assert plain == {"d": False, "u": False, "day": False, "ts": False, "i8": True, "x": True}
+    r = ParquetDeviceReader(p, ["i8", "x"], device="cpu")
+    assert p in r.native
+    np.testing.assert_array_equal(r.read().numpy()[:, 0], tbl.column("i8").to_numpy().astype(np.float32))
+    for col in ("d", "u"):
+        r = ParquetDeviceReader(p, [col, "x"], device="cpu")
+        assert p not in r.native
+        got = r.read().numpy()[:, 0]
+        want = np.array([float(v) for v in tbl.column(col).to_pylist()], dtype=np.float32)
+        np.testing.assert_allclose(got, want, rtol=1e-6)
+        assert (got >= 0).all() if col == "u" else True

@@ -153,3 +153,49 @@ def test_serving_python_predictor_and_inference_log(project_root):
     finally:
         serving.stop("irisflowerclassifier")
     assert serving.get_status("irisflowerclassifier") == "Stopped"
+
+
+def test_make_step_falls_back_when_the_persistent_grid_cannot_be_resident(monkeypatch):
+    """runtime.persist.launchable refuses a device with fewer CUs than the persistent grid (a partitioned
+    GPU) or an occupancy below one workgroup per CU, and make_step then builds a TrainStep."""
+    from hops_examples_amd.runtime import persist
+
+    monkeypatch.setattr(persist, "geometry", lambda: {"grid": 201, "max_ranks": 8})
+    monkeypatch.setattr(persist, "_occupancy", lambda dp: 1)
+    monkeypatch.setattr(persist, "_device_cus", lambda dev: 256)
+    assert persist.launchable("cuda:0") == (True, "ok")
+    monkeypatch.setattr(persist, "_device_cus", lambda dev: 128)  # e.g. a CPX-partitioned MI355X
+    ok, why = persist.launchable("cuda:0")
+    assert not ok and "128 CUs" in why
+    monkeypatch.setattr(persist, "_device_cus", lambda dev: 256)
+    monkeypatch.setattr(persist, "_occupancy", lambda dp: 0)
+    assert not persist.launchable("cuda:0")[0]
+
+
+def test_flagship_structure_match_and_make_step_cpu():
+    """The persistent engine is chosen by layer structure; on the CPU (no GPU arena) make_step builds a
+    TrainStep that trains."""
+    import torch
+
+    from hops_examples_amd import optim
+    from hops_examples_amd.models.mnist import KerasMnistCNN, MirroredMnistCNN
+    from hops_examples_amd.runtime import persist
+    from hops_examples_amd.runtime.arena import ParamArena
+    from hops_examples_amd.runtime.step import TrainStep, make_step
+
+    m = MirroredMnistCNN()
+    assert persist.flagship_layers(m) is not None
+    assert persist.flagship_layers(KerasMnistCNN(kernel=2, pool=2)) is None  # different structure (conv k, fc1)
+
+    class Sub(MirroredMnistCNN):  # same layers, same forward: still the flagship
+        pass
+
+    assert persist.flagship_layers(Sub()) is not None
+    ParamArena.from_module(m, "cpu")
+    opt = optim.Adadelta(m, lr=1.0)
+    st = make_step(m, opt, "sparse_ce", batch=32)
+    assert isinstance(st, TrainStep) and st.kind == "trainstep"
+    x = torch.randint(0, 256, (32, 28, 28, 1), dtype=torch.uint8)
+    y = torch.randint(0, 10, (32,))
+    r = st(x, y)
+    assert float(r["loss"].reshape(-1)[0]) > 0

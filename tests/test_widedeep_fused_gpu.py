@@ -1,9 +1,15 @@
-"""The fused one-launch taxi training step (widedeep_step.hip) against the fp32 CPU TrainStep of the
-same model/optimizers (FTRL wide + Adagrad deep, sigmoid cross-entropy)."""
+"""The fp32 v1 fused one-launch taxi training step (widedeep_step.hip) against the fp32 CPU TrainStep of
+the same model/optimizers (FTRL wide + Adagrad deep, sigmoid cross-entropy).  The default taxi shape
+runs the bf16 v2 kernel (tests/test_taxi_v2_gpu.py); this module pins HOPSX_TAXI_KERNEL=v1."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _v1(monkeypatch):
+    monkeypatch.setenv("HOPSX_TAXI_KERNEL", "v1")
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a GPU", allow_module_level=True)
 

@@ -51,7 +51,7 @@ persist)
   bench bench20 bench.py --steps 20 --warmup 5 --no-taxi
   bench bench200 bench.py --steps 200 --warmup 20 --no-taxi ;;
 taxi)
-  pyt $out/pytest.log tests/test_widedeep_fused_gpu.py tests/test_tfx_gpu.py
+  pyt $out/pytest.log tests/test_taxi_v2_gpu.py tests/test_widedeep_fused_gpu.py tests/test_tfx_gpu.py
   timeout -k 10 180 python -u tools/taxi_phases.py > $out/phases.txt 2>&1 || fail $out/phases.txt
   cat $out/phases.txt
   bench taxi benchmarks/run.py taxi --steps 200 --warmup 20
@@ -100,6 +100,13 @@ ab)
     r=$(env $s timeout -k 10 300 python benchmarks/run.py $args 2>>$out/err.log | tail -1) || { echo "FAIL [$s]"; fail $out/err.log; }
     echo "[$s] $args -> $(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" | tee -a $out/ab.txt
   done; done ;;
+taxipmc)
+  # PMC passes over the taxi benchmark (one counter group per run): wave-cycles split, LDS, instruction mix
+  cd /tmp
+  P="python3 $R/benchmarks/run.py taxi --steps 64 --warmup 4"
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d "$R/$out/a" -o run --output-format csv -- $P > "$R/$out/a.log" 2>&1 && \
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_IFETCH -d "$R/$out/b" -o run --output-format csv -- $P > "$R/$out/b.log" 2>&1
+  cd $R; python tools/pmcsum.py $out/a $out/b > $out/pmc.txt 2>&1; cat $out/pmc.txt | head -40 ;;
 tables)
   ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10 --inline
   ktable p50 r50_b64_kernels.txt benchmarks/run.py resnet50 --batch 64 --steps 20 --warmup 5 ;;
