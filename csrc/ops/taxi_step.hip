@@ -27,12 +27,13 @@
 //     old weight.  Biases ride the GEMMs as a ones column of A (db = that column of dW) but are
 //     applied in fp32 in the forward epilogue.  The logits layer (34 -> 1) is the dot product of
 //     the last hidden tile with w4 in the forward wave; its backward is G4 = g w4 relu'.
-//   * the wide (linear) part: the 6,287-row weight table lives in LDS (fp32), its FTRL state in the
-//     registers of the owning threads (row r -> thread r % 512).  Per step: the tile waves gather
-//     their examples' 13 rows (FWD), zero + mark the touched rows (B3) and add the example gradients
-//     with LDS float atomics (B2: each of a wave's instructions covers one column, whose id range no
-//     other column shares, so the summation order is fixed); owners apply FTRL to the marked rows
-//     and write the new weights back (B1, B0) — branch-free.
+//   * the wide (linear) part: the 6,287-row weight table lives in LDS (fp32).  Per step the tile waves
+//     gather their examples' 13 rows (FWD) while the otherwise idle gradient waves find each entry's
+//     leader — the first example of the batch with the same id in that column (the 13 columns' id
+//     ranges are disjoint) — from an LDS id table; in B3 the gradient waves sum each leader's example
+//     gradients in example order (no atomics: deterministic), and in B0 the leader applies FTRL-proximal
+//     with (z, n) from a kernel-private float2 copy in memory (fetched in B3) and writes the new weight
+//     back to the table.
 //   * the launch loads / stores the deep parameters through an LDS staging copy of their arena span
 //     (coalesced), so per-launch overhead stays small next to the 20-32 steps it runs.
 //
@@ -81,7 +82,8 @@ constexpr int BF_BYTES = BF_END * 2;
 // ---- fp32 region (float offsets from BF_BYTES)
 constexpr int F_B0 = 0, F_B1 = F_B0 + 16 * cdiv(D1, 16), F_B2 = F_B1 + 16 * cdiv(D2, 16),
               F_B3 = F_B2 + 16 * cdiv(D3, 16), F_W4 = F_B3 + 16 * cdiv(D4, 16), F_MISC = F_W4 + 48,
-              F_RED = F_MISC + 16, F_DW4 = F_RED + 16, F_WTAB = F_DW4 + 3 * 48, F_BITS = F_WTAB + MAXROWS, F_END = F_BITS + MAXROWS / 32;
+              F_RED = F_MISC + 16, F_DW4 = F_RED + 16, F_GV = F_DW4 + 3 * 48, F_IDT = F_GV + BP, F_LT = F_IDT + 16 * BP,
+              F_GS = F_LT + 16 * BP, F_WTAB = F_GS + 16 * BP, F_END = F_WTAB + MAXROWS;
 constexpr int LDS_BYTES = BF_BYTES + F_END * 4;
 constexpr int STAGE_MAX = LDS_BYTES / 4;  // floats of the deep arena span staged through LDS
 static_assert(BF_BYTES % 16 == 0 && LDS_BYTES <= 160 * 1024, "taxi2 LDS budget");
@@ -180,6 +182,10 @@ __device__ __forceinline__ int fresh_s(int x) {  // (the same for wave-uniform v
 
 __device__ __forceinline__ void stamp(const Args& a, int slot) {
   if (a.dbg && threadIdx.x == 0) a.dbg[slot] = wall_clock64();
+}
+// (HOPSX_PHASE_DBG) the shader clock next to the 100 MHz wall clock, for the clock rate of a launch
+__device__ __forceinline__ void stamp_clk(const Args& a, int slot) {
+  if (a.dbg && threadIdx.x == 0) a.dbg[slot] = __builtin_amdgcn_s_memtime();
 }
 // (HOPSX_PHASE_DBG) a stamp from lane 0 of wave w: tile wave 0 / gradient wave 3 inside a phase
 __device__ __forceinline__ void stampw(const Args& a, int slot, int w) {
@@ -502,7 +508,8 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
   bf16_raw* const Lb = (bf16_raw*)lds;
   float* const LF = (float*)(lds + BF_BYTES);
   float* const stage = (float*)lds;
-  unsigned* const bits = (unsigned*)(LF + F_BITS);
+  int* const idt = (int*)(LF + F_IDT);  // [16][BP] the step's wide ids by (column, example), -1: none
+  int* const ltab = (int*)(LF + F_LT);  // [16][BP] each entry's leader: first example with the same id
   const int tid = threadIdx.x;
   int lane = tid & 63;
   const int wave0 = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -519,27 +526,24 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     const int span = (int)(C.deep_hi - C.deep_lo);
     // deep parameters and their Adagrad state, each through a coalesced LDS staging copy of the span
     gather_in(stage, C.master + C.deep_lo, span, tid);
-    __syncthreads();
+    bar();
     own_stage<true, false>(stage, own, wave, lane);
-    __syncthreads();
+    bar();
     gather_in(stage, C.ada_s + C.deep_lo, span, tid);
-    __syncthreads();
+    bar();
     own_stage<true, true>(stage, own, wave, lane);
-    __syncthreads();
-    // the kernel-private (z, n) copy of the FTRL state (leaders read / write one float2 per row a step);
-    // 8 rows of a thread in flight at once
-    for (int base = 0; base < C.rows; base += NT * 8) {
-      float zv[8], nv[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int r = base + tid + NT * k, rc = r < C.rows ? r : 0;
-        zv[k] = C.ftrl_z[C.wide_off + rc];
-        nv[k] = C.ftrl_n[C.wide_off + rc];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (base + tid + NT * k < C.rows) C.zn[base + tid + NT * k] = make_float2(zv[k], nv[k]);
+    bar();
+    // the kernel-private (z, n) copy of the FTRL state (leaders read / write one float2 per row a step):
+    // 4 rows a lane, 16-byte accesses (a single CU's store path is the limit here)
+    const float* zs = C.ftrl_z + C.wide_off;
+    const float* ns = C.ftrl_n + C.wide_off;
+    const int r4 = ((((uintptr_t)zs | (uintptr_t)ns) & 15) == 0) ? C.rows >> 2 : 0;
+    for (int q = tid; q < r4; q += NT) {
+      const f32x4 z4 = ((const f32x4*)zs)[q], n4 = ((const f32x4*)ns)[q];
+      ((f32x4*)C.zn)[2 * q] = (f32x4){z4[0], n4[0], z4[1], n4[1]};
+      ((f32x4*)C.zn)[2 * q + 1] = (f32x4){z4[2], n4[2], z4[3], n4[3]};
     }
+    for (int r = 4 * r4 + tid; r < C.rows; r += NT) C.zn[r] = make_float2(zs[r], ns[r]);
   }
   // the batch (tile waves): lane -> example b = b0 + (lane & 15), columns c = (lane >> 4) + 4 m
   const int eb = b0 + (lane & 15), eg = lane >> 4;
@@ -568,7 +572,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     uint4* z = (uint4*)lds;
     for (int e = tid; e < LDS_BYTES / 16; e += NT) z[e] = make_uint4(0u, 0u, 0u, 0u);
   }
-  __syncthreads();
+  bar();
   // the input's ones column (db0); the fp32 bias arrays' constant tail: 1 at OUT makes the forward
   // epilogue write the next layer's ones column, -1e30 beyond makes it write zeros
   if (tid < B) {
@@ -597,20 +601,32 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     if (wave == NW - 1 && lane <= D4) LF[lane < D4 ? F_W4 + lane : F_MISC] = own.w4;
   }
   if (wave < L0::NDW) put_w<L0>(Lb, LF, wave, lane, own.w[S0]);
+  if (tw) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (eg + 4 * m < NWIDE) idt[(eg + 4 * m) * BP + eb] = cid[m];  // (-1 for examples >= B)
+  }
   gather_in(LF + F_WTAB, A.master + A.wide_off, A.rows, tid);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the zn copy has landed before any leader reads it)
-  __syncthreads();
+  // (the zn copy's stores need not land here: B3 waits for them before a leader reads (z, n))
+  bar();
   stamp(A, 1);
 
   float lsum = 0.f, csum = 0.f, gb = 0.f;
   const float invB = 1.f / (float)B;
+  stamp_clk(A, 20);
   float wv[4], zl[4], nl[4];  // (tile waves) gathered wide weights; FTRL state of the rows this lane leads
   unsigned lead = 0u;
+  // entries e = gl + 320 k of the gradient waves' leader passes: column e / BP, example e % BP
+  auto gl_entry = [&](int k, int& c, int& b) {
+    const int e = (wave - NTW) * 64 + lane + (NW - NTW) * 64 * k;
+    c = e / BP;
+    b = e - c * BP;
+  };
   for (int step = 0; step < A.nsteps; ++step) {
     const bool last = step + 1 == A.nsteps;
     const bf16_raw* A0 = Lb + OFF_A0 + (step & 1) * BP * SA0;
     if (last) stamp(A, 7);
-    // ============================================================ FWD: tile waves, no barrier inside
+    // ============================================================ FWD: tile waves, no barrier inside | leaders
     lane = fresh(tid & 63);
     wave = fresh_s(wave0);
     b0 = 16 * wave;
@@ -653,6 +669,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       const float re = __builtin_amdgcn_rcpf(1.f + e);
       const float p = z >= 0.f ? re : e * re;
       gb = vb ? (p - yv) * invB : 0.f;
+      if (eg == 0) LF[F_GV + eb] = gb;  // (the wide rows' gradients, summed per leader in B3)
       // G4[b][o] = g w4[o] relu'(a4[b][o]) (K columns 0..47 of dX3; 48..63 meet zero W3 rows)
 #pragma unroll
       for (int ot = 0; ot < L3::OT; ++ot) {
@@ -676,36 +693,46 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
         csum = (float)((p > 0.5f) == (yv > 0.5f));
       }
       if (last) stampw(A, 12, 0);
+    } else {
+      // each entry's leader: the smallest example index with the same id in its column (ids of
+      // different columns never coincide), from the column read 4 ids at a time
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {  // 2 x 320 lanes >= 13 x 48 entries
+        int c, b;
+        gl_entry(k, c, b);
+        if (c < NWIDE) {
+          const int id = idt[c * BP + b];
+          int L = b;
+#pragma unroll
+          for (int q = 0; q < BP / 4; ++q) {
+            const int4 v = *(const int4*)(idt + c * BP + 4 * q);
+            L = (v.w == id && 4 * q + 3 < L) ? 4 * q + 3 : L;
+            L = (v.z == id && 4 * q + 2 < L) ? 4 * q + 2 : L;
+            L = (v.y == id && 4 * q + 1 < L) ? 4 * q + 1 : L;
+            L = (v.x == id && 4 * q < L) ? 4 * q : L;
+          }
+          ltab[c * BP + b] = id >= 0 ? L : -1;
+        }
+      }
     }
     bar();
     if (last) stamp(A, 2);
-    // ============================================================ B3: dX3 ; mark wide rows | dW3, dW4
+    // ============================================================ B3: dX3 ; leaders fetch (z, n) | dW3, dW4, leader sums
     lane = fresh(tid & 63);
     wave = fresh_s(wave0);
     b0 = 16 * wave;
     if (tw) {
       dx_tile<L3>(Lb, Lb + OFF_GX, Lb + OFF_GY, b0, lane);
       if (last) stampw(A, 13, 0);
-      // mark the touched rows and zero their table slots (the gradient sums land there); the entry whose
-      // atomicOr sets a row's bit leads that row's FTRL and fetches its state now (used in B0).  The
-      // previous step's FTRL stores (same CU) have completed first: by now this wait costs nothing.
+      // the previous step's (z, n) stores (same CU) completed before these loads: by now the wait is free
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned old[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {  // (invalid entries or their bit 0: no-op atomics, no branch)
-        const int r = cid[m] >= 0 ? cid[m] : 0;
-        old[m] = atomicOr(bits + (r >> 5), cid[m] >= 0 ? 1u << (r & 31) : 0u);
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        if (cid[m] >= 0) LF[F_WTAB + cid[m]] = 0.f;
       lead = 0u;
       {
         const auto& C = COLD;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          const int r = cid[m];
-          if (r >= 0 && !((old[m] >> (r & 31)) & 1u)) {
+          const int c = eg + 4 * m, r = cid[m];
+          if (r >= 0 && ltab[c * BP + eb] == eb) {
             lead |= 1u << m;
             const float2 q = C.zn[r];
             zl[m] = q.x;
@@ -715,6 +742,26 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       }
       if (last) stampw(A, 14, 0);
       if (step + 1 < A.nsteps) fetch(true);  // the next batch, in flight during the backward
+    } else {
+      // the summed example gradient of every leader entry, in example order
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {  // 2 x 320 lanes >= 13 x 48 entries
+        int c, b;
+        gl_entry(k, c, b);
+        if (c < NWIDE && ltab[c * BP + b] == b) {
+          float g = 0.f;
+#pragma unroll
+          for (int q = 0; q < BP / 4; ++q) {
+            const int4 l4 = *(const int4*)(ltab + c * BP + 4 * q);
+            const f32x4 g4 = *(const f32x4*)(LF + F_GV + 4 * q);
+            g += l4.x == b ? g4[0] : 0.f;
+            g += l4.y == b ? g4[1] : 0.f;
+            g += l4.z == b ? g4[2] : 0.f;
+            g += l4.w == b ? g4[3] : 0.f;
+          }
+          LF[F_GS + c * BP + b] = g;
+        }
+      }
     }
     dw_seq<L3, R3, RSQ>(Lb + L3::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S3, own.s + S3, ha);
     if (last) stampw(A, 15, 3);
@@ -731,16 +778,11 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     }
     bar();
     if (last) stamp(A, 3);
-    // ============================================================ B2: dX2 ; wide gradients | W3 image, dW2
+    // ============================================================ B2: dX2 | W3 image, dW2
     lane = fresh(tid & 63);
     wave = fresh_s(wave0);
     b0 = 16 * wave;
-    if (tw) {
-      dx_tile<L2>(Lb, Lb + OFF_GY, Lb + OFF_GX, b0, lane);
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        if (cid[m] >= 0) atomicAdd(LF + F_WTAB + cid[m], gb);
-    }
+    if (tw) dx_tile<L2>(Lb, Lb + OFF_GY, Lb + OFF_GX, b0, lane);
     put_seq<L3, R3>(Lb, LF, perm8(wave), lane, own.w + S3);
     dw_seq<L2, R2, RSQ>(Lb + L2::OFFA, Lb + OFF_GY, perm8(wave), lane, own.w + S2, own.s + S2, ha);
     bar();
@@ -756,7 +798,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     if (last) stampw(A, 17, 3);
     bar();
     if (last) stamp(A, 5);
-    // ============================================================ B0: dW0 (+ image) ; FTRL ; next A0 | W1 image
+    // ============================================================ B0: dW0 (+ image) ; FTRL ; next batch | W1 image
     lane = fresh(tid & 63);
     wave = fresh_s(wave0);
     b0 = 16 * wave;
@@ -766,18 +808,17 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     }
     put_seq<L1, R1>(Lb, LF, perm8(wave), lane, own.w + S1);
     if (tw) {
-      // FTRL-proximal on the rows this lane leads: the summed gradient is in the table slot, the old
-      // weight in wv; the new weight goes back to the table, weight / z / n / shadow to memory
+      // FTRL-proximal on the rows this lane leads: the summed gradient from the leader sums, the old
+      // weight in wv; the new weight goes back to the table, (z, n) to the private copy
       const auto& C = COLD;
       const OptHP hf = {C.ftrl.lr, C.ftrl.gscale, C.ftrl.wd, C.ftrl.a, C.ftrl.b, C.ftrl.c, C.ftrl.d, C.ftrl.e};
+      const float ilr = __builtin_amdgcn_rcpf(hf.lr);
       float w1[4], z1[4], n1[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const int r = cid[m] >= 0 ? cid[m] : 0;
-        const float g = LF[F_WTAB + r] * hf.gscale;
+        const float g = LF[F_GS + (eg + 4 * m) * BP + eb] * hf.gscale;
         const float nn = fmaf(g, g, nl[m]);
         const float rs = __builtin_amdgcn_sqrtf(nn);
-        const float ilr = __builtin_amdgcn_rcpf(hf.lr);
         const float zz = zl[m] + g - (rs - __builtin_amdgcn_sqrtf(nl[m])) * ilr * wv[m];
         const float den = (hf.c + rs) * ilr + 2.f * hf.b;
         w1[m] = (fabsf(zz) <= hf.a) ? 0.f : -(zz - copysignf(hf.a, zz)) * __builtin_amdgcn_rcpf(den);
@@ -786,18 +827,18 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        if (lead & (1u << m)) {
-          LF[F_WTAB + cid[m]] = w1[m];
-          atomicAnd(bits + (cid[m] >> 5), ~(1u << (cid[m] & 31)));
-        }
-      // the next batch (loaded during B3) into registers / the other A0 image BEFORE the (z, n) stores:
-      // a wait for these loads must not include those stores (conditional: the compiler would wait
-      // for every outstanding access)
+        if (lead & (1u << m)) LF[F_WTAB + cid[m]] = w1[m];
+      // the next batch (loaded during B3) into registers / the other A0 image / the id table BEFORE the
+      // (z, n) stores: a wait for these loads must not include those stores (conditional: the compiler
+      // would wait for every outstanding access)
       int cn[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) cn[m] = nid[m];
       const float yn = ny;
       if (!last && evb && eg < D0) Lb[OFF_A0 + ((step + 1) & 1) * BP * SA0 + eb * SA0 + eg] = f2b(nd);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (eg + 4 * m < NWIDE) idt[(eg + 4 * m) * BP + eb] = cn[m];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
         if (lead & (1u << m)) C.zn[cid[m]] = make_float2(z1[m], n1[m]);
@@ -809,6 +850,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     bar();
     if (last) stamp(A, 6);
   }
+  stamp_clk(A, 21);
 
   // ------------------------------------------------------------------ write-back
   if (tw) {
@@ -819,7 +861,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       LF[F_RED + 8 + wave] = csum;
     }
   }
-  __syncthreads();
+  bar();
   {
     const auto& C = COLD;
     if (tid == 0) {
@@ -833,16 +875,19 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     }
     // deep parameters and state through the staging copy: sentinel-filled, the owners' values written,
     // then copied out coalesced where not the sentinel (the span's alignment gaps keep their values)
+    stamp(A, 22);
     const int span = (int)(C.deep_hi - C.deep_lo);
     unsigned* su = (unsigned*)stage;
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       float* dst = (pass ? C.ada_s : C.master) + C.deep_lo;
       for (int e = tid; e < span; e += NT) su[e] = SENT;
-      __syncthreads();
+      bar();
+      stamp(A, 23 + 3 * pass);
       if (pass) own_stage<false, true>(stage, own, wave, lane);
       else own_stage<false, false>(stage, own, wave, lane);
-      __syncthreads();
+      bar();
+      stamp(A, 24 + 3 * pass);
       // 4 elements a lane: one 16-byte store (+ 8-byte shadow) where all 4 are owned (the alignment gaps
       // between tensors are the only exceptions)
       const bool al = ((uintptr_t)dst & 15) == 0;
@@ -863,29 +908,32 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
             }
         }
       }
-      __syncthreads();
+      bar();
     }
-    // the wide part: weights from the table, (z, n) from the private copy (8 rows of a thread in flight)
-    for (int base = 0; base < C.rows; base += NT * 8) {
-      float qz[8], qn[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int r = base + tid + NT * k;
-        const float2 t = C.zn[r < C.rows ? r : 0];
-        qz[k] = t.x;
-        qn[k] = t.y;
+    stamp(A, 29);
+    // the wide part: weights from the table, (z, n) from the private copy; 4 rows a lane, 16-byte stores
+    {
+      float* wm = C.master + C.wide_off;
+      float* zs = C.ftrl_z + C.wide_off;
+      float* ns = C.ftrl_n + C.wide_off;
+      bf16_raw* sh = C.shadow ? C.shadow + C.wide_off : nullptr;
+      const int r4 = ((((uintptr_t)wm | (uintptr_t)zs | (uintptr_t)ns) & 15) == 0 && (((uintptr_t)sh) & 7) == 0)
+                         ? C.rows >> 2 : 0;
+      for (int q = tid; q < r4; q += NT) {
+        const f32x4 a = ((const f32x4*)C.zn)[2 * q], b = ((const f32x4*)C.zn)[2 * q + 1];
+        const f32x4 w = *(const f32x4*)(LF + F_WTAB + 4 * q);
+        ((f32x4*)wm)[q] = w;
+        ((f32x4*)zs)[q] = (f32x4){a[0], a[2], b[0], b[2]};
+        ((f32x4*)ns)[q] = (f32x4){a[1], a[3], b[1], b[3]};
+        if (sh) st4(sh + 4 * q, w[0], w[1], w[2], w[3]);
       }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int r = base + tid + NT * k;
-        if (r < C.rows) {
-          const long x = C.wide_off + r;
-          const float w = LF[F_WTAB + r];
-          C.master[x] = w;
-          if (C.shadow) C.shadow[x] = f2b(w);
-          C.ftrl_z[x] = qz[k];
-          C.ftrl_n[x] = qn[k];
-        }
+      for (int r = 4 * r4 + tid; r < C.rows; r += NT) {
+        const float w = LF[F_WTAB + r];
+        const float2 t = C.zn[r];
+        wm[r] = w;
+        zs[r] = t.x;
+        ns[r] = t.y;
+        if (sh) sh[r] = f2b(w);
       }
     }
     if (tid == 0) {

@@ -135,7 +135,7 @@ class FusedWideDeepStep:
         self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
         self.cursor = torch.zeros(1, device=dev, dtype=torch.int64)
         # HOPSX_PHASE_DBG=1: the kernel stamps its phase boundaries here (tools/taxi_phases.py)
-        self.dbg = (torch.zeros(20, device=dev, dtype=torch.int64)
+        self.dbg = (torch.zeros(32, device=dev, dtype=torch.int64)
                     if os.environ.get("HOPSX_PHASE_DBG") == "1" else None)
 
     def _ints(self, B: int, nbatch: int, nsteps: int = 1) -> list[int]:

@@ -30,7 +30,9 @@ if fs.kernel == "v2":
             ("  fwd: gather+L0", 7, 8), ("  fwd: L1", 8, 9), ("  fwd: L2", 9, 10), ("  fwd: L3", 10, 11),
             ("  fwd: loss+G4+dW4", 11, 12), ("  fwd: bar wait", 12, 2), ("  B3 w0: dX3", 2, 13),
             ("  B3 w0: marks", 13, 14), ("  B3 w3: dW3 x2", 2, 15), ("  B1 w0: dX1", 4, 16),
-            ("  B1 w3: put+dW1 x5", 4, 17), ("  B0 w0: dW0+FTRL", 5, 18)]
+            ("  B1 w3: put+dW1 x5", 4, 17), ("  B0 w0: dW0+FTRL", 5, 18),
+            ("  wb: loss reduce", 6, 22), ("  wb: w fill", 22, 23), ("  wb: w put", 23, 24), ("  wb: w copy", 24, 26),
+            ("  wb: s put", 26, 27), ("  wb: s copy", 27, 29), ("  wb: wide", 29, 19)]
     fs.steps_per_execution = N
     acc = {}
     for it in range(12):
@@ -41,9 +43,10 @@ if fs.kernel == "v2":
             for name, a0, a1 in rows:
                 v = (t[19] - t[1]) / N if a0 is None else t[a1] - t[a0]
                 acc.setdefault(name, []).append(v / 100.0)
+            acc.setdefault("shader clock GHz", []).append(100.0 * (t[21] - t[20]) / max(1, t[6] - t[1]) / 1000.0)
     for k, v in acc.items():
-        print(f"{k:20s} {sum(v) / len(v):8.3f} us")
-    print(f"(phase rows: the last of the launch's {N} steps)")
+        print(f"{k:20s} {sum(v) / len(v):8.3f} " + ("" if "GHz" in k else "us"))
+    print(f"(phase rows: the last of the launch's {N} steps; clock = memtime ticks per wall tick x 100 MHz)")
 else:
     names = {0: "start", 1: "staged", 10: "loss"}
     names.update({2 + l: f"fwd{l}" for l in range(8)})
