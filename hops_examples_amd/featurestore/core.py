@@ -262,6 +262,12 @@ class Query:
             if not on:
                 raise FeatureStoreException("Cannot join feature groups without common primary keys; "
                                             "pass on= or left_on=/right_on=")
+            # the order Hopsworks' query constructor emits the implicit keys in: the left feature group's
+            # primary-key order for the first join, reversed for every later one — feature_exploration.ipynb
+            # prints `store` AND `date` for sales <> exogenous (:535) but `date` AND `store` when that join
+            # follows sales <> store (:574, :610)
+            if self._joins:
+                on = on[::-1]
         self._joins.append(Join(sub_query, on or [], left_on or [], right_on or [], jt))
         return self
 

@@ -66,6 +66,22 @@ class _Staging:
 
 
 _STAGING: dict = {}
+
+
+def close_staging() -> None:
+    """Join the decode pools and free the pinned / device staging rings (parallel.dist teardown order:
+    after the comm handles, before the process group)."""
+    for st in list(_STAGING.values()):
+        for s in st.slots:
+            if s[2] is not None:
+                s[2].synchronize()
+        if st.pool is not None:
+            st.pool.shutdown(wait=True)
+            st.pool = None
+        st.slots = []
+    _STAGING.clear()
+
+
 _TLS = threading.local()  # per worker thread: {path: ParquetFile} (Arrow readers are not shared)
 
 

@@ -104,6 +104,60 @@ def self_test() -> bool:
     return ok
 
 
-def shutdown() -> None:
+# Native resources a rank holds, torn down by ``shutdown`` in a fixed order: first the P2P comm handles
+# (IPC-mapped peer buffers: unmapped while every peer and the process group still exist), then the
+# Parquet staging pools (decode threads joined, pinned memory freed while the HIP runtime is alive),
+# last the process group.  Interpreter exit runs the same order locally (atexit: no collectives), so no
+# destructor of a mapped buffer or a pool thread runs after the runtime or the group it needs is gone.
+ORDER_COMM, ORDER_STAGING = 0, 1
+_RESOURCES: list = []
+
+
+def register(obj, order: int = ORDER_COMM) -> None:
+    """Track ``obj`` (weakly) for ordered teardown: ``close()`` (collective) from ``shutdown()``,
+    ``release_local()`` (else ``close()``) at interpreter exit."""
+    import weakref
+
+    _RESOURCES.append((order, weakref.ref(obj)))
+
+
+def _teardown(collective: bool) -> list:
+    errors = []
+    for order in (ORDER_COMM, ORDER_STAGING):
+        for o, ref in reversed(list(_RESOURCES)):
+            obj = ref()
+            if o != order or obj is None:
+                continue
+            fn = obj.close if collective or not hasattr(obj, "release_local") else obj.release_local
+            try:
+                fn()
+            except Exception as e:  # noqa: BLE001 - keep tearing the rest down
+                errors.append(repr(e))
+    _RESOURCES.clear()
+    import sys
+
+    pq = sys.modules.get("hops_examples_amd.io.parquet")
+    if pq is not None:
+        pq.close_staging()
+    return errors
+
+
+def shutdown(collective: bool = True) -> None:
+    """Ordered teardown (see ``register``) and the process group.  ``collective``: every rank calls it
+    (the comm handles' close synchronises the ranks); atexit runs it with ``collective=False``."""
+    _teardown(collective)
     if dist.is_available() and dist.is_initialized():
-        dist.destroy_process_group()
+        if collective:
+            dist.destroy_process_group()
+
+
+def _at_exit() -> None:
+    try:
+        _teardown(False)
+    except Exception:  # noqa: BLE001
+        pass
+
+
+import atexit  # noqa: E402
+
+atexit.register(_at_exit)

@@ -132,6 +132,7 @@ class OneShotAllReduce:
         self._opened: list[int] = []
         self._buf, hb = C.alloc(C.STAGING_FLOATS_PER_CAP * self.cap * 4, False)
         self._flag, hf = C.alloc(C.FLAG_ROWS * C.MAX_RANKS * C.MAX_BLOCKS * 4, True)
+        hdist.register(self, hdist.ORDER_COMM)  # ordered teardown at shutdown / interpreter exit
         # two-shot (reduce-scatter + all-gather) above this size when N > 2: 2(N-1)/N * n of xGMI
         # reads per GPU instead of (N-1) * n
         self.two_shot_min = int(os.environ.get("HOPSX_TWOSHOT_MIN_KB", "256")) * 1024 // 4
@@ -248,6 +249,10 @@ class OneShotAllReduce:
             return
         torch.cuda.synchronize(self.device)
         hdist.barrier()
+        self._release()
+
+    def release_local(self) -> None:
+        """Interpreter-exit teardown (no collectives): unmap the peers' buffers, free ours."""
         self._release()
 
     def _release(self) -> None:

@@ -206,6 +206,9 @@ class PersistentMnistStep:
         g = self.geom
         local = self.loopback > 1
         err = None
+        from ..parallel import dist as hdist
+
+        hdist.register(self)  # ordered teardown (close: local) at shutdown / interpreter exit
         try:
             buf, hb = C.alloc(int(g["x_bytes"]), True)
             self._owned.append(buf)

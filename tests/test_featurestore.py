@@ -269,3 +269,25 @@ def test_training_dataset_to_device_shards_equal_rows_and_keeps_nan(fs):
     x0, _ = shards[0]
     feats = [c for c in full.columns if c != "weekly_sales"]
     np.testing.assert_allclose(x0.numpy(), full[feats].to_numpy(np.float32)[0::2][:len(full) // 2])
+
+
+def test_three_way_join_sql_matches_reference(fs):
+    """feature_exploration.ipynb:570-574 / :606-611: (sales <> store) <> exogenous, implicit keys."""
+    s = fs.create_feature_group("sales_fg", 1, primary_key=["store", "dept", "date"])
+    s.save(_sales())
+    st = fs.create_feature_group("store_fg", 1, primary_key=["store"])
+    st.save(pd.DataFrame({"store": sorted(_sales().store.unique()), "type": "A", "size": 100, "num_depts": 3}))
+    e = fs.create_feature_group("exogenous_fg", 1, primary_key=["store", "date"])
+    e.save(_exo())
+    q = s.select_all().join(st.select_all()).join(e.select(["fuel_price"]))
+    lines = q.to_string().split("\n")
+    db = fs.name
+    assert lines[1] == f"FROM `{db}`.`sales_fg_1` `fg2`"
+    assert lines[2] == f"INNER JOIN `{db}`.`store_fg_1` `fg0` ON `fg2`.`store` = `fg0`.`store`"
+    assert lines[3] == (f"INNER JOIN `{db}`.`exogenous_fg_1` `fg1` ON `fg2`.`date` = `fg1`.`date` AND "
+                        f"`fg2`.`store` = `fg1`.`store`")
+    q2 = (s.select_all().join(st.select_all()).join(e.select(["fuel_price"]).filter(e.fuel_price <= 2.7))
+          .filter(s.weekly_sales >= 50000))
+    assert q2.to_string().split("\n")[-1] == "WHERE `fg2`.`weekly_sales` >= 50000 AND `fg1`.`fuel_price` <= 2.7"
+    res = q.read()
+    assert {"type", "size", "fuel_price"} <= set(res.columns) and len(res) > 0
