@@ -333,7 +333,10 @@ inline void snappy_decompress(const uint8_t* src, size_t n, std::vector<uint8_t>
       if (off == 0 || off > op || l > len - op) throw std::runtime_error("parquet: snappy copy out of range");
       uint8_t* d = out.data() + op;
       const uint8_t* s = d - off;
-      for (size_t i = 0; i < l; ++i) d[i] = s[i];  // may overlap forward (run-length copies)
+      size_t i = 0;
+      if (off >= 8)  // 8-byte chunks never read bytes this copy writes
+        for (; i + 8 <= l; i += 8) std::memcpy(d + i, s + i, 8);
+      for (; i < l; ++i) d[i] = s[i];  // (offsets < 8: overlapping forward run-length copies, byte-wise)
       op += l;
     }
   }
