@@ -135,7 +135,14 @@ def main():
         out["r"] = step.run_resident(xs, ys, n)
 
     run.run_n = run_n
-    for i in range(a.warmup):
+    # TrainStep runs `warmup` eager steps and captures its graph on the next one: warm up past the capture
+    # (as benchmarks/run.py does), so the timed window holds replays only whatever --warmup says.  A
+    # 2-rank rehearsal with --warmup 2 otherwise timed the one-step graph's capture: 13.3 ms/step over 5
+    # steps vs 0.17 ms/step after 10 warm-up steps (profiles/r5_rehearsal_2rank_trace.txt)
+    nwarm = a.warmup
+    if step.kind == "trainstep" and getattr(step, "use_graph", False):
+        nwarm = max(nwarm, step.warmup + 2)
+    for i in range(nwarm):
         run(i)
     step.prepare_resident(xs, ys, n=a.steps)  # capture the steps_per_execution (+ remainder) graphs untimed
     el = timed(run, a.steps, dev)
@@ -195,6 +202,7 @@ def main():
                 "wire_bytes_per_param": None if dp is None else dp.wire_bytes_per_param,
                 "persistent_note": persist_note,
                 "ranks": ranks,
+                "warmup_steps_run": nwarm,
             },
             "replicas_identical": None if replicas is None else replicas["identical"],
             "final_loss": round(loss, 4),
