@@ -489,10 +489,16 @@ def cfg_resnet50(a, dev, rank, world):
     nb = 4
     xs = torch.randint(0, 256, (nb, B, 224, 224, 3), dtype=torch.uint8, device=dev)
     ys = torch.randint(0, 1000, (nb, B), device=dev)
-    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world)
+    box = {}
+    el, loss = _train_loop(m, opt, "sparse_ce", xs, ys, a.steps, a.warmup, dev, world, box=box)
+    dp = box.get("dp")
+    extra = {"final_loss": round(loss, 4)}
+    if dp is not None:
+        extra.update(allreduce=dp.path, buckets=len(getattr(dp, "buckets", [])),
+                     grad_hbm_bytes_per_param=getattr(dp, "grad_hbm_bytes_per_param", None))
     _emit(rank, "images/sec ResNet-50 224x224 (benchmark.ipynb)", B * world * a.steps / el, "images/sec", a.steps,
           a.warmup, el, world, {"model": "ResNet-50 25,557,032 params", "per_gpu_batch": B,
-                                "parallelism": f"dp{world}"}, {"final_loss": round(loss, 4)})
+                                "parallelism": f"dp{world}"}, extra)
 
 
 CONFIGS = {"mnist_launch_cpu": cfg_mnist_launch_cpu, "mnist_mirrored": cfg_mnist_mirrored, "mnist_ps": cfg_mnist_ps,

@@ -43,6 +43,34 @@
 namespace py = pybind11;
 using u = uintptr_t;
 
+// the DLPack v0 ABI (dlpack.h), the subset alloc_tensor needs to hand device memory to torch.from_dlpack
+extern "C" {
+enum { kDLFloat = 2 };
+enum { kDLROCM = 10 };
+struct DLDevice {
+  int32_t device_type;
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code, bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+}
+
 namespace {
 
 constexpr int kMaxRanks = 8;
@@ -54,6 +82,10 @@ constexpr int kWireChunk = 64;  // weight-wire mask granularity (= the arena's p
 struct Peers {
   float* buf[kMaxRanks];        // staging buffers, [parity][input | reduced | reduced bf16] = 6 * cap floats
   unsigned* flag[kMaxRanks];    // signal pages, [3 rows][kMaxRanks][kMaxBlocks] uint32 each
+};
+
+struct GradPeers {
+  const float* g[kMaxRanks];  // every rank's zero-copy arena gradient as mapped in this process
 };
 
 struct Sync {
@@ -241,6 +273,13 @@ struct DpArgs {
   unsigned long long* rng;
   const unsigned char* wmask;  // [ceil(n / 64)] 1 = bf16 weight wire for that chunk
   Prefetch pf;
+  // zero-copy gradient (fp32 wire): every rank's arena gradient IS IPC-shared memory (alloc_tensor),
+  // gpeer[r] = rank r's gradient as mapped here (own at [rank] = grad).  Phase 0 then stages nothing:
+  // owners read the peers' gradients in place, and each rank zeroes its own after the peers are done.
+  const float* gpeer[kMaxRanks];
+  int zc;           // 1: zero-copy gradients (gpeer valid)
+  int pre_reduced;  // 1: dp_rs_k already summed this rank's slice into grad (per-bucket reduce-scatter
+                    // during the backward): no gather round 1, the owner reads its own slice locally
 };
 
 // the 4 elements at i (i % 4 == 0) share one 64-element chunk
@@ -300,12 +339,50 @@ __device__ __forceinline__ float gsum1(const Peers& peers, int world, long base,
   return s;
 }
 
+// rank-ordered sum of the peers' gradients read in place (zero-copy); same order as gsum4
+__device__ __forceinline__ float4 zsum4(const DpArgs& a, int world, long i) {
+  float4 s = *reinterpret_cast<const float4*>(a.gpeer[0] + i);
+  for (int p = 1; p < world; ++p) {
+    const float4 v = *reinterpret_cast<const float4*>(a.gpeer[p] + i);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  return s;
+}
+__device__ __forceinline__ float zsum1(const DpArgs& a, int world, long j) {
+  float s = a.gpeer[0][j];
+  for (int p = 1; p < world; ++p) s += a.gpeer[p][j];
+  return s;
+}
+// the owner's summed gradient at i: staged copies (GB / copy path), the peers' gradients in place
+// (zero-copy), or this rank's own gradient already reduced by dp_rs_k (pre_reduced)
+template <bool GB>
+__device__ __forceinline__ float4 owner_g4(const DpArgs& a, const Peers& peers, int world, long base, long i) {
+  if (!GB && a.pre_reduced) return *reinterpret_cast<const float4*>(a.grad + i);
+  if (!GB && a.zc) return zsum4(a, world, i);
+  return gsum4<GB>(peers, world, base, i);
+}
+template <bool GB>
+__device__ __forceinline__ float owner_g1(const DpArgs& a, const Peers& peers, int world, long base, long j) {
+  if (!GB && a.pre_reduced) return a.grad[j];
+  if (!GB && a.zc) return zsum1(a, world, j);
+  return gsum1<GB>(peers, world, base, j);
+}
+__device__ inline void zero_range(float* g, long lo, long hi) {
+  for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+    if (i + 3 < hi) {
+      *reinterpret_cast<float4*>(g + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      for (long j = i; j < hi; ++j) g[j] = 0.f;
+    }
+  }
+}
+
 // red: this rank's reduced-fp32 region; red16: its reduced-bf16 region
 template <int KIND, bool GB>
 __device__ inline void owner_update(const DpArgs& a, const Peers& peers, int world, long base, float* red,
                                     bf16_raw* red16, long i, const OptHP& h, float bc1, float bc2) {
   constexpr int NS = nstate<KIND>();
-  const float4 g = gsum4<GB>(peers, world, base, i);
+  const float4 g = owner_g4<GB>(a, peers, world, base, i);
   float4 w = *reinterpret_cast<const float4*>(a.master + i);
   float4 x = NS >= 1 ? *reinterpret_cast<const float4*>(a.s1 + i) : make_float4(0, 0, 0, 0);
   float4 y = NS >= 2 ? *reinterpret_cast<const float4*>(a.s2 + i) : make_float4(0, 0, 0, 0);
@@ -331,7 +408,7 @@ template <int KIND, bool GB>
 __device__ inline void owner_update1(const DpArgs& a, const Peers& peers, int world, long base, float* red,
                                      bf16_raw* red16, long j, const OptHP& h, float bc1, float bc2) {
   constexpr int NS = nstate<KIND>();
-  const float g = gsum1<GB>(peers, world, base, j);
+  const float g = owner_g1<GB>(a, peers, world, base, j);
   float x = NS >= 1 ? a.s1[j] : 0.f, y = NS >= 2 ? a.s2[j] : 0.f, z = NS >= 3 ? a.s3[j] : 0.f;
   const float w = upd<KIND>(a.master[j], g * h.gscale, x, y, z, h, bc1, bc2);
   a.master[j] = w;
@@ -361,9 +438,11 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
   float* mine = peers.buf[rank] + base;
   long lo, hi;
 
+  const bool zc = !GB && a.zc;
   // phase 0: stage this workgroup's share of every slice (in the gradient wire format) and zero the
-  // local gradient for the next step's accumulation; the next batch's prefetch overlaps the wait
-  for (int sl = 0; sl < world; ++sl) {
+  // local gradient for the next step's accumulation; the next batch's prefetch overlaps the wait.
+  // Zero-copy: nothing to stage (the peers read the gradient itself); zeroing moves after the reads
+  for (int sl = 0; sl < world && !zc; ++sl) {
     S.sub(sl, b, lo, hi);
     for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
       if (i + 3 < hi) {
@@ -378,7 +457,8 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
     }
   }
   prefetch_copy(a.pf);
-  if (!flag_round(peers, rank, world, 1, b, e, sy)) return;
+  // round 1 (every rank's gradient final) — already held per bucket when dp_rs_k pre-reduced the slice
+  if (!(zc && a.pre_reduced) && !flag_round(peers, rank, world, 1, b, e, sy)) return;
 
   // phase 1: reduce + update this rank's slice; publish the new weights in their wire format
   float* red = mine + cap;
@@ -391,6 +471,9 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
       for (long j = i; j < hi; ++j) owner_update1<KIND, GB>(a, peers, world, base, red, red16, j, h, bc1, bc2);
     }
   }
+  // zero-copy: this rank's own slice of its gradient is read by nobody else — clear it now (the same
+  // threads read it above, so no barrier is needed)
+  if (zc) zero_range(a.grad, lo, hi);
   if (!flag_round(peers, rank, world, 2, b, e, sy)) return;
 
   // phase 2: every other owner's new weights -> bf16 shadow (+ fp32 master on fp32-wire chunks)
@@ -399,6 +482,9 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
     const float* src = peers.buf[p] + base + cap;
     const bf16_raw* src16 = reinterpret_cast<const bf16_raw*>(peers.buf[p] + base + 2 * cap);
     S.sub(p, b, lo, hi);
+    // zero-copy: rank p's workgroup b read our gradient over [lo, hi) in its phase 1 (or its dp_rs_k),
+    // and round 2 says it is done: clear it for the next step's accumulation
+    if (zc) zero_range(a.grad, lo, hi);
     for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
       if (i + 3 < hi) {
         if (wire16(a, i)) {
@@ -423,6 +509,49 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
   }
   if (threadIdx.x == 0) sy.epochs[b] = e;
   step_bookkeeping(a.arrive, a.step_dev, t, a.rng, a.pf);
+}
+
+// Per-bucket reduce-scatter during the backward (zero-copy gradients, fp32): launched on a side stream
+// once the bucket's last gradient kernel is done, it sums every rank's gradient over the part of THIS
+// rank's owner slice that lies in the bucket [blo, bhi) and writes the sum into this rank's own gradient
+// in place (no other rank reads this rank's gradient inside its own slice).  One flag round (row 1) per
+// launch: a peer's flag says its bucket is final.  The step tail (dp_step_k, pre_reduced) then updates
+// the slice from local memory.
+__global__ __launch_bounds__(kThreads) void dp_rs_k(float* grad, long n, long blo, long bhi, int rank, int world,
+                                                    Peers peers, GradPeers gp, Sync sy) {
+  if (poisoned(sy.err)) return;
+  const int b = blockIdx.x, G = gridDim.x;
+  const unsigned e = sy.epochs[b] + 1;
+  if (!flag_round(peers, rank, world, 1, b, e, sy)) return;
+  long L = (n + world - 1) / world;
+  L = (L + 3) & ~3L;
+  long lo = (long)rank * L, hi = lo + L;
+  if (lo < blo) lo = blo;
+  if (hi > bhi) hi = bhi;
+  if (hi > n) hi = n;
+  if (hi > lo) {
+    long per = (hi - lo + G - 1) / G;
+    per = (per + 3) & ~3L;
+    const long wlo = lo + (long)b * per;
+    const long whi = wlo + per < hi ? wlo + per : hi;
+    for (long i = wlo + 4L * threadIdx.x; i < whi; i += 4L * kThreads) {
+      if (i + 3 < whi && (i & 3) == 0) {
+        float4 s = *reinterpret_cast<const float4*>(gp.g[0] + i);
+        for (int p = 1; p < world; ++p) {
+          const float4 v = *reinterpret_cast<const float4*>(gp.g[p] + i);
+          s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        *reinterpret_cast<float4*>(grad + i) = s;
+      } else {
+        for (long j = i; j < whi && j < i + 4; ++j) {
+          float s = gp.g[0][j];
+          for (int p = 1; p < world; ++p) s += gp.g[p][j];
+          grad[j] = s;
+        }
+      }
+    }
+  }
+  if (threadIdx.x == 0) sy.epochs[b] = e;
 }
 
 py::bytes handle_of(u ptr) {
@@ -509,7 +638,7 @@ PYBIND11_MODULE(_hopsx_comm, m) {
                       u hp_dev, u step_dev, u arrive, u rng, std::vector<u> pf_src, std::vector<u> pf_dst,
                       std::vector<long> pf_bytes, u pf_cursor, int pf_nbatch, long cap, int rank, int world,
                       std::vector<u> bufs, std::vector<u> flags, u epochs, u err, int blocks, u stream,
-                      double timeout, bool grad_bf16, u wmask) {
+                      double timeout, bool grad_bf16, u wmask, std::vector<u> gpeers, bool pre_reduced) {
     const Peers pr = make_peers(rank, world, bufs, flags);
     if (n < 0 || n > cap) throw std::runtime_error("arena exceeds the staging capacity");
     if (blocks < 1 || blocks > kMaxBlocks) throw std::runtime_error("blocks out of range");
@@ -531,6 +660,19 @@ PYBIND11_MODULE(_hopsx_comm, m) {
     a.arrive = reinterpret_cast<unsigned*>(arrive);
     a.rng = reinterpret_cast<unsigned long long*>(rng);
     a.wmask = reinterpret_cast<const unsigned char*>(wmask);
+    if (!gpeers.empty()) {
+      // zero-copy gradients: one mapped pointer per rank, ours first-class at [rank] (fp32 wire only)
+      if ((int)gpeers.size() != world || grad_bf16) throw std::runtime_error("zero-copy needs one fp32 gradient per rank");
+      if (gpeers[rank] != grad) throw std::runtime_error("zero-copy: this rank's entry must be its own gradient");
+      for (int r = 0; r < world; ++r) {
+        if (!gpeers[r] || (gpeers[r] & 15u)) throw std::runtime_error("zero-copy gradients must be 16-B aligned");
+        a.gpeer[r] = reinterpret_cast<const float*>(gpeers[r]);
+      }
+      a.zc = 1;
+      a.pre_reduced = pre_reduced ? 1 : 0;
+    } else if (pre_reduced) {
+      throw std::runtime_error("pre_reduced needs zero-copy gradients");
+    }
     a.pf = Prefetch{};
     const size_t nj = std::min<size_t>(2, std::min(pf_src.size(), std::min(pf_dst.size(), pf_bytes.size())));
     if (nj > 0 && pf_cursor && pf_nbatch > 0 && arrive) {
@@ -560,5 +702,60 @@ PYBIND11_MODULE(_hopsx_comm, m) {
     }
 #undef DP_CASE
     HIP_OK(hipGetLastError());
+  });
+
+  // per-bucket reduce-scatter of zero-copy fp32 gradients (dp_rs_k): sums every rank's gradient over
+  // [blo, bhi) ∩ this rank's owner slice into this rank's own gradient; the same `blocks` on every rank
+  m.def("dp_rs", [](u grad, long n, long blo, long bhi, long cap, int rank, int world, std::vector<u> bufs,
+                    std::vector<u> flags, std::vector<u> gpeers, u epochs, u err, int blocks, u stream, double timeout) {
+    const Peers pr = make_peers(rank, world, bufs, flags);
+    if (n < 0 || n > cap || blo < 0 || bhi > n || blo > bhi) throw std::runtime_error("bad bucket range");
+    if (blocks < 1 || blocks > kMaxBlocks) throw std::runtime_error("blocks out of range");
+    if ((int)gpeers.size() != world || gpeers[rank] != grad) throw std::runtime_error("need one gradient per rank");
+    GradPeers gp{};
+    for (int r = 0; r < world; ++r) {
+      if (!gpeers[r] || (gpeers[r] & 15u)) throw std::runtime_error("gradients must be 16-B aligned");
+      gp.g[r] = reinterpret_cast<const float*>(gpeers[r]);
+    }
+    const Sync sy{reinterpret_cast<unsigned*>(epochs), reinterpret_cast<int*>(err), spin_ticks(timeout)};
+    hipLaunchKernelGGL(dp_rs_k, dim3(blocks), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<float*>(grad), n, blo, bhi, rank, world, pr, gp, sy);
+    HIP_OK(hipGetLastError());
+  });
+
+  // Device memory (hipMalloc, zeroed) handed to torch as a tensor through DLPack, plus its IPC handle:
+  // the arena gradient of the zero-copy P2P step, which the peers map and read in place.  The memory
+  // is freed when the last torch reference goes (peers' mappings keep their own reference).
+  m.def("alloc_tensor", [](long nfloats, int device) {
+    if (nfloats <= 0) throw std::runtime_error("alloc_tensor: empty");
+    void* p = nullptr;
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipMalloc(&p, nfloats * 4));
+    HIP_OK(hipMemset(p, 0, nfloats * 4));
+    HIP_OK(hipDeviceSynchronize());
+    py::bytes h = handle_of(reinterpret_cast<u>(p));
+    auto* mt = new DLManagedTensor{};
+    auto* shape = new int64_t[1]{nfloats};
+    mt->dl_tensor.data = p;
+    mt->dl_tensor.device = DLDevice{kDLROCM, device};
+    mt->dl_tensor.ndim = 1;
+    mt->dl_tensor.dtype = DLDataType{kDLFloat, 32, 1};
+    mt->dl_tensor.shape = shape;
+    mt->dl_tensor.strides = nullptr;
+    mt->dl_tensor.byte_offset = 0;
+    mt->manager_ctx = shape;
+    mt->deleter = [](DLManagedTensor* self) {
+      (void)hipFree(self->dl_tensor.data);
+      delete[] static_cast<int64_t*>(self->manager_ctx);
+      delete self;
+    };
+    // an unconsumed capsule frees the tensor itself; torch renames a consumed one "used_dltensor"
+    py::capsule cap(mt, "dltensor", [](PyObject* o) {
+      if (PyCapsule_IsValid(o, "dltensor")) {
+        auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(o, "dltensor"));
+        if (t && t->deleter) t->deleter(t);
+      }
+    });
+    return py::make_tuple(cap, reinterpret_cast<u>(p), h);
   });
 }

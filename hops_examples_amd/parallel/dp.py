@@ -41,11 +41,13 @@ from . import oneshot
 MB = 1 << 20
 
 
-def plan_buckets(arena: ParamArena, bucket_mb: float, first_bucket_mb: float | None = None):
-    """Contiguous [start, end) slices of the flat grad buffer, in backward order."""
+def plan_buckets(arena: ParamArena, bucket_mb: float, first_bucket_mb: float | None = None,
+                 min_split_mb: float = 10.0):
+    """Contiguous [start, end) slices of the flat grad buffer, in backward order; one bucket for
+    arenas of <= ``min_split_mb``."""
     ranges = arena.ranges()
     total_bytes = arena.numel * 4
-    if total_bytes <= 10 * MB or bucket_mb <= 0:
+    if total_bytes <= min_split_mb * MB or bucket_mb <= 0:
         return [(0, arena.numel, [id(p) for p, _, _ in ranges])]
     cap = int(bucket_mb * MB / 4)
     first_cap = int((first_bucket_mb or bucket_mb) * MB / 4)
@@ -77,7 +79,10 @@ class DataParallel:
             self.arena = getattr(model_or_arena, "_hx_arena", None) or ParamArena.from_module(model_or_arena)
         self.world = hdist.world_size()
         self.overlap = overlap and self.world > 1
-        self.buckets = plan_buckets(self.arena, bucket_mb)
+        # HOPSX_DP_BUCKET_MB / HOPSX_DP_MIN_SPLIT_MB override the bucket plan (tests split small models)
+        bucket_mb = float(os.environ.get("HOPSX_DP_BUCKET_MB", bucket_mb))
+        self.buckets = plan_buckets(self.arena, bucket_mb,
+                                    min_split_mb=float(os.environ.get("HOPSX_DP_MIN_SPLIT_MB", "10")))
         self._owner = {}
         for bi, (_, _, ids) in enumerate(self.buckets):
             for i in ids:
@@ -91,6 +96,12 @@ class DataParallel:
         self._oneshot = None
         if self.world > 1 and (oneshot.enabled() if p2p is None else p2p) and self.arena.grad.is_cuda:
             self._oneshot = oneshot.P2PComm.create(cap_bytes=self.arena.numel * 4, device=self.arena.grad.device)
+        self.zero_copy = False
+        if self._oneshot is not None:
+            self._setup_zero_copy()
+        self._rs_stream = None
+        self._rs_mode = False
+        self._rs_next = 0
         self._fused_opt = None
         self._wmask = None
         self._polls = 0
@@ -108,6 +119,81 @@ class DataParallel:
         if isinstance(model_or_arena, torch.nn.Module) and hasattr(model_or_arena, "register_state_dict_pre_hook"):
             model_or_arena.register_state_dict_pre_hook(self._state_dict_guard)
 
+    # -------------------------------------------------------------- zero-copy gradients
+    def _setup_zero_copy(self) -> None:
+        """Collective: put the arena gradient in IPC-shared memory that every peer maps
+        (``OneShotAllReduce.make_grad_buffer``), so the fused step's owners read the peers' gradients
+        in place — the staging copy + zeroing pass of the copy path disappears (HBM bytes per parameter
+        per step: ``grad_hbm_bytes_per_param``).  fp32 gradient wire only (a bf16 wire converts, so it
+        stages); ``HOPSX_P2P_ZEROCOPY=0`` keeps the staged copy.  The zero-copy kernels are self-tested
+        on the live buffer first; any rank failing keeps every rank on the copy path."""
+        comm = self._oneshot
+        if os.environ.get("HOPSX_P2P_ZEROCOPY", "1") != "1" or comm.grad_bf16:
+            return
+        buf = comm.make_grad_buffer(self.arena.numel)
+        if buf is None:
+            return
+        ok = False
+        try:
+            ok = oneshot.dp_self_test(comm, rounds=3)
+        except Exception:  # noqa: BLE001 - a failing self-test keeps the copy path
+            ok = False
+        if not oneshot._agree(ok):
+            comm.gpeers = []
+            return
+        self.arena.rebind_grad(buf)
+        self.zero_copy = True
+
+    @property
+    def grad_hbm_bytes_per_param(self) -> float | None:
+        """Local HBM bytes per parameter per step that the fused step tail moves for the GRADIENT (the
+        optimizer state and weights aside): staged copy = read the gradient + write the staging copy +
+        zero the gradient + the owner reading N staged copies of its 1/N slice = 4+4+4+4 = 16 (fp32 wire),
+        4+2+4+2 = 12 (bf16 wire); zero-copy = the owner's N in-place reads of its 1/N slice + the zeroing
+        = 8 (per-bucket reduce-scatter: + its 4 B in-place write and the tail's 4 B local read = 16, moved
+        into the backward's shadow)."""
+        if self._fused_opt is None:
+            return None
+        if self.zero_copy:
+            return 16.0 if self._rs_mode else 8.0
+        return 12.0 if self._oneshot.grad_bf16 else 16.0
+
+    # -------------------------------------------------------------- per-bucket reduce-scatter
+    def _rs_blocks(self) -> int:
+        return max(1, min(self._oneshot.blocks, int(os.environ.get("HOPSX_P2P_RS_BLOCKS", "64"))))
+
+    def _on_ready_rs(self, p) -> None:
+        """hooks.grad_ready subscriber of the overlapped zero-copy step: when a bucket's last gradient
+        kernel is enqueued, reduce-scatter it on the side stream while the backward goes on.  Buckets
+        are issued strictly in plan order (a bucket that completes early waits for its predecessors),
+        so every rank issues the same sequence."""
+        bi = self._owner.get(id(p))
+        if bi is None:
+            return
+        self._pending[bi] -= 1
+        while self._rs_next < len(self.buckets) and self._pending[self._rs_next] <= 0:
+            self._launch_rs(self._rs_next)
+            self._rs_next += 1
+
+    def _launch_rs(self, bi: int) -> None:
+        s, e, _ = self.buckets[bi]
+        cur = torch.cuda.current_stream(self.arena.device)
+        if self._rs_stream is None:
+            self._rs_stream = torch.cuda.Stream(self.arena.device)
+        self._rs_stream.wait_stream(cur)  # after the bucket's gradient kernels (a fork when capturing)
+        self._oneshot.dp_rs(self.arena.grad, s, e, self._rs_blocks(), self._rs_stream)
+
+    def _finish_rs(self) -> None:
+        """Issue the buckets the hooks did not (parameters without a grad_ready notification), join the
+        side stream, reset the counters for the next step."""
+        while self._rs_next < len(self.buckets):
+            self._launch_rs(self._rs_next)
+            self._rs_next += 1
+        if self._rs_stream is not None:
+            torch.cuda.current_stream(self.arena.device).wait_stream(self._rs_stream)
+        self._rs_next = 0
+        self._pending = [len(ids) for _, _, ids in self.buckets]
+
     # -------------------------------------------------------------- fused P2P step tail
     def bind_optimizer(self, opt) -> None:
         """Called by TrainStep: use the fused reduce-scatter / sharded update / all-gather kernel when
@@ -122,12 +208,24 @@ class DataParallel:
         if ok and self.overlap:
             hooks.unsubscribe(self._on_ready)  # no per-bucket all-reduce: the step tail does it all
             self.overlap = False
+            # zero-copy gradients and more than one bucket: per-bucket reduce-scatter during the backward,
+            # the tail then only updates + all-gathers (HOPSX_P2P_OVERLAP=0 keeps one tail kernel)
+            if (self.zero_copy and len(self.buckets) > 1 and not self._rs_mode
+                    and os.environ.get("HOPSX_P2P_OVERLAP", "1") == "1"):
+                self._rs_mode = True
+                self._rs_next = 0
+                self._pending = [len(ids) for _, _, ids in self.buckets]
+                hooks.subscribe(self._on_ready_rs)
 
     def fuses_optimizer(self, opt) -> bool:
         return self._fused_opt is not None and opt is self._fused_opt
 
     def fused_update(self, opt) -> None:
-        self._oneshot.dp_step(opt, self._wmask)
+        if self._rs_mode:
+            self._finish_rs()
+            self._oneshot.dp_step(opt, self._wmask, pre_reduced=True)
+        else:
+            self._oneshot.dp_step(opt, self._wmask)
         self._stale = self.master_sharded
 
     def _state_dict_guard(self, module, prefix, keep_vars) -> None:
@@ -235,7 +333,7 @@ class DataParallel:
         if self.world <= 1:
             return "none"
         if self._fused_opt is not None:
-            return "p2p-xgmi-fused-step"
+            return "p2p-xgmi-fused-step" + ("-zerocopy" if self.zero_copy else "") + ("-overlap" if self._rs_mode else "")
         if self._oneshot is not None:
             return "p2p-xgmi-allreduce"
         be = "rccl" if dist.get_backend() == "nccl" else dist.get_backend()
@@ -316,6 +414,7 @@ class DataParallel:
         """Collective.  Leaves the fp32 master complete on every rank; raises if a P2P collective
         failed since the last poll."""
         hooks.unsubscribe(self._on_ready)
+        hooks.unsubscribe(self._on_ready_rs)  # (a zero-copy gradient stays where it is: this rank's own memory)
         if getattr(self, "_closed", None) is None:
             self._closed = (self.path, self.wire_bytes_per_param, self.p2p_world)  # reported after teardown
         if self._oneshot is not None:

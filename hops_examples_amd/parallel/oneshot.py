@@ -184,10 +184,63 @@ class OneShotAllReduce:
                             (mode or self.mode(t.numel())) == "two_shot", self.timeout)
         return out
 
-    def dp_step(self, opt, wmask: torch.Tensor | None = None) -> None:
+    # ------------------------------------------------------------ zero-copy gradients
+    def make_grad_buffer(self, n: int) -> "torch.Tensor | None":
+        """Collective, fail-safe: an fp32 [n] device tensor in IPC-shared memory, mapped by every peer,
+        to be the arena gradient (``ParamArena.rebind_grad``).  The fused step then reads the peers'
+        gradients in place instead of staging a copy (``zero_copy``).  None on every rank unless every
+        rank allocated and mapped (each rank keeps its own memory either way)."""
+        C = ext()
+        t = h = None
+        try:
+            cap, ptr, h = C.alloc_tensor(int(n), self.device.index or 0)
+            t = torch.from_dlpack(cap)
+            h = bytes(h)
+        except Exception:  # noqa: BLE001 - every failure falls back to the staged copy
+            t = h = None
+        objs = [(self.rank, h)]
+        if self.world > 1:
+            objs = [None] * self.world
+            dist.all_gather_object(objs, (self.rank, h))
+        gp, opened = [0] * self.world, []
+        ok = t is not None and all(o[1] is not None for o in objs)
+        if ok:
+            try:
+                for r, hb in objs:
+                    if r == self.rank:
+                        gp[r] = t.data_ptr()
+                    else:
+                        gp[r] = C.open(hb)
+                        opened.append(gp[r])
+            except Exception:  # noqa: BLE001
+                ok = False
+        if not _agree(ok):
+            for q in opened:
+                C.close(q)
+            return None
+        self._opened += opened
+        self.gpeers = gp
+        self.zc_grad = t
+        return t
+
+    @property
+    def zero_copy(self) -> bool:
+        return bool(getattr(self, "gpeers", None)) and not self.grad_bf16
+
+    def dp_rs(self, grad: torch.Tensor, lo: int, hi: int, blocks: int, stream) -> None:
+        """Per-bucket reduce-scatter (zero-copy fp32 gradients): sum every rank's gradient over
+        [lo, hi) ∩ this rank's owner slice into ``grad`` in place, on ``stream``.  Every rank must issue
+        the same sequence of buckets with the same ``blocks``."""
+        ext().dp_rs(grad.data_ptr(), grad.numel(), int(lo), int(hi), self.cap, self.rank, self.world, self.bufs,
+                    self.flags, self.gpeers, self.epochs.data_ptr(), self.err.data_ptr(), int(blocks),
+                    stream.cuda_stream, self.timeout)
+
+    def dp_step(self, opt, wmask: torch.Tensor | None = None, pre_reduced: bool = False) -> None:
         """Reduce-scatter the arena gradient, run ``opt``'s update on this rank's slice, all-gather the
         new weights; one launch (see the module docstring).  ``opt`` must own the whole arena.
-        ``wmask`` (arena.wire_mask()): chunks whose weights travel in bf16 (ZeRO-1)."""
+        ``wmask`` (arena.wire_mask()): chunks whose weights travel in bf16 (ZeRO-1).  When the arena
+        gradient is this comm's zero-copy buffer the peers' gradients are read in place (no staging
+        copy); ``pre_reduced``: dp_rs already summed this rank's slice (per-bucket overlap)."""
         from ..ops._C import OPTIM
 
         a = opt.arena
@@ -210,7 +263,14 @@ class OneShotAllReduce:
                       opt.rng.data_ptr() if opt.rng is not None else 0, srcs, dsts, nbytes, cur, nb, self.cap,
                       self.rank, self.world, self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(),
                       self.blocks, torch.cuda.current_stream(self.device).cuda_stream, self.timeout,
-                      self.grad_bf16, wmask.data_ptr() if (wmask is not None and self.weight_bf16) else 0)
+                      self.grad_bf16, wmask.data_ptr() if (wmask is not None and self.weight_bf16) else 0,
+                      self._zc_peers(a.grad), bool(pre_reduced))
+
+    def _zc_peers(self, grad: torch.Tensor) -> list:
+        zg = getattr(self, "zc_grad", None)
+        if self.zero_copy and zg is not None and grad.data_ptr() == zg.data_ptr():
+            return list(self.gpeers)
+        return []
 
     def wire_bytes_per_param(self, bf16_fraction: float = 1.0) -> float:
         """Bytes per parameter per step of the fused step's wire (each GPU reads (N-1)/N of them);
@@ -307,6 +367,12 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
     f32 = torch.ones(n, dtype=torch.bool, device=dev)
     if wmask is not None:
         f32 = (wmask == 0).repeat_interleave(C.WIRE_CHUNK)[:n]
+    # the zero-copy gradient buffer of the comm (make_grad_buffer), when it has one
+    zg = comm.zc_grad if comm.zero_copy and getattr(comm, "zc_grad", None) is not None else None
+    if zg is not None and zg.numel() < n:
+        zg = None
+    if zg is not None:
+        saved = zg[:n].clone()
     for kind in kinds:
         k = OPTIM[kind]
         hp = _dp_selftest_hp(kind, W)
@@ -323,11 +389,23 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
         for it in range(rounds):
             grad = ((idx * (it + 3)) % 23) - 11.0 + r
             gsum = sum(((idx * (it + 3)) % 23) - 11.0 + q for q in range(W))
+            # rounds alternate the gradient paths: staged copy, zero-copy (peers read in place), and
+            # zero-copy with two per-bucket reduce-scatters ahead of a pre-reduced tail
+            zmode = it % 3 if zg is not None else 0
+            if zmode:
+                zg[:n].copy_(grad)
+                grad = zg[:n]
+            if zmode == 2:
+                half = (n // 2) & ~63
+                for lo, hi in ((half, n), (0, half)):
+                    C.dp_rs(grad.data_ptr(), n, lo, hi, comm.cap, r, W, comm.bufs, comm.flags, comm.gpeers,
+                            comm.epochs.data_ptr(), comm.err.data_ptr(), min(comm.blocks, 16), st, comm.timeout)
             C.dp_step(k, master.data_ptr(), grad.data_ptr(), states[0].data_ptr(), states[1].data_ptr(),
                       states[2].data_ptr(), shadow.data_ptr(), n, hp, hp_dev.data_ptr(), step.data_ptr(),
                       arrive.data_ptr(), 0, [], [], [], 0, 0, comm.cap, r, W, comm.bufs, comm.flags,
                       comm.epochs.data_ptr(), comm.err.data_ptr(), comm.blocks, st, comm.timeout,
-                      comm.grad_bf16, 0 if wmask is None else wmask.data_ptr())
+                      comm.grad_bf16, 0 if wmask is None else wmask.data_ptr(),
+                      list(comm.gpeers) if zmode else [], zmode == 2)
             K.optim_step(k, ref_m, gsum, ref_s[0], ref_s[1], ref_s[2], ref_sh, hp, ref_step, zero_grad=True,
                          arrive=ref_arrive, hp_dev=hp_dev)
             torch.cuda.synchronize(dev)
@@ -351,6 +429,9 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
             hdist.broadcast_(ref, 0)
             if not torch.equal(sh, ref):
                 return False
+    if zg is not None:
+        zg[:n].copy_(saved)  # the live arena gradient (zero at rest) as it was
+        torch.cuda.synchronize(dev)
     return True
 
 

@@ -93,6 +93,22 @@ class ParamArena:
                 m[o // ALIGN:-(-(o + p.numel()) // ALIGN)] = 1
         return m.to(self.device) if bool(m.any()) else None
 
+    def rebind_grad(self, buf: torch.Tensor) -> None:
+        """Move the gradient into ``buf`` (fp32, >= numel elements, same device): the zero-copy P2P step
+        hands the arena memory its peers map over xGMI (parallel/oneshot.py make_grad_buffer).  Every
+        parameter's ``.grad`` view is re-pointed; call before any graph capture (captured kernels keep
+        the pointers they were captured with)."""
+        if buf.dtype != torch.float32 or buf.numel() < self.numel or buf.device != self.device:
+            raise ValueError("rebind_grad needs an fp32 buffer of >= numel elements on the arena's device")
+        buf = buf[:self.numel]
+        with torch.no_grad():
+            buf.copy_(self.grad)
+            self.grad = buf
+            for p, o in zip(self.params, self.offsets):
+                k = p.numel()
+                p._hx_grad = self.grad[o:o + k].view(p.shape)
+                p.grad = p._hx_grad
+
     def zero_grad(self) -> None:
         self.grad.zero_()
 

@@ -54,7 +54,7 @@ def test_p2p_timeout_writes_nothing_and_poisons():
         arrive = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
         C.dp_step(3, master.data_ptr(), grad.data_ptr(), s1.data_ptr(), s2.data_ptr(), 0, shadow.data_ptr(), n,
                   [1.0, 0.5, 0.0, 0.95, 1e-7], hp.data_ptr(), step.data_ptr(), arrive.data_ptr(), 0, [], [], [], 0, 0,
-                  cap, 0, 2, bufs, flags, epochs.data_ptr(), err.data_ptr(), 8, st, 0.05, False, 0)
+                  cap, 0, 2, bufs, flags, epochs.data_ptr(), err.data_ptr(), 8, st, 0.05, False, 0, [], False)
         torch.cuda.synchronize()
         assert torch.equal(master, m0) and torch.equal(grad, g0) and float(step.item()) == 0.0
     finally:
@@ -82,14 +82,46 @@ def test_p2p_poll_and_check_raise():
     ar.close()
 
 
+# gradient paths of the fused step: zero-copy (the default: owners read the peers' arena gradients in
+# place), zero-copy + per-bucket reduce-scatter during the backward (small buckets forced so the flagship
+# model splits), and the staged copy
+DP_MODES = {
+    "zerocopy": ({}, "-zerocopy"),
+    "zerocopy-overlap": ({"HOPSX_DP_MIN_SPLIT_MB": "0", "HOPSX_DP_BUCKET_MB": "1"}, "-zerocopy-overlap"),
+    "copy": ({"HOPSX_P2P_ZEROCOPY": "0"}, ""),
+}
+
+
 @pytest.mark.gpu
-def test_dp_fused_step_two_ranks():
-    env = dict(os.environ, HOPSX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", HOPSX_P2P="1")
+@pytest.mark.parametrize("mode", sorted(DP_MODES))
+def test_dp_fused_step_two_ranks(mode):
+    extra, expect = DP_MODES[mode]
+    env = dict(os.environ, HOPSX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", HOPSX_P2P="1",
+               HOPSX_DPCHECK_EXPECT=expect, **extra)
+    port = 29641 + sorted(DP_MODES).index(mode)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29641", os.path.join(ROOT, "tools", "dp_fused_check.py")]
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "dp_fused_check.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                        timeout=110)
     assert r.returncode == 0 and "DPFUSED" in r.stdout, r.stdout[-4000:]
+    print([ln for ln in r.stdout.splitlines() if "DPFUSED" in ln][-1][:600])
+
+
+@pytest.mark.gpu
+def test_dp_step_zero_copy_self_test_world1():
+    """Zero-copy gradient paths (in place, and per-bucket reduce-scatter + pre-reduced tail) through the
+    dp self-test on a world of one (the rank is its own peer), every optimizer kind."""
+    from hops_examples_amd.parallel.oneshot import OneShotAllReduce, dp_self_test
+
+    ar = OneShotAllReduce(cap_bytes=1 << 18, device=torch.device("cuda", 0))
+    try:
+        t = ar.make_grad_buffer(1 << 16)
+        assert t is not None and ar.zero_copy and t.is_cuda and t.dtype == torch.float32
+        assert int(torch.count_nonzero(t)) == 0
+        assert dp_self_test(ar, rounds=6)
+        assert int(torch.count_nonzero(t)) == 0  # restored (zero at rest)
+    finally:
+        ar.close()
 
 
 @pytest.mark.gpu
