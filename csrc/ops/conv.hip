@@ -286,6 +286,47 @@ __global__ __launch_bounds__(256) void slab_reduce_k(const float* __restrict__ s
   }
 }
 
+// ---- small-M split-K for the forward / dgrad GEMMs of gemm_core.h's engine ------------------------
+// The stage-3/4 ResNet-50 convs at small batch (batch 8: 392 / 1,568 output pixels, K up to 4,608)
+// give a few hundred 32x32 tiles that each walk all of K alone: 58-72 us for the 7x7 3x3 layers vs
+// PyTorch's 25-28 (profiles/r5_conv_gemm_vs_torch.txt).  When plan_gemm would split K, the GEMM runs
+// as EpiAtomicTicket: every K-slice adds into a persistent zero-at-rest fp32 workspace and the slice
+// that draws the tile's last ticket applies the real epilogue (bf16 store + BN sums, or act' mask +
+// addend) and re-zeroes the tile — one launch, no memset node.  The workspaces are module-scope device
+// arrays, one per role (forward, dgrad: both only ever run on the main stream, never concurrently).
+constexpr long kConvWs = 4L << 20;  // fp32 elements per role (M x N of the GEMM)
+constexpr int kConvTk = 16384;      // tile tickets per role
+__device__ float g_conv_ws[2][kConvWs];
+__device__ unsigned g_conv_tk[2][kConvTk];
+
+static bool conv_split(int role, long M, long N, long K, float** ws, unsigned** tk) {
+  if (hopsx_deterministic() || hopsx_disabled("conv_splitk")) return false;
+  // only GEMMs with fewer tiles than CUs and a long K: at 392 tiles / K 1,024-2,304 (stage-3 convs at
+  // batch 8) the split's workspace round trip cost more than it won (profiles/r5_conv_splitk_b8.txt)
+  static const long min_k = hopsx_env_int("HOPSX_CONV_SPLIT_MINK", 2048);
+  const GemmPlan p0 = plan_gemm(M, N, K, false);
+  const int bm0 = p0.cfg == 0 ? 128 : (p0.cfg == 1 ? 64 : 32);
+  if (((M + bm0 - 1) / bm0) * ((N + bm0 - 1) / bm0) >= 256 || K < min_k) return false;
+  const GemmPlan p = plan_gemm(M, N, K, true);
+  if (p.split < 2) return false;
+  const int bm = p.cfg == 0 ? 128 : (p.cfg == 1 ? 64 : 32);
+  const long tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm);
+  if (M * N > kConvWs || tiles > kConvTk) return false;
+  static float* wsp = nullptr;
+  static unsigned* tkp = nullptr;
+  if (!wsp) {
+    void *a = nullptr, *b = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_conv_ws)) != hipSuccess ||
+        hipGetSymbolAddress(&b, HIP_SYMBOL(g_conv_tk)) != hipSuccess)
+      return false;
+    wsp = (float*)a;
+    tkp = (unsigned*)b;
+  }
+  *ws = wsp + role * kConvWs;
+  *tk = tkp + role * kConvTk;
+  return true;
+}
+
 static bool direct_ok(const ConvGeom& g) {
   const int K = g.KH * g.KW * g.C;
   return K <= 64 && g.CO % 4 == 0 && g.CO <= 256 && K * g.CO <= 1024 && !hopsx_disabled("direct_conv");
@@ -426,6 +467,13 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
   if (epi == EPI_STORE_BF16) {
     EpiStoreBF16 e{(bf16_raw*)out, N, bias, 1.f, act, colsum};
     if (gg_conv_fwd(x, w, g, e, st)) return (int)hipGetLastError();
+    float* ws;
+    unsigned* tk;
+    if (conv_split(0, M, N, K, &ws, &tk)) {
+      const SplitFinish f{tk, kEpiStoreBF16, out, N, bias, 1.f, 0.f, act, nullptr, 0, colsum, nullptr};
+      launch_gemm<true, true>(al, bl, EpiAtomicTicket{ws, N, 1.f, nullptr, f}, M, N, K, true, st);
+      return (int)hipGetLastError();
+    }
     launch_gemm<true, true>(al, bl, e, M, N, K, false, st);
   } else if (epi == EPI_STORE_F32) {
     EpiStoreF32 e{(float*)out, N, bias, 1.f, 0.f, act, colsum};
@@ -448,6 +496,13 @@ extern "C" int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int*
   DenseLoader bl{(const bf16_raw*)w, K, is_vec_ok(w, K)};
   EpiBnStatsBF16 e{(bf16_raw*)out, N, bnacc};
   if (gg_conv_fwd(x, w, g, e, st)) return (int)hipGetLastError();
+  float* ws;
+  unsigned* tk;
+  if (conv_split(0, M, N, K, &ws, &tk)) {
+    const SplitFinish f{tk, kEpiBnStatsBF16, out, N, nullptr, 1.f, 0.f, 0, nullptr, 0, bnacc, nullptr};
+    launch_gemm<true, true>(al, bl, EpiAtomicTicket{ws, N, 1.f, nullptr, f}, M, N, K, true, st);
+    return (int)hipGetLastError();
+  }
   launch_gemm<true, true>(al, bl, e, M, N, K, false, st);
   return (int)hipGetLastError();
 }
@@ -469,6 +524,14 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
   ConvWeightTLoader bl{(const bf16_raw*)w, g, (g.C % 8 == 0) && ((uintptr_t)w % 16 == 0)};
   EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act, colsum, (const bf16_raw*)addend};
   if (!y && gg_conv_dgrad(dy, w, g, e, st)) return (int)hipGetLastError();
+  float* ws;
+  unsigned* tk;
+  if (conv_split(1, M, N, K, &ws, &tk)) {
+    const SplitFinish f{tk, kEpiDActBF16, dx, N, nullptr, 1.f, 0.f, act, (const bf16_raw*)yprev, N, colsum,
+                        (const bf16_raw*)addend};
+    launch_gemm<true, false>(al, bl, EpiAtomicTicket{ws, N, 1.f, nullptr, f}, M, N, K, true, st);
+    return (int)hipGetLastError();
+  }
   launch_gemm<true, false>(al, bl, e, M, N, K, false, st);
   return (int)hipGetLastError();
 }

@@ -290,10 +290,11 @@ struct EpiAtomicF32 {  // out += alpha*acc (split-K safe)
 // re-zeroes the workspace tile and its counter — no memset node, no finishing kernel.
 // epilogue ids of ops_api.h's GemmEpi (this header does not depend on the C ABI header)
 constexpr int kEpiStoreBF16 = 0, kEpiStoreF32 = 1, kEpiDActBF16 = 3;
+constexpr int kEpiBnStatsBF16 = 4;  // (finish only) bf16 store + BN sums of the stored values (EpiBnStatsBF16)
 
 struct SplitFinish {
   unsigned* cnt;  // one counter per output tile, zero at rest
-  int epi;        // EPI_STORE_BF16 / EPI_STORE_F32 / EPI_DACT_BF16
+  int epi;        // EPI_STORE_BF16 / EPI_STORE_F32 / EPI_DACT_BF16 / kEpiBnStatsBF16
   void* out;
   long ldo;
   const float* bias;
@@ -301,7 +302,8 @@ struct SplitFinish {
   int act;
   const bf16_raw* aux;
   long ldaux;
-  float* colsum;
+  float* colsum;        // plain column sums; for kEpiBnStatsBF16 the replicas [HOPSX_BN_NREP][2N]
+  const bf16_raw* add;  // kEpiDActBF16: a gradient to add (EpiDActBF16::add), layout of out
 };
 
 struct EpiAtomicTicket {
@@ -702,7 +704,7 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
     __syncthreads();
     const SplitFinish& f = ep.fin;
     const int c = tid % BN;  // BN divides 256: a thread keeps one column
-    float csum = 0.f;
+    float csum = 0.f, csq = 0.f;
     for (int idx = tid; idx < BM * BN; idx += 256) {
       const int m = m0 + idx / BN, n = n0 + c;
       if (m >= M || n >= N) continue;
@@ -711,7 +713,13 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
       *wp = 0.f;
       if (f.epi == kEpiDActBF16) {
         if (f.aux) v *= act_grad_from_out(bf2f(f.aux[(long)m * f.ldaux + n]), f.act);
+        if (f.add) v += bf2f(f.add[(long)m * f.ldo + n]);
         ((bf16_raw*)f.out)[(long)m * f.ldo + n] = f2bf(v);
+      } else if (f.epi == kEpiBnStatsBF16) {
+        const bf16_raw b = f2bf(v);  // statistics of the stored bf16 value, as EpiBnStatsBF16
+        ((bf16_raw*)f.out)[(long)m * f.ldo + n] = b;
+        v = bf2f(b);
+        csq = fmaf(v, v, csq);
       } else {
         v = apply_act(v * f.alpha + (f.bias ? f.bias[n] : 0.f), f.act);
         if (f.epi == kEpiStoreBF16) {
@@ -725,13 +733,24 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
     }
     if (f.colsum) {
       float* red = (float*)smem;
+      const bool sq = f.epi == kEpiBnStatsBF16;
       __syncthreads();
       red[tid] = csum;
+      if (sq) red[256 + tid] = csq;
       __syncthreads();
       if (tid < BN && n0 + tid < N) {
-        float t = 0.f;
-        for (int q = tid; q < 256; q += BN) t += red[q];
-        atomicAdd(f.colsum + n0 + tid, t);
+        float t = 0.f, t2 = 0.f;
+        for (int q = tid; q < 256; q += BN) {
+          t += red[q];
+          if (sq) t2 += red[256 + q];
+        }
+        if (sq) {
+          float* d = f.colsum + (long)(bid % HOPSX_BN_NREP) * 2 * N;
+          atomicAdd(d + n0 + tid, t);
+          atomicAdd(d + N + n0 + tid, t2);
+        } else {
+          atomicAdd(f.colsum + n0 + tid, t);
+        }
       }
     }
   }

@@ -195,7 +195,7 @@ def test_bce_mse():
     close(dl, g, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("name", ["sgd", "adam", "adamw", "adadelta", "rmsprop", "adagrad"])
+@pytest.mark.parametrize("name", ["sgd", "adam", "adamw", "adadelta", "rmsprop", "rmsprop_plain", "adagrad"])
 def test_optimizers(name):
     torch.manual_seed(6)
     n = 100_003
@@ -208,6 +208,8 @@ def test_optimizers(name):
         "adamw": (torch.optim.AdamW, dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2), [1e-3, 1.0, 1e-2, 0.9, 0.999, 1e-8]),
         "adadelta": (torch.optim.Adadelta, dict(lr=1.0, rho=0.95, eps=1e-7), [1.0, 1.0, 0.0, 0.95, 1e-7]),
         "rmsprop": (torch.optim.RMSprop, dict(lr=0.01, alpha=0.9, eps=1e-7, momentum=0.5, centered=True), [0.01, 1.0, 0.0, 0.9, 1e-7, 0.5, 1.0]),
+        # no momentum, not centered: the kernel skips the two unused state streams (optim.hip s23)
+        "rmsprop_plain": (torch.optim.RMSprop, dict(lr=0.01, alpha=0.9, eps=1e-7), [0.01, 1.0, 0.0, 0.9, 1e-7, 0.0, 0.0]),
         "adagrad": (torch.optim.Adagrad, dict(lr=0.1, eps=1e-10), [0.1, 1.0, 0.0, 1e-10]),
     }[name]
     opt = cfg[0]([ref], **cfg[1])
@@ -219,12 +221,14 @@ def test_optimizers(name):
         ref.grad = g.clone()
         opt.step()
         gg = g.clone()
-        K.optim_step(_C.OPTIM[name], p, gg, s1, s2, s3, shadow, cfg[2], step)
+        K.optim_step(_C.OPTIM[name.replace("_plain", "")], p, gg, s1, s2, s3, shadow, cfg[2], step)
         assert torch.count_nonzero(gg) == 0  # zeroed for the next step
     torch.cuda.synchronize()
     assert int(step.item()) == len(grads)
     close(p, ref.detach(), rtol=1e-5, atol=1e-5)
     close(shadow, ref.detach())
+    if name == "rmsprop_plain":
+        assert torch.count_nonzero(s2) == 0 and torch.count_nonzero(s3) == 0  # never touched
 
 
 def test_dropout_mask_reuse():

@@ -1,5 +1,6 @@
 """Per-layer timing of the ResNet-50 convolution GEMMs through the hopsx dispatch (forward, dgrad,
-weight gradient), next to PyTorch's own bf16 channels-last convolution (MIOpen / hipBLASLt) for scale.
+weight gradient), next to PyTorch's own bf16 channels-last convolution (MIOpen / hipBLASLt) for scale
+(``--torch``: t_fwd / t_dgrad / t_wgrad and the hopsx / PyTorch ratios *_x).
 Run it twice — default and HOPSX_DISABLE=gg — to compare the gg engine with gemm_core.h's.
 
 usage (GPU): python tools/bench_conv_gemm.py [--batch 64] [--iters 20] [--torch]
@@ -55,6 +56,12 @@ def main():
                 dyt, xt, wt, None, [s, s], [k // 2, k // 2], [1, 1], False, [0, 0], 1, [True, False, False]), a.iters)
             row["t_dgrad"] = round(us, 1)
             tot["t_dgrad"] = tot.get("t_dgrad", 0.0) + us * n
+            us = timeit(lambda: torch.ops.aten.convolution_backward(
+                dyt, xt, wt, None, [s, s], [k // 2, k // 2], [1, 1], False, [0, 0], 1, [False, True, False]), a.iters)
+            row["t_wgrad"] = round(us, 1)
+            tot["t_wgrad"] = tot.get("t_wgrad", 0.0) + us * n
+            for name in ("fwd", "dgrad", "wgrad"):
+                row[name + "_x"] = round(row[name] / row["t_" + name], 2)
         print(json.dumps(row), flush=True)
     print(json.dumps({"batch": a.batch, "step_total_us": {k: round(v, 1) for k, v in tot.items()}}), flush=True)
 
