@@ -20,6 +20,8 @@
 
 #include "ops_api.h"
 extern "C" int hopsx_mnist_persist_occupancy(int dp);  // mnist_persist.hip
+extern "C" int hopsx_pad_cin(const float* w, long R, int C, int cp, float* out, void* out16, hipStream_t st);
+extern "C" int hopsx_unpad_cin_add(float* gpad, long R, int C, int cp, float* tgt, hipStream_t st);  // elementwise.hip
 
 namespace py = pybind11;
 extern "C" void hopsx_mlp_head_debug(void* p);
@@ -159,6 +161,12 @@ HX_PYMOD(HOPSX_MODNAME) {
                                S(st));
   });
   m.def("mnist_persist_occupancy", [](int dp) { return hopsx_mnist_persist_occupancy(dp); });
+  m.def("pad_cin", [](u w, long R, int C, int cp, u out, u out16, u st) {
+    return hopsx_pad_cin(P<float>(w), R, C, cp, P<float>(out), P<void>(out16), S(st));
+  });
+  m.def("unpad_cin_add", [](u g, long R, int C, int cp, u tgt, u st) {
+    return hopsx_unpad_cin_add(P<float>(g), R, C, cp, P<float>(tgt), S(st));
+  });
   m.def("mnist_persist_geom", []() {
     std::vector<long> g(14);
     hopsx_mnist_persist_geom(g.data());

@@ -298,3 +298,45 @@ extern "C" int hopsx_nonfinite(const void* x, long n, int is_bf16, unsigned* out
   else hipLaunchKernelGGL(nonfinite_k<float>, dim3(g), dim3(256), 0, st, (const float*)x, n, out);
   return (int)hipGetLastError();
 }
+
+// ---- input-channel padding of an image stem's conv weight (ops/functional.py _PadCinFn) ----------
+// forward: w fp32 [R][C] -> out fp32 [R][cp] and its bf16 copy (what the conv kernels read), the channels
+// C..cp-1 zero: ONE launch instead of a zero fill + a strided copy + a cast
+__global__ __launch_bounds__(256) void pad_cin_k(const float* __restrict__ w, long R, int C, int cp,
+                                                 float* __restrict__ out, bf16_raw* __restrict__ out16) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < R * cp; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cp;
+    const int c = (int)(i - r * cp);
+    const float v = c < C ? w[r * C + c] : 0.f;
+    out[i] = v;
+    out16[i] = f2bf(v);
+  }
+}
+
+// backward: tgt[R][C] += g[R][:C] (the parameter's arena gradient), g re-zeroed (a zero-at-rest
+// weight-gradient buffer the conv accumulates into): one launch instead of a zero fill + an add
+__global__ __launch_bounds__(256) void unpad_cin_add_k(float* __restrict__ g, long R, int C, int cp,
+                                                       float* __restrict__ tgt) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < R * cp; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cp;
+    const int c = (int)(i - r * cp);
+    if (c < C && tgt) tgt[r * C + c] += g[i];
+    g[i] = 0.f;
+  }
+}
+
+extern "C" int hopsx_pad_cin(const float* w, long R, int C, int cp, float* out, void* out16, hipStream_t st) {
+  if (R <= 0 || C <= 0 || cp < C) return -1;
+  long g = (R * cp + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(pad_cin_k, dim3(g), dim3(256), 0, st, w, R, C, cp, out, (bf16_raw*)out16);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hopsx_unpad_cin_add(float* gpad, long R, int C, int cp, float* tgt, hipStream_t st) {
+  if (R <= 0 || C <= 0 || cp < C) return -1;
+  long g = (R * cp + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(unpad_cin_add_k, dim3(g), dim3(256), 0, st, gpad, R, C, cp, tgt);
+  return (int)hipGetLastError();
+}

@@ -40,7 +40,11 @@ def _cpu_act(y, act):
 def _wgrad_buf(p):
     g = _arena.grad_target(p)
     if g is None:
-        g = torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+        # a zero-at-rest buffer the weight's producer keeps (the padded image-stem weight, _PadCinFn),
+        # else a fresh zeroed one
+        g = getattr(p, "_hx_wbuf", None)
+        if g is None:
+            g = torch.zeros(p.shape, device=p.device, dtype=torch.float32)
     return g
 
 
@@ -670,16 +674,35 @@ class _PadCinFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, cp):
         ctx.w = w
-        return torch.nn.functional.pad(w.detach(), (0, cp - w.shape[-1]))
+        if not w.is_cuda or "pad_cin" in _disabled():
+            return torch.nn.functional.pad(w.detach(), (0, cp - w.shape[-1]))
+        # GPU: one kernel writes the padded fp32 weight AND the bf16 copy the conv reads (tagged as its
+        # shadow); its weight gradient goes into a zero-at-rest buffer kept on the parameter, which the
+        # backward folds into the arena gradient and re-zeroes in one launch (no fill / copy / cast /
+        # add launches of PyTorch's own in the step)
+        out, out16 = K.pad_cin(w.detach(), cp)
+        out._hx_shadow = out16
+        wb = getattr(w, "_hx_padgrad", None)
+        if wb is None or wb.shape != out.shape:
+            wb = torch.zeros(out.shape, device=w.device, dtype=torch.float32)  # warm-up (eager), not in capture
+            w._hx_padgrad = wb
+        out._hx_wbuf = wb
+        return out
 
     @staticmethod
     def backward(ctx, g):
         w = ctx.w
-        gs = g[..., :w.shape[-1]]
         tgt = _arena.grad_target(w)
+        if g.is_cuda and g is getattr(w, "_hx_padgrad", None):
+            # g is the zero-at-rest buffer: add its first C channels to the arena gradient (or a fresh
+            # one) and re-zero it, one launch; accumulate BEFORE announcing (the DP overlap hook may
+            # launch this bucket's reduction the moment the stem weight, the last gradient, is ready)
+            out = tgt if tgt is not None else torch.zeros(w.shape, device=w.device, dtype=torch.float32)
+            K.unpad_cin_add(g, w.shape[-1], out)
+            hooks.grad_ready(w)
+            return (None if tgt is not None else out), None
+        gs = g[..., :w.shape[-1]]
         if tgt is not None:
-            # accumulate BEFORE announcing: the DP overlap hook may launch this bucket's all-reduce
-            # (stream-ordered) the moment the stem weight — the last gradient of backward — is ready
             tgt.add_(gs)
             hooks.grad_ready(w)
             return None, None

@@ -461,6 +461,25 @@ def cast_f32_bf16(x, out=None):
     return out
 
 
+def pad_cin(w, cp, out=None, out16=None):
+    """w fp32 [..., C] -> (fp32 [..., cp], bf16 [..., cp]) with channels C..cp-1 zero, one launch."""
+    _req(w, F32, "w")
+    shp = tuple(w.shape[:-1]) + (int(cp),)
+    out = torch.empty(shp, device=w.device, dtype=F32) if out is None else out
+    out16 = torch.empty(shp, device=w.device, dtype=BF16) if out16 is None else out16
+    R = w.numel() // w.shape[-1]
+    check(_C.ext().pad_cin(ptr(w), R, w.shape[-1], int(cp), ptr(out), ptr(out16), stream()), "pad_cin")
+    return out, out16
+
+
+def unpad_cin_add(gpad, C, tgt):
+    """tgt[..., :C] += gpad[..., :C] (tgt: [..., C] fp32, may be None), then gpad = 0; one launch."""
+    _req(gpad, F32, "gpad")
+    R = gpad.numel() // gpad.shape[-1]
+    check(_C.ext().unpad_cin_add(ptr(gpad), R, int(C), gpad.shape[-1], 0 if tgt is None else ptr(tgt), stream()),
+          "unpad_cin_add")
+
+
 _COL_DT = {torch.float32: 0, torch.float64: 1, torch.int64: 2, torch.int32: 3, torch.int16: 4, torch.int8: 5,
            torch.uint8: 6, torch.float16: 7}
 

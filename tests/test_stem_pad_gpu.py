@@ -56,3 +56,29 @@ def test_padded_stem_matches_unpadded(depth):
     torch.testing.assert_close(y1, y0, rtol=2e-2, atol=2e-2)
     rel = float((g1 - g0).norm() / g0.norm())
     assert rel < 1e-2, rel
+
+
+def test_pad_cin_kernels_and_zero_at_rest_grad_buffer():
+    """_PadCinFn on the GPU: one kernel writes the padded fp32 weight and its bf16 shadow; the conv's
+    weight gradient lands in a zero-at-rest buffer on the parameter that the backward folds into the
+    arena gradient (channels < C) and re-zeroes — three steps in a row accumulate exactly."""
+    from hops_examples_amd.ops import functional as HF
+
+    torch.manual_seed(2)
+    w = torch.nn.Parameter(torch.randn(16, 3, 3, 3, device=dev))
+    w._hx_grad = torch.zeros_like(w)
+    w.grad = w._hx_grad
+    total = torch.zeros(16, 3, 3, 8, device=dev)
+    for _ in range(3):
+        w8 = HF.pad_input_channels(w, 8)
+        assert torch.equal(w8[..., :3], w.detach()) and int(torch.count_nonzero(w8[..., 3:])) == 0
+        assert torch.equal(w8._hx_shadow, w8.to(torch.bfloat16))
+        buf = w8._hx_wbuf
+        assert buf is w._hx_padgrad and int(torch.count_nonzero(buf)) == 0
+        g = torch.randn(16, 3, 3, 8, device=dev)
+        buf.copy_(g)  # what the conv's weight-gradient kernel accumulates
+        total += g
+        w8.backward(buf)
+        torch.cuda.synchronize()
+        assert int(torch.count_nonzero(buf)) == 0  # re-zeroed
+    torch.testing.assert_close(w._hx_grad, total[..., :3])
