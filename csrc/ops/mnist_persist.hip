@@ -146,6 +146,8 @@ struct Args {
   int nsteps;
   int acquire;  // 1: agent-scope acquire after every poll (diagnostic; the sc1 form needs none)
   long long tmo;  // wall-clock ticks a poll waits before it declares the producer lost
+  int pollw, stagger;  // waves polling a hand-off wait and their start offsets (HOPSX_PERSIST_POLLW / _STAGGER)
+  int pollw_a, pollw_b, pollw_c, pollw_d;  // per hand-off (HOPSX_PERSIST_POLLW_A.._D, default POLLW; C: 4)
   float inv_gb;   // 1 / global batch (world * B): the loss is the mean over every replica's images
   // data parallel (DP instantiation)
   int world, rank;
@@ -199,33 +201,78 @@ __device__ __forceinline__ int xslot(const Args& a, int peer) { return a.loopbac
 // Wave 0 polls flags[0..n) until every word equals `epoch` (relaxed sc1 loads + s_sleep); gives up
 // on the sticky error word or after a.tmo ticks (recording `code`).  Returns the verdict to the
 // whole workgroup (uniform).
+// pollw > 1 (HOPSX_PERSIST_POLLW): that many waves poll, their first polls staggered by `stagger` x 64
+// cycles, so a flag that lands between two polls of one wave is seen by the next wave's poll — the
+// detection delay shrinks from ~half a poll round trip toward ~half of that over pollw.  The first
+// wave to see every flag (or the error) tells the others through the LDS word s_ok[1], set to this
+// wait's `code` (unique per phase and step, never 0); s_ok[0] carries the verdict as before.
 __device__ __forceinline__ bool wait_all(const unsigned* flags, int n, unsigned epoch, unsigned* err, unsigned code,
-                                      int acquire, int* s_ok, long long tmo) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
+                                      int acquire, int* s_ok, long long tmo, int pollw = 1, int stagger = 0) {
+  if (pollw <= 1) {
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      int good = 1;
+      const long long t0 = wall_clock64();
+      for (unsigned spins = 0;; ++spins) {
+        int ok = 1;
+        for (int k = lane; k < n; k += 64) ok &= flag_load(flags + k) == epoch;
+        if (__all(ok)) break;
+        if (__builtin_amdgcn_readfirstlane(flag_load(err)) != 0u) {
+          good = 0;
+          break;
+        }
+        if ((spins & 15u) == 15u && wall_clock64() - t0 > tmo) {
+          if (lane == 0) atomicCAS(err, 0u, code);
+          good = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (acquire && good) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain();
+      if (lane == 0) *s_ok = good;
+    }
+    __syncthreads();
+    const int g = *s_ok;
+    return g != 0;
+  }
+  volatile int* gen = s_ok + 1;
+  const int wave = threadIdx.x >> 6;
+  if (wave < pollw) {
+    const int lane = threadIdx.x & 63;
     int good = 1;
+    for (int d = 0; d < wave * stagger; ++d) __builtin_amdgcn_s_sleep(1);
     const long long t0 = wall_clock64();
     for (unsigned spins = 0;; ++spins) {
+      if (__builtin_amdgcn_readfirstlane(*gen) == (int)code) break;  // another wave saw it
       int ok = 1;
       for (int k = lane; k < n; k += 64) ok &= flag_load(flags + k) == epoch;
-      if (__all(ok)) break;
-      if (__builtin_amdgcn_readfirstlane(flag_load(err)) != 0u) {
-        good = 0;
+      if (__all(ok)) {
+        if (lane == 0) {
+          s_ok[0] = 1;
+          *gen = (int)code;
+        }
         break;
       }
+      if (__builtin_amdgcn_readfirstlane(flag_load(err)) != 0u) good = 0;
       if ((spins & 15u) == 15u && wall_clock64() - t0 > tmo) {
         if (lane == 0) atomicCAS(err, 0u, code);
         good = 0;
+      }
+      if (!good) {
+        if (lane == 0) {
+          s_ok[0] = 0;
+          *gen = (int)code;
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (acquire && good) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     drain();
-    if (lane == 0) *s_ok = good;
   }
   __syncthreads();
-  const int g = *s_ok;
+  const int g = s_ok[0];
   return g != 0;
 }
 
@@ -543,7 +590,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     if (s + 1 < a.nsteps) xv = xload(s + 1);  // next step's patch, consumed next iteration
     stamp(a, s, 2);
     // ---- B: dh of all 32 images ----
-    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(2, s), a.acquire, s_ok, a.tmo)) return;
+    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(2, s), a.acquire, s_ok, a.tmo, a.pollw_b, a.stagger)) return;
     if constexpr (DP) {
       drain();
       __syncthreads();
@@ -724,7 +771,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     stamp(a, s, 6);
     // ---- slice owners: fixed-order reduce of 52 params over the 169 partials, Adadelta, publish D ----
     if (owner) {
-      if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok, a.tmo)) return;
+      if (!wait_all(a.flags + FL_C, NPOS, ep, a.err, ecode(3, s), a.acquire, s_ok, a.tmo, a.pollw_c, a.stagger)) return;
       stamp(a, s, 7);
       const int e0 = p * SLICE;
       if (tid < 13 * NRED) {
@@ -869,7 +916,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     if (s + 1 < a.nsteps) draw_keep(s + 1);  // KEEP is next read after the D wait's barrier
     stamp(a, s, 9);
     // ---- D: the updated conv parameters for the next step ----
-    if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok, a.tmo)) return;
+    if (!wait_all(a.flags + FL_D, NSLICE, ep, a.err, ecode(4, s), a.acquire, s_ok, a.tmo, a.pollw_d, a.stagger)) return;
     stamp(a, s, 10);
     {
       const auto R = rsrc((const unsigned char*)a.slabD + (long)par * D_BYTES);
@@ -975,7 +1022,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     const int par = s & 1;
     const int y = (int)a.ys[((cur0 + s) % a.nbatch) * B + i];
     // ---- A: reduce the 169 fc1 partial rows of image i (fixed order) ----
-    if (!wait_all(a.flags + FL_A, NPOS, ep, a.err, ecode(1, s), a.acquire, s_ok, a.tmo)) return;
+    if (!wait_all(a.flags + FL_A, NPOS, ep, a.err, ecode(1, s), a.acquire, s_ok, a.tmo, a.pollw_a, a.stagger)) return;
     stamp(a, s, 0);
     {
       const int n4 = tid & 31, g = tid >> 5;
@@ -1044,7 +1091,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     }
     stamp(a, s, 1);
     // ---- replicated fc2 / fc1-bias update from every image's payload ----
-    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(5, s), a.acquire, s_ok, a.tmo)) return;
+    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(5, s), a.acquire, s_ok, a.tmo, a.pollw, a.stagger)) return;
     {
       const auto R = rsrc(a.slabB + (long)par * NHEAD * PAY);
       constexpr int NK = (NHEAD * PAY / 4 + 255) / 256;
@@ -1185,14 +1232,15 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
 template <bool DP>
 __global__ __launch_bounds__(256, 1) void mnist_persist_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int s_ok;
+  __shared__ int s_ok[2];  // [0] a wait's verdict, [1] the multi-wave wait's done word (wait_all)
+  if (threadIdx.x == 0) s_ok[0] = s_ok[1] = 0;  // (read after the first barrier of either role)
   const OptHP hp = load_hp(a.hp, a.hp_dev);
   const long long cur0 = a.cursor[0];
   const long long xs0 = DP ? a.xstep[0] : 0;
   if (blockIdx.x < NPOS) {
-    position_wg<DP>(a, smem, &s_ok, hp, cur0, a.rng[0], a.rng[1], xs0);
+    position_wg<DP>(a, smem, s_ok, hp, cur0, a.rng[0], a.rng[1], xs0);
   } else {
-    head_wg<DP>(a, smem, &s_ok, hp, cur0, xs0);
+    head_wg<DP>(a, smem, s_ok, hp, cur0, xs0);
   }
 }
 
@@ -1240,6 +1288,20 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.loopback = (int)iv[15];
   a.xfence = (int)iv[17];
   a.tmo = (long long)iv[16] * 100000ll;  // ms -> 100 MHz ticks
+  a.pollw = (int)hopsx_env_int("HOPSX_PERSIST_POLLW", 1);
+  a.stagger = (int)hopsx_env_int("HOPSX_PERSIST_STAGGER", 12);
+  if (a.pollw < 1 || a.pollw > 4) a.pollw = 1;
+  // per hand-off: the slice owners' wait on the 169 conv-gradient partials polls from 4 waves by default
+  // (C hop 2.6 -> 1.9 us, bench 1.16 -> 1.22 M img/s at 200 steps: profiles/r5_persist_pollw_ab.txt);
+  // the same on every wait made the head and B hops slower (more pollers on the flag lines)
+  auto pw = [&](const char* name, long dflt) {
+    const long v = hopsx_env_int(name, dflt);
+    return (int)(v >= 1 && v <= 4 ? v : 1);
+  };
+  a.pollw_a = pw("HOPSX_PERSIST_POLLW_A", a.pollw);
+  a.pollw_b = pw("HOPSX_PERSIST_POLLW_B", a.pollw);
+  a.pollw_c = pw("HOPSX_PERSIST_POLLW_C", 4);
+  a.pollw_d = pw("HOPSX_PERSIST_POLLW_D", a.pollw);
   a.inv_gb = 1.f / (float)(world * B);
   if (dp) {
     a.xstep = (long long*)p[18];
