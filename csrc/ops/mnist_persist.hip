@@ -241,7 +241,10 @@ __device__ __forceinline__ bool wait_all(const unsigned* flags, int n, unsigned 
   if (wave < pollw) {
     const int lane = threadIdx.x & 63;
     int good = 1;
-    for (int d = 0; d < wave * stagger; ++d) __builtin_amdgcn_s_sleep(1);
+    // (the stagger checks the done word too: when the flags are already there, wave 0's first poll ends
+    // the wait and the later waves must not sleep out their offsets before the barrier)
+    for (int d = 0; d < wave * stagger && __builtin_amdgcn_readfirstlane(*gen) != (int)code; ++d)
+      __builtin_amdgcn_s_sleep(1);
     const long long t0 = wall_clock64();
     for (unsigned spins = 0;; ++spins) {
       if (__builtin_amdgcn_readfirstlane(*gen) == (int)code) break;  // another wave saw it
