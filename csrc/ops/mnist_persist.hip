@@ -148,6 +148,7 @@ struct Args {
   long long tmo;  // wall-clock ticks a poll waits before it declares the producer lost
   int pollw, stagger;  // waves polling a hand-off wait and their start offsets (HOPSX_PERSIST_POLLW / _STAGGER)
   int pollw_a, pollw_b, pollw_c, pollw_d;  // per hand-off (HOPSX_PERSIST_POLLW_A.._D, default POLLW; C: 4)
+  int head1w;          // 1: one wave computes the head from registers and publishes B (HOPSX_PERSIST_HEAD1W)
   float inv_gb;   // 1 / global batch (world * B): the loss is the mean over every replica's images
   // data parallel (DP instantiation)
   int world, rank;
@@ -164,6 +165,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
 // write-through (sc1) 16-B store / sc1 16-B load (L1 bypass): the hand-off payload path
 __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, byte_off, 0, 16);
+}
+__device__ __forceinline__ void st_sc1x2(__amdgpu_buffer_rsrc_t r, int byte_off, float x, float y) {
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64((v2i){__float_as_int(x), __float_as_int(y)}, r, byte_off, 0, 16);
 }
 __device__ __forceinline__ f32x4 ld_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
@@ -1044,6 +1049,67 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
       *(f32x4*)(RED + g * HID + n4 * 4) = acc;
     }
     __syncthreads();
+    if (a.head1w) {
+      // one wave does the whole head from registers (HOPSX_PERSIST_HEAD1W): lane l owns hidden units 2l,
+      // 2l+1, the 10 logits are wave sums, softmax / dlogits / dh in registers, and the B payload leaves
+      // as 8-B write-through stores from this wave alone (its drain then its flag: no barrier, no LDS
+      // round trip) — four barriers and three LDS passes off the critical A -> B chain
+      if (tid < 64) {
+        const int n0 = 2 * lane;
+        float h[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float v = 0.f;
+#pragma unroll
+          for (int g = 0; g < 8; ++g) v += RED[g * HID + n0 + u];
+          h[u] = fmaxf(v + HB1[n0 + u], 0.f);
+        }
+        float z[NCLS];
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c)
+          z[c] = wave_sum(fmaf(h[1], HW[c * HID + n0 + 1], h[0] * HW[c * HID + n0])) + HB2[c];
+        float m = z[0];
+#pragma unroll
+        for (int c = 1; c < NCLS; ++c) m = fmaxf(m, z[c]);
+        float e[NCLS], se = 0.f, zy = 0.f;
+        int am = NCLS;
+#pragma unroll
+        for (int c = NCLS - 1; c >= 0; --c) {
+          e[c] = __expf(z[c] - m);
+          if (z[c] == m) am = c;  // the first maximum
+          if (c == y) zy = z[c];
+        }
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) se += e[c];
+        const float inv_se = 1.f / se;
+        float dl[NCLS];
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) dl[c] = (e[c] * inv_se - (c == y ? 1.f : 0.f)) * a.inv_gb;
+        float dh[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float d = 0.f;
+#pragma unroll
+          for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], HW[c * HID + n0 + u], d);
+          dh[u] = h[u] > 0.f ? d : 0.f;
+        }
+        const auto R = rsrc(a.slabB + ((long)par * NHEAD + i) * PAY);
+        st_sc1x2(R, (PAY_DH + n0) * 4, dh[0], dh[1]);
+        st_sc1x2(R, (PAY_H + n0) * 4, h[0], h[1]);
+        float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCLS; c += 2)
+          if (lane == c / 2) {
+            p0 = dl[c];
+            p1 = dl[c + 1];
+          }
+        if (lane < NCLS / 2) st_sc1x2(R, (PAY_DL + 2 * lane) * 4, p0, p1);
+        if (lane == NCLS / 2) st_sc1x2(R, PAY_LOSS * 4, __logf(se) + m - zy, am == y ? 1.f : 0.f);
+        drain();
+        if (lane == 0) flag_store(a.flags + FL_B + i, ep);
+      }
+    }
+    if (!a.head1w) {
     if (tid < HID) {
       float v = 0.f;
 #pragma unroll
@@ -1091,6 +1157,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
       drain();
       __syncthreads();
       if (tid == 0) flag_store(a.flags + FL_B + i, ep);
+    }
     }
     stamp(a, s, 1);
     // ---- replicated fc2 / fc1-bias update from every image's payload ----
@@ -1305,6 +1372,7 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.pollw_b = pw("HOPSX_PERSIST_POLLW_B", a.pollw);
   a.pollw_c = pw("HOPSX_PERSIST_POLLW_C", 4);
   a.pollw_d = pw("HOPSX_PERSIST_POLLW_D", a.pollw);
+  a.head1w = (int)hopsx_env_int("HOPSX_PERSIST_HEAD1W", 1);  // 25.8 -> 25.5 us/step (r5_persist_pollw_ab.txt)
   a.inv_gb = 1.f / (float)(world * B);
   if (dp) {
     a.xstep = (long long*)p[18];
