@@ -33,7 +33,8 @@
 // payload stored write-through (16-B `sc1` buffer stores), every storing wave drains vmcnt, a
 // workgroup barrier, ONE lane stores the flag (agent-scope relaxed = `global_store sc1`); the consumer
 // polls the flags relaxed from one wave, then a barrier, then EVERY payload load is an `sc1` buffer
-// load.  Flags are zeroed by a memset node before every launch; epoch = step + 1 (never 0).  Every
+// load.  Flag epochs grow across launches (epoch = base + step + 1, the 64-bit base kept after the flag
+// rows and advanced by nsteps at the end of each launch), so no memset precedes a launch.  Every
 // poll is bounded (wall clock) and also watches a sticky error word, so a fault drains the grid.
 // Payload buffers are double-buffered by step parity.
 //
@@ -57,6 +58,7 @@ constexpr int GRID = NPOS + NHEAD;  // 201 workgroups, one per CU
 constexpr int PAY = 272;            // head payload floats
 constexpr int PAY_DH = 0, PAY_H = 128, PAY_DL = 256, PAY_LOSS = 268, PAY_COR = 269;
 constexpr int FL_A = 0, FL_B = 256, FL_C = 512, FL_D = 768, FL_WORDS = 1024;
+constexpr int FL_EPOCH = FL_WORDS - 2;  // 64-bit epoch base after the flag rows (8-B aligned)
 // D payload (updated conv parameters): the conv2 weights as bf16 (what the MFMAs read), then the 224
 // small fp32 parameters [b2 | conv1 w | conv1 b]
 constexpr int D_F32 = OFF_B2 * 2;                 // byte offset of the fp32 part
@@ -136,7 +138,7 @@ struct Args {
   float* slabB;  // [2][32][PAY]
   float* slabC;  // [2][169][NCONV]
   float* slabD;  // [2][D_BYTES / 4]
-  unsigned* flags;  // [FL_WORDS], zeroed before the launch
+  unsigned* flags;  // [FL_WORDS]: flag rows + the epoch base (zeroed once at allocation)
   unsigned* err;    // sticky error word (0 = ok)
   float* out;       // [nsteps][2]: mean loss, correct count
   unsigned long long* dbg;  // optional [GRID][nsteps][16] wall-clock phase stamps
@@ -375,7 +377,7 @@ __device__ __forceinline__ void stamp(const Args& a, int s, int ph) {
 template <bool DP>
 __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, int* s_ok, const OptHP& hp,
                                             long long cur0, unsigned long long seed, unsigned long long ctr0,
-                                            long long xs0) {
+                                            long long xs0, unsigned long long eb) {
   const int p = blockIdx.x, ph = p / PH, pw = p - ph * PH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int tq = fr >> 2, tp = fr & 3;
@@ -456,7 +458,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
   __syncthreads();
 
   for (int s = 0; s < a.nsteps; ++s) {
-    const unsigned ep = (unsigned)s + 1u;
+    const unsigned ep = (unsigned)(eb + (unsigned long long)s + 1ull);
     const int par = s & 1;
     // lane indices re-derived from an opaque zero every step: otherwise the compiler hoists every
     // LDS address of the step body out of the loop and runs out of registers (spills to scratch)
@@ -978,6 +980,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
   if (p == 0 && tid == 0) {
     if constexpr (DP) a.xstep[0] = xs0 + a.nsteps;
     a.cursor[0] = (cur0 + a.nsteps) % a.nbatch;
+    *(unsigned long long*)(a.flags + FL_EPOCH) = eb + (unsigned long long)a.nsteps;
     a.rng[1] = ctr0 + (unsigned long long)a.nsteps;
     if (a.step_dev) a.step_dev[0] += (float)a.nsteps;
   }
@@ -989,7 +992,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
 // ------------------------------------------------------------------------------------------------
 template <bool DP>
 __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int* s_ok, const OptHP& hp,
-                                        long long cur0, long long xs0) {
+                                        long long cur0, long long xs0, unsigned long long eb) {
   const int i = blockIdx.x - NPOS;
   const int tid = threadIdx.x, lane = tid & 63;
   float* HW = (float*)(smem + H_W2);
@@ -1026,7 +1029,7 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
   __syncthreads();
 
   for (int s = 0; s < a.nsteps; ++s) {
-    const unsigned ep = (unsigned)s + 1u;
+    const unsigned ep = (unsigned)(eb + (unsigned long long)s + 1ull);
     const int par = s & 1;
     const int y = (int)a.ys[((cur0 + s) % a.nbatch) * B + i];
     // ---- A: reduce the 169 fc1 partial rows of image i (fixed order) ----
@@ -1307,10 +1310,11 @@ __global__ __launch_bounds__(256, 1) void mnist_persist_k(const Args a) {
   const OptHP hp = load_hp(a.hp, a.hp_dev);
   const long long cur0 = a.cursor[0];
   const long long xs0 = DP ? a.xstep[0] : 0;
+  const unsigned long long eb = *(const unsigned long long*)(a.flags + FL_EPOCH);
   if (blockIdx.x < NPOS) {
-    position_wg<DP>(a, smem, s_ok, hp, cur0, a.rng[0], a.rng[1], xs0);
+    position_wg<DP>(a, smem, s_ok, hp, cur0, a.rng[0], a.rng[1], xs0, eb);
   } else {
-    head_wg<DP>(a, smem, s_ok, hp, cur0, xs0);
+    head_wg<DP>(a, smem, s_ok, hp, cur0, xs0, eb);
   }
 }
 
@@ -1320,6 +1324,9 @@ __global__ __launch_bounds__(256, 1) void mnist_persist_k(const Args a) {
 //       [xstep xbuf[world] xflag[world]]   (world > 1: the data-parallel instantiation)
 // iv:   off[8] nbatch salt nsteps batch acquire world rank loopback timeout_ms xfence
 // fv:   drop_p xscale xshift lr gscale wd rho eps
+static int g_persist_reload = 0;
+extern "C" void hopsx_mnist_persist_reload_knobs() { g_persist_reload = 1; }
+
 extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, int ni, const float* fv, int nf,
                                    hipStream_t st) {
   using namespace mnistp;
@@ -1358,21 +1365,34 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.loopback = (int)iv[15];
   a.xfence = (int)iv[17];
   a.tmo = (long long)iv[16] * 100000ll;  // ms -> 100 MHz ticks
-  a.pollw = (int)hopsx_env_int("HOPSX_PERSIST_POLLW", 1);
-  a.stagger = (int)hopsx_env_int("HOPSX_PERSIST_STAGGER", 12);
-  if (a.pollw < 1 || a.pollw > 4) a.pollw = 1;
-  // per hand-off: the slice owners' wait on the 169 conv-gradient partials polls from 4 waves by default
-  // (C hop 2.6 -> 1.9 us, bench 1.16 -> 1.22 M img/s at 200 steps: profiles/r5_persist_pollw_ab.txt);
-  // the same on every wait made the head and B hops slower (more pollers on the flag lines)
-  auto pw = [&](const char* name, long dflt) {
-    const long v = hopsx_env_int(name, dflt);
-    return (int)(v >= 1 && v <= 4 ? v : 1);
-  };
-  a.pollw_a = pw("HOPSX_PERSIST_POLLW_A", a.pollw);
-  a.pollw_b = pw("HOPSX_PERSIST_POLLW_B", a.pollw);
-  a.pollw_c = pw("HOPSX_PERSIST_POLLW_C", 4);
-  a.pollw_d = pw("HOPSX_PERSIST_POLLW_D", a.pollw);
-  a.head1w = (int)hopsx_env_int("HOPSX_PERSIST_HEAD1W", 1);  // 25.8 -> 25.5 us/step (r5_persist_pollw_ab.txt)
+  // launch knobs (environment), read once and again after hopsx_mnist_persist_reload_knobs (tools/persist_ab.py)
+  static int kn_ok = 0, kn_pollw, kn_stagger, kn_a, kn_b, kn_c, kn_d, kn_head1w, kn_memset;
+  if (!kn_ok || g_persist_reload) {
+    auto pw = [&](const char* name, long dflt) {
+      const long v = hopsx_env_int(name, dflt);
+      return (int)(v >= 1 && v <= 4 ? v : 1);
+    };
+    kn_pollw = pw("HOPSX_PERSIST_POLLW", 1);
+    kn_stagger = (int)hopsx_env_int("HOPSX_PERSIST_STAGGER", 12);
+    // per hand-off: the slice owners' wait on the 169 conv-gradient partials polls from 4 waves by default
+    // (C hop 2.6 -> 1.9 us, 27.6 -> 26.0 us/step: profiles/r5_persist_pollw_ab.txt); the same on the other
+    // waits measured slower (more pollers on the flag lines)
+    kn_a = pw("HOPSX_PERSIST_POLLW_A", kn_pollw);
+    kn_b = pw("HOPSX_PERSIST_POLLW_B", kn_pollw);
+    kn_c = pw("HOPSX_PERSIST_POLLW_C", 4);
+    kn_d = pw("HOPSX_PERSIST_POLLW_D", kn_pollw);
+    kn_head1w = (int)hopsx_env_int("HOPSX_PERSIST_HEAD1W", 1);  // 25.8 -> 25.5 us/step (same profile)
+    kn_memset = (int)hopsx_env_int("HOPSX_PERSIST_MEMSET", 0);  // (the round-4 form, for A/B)
+    kn_ok = 1;
+    g_persist_reload = 0;
+  }
+  a.pollw = kn_pollw;
+  a.stagger = kn_stagger;
+  a.pollw_a = kn_a;
+  a.pollw_b = kn_b;
+  a.pollw_c = kn_c;
+  a.pollw_d = kn_d;
+  a.head1w = kn_head1w;
   a.inv_gb = 1.f / (float)(world * B);
   if (dp) {
     a.xstep = (long long*)p[18];
@@ -1393,8 +1413,10 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
     if (e != hipSuccess) return (int)e;
     attr[dp] = true;
   }
-  hipError_t e = hipMemsetAsync(a.flags, 0, FL_WORDS * sizeof(unsigned), st);
-  if (e != hipSuccess) return (int)e;
+  if (kn_memset) {  // (the round-4 form, for A/B: zeroed flags each launch)
+    const hipError_t e = hipMemsetAsync(a.flags, 0, FL_WORDS * sizeof(unsigned), st);
+    if (e != hipSuccess) return (int)e;
+  }
   if (dp)
     hipLaunchKernelGGL(mnist_persist_k<true>, dim3(GRID), dim3(256), LDS_BYTES, st, a);
   else

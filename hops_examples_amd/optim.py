@@ -103,6 +103,7 @@ class FusedOptimizer:
             return
         self.lr = self.param_groups[0]["lr"]
         hp = [float(v) for v in self._hp()]
+        # (compared first: the capture query is a runtime call, and this runs before every launch / replay)
         if hp != self._hp_up and not torch.cuda.is_current_stream_capturing():
             self._hp_dev.copy_(torch.tensor((hp + [0.0] * 8)[:8], dtype=torch.float32))
             self._hp_up = hp

@@ -321,6 +321,9 @@ class PersistentMnistStep:
 
     # ------------------------------------------------------------------ launch
     def _check_data(self, xs, ys):
+        chk = getattr(self, "_checked", None)
+        if chk is not None and chk[0] is xs and chk[1] is ys and chk[2] == (xs.data_ptr(), ys.data_ptr()):
+            return chk[3]  # the same resident epoch as the last call (the common case: every launch)
         B = self.geom["batch"]
         if xs.dtype != torch.uint8 or not xs.is_contiguous() or xs.device != self.device:
             raise ValueError("xs must be a contiguous uint8 tensor on the model's device")
@@ -329,14 +332,30 @@ class PersistentMnistStep:
         nb = xs.shape[0]
         if ys.dtype != torch.int64 or tuple(ys.shape) != (nb, B) or not ys.is_contiguous() or ys.device != self.device:
             raise ValueError(f"ys must be a contiguous int64 [{nb}, {B}] tensor on the model's device")
+        self._checked = (xs, ys, (xs.data_ptr(), ys.data_ptr()), nb)
         return nb
 
     def _launch(self, xs, ys, nb: int, k: int) -> None:
         from ..ops import _C
 
-        opt, a, m = self.opt, self.arena, self.model
+        opt = self.opt
         opt.sync_hp()
         hp = [float(v) for v in opt._hp()]  # lr gscale wd rho eps
+        # the argument vectors are rebuilt only when something in them changes: at bench.py's 20 steps per
+        # launch the host-side preparation is in the timed window while the GPU idles
+        pool = self.model.pool
+        key = (xs.data_ptr(), ys.data_ptr(), nb, k, float(pool.dropout) if pool.training else 0.0, int(pool.salt),
+               tuple(hp), self.acquire, self.xfence, self.timeout_ms, id(self.dbg), id(self.cursor), id(self.rng),
+               id(self.arena.master), id(self.s1))
+        ext = self._ext
+        if getattr(self, "_args_key", None) != key:
+            # converted once into a C++-side slot; a launch then passes the slot id and the stream only
+            self._slot = ext.mnist_persist_store(getattr(self, "_slot", -1), *self._build_args(xs, ys, nb, k, hp))
+            self._args_key = key
+        _C.check(ext.mnist_persist_slot(self._slot, _C.stream()), "mnist_persist")
+
+    def _build_args(self, xs, ys, nb: int, k: int, hp: list):
+        opt, a, m = self.opt, self.arena, self.model
         ptrs = [a.master.data_ptr(), a.shadow.data_ptr(), self.s1.data_ptr(), self.s2.data_ptr(), xs.data_ptr(),
                 ys.data_ptr(), self.cursor.data_ptr(), self.rng.data_ptr(), opt.step_count.data_ptr(),
                 opt._hp_dev.data_ptr() if opt._hp_dev is not None else 0, self.slabA.data_ptr(),
@@ -349,7 +368,7 @@ class PersistentMnistStep:
         iv = self.offs + [nb, int(pool.salt), int(k), self.geom["batch"], self.acquire, self.world, self.rank,
                           1 if self.loopback > 1 else 0, self.timeout_ms, self.xfence]
         fv = [drop, float(scale), float(shift)] + (hp + [0.0] * 5)[:5]
-        _C.check(self._ext.mnist_persist(ptrs, iv, fv, _C.stream()), "mnist_persist")
+        return ptrs, iv, fv
 
     @property
     def _ext(self):
@@ -394,6 +413,9 @@ class PersistentMnistStep:
         """Raise if a hand-off of any launch timed out or was aborted (sticky device error word)."""
         e = int(self.err[0].item()) & 0xFFFFFFFF
         if e:
+            # a launch that gave up left flag epochs behind without advancing the epoch base: clear them,
+            # so a later launch (after the caller resets err) cannot match a stale flag
+            self.flags.zero_()
             phase, step, wg = (e >> 24) & 0x7F, (e >> 12) & 0xFFF, e & 0xFFF
             raise PersistentError(f"mnist_persist: hand-off wait timed out (phase {phase}, step {step}, "
                                   f"workgroup {wg}); arena state of the failed launch is partial")
