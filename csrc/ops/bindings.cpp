@@ -106,6 +106,28 @@ HX_PYMOD(HOPSX_MODNAME) {
   m.def("taxi_step2", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, long rows, u st) {
     return hopsx_taxi_step2(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(), rows, S(st));
   });
+  // launch-argument slots of the v2 taxi step (models/widedeep.py _launch), as mnist_persist_store below
+  struct TaxiSlot {
+    std::vector<uint64_t> p;
+    std::vector<long> iv;
+    std::vector<float> fv;
+    long rows;
+  };
+  static std::vector<TaxiSlot> taxi_slots;
+  m.def("taxi_step2_store", [](int slot, std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, long rows) {
+    if (slot < 0 || slot >= (int)taxi_slots.size()) {
+      taxi_slots.push_back({});
+      slot = (int)taxi_slots.size() - 1;
+    }
+    taxi_slots[slot] = TaxiSlot{std::move(p), std::move(iv), std::move(fv), rows};
+    return slot;
+  });
+  m.def("taxi_step2_slot", [](int slot, u st) {
+    if (slot < 0 || slot >= (int)taxi_slots.size()) return (int)hipErrorInvalidValue;
+    const TaxiSlot& a = taxi_slots[slot];
+    return hopsx_taxi_step2(a.p.data(), (int)a.p.size(), a.iv.data(), (int)a.iv.size(), a.fv.data(), (int)a.fv.size(),
+                            a.rows, S(st));
+  });
   m.def("widedeep_step_lds", [](std::vector<long> iv) { return hopsx_widedeep_step_lds(iv.data(), (int)iv.size()); });
   m.def("set_deterministic", [](int on) {
     int e = 0;

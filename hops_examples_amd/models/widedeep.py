@@ -130,6 +130,7 @@ class FusedWideDeepStep:
         self._B = None
         self._v2: dict = {}
         self._zn = None
+        self._v2key, self._v2slot = None, -1  # cached v2 launch arguments (C++ slot, _launch)
         dev = self.arena.device
         self.loss = torch.zeros(1, device=dev)
         self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -199,22 +200,34 @@ class FusedWideDeepStep:
         a = self.arena
         B = dense.shape[-2]
         self._B = B
+        if self.v2(B):
+            fl = self._floats()
+            key = (dense.data_ptr(), cat.data_ptr(), label.data_ptr(), nbatch, cursor.data_ptr(), nsteps, B,
+                   tuple(fl), id(a.master), self.dbg is not None)
+            ext = _C.ext()
+            if self._v2key != key:
+                # the argument vectors change only with the data, the step count or the hyper-parameters
+                ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
+                rows = int(self.model.wide.weight.shape[0])
+                if self._zn is None:
+                    self._zn = torch.empty(rows, 2, device=a.device)  # the kernel's (z, n) scratch
+                # Adagrad as w -= lr g rsq(s) (one transcendental): exact to fp32 when wd == 0 and eps is
+                # below the resolution of sqrt(s), whose floor is the initial accumulator
+                floor = float(getattr(self.ada, "initial_accumulator_value", 0.0))
+                rsq = int(self.ada.weight_decay == 0 and floor > 0 and self.ada.hp["eps"] < 1e-7 * math.sqrt(floor))
+                ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")),
+                        ptr(a.state("ftrl_s0")), ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label),
+                        ptr(cursor), ptr(self.loss), ptr(self.correct), ptr(self.ada.step_count),
+                        ptr(self.ftrl.step_count), ptr(rng_state(a.device)), ptr(self.dbg), ptr(self._zn), rsq]
+                self._v2slot = ext.taxi_step2_store(self._v2slot, ptrs, self._ints(B, nbatch, nsteps), fl, rows)
+                self._v2key = key
+            check(ext.taxi_step2_slot(self._v2slot, stream()), "taxi_step2")
+            return
         ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
         ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")), ptr(a.state("ftrl_s0")),
                 ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label), ptr(cursor), ptr(self.loss),
                 ptr(self.correct), ptr(self.ada.step_count), ptr(self.ftrl.step_count), ptr(rng_state(a.device)),
                 ptr(self.dbg)]
-        if self.v2(B):
-            rows = int(self.model.wide.weight.shape[0])
-            if self._zn is None:
-                self._zn = torch.empty(rows, 2, device=a.device)  # the kernel's (z, n) scratch
-            # Adagrad as w -= lr g rsq(s) (one transcendental): exact to fp32 when wd == 0 and eps is below
-            # the resolution of sqrt(s), whose floor is the initial accumulator
-            floor = float(getattr(self.ada, "initial_accumulator_value", 0.0))
-            rsq = int(self.ada.weight_decay == 0 and floor > 0 and self.ada.hp["eps"] < 1e-7 * math.sqrt(floor))
-            check(_C.ext().taxi_step2(ptrs + [ptr(self._zn), rsq], self._ints(B, nbatch, nsteps), self._floats(),
-                                      rows, stream()), "taxi_step2")
-            return
         ptrs.append(ptr(self._slots(B)))
         check(_C.ext().widedeep_step(ptrs, self._ints(B, nbatch, nsteps), self._floats(), stream()),
               "widedeep_step")
@@ -266,6 +279,13 @@ class FusedWideDeepStep:
                 self.dp.poll()
         return {"loss": self.loss, "correct": self.correct, "count": dense.shape[1]}
 
+    def _direct(self, dense) -> bool:
+        """Single-GPU v2 step with its in-kernel step loop: launched directly (``HOPSX_TAXI_DIRECT=0``
+        keeps the graph replays)."""
+        return (self.dp is None and self.arena.device.type == "cuda" and self.v2(dense.shape[-2])
+                and os.environ.get("HOPSX_TAXI_INKERNEL_LOOP", "1") == "1"
+                and os.environ.get("HOPSX_TAXI_DIRECT", "1") == "1")
+
     def _graphable(self) -> bool:
         """One GPU, or a data-parallel engine whose collectives are graph-capturable (P2P kernels)."""
         return self.arena.device.type == "cuda" and (
@@ -316,15 +336,25 @@ class FusedWideDeepStep:
         U = self.steps_per_execution
         dense, cat = xs
         r = None
+        if graph and self._direct(dense):
+            # one GPU, whole steps in one kernel: each launch runs up to U steps in-kernel, launched
+            # directly (a one-node graph replay costs more host time than the launch it replaces) with
+            # the argument vectors kept in a C++ slot
+            while n > 0:
+                k = min(n, U)
+                health.beat_range(self._n + 1, k)
+                self._n += k
+                self._launch(dense, cat, ys, dense.shape[0], self.cursor, nsteps=k)
+                n -= k
+            return {"loss": self.loss, "correct": self.correct, "count": dense.shape[1]}
         while n > 0:
             usable = U > 1 and graph and self._graphable() and self._graph is not None
             if usable and n < U and n in self._graphR:
                 self.prepare_resident(xs, ys)  # (re-keys on new data / hyper-parameters)
                 g = self._graphR.get(n)
                 if g is not None:
-                    for _ in range(n):
-                        self._n += 1
-                        health.beat(self._n)
+                    health.beat_range(self._n + 1, n)
+                    self._n += n
                     g.replay()
                     if self.dp is not None:
                         self.dp.poll()
@@ -336,9 +366,8 @@ class FusedWideDeepStep:
                 n -= 1
                 continue
             self.prepare_resident(xs, ys)
-            for _ in range(U):
-                self._n += 1
-                health.beat(self._n)
+            health.beat_range(self._n + 1, U)
+            self._n += U
             self._graphU.replay()
             if self.dp is not None:
                 self.dp.poll()

@@ -74,8 +74,39 @@ def beat(step: int | None = None) -> None:
     if step is not None:
         maybe_fault(step)
     now = time.monotonic()
-    if now - _last[0] < float(os.environ.get("HOPSX_HEARTBEAT_S", "1.0")):
+    if now - _last[0] < _interval():
         return
+    _touch(now)
+
+
+def beat_range(first: int, n: int) -> None:
+    """One heartbeat for the n steps first .. first + n - 1 that ONE launch / graph replay runs (the fault
+    hook still fires when its step is among them): per-step beats cost ~2 us of host time each, which at
+    20 steps per launch sits inside a timed window while the GPU waits."""
+    if n <= 0:
+        return
+    if _fault[0] is None:
+        _fault[0] = _parse_fault()
+    f = _fault[0]
+    if f and f[0] == _rank() and first <= f[1] < first + n:
+        maybe_fault(f[1])
+    now = time.monotonic()
+    if now - _last[0] < _interval():
+        return
+    _touch(now)
+
+
+_IVAL: list = [None, None]  # (env string, seconds)
+
+
+def _interval() -> float:
+    v = os.environ.get("HOPSX_HEARTBEAT_S", "1.0")
+    if _IVAL[0] != v:
+        _IVAL[0], _IVAL[1] = v, float(v)
+    return _IVAL[1]
+
+
+def _touch(now: float) -> None:
     _last[0] = now
     if _path[0] is None:
         d = os.environ.get("HOPSX_LOGDIR")

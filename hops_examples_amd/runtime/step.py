@@ -312,9 +312,8 @@ class TrainStep:
                 self._gR[rem] = self._capture_multi(xs, ys, rem)
 
     def _replay_multi(self, g, U: int):
-        for _ in range(U):
-            self._n += 1
-            health.beat(self._n)
+        health.beat_range(self._n + 1, U)  # one heartbeat (and fault check) for the U replayed steps
+        self._n += U
         self._sync_hp()
         g.replay()
         self._after_replay()
