@@ -138,3 +138,19 @@ def test_dp_step_self_test_every_wire_format(grad_bf16, weight_bf16):
         assert ar.wire_bytes_per_param(1.0) == (2 if grad_bf16 else 4) + (2 if weight_bf16 else 4)
     finally:
         ar.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["pg", "p2p"])
+def test_dp_resnet_overlap_two_ranks(mode):
+    """ResNet-20 (padded 8-channel stem, BN, shortcuts) on 2 ranks with the gradient exchange overlapped
+    with the backward — process-group bucket all-reduces from grad_ready (pg) or the fused zero-copy
+    step's per-bucket reduce-scatters (p2p) — keeps the replicas bit-identical (tools/dp_resnet_check.py)."""
+    env = dict(os.environ, HOPSX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", HOPSX_DPR_MODE=mode)
+    port = 29651 + (mode == "p2p")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "dp_resnet_check.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "DPRESNET" in r.stdout, r.stdout[-4000:]
+    print([ln for ln in r.stdout.splitlines() if "DPRESNET" in ln][-1][:400])
