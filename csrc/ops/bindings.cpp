@@ -286,11 +286,17 @@ HX_PYMOD(HOPSX_MODNAME) {
   });
   m.def("conv2d_bwd_pair", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact,
                               std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u add,
-                              u st) {
+                              u bnz, u bnmean, u bnrstd, u bnacc, u st) {
     return hopsx_conv2d_bwd_pair(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act,
                                  P<float>(colsum), P<void>(y), yact, g0.empty() ? nullptr : g0.data(), P<void>(x0),
                                  xscale, xshift, P<float>(dw0), P<void>(x), P<float>(dw), P<float>(db), P<void>(add),
-                                 S(st));
+                                 P<void>(bnz), P<float>(bnmean), P<float>(bnrstd), P<float>(bnacc), S(st));
+  });
+  m.def("conv2d_bwd_pair_bn_ok", [](std::vector<int> g) { return hopsx_conv2d_bwd_pair_bn_ok(g.data()); });
+  m.def("bn_bwd_pre", [](u dy, u x, u gamma, u mean, u rstd, u dx, u dgamma, u dbeta, u ws, int M, int C, u acc,
+                         u st) {
+    return hopsx_bn_bwd_pre(P<void>(dy), P<void>(x), P<float>(gamma), P<float>(mean), P<float>(rstd), P<void>(dx),
+                            P<float>(dgamma), P<float>(dbeta), P<float>(ws), M, C, P<float>(acc), S(st));
   });
   m.def("conv2d_bwd_pair_opt", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act, u colsum, u y, int yact,
                                   std::vector<int> g0, u x0, float xscale, float xshift, u dw0, u x, u dw, u db, u add,

@@ -370,6 +370,16 @@ struct DgradArgs {
   const bf16_raw* addend;
   // 1: XCD-aware block order (consecutive pixel groups, which share dY halo rows, on one XCD's L2)
   int xcd;
+  // BN column reduction in the epilogue (bnacc != null): this conv's input is the output of a training
+  // BatchNorm whose only autograd consumer is this conv, so the stored dX (after the addend and the
+  // act'(yprev) mask) IS that BN's masked output gradient g.  The epilogue adds sum g and
+  // sum g * (z - mean) * rstd (z = the BN input, bnz) per channel into the zero-at-rest replica rows
+  // bnacc[bid % HOPSX_BN_NREP][2C] that norm.hip bn_bwd_apply_fin8_k folds: the BN backward's own
+  // column-reduction launch (bn_colred8_k) disappears.
+  const bf16_raw* bnz;
+  const float* bnmean;
+  const float* bnrstd;
+  float* bnacc;
 };
 
 // bid / nblk: this workgroup's index and the number of workgroups doing dgrad work (a paired
@@ -442,9 +452,11 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     }
   }
   float* cwsum = csum + CM_RSLOTS * CI;  // [slot][CI][K0] (K0 > 0); csum is [slot][CI]
+  const bool bn = A.bnacc != nullptr;
+  float* csum2 = cwsum + CM_RSLOTS * CI * (K0 > 0 ? K0 : 0);  // [slot][CI] (bn): sum g * xhat
   // per (K step, fq) gather constants, built once per workgroup: output-pixel displacement of the
   // tap and the element offset relative to the lane's own pixel (x: dh, y: dw, z: offset, w: valid)
-  int4* ktab = (int4*)(cwsum + CM_RSLOTS * CI * (K0 > 0 ? K0 : 0));
+  int4* ktab = (int4*)(csum2 + (bn ? CM_RSLOTS * CI : 0));
   for (int i = threadIdx.x; i < KS * 4; i += blockDim.x) {
     const int kk = i >> 2, q = i & 3;
     const int k0 = kk * 32 + 8 * q;
@@ -464,6 +476,16 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
   const bf16_raw* ypp = yprev ? yprev : dx;
   bf16_raw* sc = scratch + wave * 16 * CI;
   float cacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // bn: sum g * xhat, and the batch mean / rstd of this lane's 8 fixed output channels
+  float cacc2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bmu[8], brs[8];
+  if (bn) {
+    const int col = (lane % (CI / 8)) * 8;  // (lane + 64 q) % (CI / 8): CI / 8 divides 64
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmu[j] = A.bnmean[col + j];
+      brs[j] = A.bnrstd[col + j];
+    }
+  }
   float cw[8][K0 > 0 ? K0 : 1];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
@@ -483,6 +505,7 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
   for (int g0 = (bid * CM_WAVES + wave) * UN; g0 < ngroups; g0 += nblk * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
     bf16x8 pmv[UN][CPL];  // epilogue operands prefetched with the A fragments: one round trip
+    bf16x8 bzv[UN][CPL];  // bn: the BN input z at the stored chunks
     // input-layer pixels for the fused wgrad: RAW loads (uint8 or bf16 bits) with the validity kept
     // aside and the conversion at the consumer — a conversion next to its load makes the compiler
     // wait for each load in turn (one full memory round trip per tap)
@@ -509,6 +532,7 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
         const bool okc = c < NCH && (g0 + u) < ngroups && p < M;
         const int pc = okc ? p : 0;
         pmv[u][q] = *(const bf16x8*)(ypp + (pc * CI + (okc ? col : 0)));  // unconditional (ypp = yprev or dx)
+        if (bn) bzv[u][q] = *(const bf16x8*)(A.bnz + (pc * CI + (okc ? col : 0)));
         if constexpr (K0 > 0) {
           // im2col row of the input layer at this pixel (= the input layer's output pixel)
           const int bb = g.fHW.div(pc), rr = pc - bb * (g.H * g.W);
@@ -610,6 +634,11 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
             *(bf16x8*)(dx + (long)(base + row) * CI + col) = v;
 #pragma unroll
             for (int j = 0; j < 8; ++j) cacc[j] += bf2f((uint16_t)v[j]);
+            if (bn) {  // the stored bf16 g, as bn_colred8_k would read it back
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                cacc2[j] = fmaf(bf2f((uint16_t)v[j]), (bf2f((uint16_t)bzv[u][q][j]) - bmu[j]) * brs[j], cacc2[j]);
+            }
           }
         }
       }
@@ -617,7 +646,7 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     }
   }
   phase_mark(dbg, 2);
-  if (colsum) {
+  if (colsum || bn) {
     // lanes l, l + CI/8, l + 2*CI/8, ... own the same 8 columns: fold them inside each 16-lane row
     // with DPP rotations (plain VALU; ds_bpermute shuffles were ~160 LDS round trips here), then
     // one LDS partial per (wave, row), summed after one barrier
@@ -628,6 +657,14 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     if (rl < CW) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) csum[slot * CI + rl * 8 + j] = cacc[j];
+    }
+    if (bn) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cacc2[j] = row_fold<CW>(cacc2[j]);
+      if (rl < CW) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) csum2[slot * CI + rl * 8 + j] = cacc2[j];
+      }
     }
     if constexpr (K0 > 0) {
 #pragma unroll
@@ -644,12 +681,22 @@ __device__ __forceinline__ void conv_dgrad_body(const DgradArgs& A, int bid, int
     __syncthreads();
     const bool det = det_on();
     if (det) det_turn_begin(DET_DGRAD_COLSUM, (unsigned)bid);
+    // bn: this workgroup's replica row of the BN accumulator ([sum g | sum g * xhat]), else the bias
+    // gradient (the host never asks for both)
+    float* d1 = bn ? A.bnacc + (long)(bid % HOPSX_BN_NREP) * 2 * CI : colsum;
     for (int i = threadIdx.x; i < CI; i += blockDim.x) {
       float v = 0.f;
 #pragma unroll
       for (int r = 0; r < CM_RSLOTS; ++r) v += csum[r * CI + i];
-      if (v != 0.f) atomicAdd(colsum + i, v);
+      if (v != 0.f) atomicAdd(d1 + i, v);
     }
+    if (bn)
+      for (int i = threadIdx.x; i < CI; i += blockDim.x) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < CM_RSLOTS; ++r) v += csum2[r * CI + i];
+        if (v != 0.f) atomicAdd(d1 + CI + i, v);
+      }
     if constexpr (K0 > 0) {
       // no-return f32 atomics: ~1 us for ~200 workgroups into these few rows (row 'Global float atomics')
       for (int i = threadIdx.x; i < CI * K0; i += blockDim.x) {
@@ -906,8 +953,8 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_pair_k(DgradArgs A, WgradArgs
 // KH*KW*CO > 512: ResNet stage-3 3x3x64 and the strided / projection convs): the first nA
 // workgroups are the dgrad GEMM's tiles (mfma_gemm_body, one K split), the rest the direct MFMA
 // weight gradient.  Each part alone leaves most CUs idle at these sizes.
-template <int BM, int NFC>
-__global__ __launch_bounds__(256) void conv_bwd_pair_gemm_k(ConvDgradALoader al, ConvWeightTLoader bl, EpiDActBF16 ep,
+template <int BM, int NFC, class EP = EpiDActBF16>
+__global__ __launch_bounds__(256) void conv_bwd_pair_gemm_k(ConvDgradALoader al, ConvWeightTLoader bl, EP ep,
                                                            int M, int N, int K, int kps, int nA, WgradArgs B,
                                                            int nBx) {
   if ((int)blockIdx.x < nA) {
@@ -1150,10 +1197,19 @@ static void pair_wgrad_plan(const ConvGeom& g, long slots, int& cpw, long& nBx, 
   shm = std::max(stage, redb);
 }
 
-// dgrad on the implicit GEMM + wgrad on the direct MFMA kernel in one launch (conv_bwd_pair_gemm_k)
+// The BN whose output is this conv's input (DgradArgs bnz / bnmean / bnrstd / bnacc); acc == null: none
+struct BnPre {
+  const void* z;
+  const float* mean;
+  const float* rstd;
+  float* acc;
+};
+
+// dgrad on the implicit GEMM + wgrad on the direct MFMA kernel in one launch (conv_bwd_pair_gemm_k);
+// bp.acc: the input BN's backward column sums in the dgrad epilogue (EpiDgradBnBF16; yprev = x)
 static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                               int act_prev, float* colsum, const void* y, int yact, const void* x, float* dw,
-                              float* dbias, const void* addend, hipStream_t st) {
+                              float* dbias, const void* addend, hipStream_t st, const BnPre& bp = BnPre{}) {
   if (hopsx_disabled("bwd_pair_gemm")) return -2;
   ConvGeom g = cm_geom(geom);
   if (g.C % 8 != 0 || g.CO % 8 != 0 || ((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)w) % 16 != 0)
@@ -1182,10 +1238,16 @@ static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, vo
   ConvWeightTLoader bl{(const bf16_raw*)w, g, 1};
   // addend: another consumer's gradient of x, added after the dgrad (no act' of a producing layer here)
   EpiDActBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, N, act_prev, colsum, (const bf16_raw*)addend};
+  const EpiDgradBnBF16 eb{(bf16_raw*)dx, N, (const bf16_raw*)yprev, act_prev, (const bf16_raw*)addend,
+                          (const bf16_raw*)bp.z, bp.mean, bp.rstd, bp.acc};
 #define HOPSX_PG(BMv, NFCv)                                                                                   \
   if (BM == BMv && g.CO / 16 == NFCv) {                                                                     \
-    hipLaunchKernelGGL((conv_bwd_pair_gemm_k<BMv, NFCv>), dim3((unsigned)total), dim3(256), shm, st, al, bl, e, M, \
-                       N, K, p.kps, (int)nA, WA, (int)nBx);                                                   \
+    if (bp.acc)                                                                                             \
+      hipLaunchKernelGGL((conv_bwd_pair_gemm_k<BMv, NFCv, EpiDgradBnBF16>), dim3((unsigned)total), dim3(256), shm, \
+                         st, al, bl, eb, M, N, K, p.kps, (int)nA, WA, (int)nBx);                              \
+    else                                                                                                    \
+      hipLaunchKernelGGL((conv_bwd_pair_gemm_k<BMv, NFCv>), dim3((unsigned)total), dim3(256), shm, st, al, bl, e, \
+                         M, N, K, p.kps, (int)nA, WA, (int)nBx);                                              \
     return (int)hipGetLastError();                                                                          \
   }
   HOPSX_PG(32, 1) HOPSX_PG(32, 2) HOPSX_PG(32, 4) HOPSX_PG(64, 1) HOPSX_PG(64, 2) HOPSX_PG(64, 4)
@@ -1200,16 +1262,28 @@ static int conv_bwd_pair_gemm(const void* dy, const void* w, const int* geom, vo
 static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                 int act_prev, float* colsum, const void* y, int yact, const int* geom0, const void* x0,
                                 float xscale, float xshift, float* dw0, const void* x, float* dw, float* dbias,
-                                const void* addend, const OptSlice& os, int opt_first, hipStream_t st);
+                                const void* addend, const OptSlice& os, int opt_first, hipStream_t st,
+                                const BnPre& bp = BnPre{});
+
+// the paired backward can also reduce the input BatchNorm's backward column sums (BnPre): either dgrad
+// variant (direct MFMA or implicit GEMM), no fused input layer, no bias gradient
+extern "C" int hopsx_conv2d_bwd_pair_bn_ok(const int* geom) {
+  // (the implicit-GEMM dgrad variant may still refuse a shape at launch: -2, nothing launched)
+  return hopsx_conv_wgrad_mfma_ok(geom) && geom[3] % 8 == 0 && !hopsx_disabled("bwd_pair") &&
+                 !hopsx_disabled("bn_dgrad_sums") && hopsx_bn_prestats_ok(geom[3])
+             ? 1
+             : 0;
+}
 
 extern "C" int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                      int act_prev, float* colsum, const void* y, int yact, const int* geom0,
                                      const void* x0, float xscale, float xshift, float* dw0, const void* x,
-                                     float* dw, float* dbias, const void* addend, hipStream_t st) {
+                                     float* dw, float* dbias, const void* addend, const void* bnz,
+                                     const float* bnmean, const float* bnrstd, float* bnacc, hipStream_t st) {
   OptSlice none{};
   none.kind = -1;
   return conv2d_bwd_pair_impl(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, geom0, x0, xscale, xshift, dw0, x, dw,
-                              dbias, addend, none, 0, st);
+                              dbias, addend, none, 0, st, BnPre{bnz, bnmean, bnrstd, bnacc});
 }
 
 // The same launch + a fused optimizer's update of the arena slice [p, p + n) (its gradients final),
@@ -1246,17 +1320,24 @@ extern "C" int hopsx_conv2d_bwd_pair_opt(const void* dy, const void* w, const in
 static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                 int act_prev, float* colsum, const void* y, int yact, const int* geom0, const void* x0,
                                 float xscale, float xshift, float* dw0, const void* x, float* dw, float* dbias,
-                                const void* addend, const OptSlice& os, int opt_first, hipStream_t st) {
+                                const void* addend, const OptSlice& os, int opt_first, hipStream_t st,
+                                const BnPre& bp) {
   if (hopsx_disabled("bwd_pair") || !hopsx_conv_wgrad_mfma_ok(geom)) return -2;
   const bool fused = geom0 != nullptr;
   if (fused && addend) return -2;
+  const bool bn = bp.acc != nullptr;
+  if (bn && (fused || colsum || !dx || !bp.z || !bp.mean || !bp.rstd || !hopsx_conv2d_bwd_pair_bn_ok(geom) ||
+             (uintptr_t)bp.z % 16 || os.kind >= 0))
+    return -2;
   if ((uintptr_t)addend % 16 != 0) return -3;
   if (!hopsx_conv_dgrad_mfma_ok(geom)) {
     // the GEMM variant adds an addend in its epilogue after the dgrad; with an act' of the producing
     // layer (yprev) the sum would have to come first: call again without it and add afterwards
-    if (addend && yprev) return -3;
+    // (bn: the BN epilogue adds first, then masks)
+    if (addend && yprev && !bn) return -3;
     if (os.kind >= 0) return -2;
-    return fused ? -2 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, addend, st);
+    return fused ? -2
+                 : conv_bwd_pair_gemm(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, x, dw, dbias, addend, st, bp);
   }
   if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
   if (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)yprev) % 16 != 0) return -2;
@@ -1271,11 +1352,12 @@ static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, 
   if (nA > 1024) nA = 1024;
   if (colsum && nA > 512) nA = 512;
   const size_t shmA = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                      (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float) + (size_t)KS * 4 * 16;
+                      (size_t)CM_RSLOTS * g.C * (1 + K0 + (bn ? 1 : 0)) * sizeof(float) + (size_t)KS * 4 * 16;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
                      (const bf16_raw*)y, yact, g, Kd, (int)((uintptr_t)w % 16 == 0), x0, xscale, xshift, g0, dw0, dbg,
-                     (const bf16_raw*)addend, (int)hopsx_env_int("HOPSX_DGRAD_XCD", 0)};
+                     (const bf16_raw*)addend, (int)hopsx_env_int("HOPSX_DGRAD_XCD", 0), (const bf16_raw*)bp.z,
+                     bp.mean, bp.rstd, bp.acc};
   // ---- wgrad part (32-column blocks)
   const int Kw = g.KH * g.KW * g.C;
   const long nchunks = ((long)g.B * g.OH * g.OW + WG_PX - 1) / WG_PX;

@@ -372,6 +372,40 @@ struct EpiDActBF16 {
   }
 };
 
+// Conv dgrad whose input x is a training BatchNorm's output consumed only by this conv (see
+// conv_mfma.hip DgradArgs bnacc): g = act'(y) * (acc + add) is stored (bf16) and its column sums
+// sum g (the plain colsum) and sum g * (z - mean) * rstd (second()) go to the BN accumulator's replica
+// rows colsum[HOPSX_BN_NREP][2N] (kSq layout), which the BN's apply-only backward folds.
+struct EpiDgradBnBF16 {
+  static constexpr bool kSq = true;
+  static constexpr bool kBn2 = true;
+  bf16_raw* out;
+  long ldo;
+  const bf16_raw* y;    // the BN output (= this conv's input), for act'; null: no activation
+  int act;
+  const bf16_raw* add;  // optional: a shortcut's gradient of x, added before the mask
+  const bf16_raw* z;    // the BN input, layout of out
+  const float* mean;
+  const float* rstd;
+  float* colsum;
+  __device__ __forceinline__ float operator()(int m, int n, float v) const {
+    const long o = (long)m * ldo + n;
+    if (add) v += bf2f(add[o]);
+    if (y) v *= act_grad_from_out(bf2f(y[o]), act);
+    const bf16_raw b = f2bf(v);
+    out[o] = b;
+    return bf2f(b);  // the sums see the stored value, as the BN's own reduction would
+  }
+  __device__ __forceinline__ float second(int m, int n, float g) const {
+    return g * ((bf2f(z[(long)m * ldo + n]) - mean[n]) * rstd[n]);
+  }
+};
+
+template <class EP, class = void>
+struct has_bn2 { static constexpr bool value = false; };
+template <class EP>
+struct has_bn2<EP, decltype((void)EP::kBn2)> { static constexpr bool value = EP::kBn2; };
+
 // Linear dgrad whose input came from a non-overlapping max-pool (exact windows): the epilogue IS
 // the pool backward — each pooled-gradient element (row m, column n = (ph, pw, c)) is routed to
 // its argmax position of the pool input (dropout mask regenerated, ReLU' of the pool input
@@ -649,7 +683,8 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
           if (m < M && n < N) {
             const float v = ep(m, n, acc[i][j][r]);
             cs[j] += v;
-            if constexpr (has_sq<EP>::value) cs2[j] = fmaf(v, v, cs2[j]);
+            if constexpr (has_bn2<EP>::value) cs2[j] += ep.second(m, n, v);
+            else if constexpr (has_sq<EP>::value) cs2[j] = fmaf(v, v, cs2[j]);
           }
         }
       }

@@ -937,6 +937,28 @@ extern "C" int hopsx_bn_fwd_infer(const void* x, void* y, const float* gamma, co
   return (int)hipGetLastError();
 }
 
+// The column sums already sit in acc's replica rows (a consumer conv's dgrad epilogue reduced them:
+// conv_mfma.hip DgradArgs bnacc) and dy is the masked output gradient: the apply alone, no act' and no
+// residual gradient (the caller hands dy itself on as the residual's gradient).
+extern "C" int hopsx_bn_bwd_pre(const void* dy, const void* x, const float* gamma, const float* mean,
+                                const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C,
+                                float* acc, hipStream_t st) {
+  if (!acc || !bn_vec_ok(C, {dy, x, dx})) return -2;
+  const long n = (long)M * C;
+  const BnFin fin{nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ws, dgamma, dbeta, 1};
+  if (bn_fold_first(C)) {
+    hipLaunchKernelGGL(bn_fold_k<1>, dim3((C + 255) / 256), dim3(256), 0, st, acc, M, C, fin);
+    hipLaunchKernelGGL(bn_bwd_apply8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
+                       (const bf16_raw*)x, (const bf16_raw*)nullptr, gamma, mean, rstd, ws, (bf16_raw*)dx,
+                       (bf16_raw*)nullptr, n / 8, M, C, (int)ACT_NONE);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(bn_bwd_apply_fin8_k, dim3(apply_grid(n / 8, C)), dim3(256), 0, st, (const bf16_raw*)dy,
+                     (const bf16_raw*)x, (const bf16_raw*)nullptr, gamma, mean, rstd, acc, (bf16_raw*)dx,
+                     (bf16_raw*)nullptr, n / 8, M, C, (int)ACT_NONE, fin, (const float*)nullptr);
+  return (int)hipGetLastError();
+}
+
 // zbeta: the BN's beta when its forward had no residual (ReLU: act' taken from x, see bn_shift); else null
 extern "C" int hopsx_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean,
                             const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int C,

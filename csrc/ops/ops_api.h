@@ -149,7 +149,13 @@ bool hopsx_conv_wgrad_mfma_ok(const int* geom);
 int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act_prev,
                           float* colsum, const void* y, int yact, const int* geom0, const void* x0, float xscale,
                           float xshift, float* dw0, const void* x, float* dw, float* dbias, const void* addend,
-                          hipStream_t st);
+                          const void* bnz, const float* bnmean, const float* bnrstd, float* bnacc, hipStream_t st);
+// 1 when hopsx_conv2d_bwd_pair takes bnacc (the input BN's backward column sums in the dgrad epilogue)
+int hopsx_conv2d_bwd_pair_bn_ok(const int* geom);
+// BN backward whose column sums are already in the replica rows of acc (a consumer conv's dgrad
+// epilogue, hopsx_conv2d_bwd_pair bnacc) and whose dy is the masked output gradient: one apply launch
+int hopsx_bn_bwd_pre(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
+                     void* dx, float* dgamma, float* dbeta, float* ws, int M, int C, float* acc, hipStream_t st);
 int hopsx_wgrad_debug_times(unsigned long long* host_out, int n);
 // conv weight gradient through LDS-DMA staged 128x128 MFMA tiles (wgrad_glds.hip): no dY activation
 // mask, no bias gradient, C % 8 == 0, CO % 8 == 0; -2: unsupported (nothing launched)

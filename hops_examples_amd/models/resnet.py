@@ -30,10 +30,13 @@ class ConvBN(nn.Module):
         self.conv = hnn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False, init="he")
         self.bn = hnn.BatchNorm2d(cout, activation=act)
 
-    def forward(self, x, residual=None, gslot=None, res_gslot=None):
+    def forward(self, x, residual=None, gslot=None, res_gslot=None, sole=False):
         # training: the conv epilogue accumulates the BN statistics (functional.conv2d bnstats), so
         # the BN is one apply launch instead of a statistics pass + an apply.  gslot / res_gslot:
-        # see BasicBlock.forward
+        # see BasicBlock.forward.  sole: this conv is the only autograd consumer of x (when x is a BN
+        # output, the conv's dgrad epilogue then reduces that BN's backward column sums)
+        if sole:
+            HF.bn_sole_consumer(x)
         return self.bn(self.conv(x, bnstats=self.bn.training, gslot=gslot), residual, gslot=res_gslot)
 
 
@@ -56,16 +59,17 @@ class BasicBlock(nn.Module):
                 "res_addend" not in os.environ.get("HOPSX_DISABLE", ""):
             # identity shortcut: the residual's gradient (from b's BN backward, which always runs
             # first) is handed to a's conv backward, whose dgrad epilogue adds it — no autograd add
+            # (a's conv is then x's only autograd consumer, and b's conv always is a's output's)
             slot = {}
-            return self.b(self.a(x, gslot=slot), residual=x, res_gslot=slot)
+            return self.b(self.a(x, gslot=slot, sole=True), residual=x, res_gslot=slot, sole=True)
         if self.short is not None and _fuse_proj(self, x):
             # projection shortcut: conv a's dX goes to the short conv's dgrad epilogue (backpropagated
             # after a's: created first), not to an autograd add (ops.functional.GiveGrad)
             slot = {}
             s = self.short(x, gslot=slot)
-            return self.b(self.a(x, gslot=HF.GiveGrad(slot)), residual=s)
+            return self.b(self.a(x, gslot=HF.GiveGrad(slot)), residual=s, sole=True)
         s = x if self.short is None else self.short(x)
-        return self.b(self.a(x), residual=s)
+        return self.b(self.a(x), residual=s, sole=True)
 
 
 class Bottleneck(nn.Module):
@@ -85,13 +89,14 @@ class Bottleneck(nn.Module):
             # identity shortcut: c's BN backward hands the residual's gradient to a's (1x1) dgrad,
             # whose vectorized epilogue adds it (gemm_glds.h store8) — no autograd add launch
             slot = {}
-            return self.c(self.b(self.a(x, gslot=slot)), residual=x, res_gslot=slot)
+            return self.c(self.b(self.a(x, gslot=slot, sole=True), sole=True), residual=x, res_gslot=slot,
+                          sole=True)
         if self.short is not None and _fuse_proj(self, x):  # (see BasicBlock.forward)
             slot = {}
             s = self.short(x, gslot=slot)
-            return self.c(self.b(self.a(x, gslot=HF.GiveGrad(slot))), residual=s)
+            return self.c(self.b(self.a(x, gslot=HF.GiveGrad(slot)), sole=True), residual=s, sole=True)
         s = x if self.short is None else self.short(x)
-        return self.c(self.b(self.a(x)), residual=s)
+        return self.c(self.b(self.a(x), sole=True), residual=s, sole=True)
 
 
 class CifarResNet(nn.Module):

@@ -327,6 +327,7 @@ class _Conv2dFn(torch.autograd.Function):
         g = K.conv_geom(x.shape, w.shape, stride, padding, dilation)
         ctx.pool = None
         ctx.give = None
+        ctx.bnin = _take_bn_input(x)  # x is a training BN's output consumed only here (bn_sole_consumer)
         if isinstance(gslot, GiveGrad):
             ctx.give, gslot = gslot.slot, None
         # gslot: a dict through which a later-backpropagated consumer of x (a ResNet block's identity
@@ -458,8 +459,17 @@ class _Conv2dFn(torch.autograd.Function):
             addend = ctx.gslot.get("g") if (ctx.gslot is not None and pprev is None) else None
             co = _colaunch_slice((w, b) + ((ctx.prev[0], ctx.prev[1]) if ctx.prev is not None else ())) \
                 if (ctx.prev is not None and addend is None) else None
-            r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, dbias=gb, y=ymask, act=act, prev=pprev,
-                                  addend=addend, opt_slice=co[1] if co is not None else None)
+            bn = _bn_sums_request(ctx, x, g, pprev, gb, addend)
+            r = False
+            if bn is not None:
+                # dX is x's whole gradient (sole consumer; a shortcut's part is the addend): its dgrad
+                # epilogue masks it and reduces the input BN's backward column sums
+                r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, y=ymask, act=act, addend=addend, bn=bn)
+                if r is not False and r is not None:
+                    _BNPRE[r.data_ptr()] = weakref.ref(r)
+            if r is False:
+                r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, dbias=gb, y=ymask, act=act, prev=pprev,
+                                      addend=addend, opt_slice=co[1] if co is not None else None)
             if co is not None and r is not False:
                 COLAUNCH["lo"] = co[0]  # the optimizer's launch now updates only the prefix
                 COLAUNCH["launched"] += 1
@@ -507,6 +517,43 @@ class GiveGrad:
 
     def __init__(self, slot: dict):
         self.slot = slot
+
+
+# BN backward column sums reduced by a consumer conv's dgrad epilogue (conv_mfma.hip DgradArgs bnacc):
+# data_ptr of that dX -> weakref.  _BNFn.backward pops its dy here and then runs only the apply
+# (K.bn_bwd_pre).  Written and consumed within one backward pass.
+_BNPRE: dict = {}
+
+
+def bn_sole_consumer(t):
+    """Declare that the next hopsx conv applied to ``t`` (a training batch_norm output) is its ONLY autograd
+    consumer — other consumers hand their gradient of ``t`` to that conv as an epilogue addend (gslot) —
+    so the conv's backward may reduce the BN's backward column sums in its dgrad epilogue.  The ResNet
+    blocks call this where the structure guarantees it."""
+    if getattr(t, "_hx_bnsrc", None) is not None and "bn_dgrad_sums" not in _disabled():
+        t._hx_bn_sole = True
+    return t
+
+
+def _take_bn_input(x):
+    if not getattr(x, "_hx_bn_sole", False):
+        return None
+    x._hx_bn_sole = False  # one consumer
+    return x._hx_bnsrc
+
+
+def _bn_sums_request(ctx, x, g, pprev, gb, addend):
+    """(z, mean, rstd, yprev, act) for K.conv2d_bwd_pair(bn=...) when this conv's dgrad can carry its input
+    BN's column sums, else None."""
+    src = getattr(ctx, "bnin", None)
+    if (src is None or pprev is not None or gb is not None or ctx.give is not None or not ctx.needs_input_grad[0]
+            or (ctx.gslot is not None and addend is None)  # a shortcut part not handed over yet: sums incomplete
+            or not K.conv2d_bwd_pair_bn_ok(g)):
+        return None
+    z2, mean, rstd, act = src
+    if z2.numel() != x.numel() or x.dtype != BF16:
+        return None
+    return (z2, mean, rstd, x if act else None, act)
 
 
 def _take_addend(ctx):
@@ -938,16 +985,32 @@ class _BNFn(torch.autograd.Function):
         ctx.save_for_backward(x2, y, mean, rstd)
         ctx.p = (gamma, beta, act, x.shape, residual is not None)
         ctx.gslot = gslot  # the residual's gradient goes to the conv that also consumes it (_Conv2dFn)
-        return y.view(x.shape)
+        out = y.view(x.shape)
+        if x.is_cuda and out.dtype == BF16:
+            out._hx_bnsrc = (x2, mean, rstd, act)  # for a consumer conv's dgrad epilogue (bn_sole_consumer)
+        return out
 
     @staticmethod
     def backward(ctx, dy):
         x2, y, mean, rstd = ctx.saved_tensors
         gamma, beta, act, shape, has_res = ctx.p
         C = shape[-1]
-        dy2 = dy.to(BF16).contiguous().view(-1, C)
         gg, gb = _wgrad_buf(gamma), _wgrad_buf(beta)
         ws = torch.empty(2 * C, device=dy.device)
+        ent = _BNPRE.pop(dy.data_ptr(), None)
+        src = ent() if ent is not None else None
+        if src is not None and src.numel() == dy.numel() and dy.dtype == BF16 and dy.is_contiguous():
+            # the consuming conv's dgrad already masked dy and reduced the column sums: apply only; the
+            # masked dy IS the residual's gradient
+            dy2 = dy.view(-1, C)
+            dx = K.bn_bwd_pre(dy2, x2, gamma, mean, rstd, gg, gb, ws)
+            dres = dy2 if has_res else None
+            if has_res and ctx.gslot is not None:
+                ctx.gslot["g"] = dres.view(shape)
+                dres = None
+            return (dx.view(shape), _ret_grad(gamma, gg), _ret_grad(beta, gb), None, None, None, None,
+                    dres.view(shape) if dres is not None else None, None, None, None)
+        dy2 = dy.to(BF16).contiguous().view(-1, C)
         dres = torch.empty_like(dy2) if has_res else None
         # no residual + ReLU: the backward recomputes the act' mask from x (no read of y; K.bn_bwd zbeta)
         zb = beta.detach() if (beta is not None and not has_res and K.act_id(act) == 1) else None

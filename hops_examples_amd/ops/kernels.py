@@ -278,14 +278,33 @@ def conv2d_dgrad_fused_wgrad(dy, w, geom, yprev, act_prev, y, act, x0, geom0, dw
           "conv2d_dgrad_fused_wgrad")
 
 
-def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, addend=None, opt_slice=None):
+def conv2d_bwd_pair_bn_ok(geom) -> bool:
+    """conv2d_bwd_pair(bn=...) covers this conv: its dgrad epilogue can reduce the input BN's backward
+    column sums."""
+    return bool(_C.ext().conv2d_bwd_pair_bn_ok(list(geom)))
+
+
+def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, addend=None, opt_slice=None, bn=None):
     """A conv layer's dgrad and wgrad in ONE launch (conv_mfma.hip conv_bwd_pair_k).  ``prev`` =
     (x0, geom0, dw0, db0, yprev, act_prev, in_affine) fuses the input layer's weight gradient into the
     dgrad (no dX).  ``addend``: another consumer's gradient of the same input, added to dX in the
-    epilogue where the kernel has it (else added afterwards).  Returns dX (None when fused), or
+    epilogue where the kernel has it (else added afterwards).  ``bn`` = (z, mean, rstd, yprev, act_prev):
+    x is the output of a training BatchNorm (input z [M, C], batch mean / rstd) consumed only by this
+    conv — dX is masked by act_prev'(yprev) and the BN's backward column sums go into its accumulator
+    (``bn_bwd_pre`` then finishes that BN's backward in one launch).  Returns dX (None when fused), or
     False when the shapes are not covered."""
     B, H, W, C = geom[:4]
-    if prev is None:
+    bnargs = (0, 0, 0, 0)
+    if bn is not None:
+        if prev is not None or opt_slice is not None or dbias is not None:
+            raise ValueError("conv2d_bwd_pair: bn excludes prev / opt_slice / dbias")
+        z, mean, rstd, yprev, act_prev = bn
+        _req(z, BF16, "bn z")
+        bnargs = (ptr(z), ptr(mean), ptr(rstd), ptr(bn_acc(dy.device, C)))
+        dx = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+        args = (ptr(dx), ptr(yprev), act_id(act_prev) if yprev is not None else 0, 0, ptr(y), act_id(act), [], 0, 0.0,
+                0.0, 0)
+    elif prev is None:
         dx = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
         args = (ptr(dx), 0, 0, 0, ptr(y), act_id(act), [], 0, 0.0, 0.0, 0)
     else:
@@ -312,10 +331,12 @@ def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, ad
         check(rc, "conv2d_bwd_pair_opt")
         return dx
     rc = _C.ext().conv2d_bwd_pair(ptr(dy), ptr(w), list(geom), dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_, dw0p,
-                                  ptr(x), ptr(dw), ptr(dbias), ptr(addend), stream())
+                                  ptr(x), ptr(dw), ptr(dbias), ptr(addend), *bnargs, stream())
     if rc == -3:  # no epilogue addend for this shape: nothing launched; pair without it, then add
+        if bn is not None:
+            return False  # (the sums would miss the addend)
         rc = _C.ext().conv2d_bwd_pair(ptr(dy), ptr(w), list(geom), dxp, yp, ap, cs, yy, ya, g0l, x0p, sc_, sh_,
-                                      dw0p, ptr(x), ptr(dw), ptr(dbias), 0, stream())
+                                      dw0p, ptr(x), ptr(dw), ptr(dbias), 0, 0, 0, 0, 0, stream())
         if rc == 0 and dx is not None:
             dx.add_(addend.view(dx.shape))
     if rc == -2:
@@ -635,6 +656,17 @@ def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None
     check(_C.ext().bn_bwd(ptr(dy), ptr(x), ptr(y), ptr(gamma), ptr(mean), ptr(rstd), ptr(out), ptr(dgamma),
                           ptr(dbeta), ptr(ws), M, C, act_id(act), ptr(dresidual), ptr(bn_acc(dy.device, C)),
                           ptr(zbeta), stream()), "bn_bwd")
+    return out
+
+
+def bn_bwd_pre(g, x, gamma, mean, rstd, dgamma, dbeta, ws, out=None):
+    """BN backward whose column sums a consumer conv's dgrad epilogue already reduced into the width's
+    accumulator (conv2d_bwd_pair bn=...); ``g`` is the act'-masked output gradient.  One apply launch."""
+    M, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    check(_C.ext().bn_bwd_pre(ptr(g), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(out), ptr(dgamma), ptr(dbeta),
+                              ptr(ws), M, C, ptr(bn_acc(g.device, C)), stream()), "bn_bwd_pre")
     return out
 
 
