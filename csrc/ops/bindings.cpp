@@ -292,6 +292,11 @@ HX_PYMOD(HOPSX_MODNAME) {
                                  xscale, xshift, P<float>(dw0), P<void>(x), P<float>(dw), P<float>(db), P<void>(add),
                                  P<void>(bnz), P<float>(bnmean), P<float>(bnrstd), P<float>(bnacc), S(st));
   });
+  m.def("conv2d_dgrad_bn", [](u dy, u w, std::vector<int> g, u dx, u yprev, int act_prev, u add, u bnz, u bnmean,
+                              u bnrstd, u bnacc, u st) {
+    return hopsx_conv2d_dgrad_bn(P<void>(dy), P<void>(w), g.data(), P<void>(dx), P<void>(yprev), act_prev, P<void>(add),
+                                 P<void>(bnz), P<float>(bnmean), P<float>(bnrstd), P<float>(bnacc), S(st));
+  });
   m.def("conv2d_bwd_pair_bn_ok", [](std::vector<int> g) { return hopsx_conv2d_bwd_pair_bn_ok(g.data()); });
   m.def("bn_bwd_pre", [](u dy, u x, u gamma, u mean, u rstd, u dx, u dgamma, u dbeta, u ws, int M, int C, u acc,
                          u st) {

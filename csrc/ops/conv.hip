@@ -536,6 +536,41 @@ extern "C" int hopsx_conv2d_dgrad(const void* dy, const void* w, const int* geom
   return (int)hipGetLastError();
 }
 
+// dX of a conv whose input x is a training BatchNorm's output consumed only by this conv: the epilogue
+// adds `addend` (a shortcut's gradient of x), masks by act_prev'(yprev = x), stores g and reduces the
+// BN's backward column sums (sum g, sum g * xhat) into the replica rows bnacc[HOPSX_BN_NREP][2C]
+// (gemm_core.h EpiDgradBnBF16; conv_mfma.hip DgradArgs bnacc for the direct MFMA shapes).  Stride-1
+// convs on the direct MFMA kernel, the gg engine (1x1 and implicit-GEMM gathers) or gemm_core.h's
+// engine without split-K; anything else (strided parity GEMMs, split-K) returns -2 with nothing
+// launched and the caller runs the plain dgrad + the full BN backward.
+extern "C" int hopsx_conv2d_dgrad_bn(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                     int act_prev, const void* addend, const void* bnz, const float* bnmean,
+                                     const float* bnrstd, float* bnacc, hipStream_t st) {
+  ConvGeom g = make_geom(geom);
+  if (!bnacc || !bnz || !bnmean || !bnrstd || hopsx_disabled("bn_dgrad_sums") || g.sh != 1 || g.sw != 1 ||
+      g.C % 8 || g.CO % 8 || !hopsx_bn_prestats_ok(g.C) ||
+      ((uintptr_t)dy | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)yprev | (uintptr_t)addend | (uintptr_t)bnz) % 16)
+    return -2;
+  const int r = hopsx_conv2d_dgrad_mfma_bn(dy, w, geom, dx, yprev, act_prev, addend, bnz, bnmean, bnrstd, bnacc, st);
+  if (r != -2) return r;
+  const int M = g.B * g.H * g.W, N = g.C, K = g.KH * g.KW * g.CO;
+  const EpiDgradBnBF16 e{(bf16_raw*)dx, N, (const bf16_raw*)yprev, act_prev, (const bf16_raw*)addend,
+                         (const bf16_raw*)bnz, bnmean, bnrstd, bnacc};
+  if (!hopsx_disabled("gg_dgrad") && !gg_narrow(g, N)) {
+    const GgWeightT ws{(const bf16_raw*)w, g, K, N};
+    if (gg_1x1(g) ? launch_gg<true, false>(GgDense{(const bf16_raw*)dy, (long)g.CO, M, K}, ws, e, M, N, K, false, st)
+                  : launch_gg<true, false>(GgDgradA{(const bf16_raw*)dy, g, M, K}, ws, e, M, N, K, false, st))
+      return (int)hipGetLastError();
+  }
+  float* sws;
+  unsigned* stk;
+  if (conv_split(1, M, N, K, &sws, &stk)) return -2;  // the plain dgrad would split K: keep it
+  ConvDgradALoader al{(const bf16_raw*)dy, g, 1, nullptr, 0};
+  ConvWeightTLoader bl{(const bf16_raw*)w, g, 1};
+  launch_gemm<true, false>(al, bl, e, M, N, K, false, st);
+  return (int)hipGetLastError();
+}
+
 // dW[co][k] += sum_m dY[m][co] * im2col(X)[m][k]; db[co] += sum_m dY[m][co] when colsum given
 static bool smallk_ok(const ConvGeom& g, const void* dy, const void* y, const float* ws, long ws_elems,
                       const unsigned* counter) {

@@ -974,7 +974,8 @@ int cm_ks5(int ks) { return ks == 5 && !hopsx_disabled("ks5") ? 5 : cm_ks(ks); }
 
 int cm_grid(long ngroups, int un = CM_UN) {
   long blocks = (ngroups + CM_WAVES * un - 1) / (CM_WAVES * un);
-  if (blocks > 1024) blocks = 1024;
+  static const long cap = hopsx_env_int("HOPSX_CM_MAXWG", 1024);  // A/B knob: workgroups of the direct convs
+  if (blocks > cap) blocks = cap;
   return (int)(blocks < 1 ? 1 : blocks);
 }
 
@@ -1072,9 +1073,34 @@ extern "C" int hopsx_conv2d_dgrad_mfma(const void* dy, const void* w, const int*
                                     nullptr, st);
 }
 
+static int dgrad_mfma_impl(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act_prev,
+                           float* colsum, const void* y, int yact, const int* geom0, const void* x0, float xscale,
+                           float xshift, float* dw0, const void* addend, const void* bnz, const float* bnmean,
+                           const float* bnrstd, float* bnacc, hipStream_t st);
+
 extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
                                           int act_prev, float* colsum, const void* y, int yact, const int* geom0,
                                           const void* x0, float xscale, float xshift, float* dw0, hipStream_t st) {
+  return dgrad_mfma_impl(dy, w, geom, dx, yprev, act_prev, colsum, y, yact, geom0, x0, xscale, xshift, dw0, nullptr,
+                         nullptr, nullptr, nullptr, nullptr, st);
+}
+
+// the direct MFMA dgrad with the input BN's backward column sums in its epilogue (DgradArgs bnacc) and an
+// optional shortcut gradient added before the act'(yprev) mask; -2: not this kernel's shape (nothing launched)
+extern "C" int hopsx_conv2d_dgrad_mfma_bn(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                                          int act_prev, const void* addend, const void* bnz, const float* bnmean,
+                                          const float* bnrstd, float* bnacc, hipStream_t st) {
+  if (!hopsx_conv_dgrad_mfma_ok(geom) || !bnacc || !bnz || !bnmean || !bnrstd ||
+      ((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)yprev | (uintptr_t)addend | (uintptr_t)bnz) % 16)
+    return -2;
+  return dgrad_mfma_impl(dy, w, geom, dx, yprev, act_prev, nullptr, nullptr, 0, nullptr, nullptr, 0.f, 0.f, nullptr,
+                         addend, bnz, bnmean, bnrstd, bnacc, st);
+}
+
+static int dgrad_mfma_impl(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act_prev,
+                           float* colsum, const void* y, int yact, const int* geom0, const void* x0, float xscale,
+                           float xshift, float* dw0, const void* addend, const void* bnz, const float* bnmean,
+                           const float* bnrstd, float* bnacc, hipStream_t st) {
   const bool fused = geom0 != nullptr;
   if (fused && (!hopsx_conv_dgrad_fused_wgrad_ok(geom, geom0) || !yprev || !colsum || !dw0 || !x0)) return -4;
   ConvGeom g0 = fused ? cm_geom(geom0) : ConvGeom{};
@@ -1091,12 +1117,13 @@ extern "C" int hopsx_conv2d_dgrad_mfma_ex(const void* dy, const void* w, const i
   if (blocks > 1024) blocks = 1024;
   if (colsum && blocks > 512) blocks = 512;  // one colsum atomic per channel per workgroup
   const size_t shm = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
-                     (size_t)CM_RSLOTS * g.C * (1 + K0) * sizeof(float) + (size_t)KS * 4 * 16;
+                     (size_t)CM_RSLOTS * g.C * (1 + K0 + (bnacc ? 1 : 0)) * sizeof(float) + (size_t)KS * 4 * 16;
+  if (shm > 160u * 1024u) return -2;  // gfx950 LDS per workgroup (C = 128 at K = 512 with the BN sums: 161 KB)
   const int wvec = (uintptr_t)w % 16 == 0;
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const DgradArgs DA{(const bf16_raw*)dy, (const bf16_raw*)w, (bf16_raw*)dx, (const bf16_raw*)yprev, act_prev, colsum,
-                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg, nullptr,
-                     (int)hopsx_env_int("HOPSX_DGRAD_XCD", 0)};
+                     (const bf16_raw*)y, yact, g, K, wvec, x0, xscale, xshift, g0, dw0, dbg, (const bf16_raw*)addend,
+                     (int)hopsx_env_int("HOPSX_DGRAD_XCD", 0), (const bf16_raw*)bnz, bnmean, bnrstd, bnacc};
 #define HOPSX_CMD(NF, KSV, K0V)                                                                                \
   if (un == 1) hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 1>), dim3(blocks), dim3(256), shm, st, DA); \
   else hipLaunchKernelGGL((conv_dgrad_mfma_k<NF, KSV, K0V, 2>), dim3(blocks), dim3(256), shm, st, DA)
@@ -1349,7 +1376,8 @@ static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, 
   const int KS = cm_ks5((Kd + 31) / 32);
   const long Md = (long)g.B * g.H * g.W;
   long nA = ((Md + 15) / 16 + CM_WAVES * 2 - 1) / (CM_WAVES * 2);
-  if (nA > 1024) nA = 1024;
+  static const long pair_cap = hopsx_env_int("HOPSX_PAIR_DGRAD_MAXWG", 1024);  // A/B knob
+  if (nA > pair_cap) nA = pair_cap;
   if (colsum && nA > 512) nA = 512;
   const size_t shmA = (size_t)(g.C * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.C) * sizeof(bf16_raw) +
                       (size_t)CM_RSLOTS * g.C * (1 + K0 + (bn ? 1 : 0)) * sizeof(float) + (size_t)KS * 4 * 16;

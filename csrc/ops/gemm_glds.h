@@ -651,7 +651,8 @@ __global__ __launch_bounds__(512) void gg_kernel(const AS as, const BS bs, const
         if (m < M && n < N) {
           const float vv = ep(m, n, acc[i][j][r]);
           cs[j] += vv;
-          if constexpr (has_sq<EP>::value) cs2[j] = fmaf(vv, vv, cs2[j]);
+          if constexpr (has_bn2<EP>::value) cs2[j] += ep.second(m, n, vv);
+          else if constexpr (has_sq<EP>::value) cs2[j] = fmaf(vv, vv, cs2[j]);
         }
       }
     }

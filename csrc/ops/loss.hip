@@ -258,6 +258,14 @@ extern "C" int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, 
 constexpr int HEAD_ROWS = 32;
 constexpr int HEAD_CMAX = 32;
 
+// Several row blocks (B > HEAD_ROWS): each (bx, 0) workgroup leaves its loss / correct partial in a slot
+// and the last to arrive sums the slots in row-block order and STORES the totals (no zeroing launches of
+// the two outputs before the kernel, no float atomics, a deterministic sum).  <= HEAD_PART_MAX blocks.
+constexpr int HEAD_PART_MAX = 64;
+__device__ float g_head_part_l[HEAD_PART_MAX];
+__device__ int g_head_part_c[HEAD_PART_MAX];
+__device__ unsigned g_head_arrive;
+
 // LDS: h tile [HEAD_ROWS][KD] bf16 | W [C][KD] bf16 | dlogits [HEAD_ROWS][C] f32 (dynamic size)
 // The body takes its block coordinates explicitly (bx of gx row blocks, by of gy column blocks) so
 // the fused Dense -> head kernel (mlp_head_k) can run it in its last workgroup; h == nullptr: the
@@ -352,6 +360,23 @@ __device__ inline void head_ce_body(int kind, const void* __restrict__ logits, i
     if (gx == 1) {
       if (loss_sum) *loss_sum = l;
       if (correct) *correct = c;
+    } else if (gx <= HEAD_PART_MAX) {  // (deterministic as it is: a fixed-order sum)
+      g_head_part_l[bx] = l;
+      g_head_part_c[bx] = c;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned t = __hip_atomic_fetch_add(&g_head_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == (unsigned)gx - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        float lt = 0.f;
+        int ct = 0;
+        for (int q = 0; q < gx; ++q) {
+          lt += __hip_atomic_load(g_head_part_l + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ct += __hip_atomic_load(g_head_part_c + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (loss_sum) *loss_sum = lt;
+        if (correct) *correct = ct;
+        __hip_atomic_store(&g_head_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {
       if (loss_sum) atomicAdd(loss_sum, l);
       if (correct) atomicAdd(correct, c);
@@ -438,7 +463,8 @@ extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const
   int gy = KD / 32;
   if (gy > 8) gy = 8;
   if (gy < 1) gy = 1;
-  if (grid > 1) {  // (one row block: the blockIdx.y == 0 workgroup overwrites the totals)
+  // (up to HEAD_PART_MAX row blocks the totals are stored, see g_head_part_l; more: atomics into zeroed totals)
+  if (grid > HEAD_PART_MAX) {
     if (loss_sum) hopsx_zero(loss_sum, sizeof(float), st);
     if (correct) hopsx_zero(correct, sizeof(int), st);
   }

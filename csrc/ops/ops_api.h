@@ -150,6 +150,14 @@ int hopsx_conv2d_bwd_pair(const void* dy, const void* w, const int* geom, void* 
                           float* colsum, const void* y, int yact, const int* geom0, const void* x0, float xscale,
                           float xshift, float* dw0, const void* x, float* dw, float* dbias, const void* addend,
                           const void* bnz, const float* bnmean, const float* bnrstd, float* bnacc, hipStream_t st);
+// dgrad with the input BN's backward column sums in the epilogue (conv.hip; -2: shape not covered, nothing
+// launched); the _mfma_bn variant is the direct MFMA kernel alone
+int hopsx_conv2d_dgrad_bn(const void* dy, const void* w, const int* geom, void* dx, const void* yprev, int act_prev,
+                          const void* addend, const void* bnz, const float* bnmean, const float* bnrstd, float* bnacc,
+                          hipStream_t st);
+int hopsx_conv2d_dgrad_mfma_bn(const void* dy, const void* w, const int* geom, void* dx, const void* yprev,
+                               int act_prev, const void* addend, const void* bnz, const float* bnmean,
+                               const float* bnrstd, float* bnacc, hipStream_t st);
 // 1 when hopsx_conv2d_bwd_pair takes bnacc (the input BN's backward column sums in the dgrad epilogue)
 int hopsx_conv2d_bwd_pair_bn_ok(const int* geom);
 // BN backward whose column sums are already in the replica rows of acc (a consumer conv's dgrad

@@ -411,8 +411,10 @@ class _Conv2dFn(torch.autograd.Function):
                     if addend is not None:
                         dx.add_(addend)
                 else:  # the shortcut's gradient is added in the dgrad epilogue (no separate add launch)
-                    dx = K.conv2d_dgrad(dy2.view(dy.shape), _arena.weight_bf16(w), g,
-                                        addend=None if addend is None else addend.to(BF16).contiguous().view(x.shape))
+                    add = None if addend is None else addend.to(BF16).contiguous().view(x.shape)
+                    dx = _dgrad_bn(ctx, dy2.view(dy.shape), w, g, x, add, addend)
+                    if dx is None:
+                        dx = K.conv2d_dgrad(dy2.view(dy.shape), _arena.weight_bf16(w), g, addend=add)
             gw = _wgrad_buf(w)
             if os.environ.get("HOPSX_BLASLT_WGRAD", "0") != "1":
                 # the library's fp32-out tall-skinny reductions (K = B*H*W) measured slower than the
@@ -459,9 +461,9 @@ class _Conv2dFn(torch.autograd.Function):
             addend = ctx.gslot.get("g") if (ctx.gslot is not None and pprev is None) else None
             co = _colaunch_slice((w, b) + ((ctx.prev[0], ctx.prev[1]) if ctx.prev is not None else ())) \
                 if (ctx.prev is not None and addend is None) else None
-            bn = _bn_sums_request(ctx, x, g, pprev, gb, addend)
+            bn = _bn_sums_request(ctx, x, pprev, gb, addend)
             r = False
-            if bn is not None:
+            if bn is not None and K.conv2d_bwd_pair_bn_ok(g):
                 # dX is x's whole gradient (sole consumer; a shortcut's part is the addend): its dgrad
                 # epilogue masks it and reduces the input BN's backward column sums
                 r = K.conv2d_bwd_pair(dy, _arena.weight_bf16(w), g, x, gw, y=ymask, act=act, addend=addend, bn=bn)
@@ -499,9 +501,10 @@ class _Conv2dFn(torch.autograd.Function):
             hooks.grad_ready(b0)
         elif ctx.needs_input_grad[0]:
             addend = _take_addend(ctx)  # a shortcut's gradient of x: added in the dgrad epilogue
-            if addend is not None:
-                addend = addend.to(BF16).contiguous().view(x.shape)
-            dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act, addend=addend)
+            add = addend.to(BF16).contiguous().view(x.shape) if addend is not None else None
+            dx = _dgrad_bn(ctx, dy, w, g, x, add, addend) if ymask is None else None
+            if dx is None:
+                dx = K.conv2d_dgrad(dy, _arena.weight_bf16(w), g, y=ymask, act=act, addend=add)
         if not side_ok:
             K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
         return (dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None, None,
@@ -542,18 +545,39 @@ def _take_bn_input(x):
     return x._hx_bnsrc
 
 
-def _bn_sums_request(ctx, x, g, pprev, gb, addend):
-    """(z, mean, rstd, yprev, act) for K.conv2d_bwd_pair(bn=...) when this conv's dgrad can carry its input
-    BN's column sums, else None."""
+def _bn_sums_request(ctx, x, pprev, gb, addend):
+    """(z, mean, rstd, yprev, act) for a dgrad that can carry its input BN's column sums (K.conv2d_bwd_pair
+    / K.conv2d_dgrad_bn bn=...), else None."""
     src = getattr(ctx, "bnin", None)
     if (src is None or pprev is not None or gb is not None or ctx.give is not None or not ctx.needs_input_grad[0]
-            or (ctx.gslot is not None and addend is None)  # a shortcut part not handed over yet: sums incomplete
-            or not K.conv2d_bwd_pair_bn_ok(g)):
+            or (ctx.gslot is not None and addend is None)):  # a shortcut part not handed over yet: sums incomplete
         return None
     z2, mean, rstd, act = src
     if z2.numel() != x.numel() or x.dtype != BF16:
         return None
     return (z2, mean, rstd, x if act else None, act)
+
+
+# The same on the separate (unpaired) dgrad launches: opt-in.  Measured on ResNet-50 (round 5): B=8 flat
+# (1,532 vs 1,528 img/s), B=64 SLOWER (5.11-5.18 k vs 5.59 k) — the gg engine's per-element epilogue
+# (no 16-B vector path for the three extra operands) costs more on its big tiles than the reduction launch
+# it saves (profiles/r5_bn_dgrad_sums.txt).  The paired backward (CIFAR ResNets) keeps it on.
+_BN_SEPARATE = os.environ.get("HOPSX_BN_SUMS_SEPARATE_DGRAD", "0") == "1"
+
+
+def _dgrad_bn(ctx, dy, w, g, x, add, addend):
+    """dX through K.conv2d_dgrad_bn when x is a sole-consumed BN output and the kernel covers the shape (the
+    BN's backward column sums ride on the epilogue; registered for _BNFn.backward), else None."""
+    if not _BN_SEPARATE:
+        return None
+    bn = _bn_sums_request(ctx, x, None, None, addend)
+    if bn is None or dy.dtype != BF16:
+        return None
+    dx = K.conv2d_dgrad_bn(dy.contiguous(), _arena.weight_bf16(w), g, bn, addend=add)
+    if dx is False:
+        return None
+    _BNPRE[dx.data_ptr()] = weakref.ref(dx)
+    return dx
 
 
 def _take_addend(ctx):

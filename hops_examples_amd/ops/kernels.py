@@ -258,6 +258,27 @@ def conv2d_dgrad(dy, w, geom, yprev=None, act_prev=0, out=None, colsum=None, y=N
     return out
 
 
+def conv2d_dgrad_bn(dy, w, geom, bn, addend=None):
+    """dX of a conv whose input is a sole-consumed training BN output, ``bn`` = (z, mean, rstd, yprev,
+    act_prev): the epilogue adds ``addend``, applies act_prev'(yprev), stores g and reduces the BN's backward
+    column sums into its accumulator (finish with ``bn_bwd_pre``).  False: shape not covered (nothing
+    launched)."""
+    _req(dy, BF16, "dy")
+    z, mean, rstd, yprev, act_prev = bn
+    _req(z, BF16, "bn z")
+    B, H, W, C = geom[:4]
+    if addend is not None:
+        _req(addend, BF16, "addend")
+    out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
+    rc = _C.ext().conv2d_dgrad_bn(ptr(dy), ptr(w), list(geom), ptr(out), ptr(yprev),
+                                  act_id(act_prev) if yprev is not None else 0, ptr(addend), ptr(z), ptr(mean),
+                                  ptr(rstd), ptr(bn_acc(dy.device, C)), stream())
+    if rc == -2:
+        return False
+    check(rc, "conv2d_dgrad_bn")
+    return out
+
+
 def conv_dgrad_fused_wgrad_ok(geom, geom0) -> bool:
     """conv(geom)'s dgrad can carry the weight gradient of the input layer conv(geom0) feeding it."""
     return bool(_C.ext().conv2d_dgrad_fused_wgrad_ok(list(geom), list(geom0)))

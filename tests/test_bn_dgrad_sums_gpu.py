@@ -120,4 +120,126 @@ def test_resnet20_step_with_bn_sums_in_dgrad():
     assert calls[0] >= 15 and calls[1] == 0, calls
     noise = float(F.cosine_similarity(g1b, g1, dim=0))
     cos = float(F.cosine_similarity(g1, g0, dim=0))
-    assert cos > 0.99 and cos > noise - 0.01, (cos, noise)
+    # run-to-run noise of this random-init network is itself cos ~0.99 (float-atomic orders, amplified; see
+    # test_bnstats_gpu.test_resnet20_step_bnstats_matches_unfused): compare against it
+    assert cos > 0.97 and cos > noise - 0.01, (cos, noise)
+
+
+# the separate dgrad launch (conv.hip hopsx_conv2d_dgrad_bn): direct MFMA, gg 1x1 / implicit GEMM, gemm_core
+@pytest.mark.parametrize("shape", [(8, 16, 16, 32, 32, 3), (8, 14, 14, 64, 64, 3), (8, 14, 14, 256, 64, 1),
+                                   (8, 28, 28, 128, 128, 3), (2, 7, 7, 512, 128, 1), (4, 28, 28, 128, 512, 1)])
+@pytest.mark.parametrize("with_addend", [False, True])
+def test_dgrad_bn_sums_match_unfused(shape, with_addend):
+    B, H, W, C, CO, k = shape
+    torch.manual_seed(11)
+    g = K.conv_geom((B, H, W, C), (CO, k, k, C), (1, 1), (k // 2, k // 2), (1, 1))
+    z = bf(torch.randn(B * H * W, C, device=dev) * 1.5 - 0.2)
+    zf = z.float()
+    mean = zf.mean(0)
+    rstd = (zf.var(0, unbiased=False) + 1e-5).rsqrt()
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.5
+    x = bf(((zf - mean) * rstd * gamma + beta).relu()).view(B, H, W, C)
+    w = bf(torch.randn(CO, k, k, C, device=dev) / (k * k * C) ** 0.5)
+    dy = bf(torch.randn(B, H, W, CO, device=dev))
+    add = bf(torch.randn(B, H, W, C, device=dev)) if with_addend else None
+    gg, gb, ws = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.empty(2 * C, device=dev)
+    dX = K.conv2d_dgrad_bn(dy, w, g, (z, mean, rstd, x, "relu"), addend=add)
+    assert dX is not False, "shape should be covered"
+    dz = K.bn_bwd_pre(dX.view(-1, C), z, gamma, mean, rstd, gg, gb, ws)
+    # reference: fp32 dgrad (+ addend), mask, fp32 autograd BN backward
+    dXr = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 1, k // 2)
+    dXr = dXr.permute(0, 2, 3, 1)
+    if add is not None:
+        dXr = dXr + add.float()
+    dXr = dXr * (x > 0)
+    torch.testing.assert_close(dX.float(), dXr, rtol=2e-2, atol=2e-2)
+    zr = zf.clone().requires_grad_(True)
+    F.batch_norm(zr, None, None, gamma, beta, True, 0.0, 1e-5).relu().backward(dX.float().view(-1, C))
+    torch.testing.assert_close(dz.float(), zr.grad, rtol=3e-2, atol=3e-2)
+    gref = dX.float().view(-1, C)
+    torch.testing.assert_close(gb, gref.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(gg, (gref * (zf - mean) * rstd).sum(0), rtol=1e-3, atol=1e-2)
+    torch.cuda.synchronize()
+    _acc_clean()
+
+
+def _counting(fn):
+    real, n = K.bn_bwd_pre, [0]
+
+    def counting(*a, **kw):
+        n[0] += 1
+        return real(*a, **kw)
+
+    K.bn_bwd_pre = counting
+    try:
+        return fn(), n[0]
+    finally:
+        K.bn_bwd_pre = real
+
+
+@pytest.fixture
+def separate_dgrad_bn(monkeypatch):
+    monkeypatch.setattr(HF, "_BN_SEPARATE", True)  # (opt-in on the unpaired dgrads)
+
+
+def test_bottleneck_pair_grads_with_bn_sums_match_unfused(separate_dgrad_bn):
+    """Two identity Bottlenecks (256 -> 64 -> 256) in sequence: bn_a -> 3x3 conv_b (implicit-GEMM dgrad), bn_b ->
+    1x1 conv_c (plain 1x1 path), and the first block's output BN (residual + ReLU) -> the second block's conv_a
+    with the shortcut gradient as the epilogue addend.  Input / parameter gradients fused vs unfused."""
+    from torch import nn
+
+    from hops_examples_amd.models.resnet import Bottleneck
+
+    out, calls = {}, {}
+    for dis in ("bn_dgrad_sums", ""):
+        old = os.environ.get("HOPSX_DISABLE", "")
+        os.environ["HOPSX_DISABLE"] = dis
+        try:
+            torch.manual_seed(2)
+            m = nn.Sequential(Bottleneck(256, 64), Bottleneck(256, 64)).to(dev).train()
+            x = bf(torch.randn(8, 14, 14, 256, device=dev)).requires_grad_(True)
+            dy = bf(torch.randn(8, 14, 14, 256, device=dev))
+
+            def run():
+                y = m(x)
+                gs = torch.autograd.grad(y, [x] + list(m.parameters()), dy)
+                return [t.float().reshape(-1) for t in gs]
+
+            out[dis], calls[dis] = _counting(run)
+        finally:
+            os.environ["HOPSX_DISABLE"] = old
+    torch.cuda.synchronize()
+    _acc_clean()
+    assert not HF._BNPRE
+    assert calls == {"bn_dgrad_sums": 0, "": 5}, calls
+    a, b = torch.cat(out[""]), torch.cat(out["bn_dgrad_sums"])
+    cos = float(F.cosine_similarity(a, b, dim=0))
+    # per tensor (input gradient, then every parameter): relative L2 error
+    rel = [float((u - v).norm() / v.norm().clamp_min(1e-12)) for u, v in zip(out[""], out["bn_dgrad_sums"])]
+    print("bottleneck pair: cos", cos, "worst per-tensor rel. L2 error", max(rel))
+    assert cos > 0.999, cos
+    assert max(rel) < 0.05, rel
+
+
+def test_resnet50_step_with_bn_sums_in_dgrad(separate_dgrad_bn):
+    """A whole ResNet-50 step (B=2, 64x64) takes the fused path on most BNs, leaves no sums behind and gives
+    finite gradients (at this size the network is too chaotic for a gradient comparison between runs:
+    two identical unfused runs agree only to cos ~0.4; the block-level test above compares)."""
+    from hops_examples_amd.models.resnet import resnet50
+
+    def run():
+        torch.manual_seed(0)
+        m = resnet50(num_classes=10).to(dev).train()
+        x = torch.randint(0, 256, (2, 64, 64, 3), device=dev, dtype=torch.uint8)
+        y = torch.randint(0, 10, (2,), device=dev)
+        F.cross_entropy(m(x).float(), y).backward()
+        torch.cuda.synchronize()
+        return torch.cat([p.grad.float().reshape(-1) for p in m.parameters() if p.grad is not None])
+
+    g, n = _counting(run)
+    _acc_clean()
+    assert not HF._BNPRE
+    print("resnet50 BNs with the sums in a dgrad epilogue:", n)
+    assert n >= 30, n
+    assert bool(torch.isfinite(g).all())

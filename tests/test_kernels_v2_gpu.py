@@ -323,8 +323,10 @@ def test_plain_1x1_conv_library_gemm_matches_kernel(monkeypatch):
         torch.testing.assert_close(a, b, atol=2e-2 * b.abs().max().item(), rtol=2e-2)
 
 
+# B = 200: 7 row blocks (loss totals summed from per-block slots by the last to arrive); B = 2100: 66 row
+# blocks (more than the slots: zeroed totals + atomics)
 @pytest.mark.parametrize("kind,C,B", [("sparse_ce", 10, 32), ("sparse_ce", 10, 200), ("ce", 10, 17),
-                                      ("bce_logits", 1, 40), ("mse", 3, 9)])
+                                      ("bce_logits", 1, 40), ("mse", 3, 9), ("sparse_ce", 10, 2100)])
 def test_fused_classifier_head(monkeypatch, kind, C, B):
     """loss_and_grad_root on a linear logits layer: one head_ce launch (loss, dW, db, dh) must give
     the same loss and gradients as the loss kernel + the layer's backward GEMMs."""
@@ -358,6 +360,13 @@ def test_fused_classifier_head(monkeypatch, kind, C, B):
     (l0, c0, g0, d0), (l1, c1, g1, d1) = res
     torch.testing.assert_close(l0, l1, rtol=1e-4, atol=1e-5)
     assert int(c0) == int(c1)
+    monkeypatch.setenv("HOPSX_DISABLE", "")
+    for _ in range(2):  # more launches: the row-block slots' arrival counter is back at zero after each
+        out2 = HF.linear(h0.clone().requires_grad_(True), lin.weight, lin.bias, out_f32=True)
+        loss2, correct2 = HF.loss_and_grad_root(out2, t, kind)[:2]
+        torch.cuda.synchronize()
+        torch.testing.assert_close(loss2, l1, rtol=1e-4, atol=1e-5)
+        assert int(correct2) == int(c1)
     torch.testing.assert_close(g0, g1, rtol=2e-2, atol=2e-2 * g1.abs().max().item())
     torch.testing.assert_close(d0, d1, rtol=2e-2, atol=2e-2 * d1.abs().max().item())
 

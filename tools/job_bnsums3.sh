@@ -1,0 +1,11 @@
+set -o pipefail
+o=gpurun_out/${1:-r5_bns3}; mkdir -p $o; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_bn_dgrad_sums_gpu.py tests/test_bnstats_gpu.py tests/test_models_gpu.py tests/test_kernels_v2_gpu.py tests/test_mlp_head_gpu.py tests/test_graph_replay_gpu.py > $o/t.log 2>&1 || { grep -E "PASS|FAIL|Error|error|assert" $o/t.log | tail -30; exit 1; }
+grep -E "calls / cos|passed|failed" $o/t.log | tail -3
+run() { env $1 timeout -k 10 300 python benchmarks/run.py $2 > $o/r.json 2> $o/err.log || { tail -20 $o/err.log; exit 1; }
+  echo "[$1] $2 -> $(python -c "import json; r=json.loads(open('$o/r.json').read().strip().splitlines()[-1]); print(r['value'], r['ms_per_step'])")"; }
+for d in X=0 HOPSX_DISABLE=bn_dgrad_sums X=0; do
+  run $d "resnet50 --batch 8 --steps 30 --warmup 5"
+  run $d "resnet50 --batch 64 --steps 12 --warmup 4"
+done
+run X=0 "cifar_resnet --depth 20 --batch 128 --steps 100 --warmup 10"
