@@ -191,9 +191,14 @@ class _Reshape(tnn.Module):
 
 
 class _InputNorm(tnn.Module):
-    """uint8 inputs are normalised to [0,1] on the device (one vectorised kernel)."""
+    """uint8 inputs are normalised to [0,1] on the device (one vectorised kernel) — or, when the first
+    layer is a conv that applies the normalisation itself (``raw_u8``: its ``in_affine``), passed on raw."""
+
+    raw_u8 = False
 
     def forward(self, x):
+        if x.dtype == torch.uint8 and self.raw_u8:
+            return x
         if x.dtype == torch.uint8:
             if x.is_cuda:
                 from .ops import kernels as K
@@ -430,6 +435,13 @@ class Sequential(tnn.Module):
             l.output_shape = (None,) + tuple(shape)
             if not (isinstance(l, Dropout) and l.rate == 0.0):
                 mods.append(l.module)
+        # uint8 pixels go straight into a first conv, which applies x / 255 itself (fused into its kernel
+        # where the layer qualifies): the same arithmetic as _InputNorm, one launch less, and the layout the
+        # persistent MNIST engine expects (see _flagship_view)
+        first = next((m for m in mods[1:] if not isinstance(m, _Reshape)), None)
+        if isinstance(first, hnn.Conv2d) and first.in_affine is None:
+            first.in_affine = (1.0 / 255.0, 0.0)
+            mods[0].raw_u8 = True
         self.net = tnn.Sequential(*mods)
         self._input_shape = shape
 
@@ -455,6 +467,45 @@ class Sequential(tnn.Module):
         self._loss_name = loss
         self._metrics = list(metrics or [])
         self._step = None
+        self._fast = None
+
+    def _flagship_view(self):
+        """A MirroredMnistCNN-shaped view sharing this model's layers when the stack is the reference's
+        MirroredStrategy MNIST CNN (mirroredstrategy_mnist_example.ipynb:189-207: Conv2D(32, 2, relu),
+        Conv2D(64, 2, relu), MaxPooling2D + Dropout, Flatten, Dense(128, relu), Dense(10[, softmax])) —
+        matched on the layers by runtime.persist.flagship_layers — else None."""
+        from .models.mnist import MirroredMnistCNN
+        from .runtime.persist import flagship_layers
+
+        mods = [m for m in self.net if not isinstance(m, (_InputNorm, _Reshape, hnn.Flatten))]
+        if len(mods) != 5:
+            return None
+        c1, c2, pool, f1, f2 = mods
+        if isinstance(f2, tnn.Sequential) and len(f2) == 2 and isinstance(f2[1], _Softmax):
+            f2 = f2[0]
+        v = MirroredMnistCNN.__new__(MirroredMnistCNN)
+        tnn.Module.__init__(v)
+        v.conv1, v.conv2, v.pool, v.fc1, v.fc2 = c1, c2, pool, f1, f2
+        return v if flagship_layers(v) is not None else None
+
+    def _prepare_fast(self, batch_size):
+        """The persistent whole-step engine (runtime.persist, via runtime.step.make_step) for fit's
+        resident-epoch path when this model is the flagship MNIST CNN with sparse CE, Adadelta and
+        batch 32 on a GPU that can hold its grid; else None (fit keeps the TrainStep)."""
+        if self.device.type != "cuda" or self._kind != "sparse_ce":  # (HOPSX_PERSIST=0: supported() says no)
+            return None
+        view = self._flagship_view()
+        if view is None:
+            return None
+        from .parallel import dist as hdist
+        from .runtime.persist import PersistentMnistStep
+        from .runtime.step import make_step
+
+        view.train(self.training)
+        if not PersistentMnistStep.supported(view, self.optimizer, int(batch_size), hdist.world_size()):
+            return None
+        eng = make_step(view, self.optimizer, self._kind, dp="auto", graph=True, batch=int(batch_size))
+        return eng if getattr(eng, "kind", None) == "persistent" else None
 
     def _prepare(self, xb):
         if self.net is None:
@@ -486,6 +537,52 @@ class Sequential(tnn.Module):
             fwd = self._train_fwd
             self._step = TrainStep(self, self.optimizer, kind, graph=True,
                                    forward_fn=(lambda m, x: fwd(x)) if fwd is not None else None)
+            self._fast = self._prepare_fast(self._batch_hint) if getattr(self, "_batch_hint", None) else None
+            self.geom_batch = getattr(self, "_batch_hint", None)
+
+    def _resident(self, x, y):
+        """Device copies of a whole uint8 image array [N, 28, 28(, 1)] and its int labels, uploaded once
+        and kept while fit is called with the same arrays."""
+        key = (id(x), id(y), len(x))
+        c = getattr(self, "_res_cache", None)
+        if c is not None and c[0] == key:
+            return c[1], c[2]
+        xs = _to_tensor(x, self.device).reshape(len(x), 28, 28, 1).contiguous()
+        ys = _to_tensor(y, self.device, label=True).reshape(-1).contiguous()
+        self._res_cache = (key, xs, ys)
+        return xs, ys
+
+    def _fit_epoch_fast(self, x, y, shuffle, rng):
+        """One epoch on the persistent engine: the epoch's batches (shuffled on the device) resident in
+        HBM, 32 steps per launch, per-step loss / correct read back once per launch on the device; a
+        last partial batch goes through the TrainStep.  Returns device (sum of losses * n, correct, n)."""
+        eng = self._fast
+        xs_all, ys_all = self._resident(x, y)
+        N = xs_all.shape[0]
+        B = int(self.geom_batch)
+        nb = N // B
+        if shuffle:
+            g = torch.Generator(device=self.device)
+            g.manual_seed(int(rng.integers(1 << 62)))
+            idx = torch.randperm(N, device=self.device, generator=g)
+        else:
+            idx = torch.arange(N, device=self.device)
+        xs = xs_all.index_select(0, idx[: nb * B]).view(nb, B, 28, 28, 1)
+        ys = ys_all.index_select(0, idx[: nb * B]).view(nb, B)
+        eng.cursor.zero_()  # the epoch starts at its first batch
+        tot = torch.zeros(2, device=self.device)
+        left = nb
+        while left > 0:
+            k = min(left, eng.spl)
+            eng.run_resident(xs, ys, k)
+            L = eng.losses(k)
+            tot += torch.stack((L[:, 0].sum() * B, L[:, 1].sum()))
+            left -= k
+        n = nb * B
+        if N > n:  # the remainder (Keras trains on the partial last batch too)
+            r = self._step(xs_all.index_select(0, idx[n:]), ys_all.index_select(0, idx[n:]))
+            tot += torch.stack((r["loss"].reshape(-1)[0] * (N - n), r["correct"].reshape(-1)[0].float()))
+        return tot[0], tot[1], N
 
     def _strip_last(self, cls):
         last = self.net[-1]
@@ -527,6 +624,15 @@ class Sequential(tnn.Module):
         rng = np.random.default_rng(seed)
         self.stop_training = False
         self.train()
+        # resident-epoch path on the persistent engine (runtime.persist): whole arrays of uint8 images, no
+        # per-batch callbacks — the model then trains 32 steps per launch (see _fit_epoch_fast)
+        arrays = isinstance(x, (np.ndarray, torch.Tensor)) and y is not None
+        fast_ok = (arrays and not per_batch and steps_per_epoch is None and len(x) >= batch_size
+                   and str(x.dtype) in ("uint8", "torch.uint8") and tuple(x.shape[1:]) in ((28, 28), (28, 28, 1)))
+        if fast_ok and self._step is None:
+            self._batch_hint = int(batch_size)
+            self._prepare(_to_tensor(x[:1], "cpu"))
+        fast = fast_ok and self._fast is not None and int(batch_size) == self.geom_batch
         for c in cbs:
             getattr(c, "on_train_begin", lambda *a: None)({})
         dataset_iter = None
@@ -534,6 +640,23 @@ class Sequential(tnn.Module):
             t0 = time.time()
             for c in cbs:
                 getattr(c, "on_epoch_begin", lambda *a: None)(epoch, {})
+            if fast:
+                tl, tcor, tn = self._fit_epoch_fast(x, y, shuffle, rng)
+                logs = {"loss": float(tl) / tn}
+                if "accuracy" in self._metrics or "acc" in self._metrics:
+                    logs["accuracy"] = float(tcor) / tn
+                if validation_data is not None:
+                    vl = self.evaluate(*validation_data, batch_size=batch_size, verbose=0, return_dict=True)
+                    logs.update({"val_" + k: v for k, v in vl.items()})
+                    self.train()
+                if verbose:
+                    s = " - ".join(f"{k}: {v:.4f}" for k, v in logs.items())
+                    print(f"Epoch {epoch + 1}/{epochs} - {time.time() - t0:.1f}s - {s}", flush=True)
+                for cb in cbs:
+                    getattr(cb, "on_epoch_end", lambda *a: None)(epoch, logs)
+                if self.stop_training:
+                    break
+                continue
             if y is None and x is not None and not isinstance(x, (np.ndarray, torch.Tensor)):
                 if dataset_iter is None or steps_per_epoch is None:
                     dataset_iter = iter(x)

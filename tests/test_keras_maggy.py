@@ -188,3 +188,53 @@ def test_ablation_loco_trials(project_root, monkeypatch):
     assert res["results"]["base"] > 0.8
     # removing the only informative feature hurts
     assert res["results"]["feature-pclass"] < res["results"]["base"]
+
+
+def _flagship_keras(keras, dense_act="softmax"):
+    """The reference's MirroredStrategy MNIST model, written the notebook's way
+    (mirroredstrategy_mnist_example.ipynb:189-207)."""
+    return keras.Sequential([
+        keras.layers.Conv2D(32, 2, activation="relu", input_shape=(28, 28, 1)),
+        keras.layers.Conv2D(64, 2, activation="relu"),
+        keras.layers.MaxPooling2D(),
+        keras.layers.Dropout(0.01),
+        keras.layers.Flatten(),
+        keras.layers.Dense(128, activation="relu"),
+        keras.layers.Dense(10, activation=dense_act),
+    ])
+
+
+def test_keras_flagship_stack_matches_the_persistent_engine_structurally():
+    """fit's resident-epoch path can run the persistent engine only on the reference model's exact layer
+    stack (runtime.persist.flagship_layers over a view of the Keras modules); uint8 pixels go straight
+    into the first conv, which normalises them itself (same values as the separate x / 255 pass)."""
+    import torch
+
+    from hops_examples_amd import keras
+    from hops_examples_amd.runtime.persist import flagship_layers
+
+    m = _flagship_keras(keras)
+    m.build()
+    v = m._flagship_view()
+    assert v is not None and flagship_layers(v) is not None
+    assert v.conv1.in_affine == (1.0 / 255.0, 0.0) and v.fc2.weight.shape == (10, 128)
+    from hops_examples_amd import nn as hnn
+
+    lins = [mod for mod in m.net.modules() if isinstance(mod, hnn.Linear)]
+    assert v.fc1 is lins[0] and v.fc2 is lins[1]  # the view shares the Keras model's layers (and parameters)
+    for other in (
+        keras.Sequential([keras.layers.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)),
+                          keras.layers.Conv2D(64, 2, activation="relu"), keras.layers.MaxPooling2D(),
+                          keras.layers.Flatten(), keras.layers.Dense(128, activation="relu"),
+                          keras.layers.Dense(10, activation="softmax")]),  # k3 first conv
+        keras.Sequential([keras.layers.Dense(64, activation="relu", input_shape=(784,)),
+                          keras.layers.Dense(10, activation="softmax")]),
+    ):
+        other.build()
+        assert other._flagship_view() is None
+    # raw uint8 into conv1 (in_affine) == the normalised float input
+    x8 = torch.randint(0, 256, (2, 28, 28, 1), dtype=torch.uint8)
+    m.eval()
+    a = m(x8)
+    b = m.net[1:](x8.float() / 255.0)
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
