@@ -696,6 +696,37 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
       // split-K there, so every tile of the launch reaches this point exactly once)
       const bool det = det_on();
       const unsigned dmy = (unsigned)(by * gx + bx), dtot = (unsigned)(gx * gy);
+      if (WAVES_M > 1 && det) {
+        // the WAVES_M waves of a column add to the same addresses: in deterministic mode they first meet
+        // in LDS (fixed order), and only the wm == 0 waves issue the atomics
+        float* red = (float*)smem;  // [WAVES_M][2][BN] (the staging tiles are free after the main loop)
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float v = cs[j], q = cs2[j];
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          q += __shfl_xor(q, 16, 64);
+          q += __shfl_xor(q, 32, 64);
+          if (fq == 0) {
+            red[(wm * 2) * BN + wn * WTN + j * 16 + fr] = v;
+            red[(wm * 2 + 1) * BN + wn * WTN + j * 16 + fr] = q;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float v = 0.f, q = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES_M; ++w) {
+            v += red[(w * 2) * BN + wn * WTN + j * 16 + fr];
+            q += red[(w * 2 + 1) * BN + wn * WTN + j * 16 + fr];
+          }
+          // lanes fr of quarter 0 of the wm == 0 waves hold the column totals below
+          cs[j] = (wm == 0 && fq == 0) ? v : 0.f;
+          cs2[j] = (wm == 0 && fq == 0) ? q : 0.f;
+        }
+      }
       if (det) det_turn_begin(DET_GEMM_COLSUM, dmy);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -703,6 +734,7 @@ __device__ __forceinline__ void mfma_gemm_body(const AL& al, const BL& bl, const
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
         const int n = n0 + wn * WTN + j * 16 + fr;
+        if (WAVES_M > 1 && det && wm != 0) continue;  // (their sums went through LDS above)
         if constexpr (has_sq<EP>::value) {
           float q = cs2[j];
           q += __shfl_xor(q, 16, 64);

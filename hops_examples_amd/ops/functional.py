@@ -552,10 +552,10 @@ def _bn_sums_request(ctx, x, pprev, gb, addend):
     if (src is None or pprev is not None or gb is not None or ctx.give is not None or not ctx.needs_input_grad[0]
             or (ctx.gslot is not None and addend is None)):  # a shortcut part not handed over yet: sums incomplete
         return None
-    z2, mean, rstd, act = src
+    z2, mean, rstd, act, acc = src
     if z2.numel() != x.numel() or x.dtype != BF16:
         return None
-    return (z2, mean, rstd, x if act else None, act)
+    return (z2, mean, rstd, x if act else None, act, acc)
 
 
 # The same on the separate (unpaired) dgrad launches: opt-in.  Measured on ResNet-50 (round 5): B=8 flat
@@ -1010,8 +1010,10 @@ class _BNFn(torch.autograd.Function):
         ctx.p = (gamma, beta, act, x.shape, residual is not None)
         ctx.gslot = gslot  # the residual's gradient goes to the conv that also consumes it (_Conv2dFn)
         out = y.view(x.shape)
-        if x.is_cuda and out.dtype == BF16:
-            out._hx_bnsrc = (x2, mean, rstd, act)  # for a consumer conv's dgrad epilogue (bn_sole_consumer)
+        if x.is_cuda and out.dtype == BF16 and "bn_dgrad_sums" not in _disabled():
+            # for a consumer conv's dgrad epilogue (bn_sole_consumer): the BN input, its batch statistics and
+            # this BN's private sums accumulator
+            out._hx_bnsrc = (x2, mean, rstd, act, K.bn_sums_acc(gamma, x.device, C))
         return out
 
     @staticmethod
@@ -1027,7 +1029,7 @@ class _BNFn(torch.autograd.Function):
             # the consuming conv's dgrad already masked dy and reduced the column sums: apply only; the
             # masked dy IS the residual's gradient
             dy2 = dy.view(-1, C)
-            dx = K.bn_bwd_pre(dy2, x2, gamma, mean, rstd, gg, gb, ws)
+            dx = K.bn_bwd_pre(dy2, x2, gamma, mean, rstd, gg, gb, ws, K.bn_sums_acc(gamma, dy.device, C))
             dres = dy2 if has_res else None
             if has_res and ctx.gslot is not None:
                 ctx.gslot["g"] = dres.view(shape)

@@ -264,7 +264,7 @@ def conv2d_dgrad_bn(dy, w, geom, bn, addend=None):
     column sums into its accumulator (finish with ``bn_bwd_pre``).  False: shape not covered (nothing
     launched)."""
     _req(dy, BF16, "dy")
-    z, mean, rstd, yprev, act_prev = bn
+    z, mean, rstd, yprev, act_prev, acc = bn
     _req(z, BF16, "bn z")
     B, H, W, C = geom[:4]
     if addend is not None:
@@ -272,7 +272,7 @@ def conv2d_dgrad_bn(dy, w, geom, bn, addend=None):
     out = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
     rc = _C.ext().conv2d_dgrad_bn(ptr(dy), ptr(w), list(geom), ptr(out), ptr(yprev),
                                   act_id(act_prev) if yprev is not None else 0, ptr(addend), ptr(z), ptr(mean),
-                                  ptr(rstd), ptr(bn_acc(dy.device, C)), stream())
+                                  ptr(rstd), ptr(acc), stream())
     if rc == -2:
         return False
     check(rc, "conv2d_dgrad_bn")
@@ -319,9 +319,9 @@ def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, ad
     if bn is not None:
         if prev is not None or opt_slice is not None or dbias is not None:
             raise ValueError("conv2d_bwd_pair: bn excludes prev / opt_slice / dbias")
-        z, mean, rstd, yprev, act_prev = bn
+        z, mean, rstd, yprev, act_prev, acc = bn
         _req(z, BF16, "bn z")
-        bnargs = (ptr(z), ptr(mean), ptr(rstd), ptr(bn_acc(dy.device, C)))
+        bnargs = (ptr(z), ptr(mean), ptr(rstd), ptr(acc))
         dx = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
         args = (ptr(dx), ptr(yprev), act_id(act_prev) if yprev is not None else 0, 0, ptr(y), act_id(act), [], 0, 0.0,
                 0.0, 0)
@@ -608,6 +608,22 @@ def bn_acc(device, C) -> torch.Tensor:
     return t
 
 
+def bn_sums_acc(owner, device, C) -> torch.Tensor:
+    """A zero-at-rest accumulator (bn_acc's layout) private to ONE BatchNorm (kept on ``owner``, its gamma):
+    the backward column sums that a consumer conv's dgrad epilogue reduces (conv2d_bwd_pair /
+    conv2d_dgrad_bn bn=...) wait there until that BN's apply (bn_bwd_pre) folds and re-zeroes them, so no
+    other BN reduction of the same width that autograd schedules in between can mix into them."""
+    t = getattr(owner, "_hx_bnsum_acc", None) if owner is not None else None
+    if t is None or t.numel() != BN_NREP * 2 * C + 12 * 32 or t.device != torch.device(device):
+        if owner is None:
+            return bn_acc(device, C)
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("BN accumulator must be created before graph capture (run an eager step first)")
+        t = torch.zeros(BN_NREP * 2 * C + 12 * 32, device=device, dtype=F32)
+        owner._hx_bnsum_acc = t
+    return t
+
+
 def bn_fwd_train(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, residual=None, act=0, out=None):
     M, C = x2d.shape
     if out is None:
@@ -680,14 +696,15 @@ def bn_bwd(dy, x, y, gamma, mean, rstd, dgamma, dbeta, ws, act=0, dresidual=None
     return out
 
 
-def bn_bwd_pre(g, x, gamma, mean, rstd, dgamma, dbeta, ws, out=None):
-    """BN backward whose column sums a consumer conv's dgrad epilogue already reduced into the width's
-    accumulator (conv2d_bwd_pair bn=...); ``g`` is the act'-masked output gradient.  One apply launch."""
+def bn_bwd_pre(g, x, gamma, mean, rstd, dgamma, dbeta, ws, acc, out=None):
+    """BN backward whose column sums a consumer conv's dgrad epilogue already reduced into ``acc`` (the BN's
+    own accumulator, bn_sums_acc; conv2d_bwd_pair bn=...); ``g`` is the act'-masked output gradient.  One
+    apply launch, which also re-zeroes ``acc``."""
     M, C = x.shape
     if out is None:
         out = torch.empty_like(x)
     check(_C.ext().bn_bwd_pre(ptr(g), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(out), ptr(dgamma), ptr(dbeta),
-                              ptr(ws), M, C, ptr(bn_acc(g.device, C)), stream()), "bn_bwd_pre")
+                              ptr(ws), M, C, ptr(acc), stream()), "bn_bwd_pre")
     return out
 
 

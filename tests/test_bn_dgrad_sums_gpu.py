@@ -53,9 +53,11 @@ def test_pair_bn_sums_match_unfused(shape, with_addend):
         dw = torch.zeros(CO, k, k, C, device=dev)
         gg, gb, ws = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.empty(2 * C, device=dev)
         if mode == "bn":
-            dX = K.conv2d_bwd_pair(dy, w, g, x, dw, addend=add, bn=(z, mean, rstd, x, "relu"))
+            acc = K.bn_sums_acc(gamma, dev, C)
+            dX = K.conv2d_bwd_pair(dy, w, g, x, dw, addend=add, bn=(z, mean, rstd, x, "relu", acc))
             assert dX is not False
-            dz = K.bn_bwd_pre(dX.view(-1, C), z, gamma, mean, rstd, gg, gb, ws)
+            dz = K.bn_bwd_pre(dX.view(-1, C), z, gamma, mean, rstd, gg, gb, ws, acc)
+            assert int(torch.count_nonzero(acc[: K.BN_NREP * 2 * C])) == 0  # folded and re-zeroed
         else:
             dX = K.conv2d_bwd_pair(dy, w, g, x, dw, addend=add)
             assert dX is not False
@@ -144,9 +146,10 @@ def test_dgrad_bn_sums_match_unfused(shape, with_addend):
     dy = bf(torch.randn(B, H, W, CO, device=dev))
     add = bf(torch.randn(B, H, W, C, device=dev)) if with_addend else None
     gg, gb, ws = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.empty(2 * C, device=dev)
-    dX = K.conv2d_dgrad_bn(dy, w, g, (z, mean, rstd, x, "relu"), addend=add)
+    acc = K.bn_sums_acc(gamma, dev, C)
+    dX = K.conv2d_dgrad_bn(dy, w, g, (z, mean, rstd, x, "relu", acc), addend=add)
     assert dX is not False, "shape should be covered"
-    dz = K.bn_bwd_pre(dX.view(-1, C), z, gamma, mean, rstd, gg, gb, ws)
+    dz = K.bn_bwd_pre(dX.view(-1, C), z, gamma, mean, rstd, gg, gb, ws, acc)
     # reference: fp32 dgrad (+ addend), mask, fp32 autograd BN backward
     dXr = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 1, k // 2)
     dXr = dXr.permute(0, 2, 3, 1)
