@@ -399,6 +399,36 @@ struct EpiDgradBnBF16 {
   __device__ __forceinline__ float second(int m, int n, float g) const {
     return g * ((bf2f(z[(long)m * ldo + n]) - mean[n]) * rstd[n]);
   }
+  // the gg engine's 16-B epilogue (gemm_glds.h): 8 columns n..n+7 of row m, their g and g * xhat added
+  // to the caller's per-thread column sums s1 / s2
+  static constexpr bool kVec8 = true;
+  __host__ __device__ bool vec8_ok() const {
+    return ldo % 8 == 0 && (uintptr_t)out % 16 == 0 && (uintptr_t)y % 16 == 0 && (uintptr_t)add % 16 == 0 &&
+           (uintptr_t)z % 16 == 0;
+  }
+  __device__ __forceinline__ void store8_bn(int m, int n, const float* v, float* s1, float* s2) const {
+    const long o = (long)m * ldo + n;
+    const bf16x8 zero = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16x8 av = add ? *(const bf16x8*)(add + o) : zero;
+    const bf16x8 yv = y ? *(const bf16x8*)(y + o) : zero;
+    const bf16x8 zv = *(const bf16x8*)(z + o);
+    const f32x4 mu0 = *(const f32x4*)(mean + n), mu1 = *(const f32x4*)(mean + n + 4);
+    const f32x4 rs0 = *(const f32x4*)(rstd + n), rs1 = *(const f32x4*)(rstd + n + 4);
+    const float mu[8] = {mu0[0], mu0[1], mu0[2], mu0[3], mu1[0], mu1[1], mu1[2], mu1[3]};
+    const float rs[8] = {rs0[0], rs0[1], rs0[2], rs0[3], rs1[0], rs1[1], rs1[2], rs1[3]};
+    bf16x8 q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j];
+      if (add) t += bf2f((uint16_t)av[j]);
+      if (y) t *= act_grad_from_out(bf2f((uint16_t)yv[j]), act);
+      q[j] = (short)f2bf(t);
+      const float g = bf2f((uint16_t)q[j]);
+      s1[j] += g;
+      s2[j] = fmaf(g, (bf2f((uint16_t)zv[j]) - mu[j]) * rs[j], s2[j]);
+    }
+    *(bf16x8*)(out + o) = q;
+  }
 };
 
 template <class EP, class = void>

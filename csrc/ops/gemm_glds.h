@@ -608,7 +608,62 @@ __global__ __launch_bounds__(512) void gg_kernel(const AS as, const BS bs, const
   // vectorized epilogue (epilogues with store8, no column sum, N % 8 == 0): the tile goes through LDS
   // as fp32 rows and leaves as 16-B stores of 8 consecutive columns (the fragment layout stores 2-B
   // values, four 32-B pieces per wave instruction) — also 16-B loads of the act' / addend operands
-  if constexpr (has_vec8<EP>::value) {
+  // BN-backward dgrad epilogue (EpiDgradBnBF16): the same LDS-staged 16-B path, and each thread's column
+  // sums (its 8-column chunk is fixed: 512 threads, BN / 8 chunks per row) meet in LDS in a fixed order
+  // before one atomic pair per column into this tile's replica row
+  if constexpr (has_bn2<EP>::value) {
+    constexpr int SR = BN + 4;
+    static_assert(BM * SR * 4 <= C::LDS && 512 * 16 * 4 <= C::LDS, "BN epilogue staging must fit the tile's LDS");
+    if (N % 8 == 0 && ep.vec8_ok()) {
+      float* st = (float*)smem;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[(wm * C::WTM + i * 16 + fq * 4 + r) * SR + wn * C::WTN + j * 16 + fr] = acc[i][j][r];
+      __syncthreads();
+      constexpr int CPR = BN / 8;
+      static_assert(512 % CPR == 0, "a thread's column chunk must stay fixed");
+      float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int c = tid; c < BM * CPR; c += 512) {
+        const int row = c / CPR, col = (c - row * CPR) * 8;
+        const int m = m0 + row, n = n0 + col;
+        if (m < M && n < N) {
+          const f32x4 v0 = *(const f32x4*)(st + row * SR + col), v1 = *(const f32x4*)(st + row * SR + col + 4);
+          const float vv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          ep.store8_bn(m, n, vv, s1, s2);
+        }
+      }
+      __syncthreads();  // the staged tile is consumed: its LDS takes the per-thread sums
+      float* red = (float*)smem;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[tid * 16 + j] = s1[j];
+        red[tid * 16 + 8 + j] = s2[j];
+      }
+      __syncthreads();
+      const bool det = det_on();
+      if (det) det_turn_begin(DET_GG_COLSUM, (unsigned)blockIdx.x);
+      if (tid < BN && n0 + tid < N) {
+        const int ch = tid >> 3, j = tid & 7;
+        float a = 0.f, b = 0.f;
+        for (int q = ch; q < 512; q += CPR) {
+          a += red[q * 16 + j];
+          b += red[q * 16 + 8 + j];
+        }
+        float* d = ep.colsum + (long)(v % HOPSX_BN_NREP) * 2 * N;
+        atomicAdd(d + n0 + tid, a);
+        atomicAdd(d + N + n0 + tid, b);
+      }
+      if (det) det_turn_end(DET_GG_COLSUM, (unsigned)blockIdx.x, gridDim.x);
+      return;
+    }
+  }
+  if constexpr (has_vec8<EP>::value && !has_bn2<EP>::value) {
     constexpr int SR = BN + 4;  // fp32 row stride (bank offset 4 between the fragment's 4 rows)
     static_assert(BM * SR * 4 <= C::LDS, "vector epilogue staging must fit the tile's LDS");
     if (N % 8 == 0 && ep.vec8_ok()) {

@@ -558,11 +558,11 @@ def _bn_sums_request(ctx, x, pprev, gb, addend):
     return (z2, mean, rstd, x if act else None, act, acc)
 
 
-# The same on the separate (unpaired) dgrad launches: opt-in.  Measured on ResNet-50 (round 5): B=8 flat
-# (1,532 vs 1,528 img/s), B=64 SLOWER (5.11-5.18 k vs 5.59 k) — the gg engine's per-element epilogue
-# (no 16-B vector path for the three extra operands) costs more on its big tiles than the reduction launch
-# it saves (profiles/r5_bn_dgrad_sums.txt).  The paired backward (CIFAR ResNets) keeps it on.
-_BN_SEPARATE = os.environ.get("HOPSX_BN_SUMS_SEPARATE_DGRAD", "0") == "1"
+# The same on the separate (unpaired) dgrad launches (ResNet-50).  With the gg engine's per-element
+# epilogue it measured slower (B=64 5.1 k vs 5.59 k img/s); with the 16-B LDS-staged BN epilogue
+# (gemm_glds.h, EpiDgradBnBF16::store8_bn) it wins at every batch: B=8 1,530 -> 1,608, B=64 5.58-5.68 k ->
+# 5.94-5.99 k, B=256 8,081 -> 8,503 img/s (profiles/r5_bn_dgrad_sums.txt).  HOPSX_BN_SUMS_SEPARATE_DGRAD=0: off
+_BN_SEPARATE = os.environ.get("HOPSX_BN_SUMS_SEPARATE_DGRAD", "1") == "1"
 
 
 def _dgrad_bn(ctx, dy, w, g, x, add, addend):
@@ -827,9 +827,10 @@ def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, act=None, in_affine=No
         y = F.conv2d(xr, w.permute(0, 3, 1, 2), b, st, pd, dl)
         return _cpu_act(y, a).permute(0, 2, 3, 1).contiguous()
     if padding == "same" and (w.shape[1] % 2 == 0 or w.shape[2] % 2 == 0):
+        # TF 'same' with an even kernel: the extra row / column of padding goes at the end — an asymmetric
+        # geometry (K.conv_geom), not a padded copy of x
         th, tw = dl[0] * (w.shape[1] - 1), dl[1] * (w.shape[2] - 1)
-        x = F.pad(to_compute(x), (0, 0, tw // 2, tw - tw // 2, th // 2, th - th // 2))
-        pd = (0, 0)
+        pd = (th // 2, tw // 2, th - th // 2, tw - tw // 2)
     return _conv_apply(to_compute(x), w, b, st, pd, dl, a, None, bnstats=bnstats and x.is_cuda,
                        gslot=gslot if x.is_cuda else None)
 

@@ -146,14 +146,19 @@ def colsum(x, out):
 
 # -------------------------------------------------------------- conv2d NHWC
 def conv_geom(x_shape, w_shape, stride, padding, dilation):
+    """The kernels' geometry vector.  ``padding`` = (ph, pw), symmetric, or (ph, pw, eh, ew): ph / pw
+    rows / columns of zeros before the input and eh / ew after it (TF 'same' with an even kernel pads
+    one more at the end).  The kernels only see the leading pad and the output size: every gather
+    bounds-checks against H / W, so the trailing pad needs no data."""
     B, H, W, C = x_shape
     CO, KH, KW, CI = w_shape
     assert CI == C, (x_shape, w_shape)
     sh, sw = stride
-    ph, pw = padding
+    ph, pw = padding[:2]
+    eh, ew = (padding[2], padding[3]) if len(padding) == 4 else (ph, pw)
     dh, dw = dilation
-    OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
-    OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+    OH = (H + ph + eh - dh * (KH - 1) - 1) // sh + 1
+    OW = (W + pw + ew - dw * (KW - 1) - 1) // sw + 1
     return [B, H, W, C, OH, OW, CO, KH, KW, sh, sw, ph, pw, dh, dw]
 
 

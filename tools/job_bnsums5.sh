@@ -1,0 +1,13 @@
+set -o pipefail
+o=gpurun_out/${1:-r5_bns5}; mkdir -p $o; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_bn_dgrad_sums_gpu.py tests/test_conv_same_even_gpu.py tests/test_models_gpu.py tests/test_keras_persist_gpu.py > $o/t.log 2>&1 || { grep -E "FAIL|Error|assert" $o/t.log | tail -20; exit 1; }
+tail -1 $o/t.log
+run() { env $1 timeout -k 10 300 python benchmarks/run.py $2 > $o/r.json 2> $o/err.log || { tail -20 $o/err.log; exit 1; }
+  echo "[$1] $2 -> $(python -c "import json; r=json.loads(open('$o/r.json').read().strip().splitlines()[-1]); print(r['value'], r['ms_per_step'])")"; }
+for d in HOPSX_BN_SUMS_SEPARATE_DGRAD=1 X=0 HOPSX_BN_SUMS_SEPARATE_DGRAD=1 X=0; do
+  run $d "resnet50 --batch 64 --steps 12 --warmup 4"
+done
+run HOPSX_BN_SUMS_SEPARATE_DGRAD=1 "resnet50 --batch 8 --steps 30 --warmup 5"
+run X=0 "resnet50 --batch 8 --steps 30 --warmup 5"
+run HOPSX_BN_SUMS_SEPARATE_DGRAD=1 "resnet50 --batch 256 --steps 8 --warmup 3"
+run X=0 "resnet50 --batch 256 --steps 8 --warmup 3"
