@@ -297,6 +297,11 @@ class PersistentMnistStep:
         B = self.geom["batch"]
         saved = [t.clone() for t in (a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor)]
         ok = True
+        # the self-test's launches start together (right after a collective): a hand-off that has not
+        # arrived within a few seconds never will, so a broken exchange costs seconds here, not the
+        # 60 s a training launch waits for a late peer (HOPSX_PERSIST_SELFTEST_TIMEOUT_S)
+        t_run = self.timeout_ms
+        self.timeout_ms = min(t_run, int(1000 * float(os.environ.get("HOPSX_PERSIST_SELFTEST_TIMEOUT_S", "8"))))
         try:
             xs = torch.randint(0, 256, (2, B, 28, 28, 1), dtype=torch.uint8, device=self.device)
             ys = torch.randint(0, 10, (2, B), dtype=torch.int64, device=self.device)
@@ -308,6 +313,7 @@ class PersistentMnistStep:
         except Exception:
             ok, dig = False, None
         finally:
+            self.timeout_ms = t_run
             for t, s in zip((a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor), saved):
                 t.copy_(s)
             torch.cuda.synchronize(self.device)
