@@ -796,7 +796,11 @@ static int colred_grid(int M, int C, int& rpb) {
 static int apply_grid(long nch, int C) {
   const int CG = C >> 3;
   long g = (nch + 511) / 512;  // two chunks per thread per trip
-  static const long maxg = hopsx_env_int("HOPSX_BN_APPLY_MAXG", 4096);
+  // at most 1024 workgroups (several trips per thread on the big ResNet-50 tensors): every workgroup folds
+  // the BN_NREP x 2C replica floats first, so fewer of them means less fold traffic — ResNet-50 B=64
+  // 5.95 k -> 6.07-6.21 k img/s, B=256 8.48 k -> 8.68 k vs 4096 (profiles/r5_bn_apply_grid_ab.txt); the CIFAR
+  // ResNets' tensors need <= 512
+  static const long maxg = hopsx_env_int("HOPSX_BN_APPLY_MAXG", 1024);
   if (g > maxg) g = maxg;
   if (g < 1) g = 1;
   // gridDim*256 must be a multiple of CG (per-thread channel group); CG divides 256

@@ -1,0 +1,7 @@
+set -o pipefail
+o=gpurun_out/${1:-r5_bnknobs2}; mkdir -p $o; export TMPDIR=/tmp
+run() { env $1 timeout -k 10 200 python benchmarks/run.py $2 > $o/r.json 2> $o/err.log || { tail -20 $o/err.log; exit 1; }
+  echo "[$1] $2 -> $(python -c "import json; r=json.loads(open('$o/r.json').read().strip().splitlines()[-1]); print(r['value'], r['ms_per_step'])")"; }
+for k in X=0 HOPSX_BN_APPLY_MAXG=512 HOPSX_BN_APPLY_MAXG=768 HOPSX_BN_APPLY_MAXG=1024 X=0 HOPSX_BN_APPLY_MAXG=1024; do run $k "resnet50 --batch 64 --steps 12 --warmup 4"; done
+for k in X=0 HOPSX_BN_APPLY_MAXG=1024 HOPSX_BN_APPLY_MAXG=512; do run $k "resnet50 --batch 256 --steps 8 --warmup 3"; done
+for k in X=0 HOPSX_BN_APPLY_MAXG=1024; do run $k "resnet50 --batch 8 --steps 30 --warmup 5"; done
