@@ -485,8 +485,11 @@ class _Conv2dFn(torch.autograd.Function):
                     hooks.grad_ready(ctx.prev[1])
                 return (r, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None, None,
                         None, None, None, None, None)
-        side_ok = not K.conv_wgrad_uses_ticket(g, ctx.in_affine)
-        if side_ok:  # wgrad || dgrad on a parallel branch (its kernels keep no shared ticket/workspace)
+        # wgrad || dgrad on a parallel branch (its kernels keep no shared ticket/workspace) — only when there
+        # IS a dgrad to overlap: a layer whose input needs no gradient (the image stem) would only pay the
+        # cross-queue join (ResNet-50 B=8: +4 % with the stem's weight gradient inline, r5_side_stream_ab.txt)
+        side_ok = not K.conv_wgrad_uses_ticket(g, ctx.in_affine) and (ctx.prev is not None or ctx.needs_input_grad[0])
+        if side_ok:
             with _on_side(dy.device, dy, x, ymask, flop=2.0 * dy.numel() * g[7] * g[8] * g[3]):
                 K.conv2d_wgrad(dy, x, g, gw, dbias=gb, y=ymask, act=act, in_affine=ctx.in_affine)
         if ctx.prev is not None:
