@@ -884,7 +884,8 @@ inline GemmPlan plan_gemm(long M, long N, long K, bool allow_split, int num_cu =
   static const long t64_min = hopsx_env_int("HOPSX_GEMM_T64_MIN", 2L * num_cu);
   static const long t128_min = hopsx_env_int("HOPSX_GEMM_T128_MIN", num_cu);
   static const long split_cfg = hopsx_env_int("HOPSX_GEMM_SPLIT_CFG", 1);
-  static const long split_target = hopsx_env_int("HOPSX_GEMM_SPLIT_TARGET", 2);
+  // 4 (was 2): ResNet-50 B=8 +1 %, with HOPSX_GG_MIN_WG=32 +1.7 %; B=64 / CIFAR flat (profiles/r5_gemm_knobs_b8_ab.txt)
+  static const long split_target = hopsx_env_int("HOPSX_GEMM_SPLIT_TARGET", 4);
   const long t64_lim = t64_min >= 0 ? t64_min : num_cu / 2;
   if (M >= 128 && N >= 128 && t128 >= t128_min) p.cfg = 0;
   else if (M >= 48 && N >= 48 && t64 >= t64_lim) p.cfg = 1;

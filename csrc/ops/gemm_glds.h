@@ -748,8 +748,9 @@ inline bool gg_plan(long M, long N, long K, bool allow_split, GgPlan& p, long mi
                     int num_cu = 256) {
   static const long force = hopsx_env_int("HOPSX_GG_CFG", -1);
   // 64: the stage-4 ResNet-50 shapes (7x7, 100 tiles of 128x128) run 1.5-2.2x faster on gg than on
-  // gemm_core.h even at 0.4 workgroups per CU (profiles/r4_gg_min_wg_ab.txt)
-  static const long min_wg_env = hopsx_env_int("HOPSX_GG_MIN_WG", 64);
+  // gemm_core.h even at 0.4 workgroups per CU (profiles/r4_gg_min_wg_ab.txt); 32 (round 5): the B=8
+  // shapes with 32-63 tiles too (ResNet-50 B=8 +1.5 %, B=64 / CIFAR flat: profiles/r5_gemm_knobs_b8_ab.txt)
+  static const long min_wg_env = hopsx_env_int("HOPSX_GG_MIN_WG", 32);
   const long min_wg = min_wg_override >= 0 ? min_wg_override : min_wg_env;
   static const long split_target = hopsx_env_int("HOPSX_GG_SPLIT_TARGET", 1);
   static const long min_ks = hopsx_env_int("HOPSX_GG_SPLIT_MINKT", 8);
