@@ -18,6 +18,7 @@ MI355X-specific choices:
 """
 from __future__ import annotations
 
+import os
 import time
 from pathlib import Path
 
@@ -364,6 +365,14 @@ def _default_device() -> torch.device:
     return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
 
 
+def _fits_hbm(x, y, limit=8 << 30) -> bool:
+    """Whole training arrays small enough to keep resident on the device during fit."""
+    def nbytes(a):
+        return a.numel() * a.element_size() if isinstance(a, torch.Tensor) else np.asarray(a).nbytes
+
+    return os.environ.get("HOPSX_KERAS_DEVICE_BATCHES", "1") == "1" and nbytes(x) + nbytes(y) <= limit
+
+
 def _batches(x, y, batch_size, shuffle, rng):
     n = len(x)
     idx = rng.permutation(n) if shuffle else np.arange(n)
@@ -552,6 +561,77 @@ class Sequential(tnn.Module):
         self._res_cache = (key, xs, ys)
         return xs, ys
 
+    def _device_batches(self, x, y, batch_size, shuffle, rng):
+        key = (id(x), id(y), len(x), "any")
+        c = getattr(self, "_res_any", None)
+        if c is None or c[0] != key:
+            xs = _to_tensor(x, self.device)
+            ys = _to_tensor(y, self.device, label=True)
+            self._res_any = c = (key, xs, ys)
+        xs, ys = c[1], c[2]
+        n = xs.shape[0]
+        if shuffle:
+            g = torch.Generator(device=self.device)
+            g.manual_seed(int(rng.integers(1 << 62)))
+            idx = torch.randperm(n, device=self.device, generator=g)
+        else:
+            idx = torch.arange(n, device=self.device)
+        for s in range(0, n, batch_size):
+            j = idx[s:s + batch_size]
+            yield xs.index_select(0, j), ys.index_select(0, j)
+
+    def _fit_epoch_resident(self, x, y, batch_size, shuffle, rng):
+        """One epoch of the multi-kernel TrainStep on device-resident data: the epoch's shuffled batches are
+        written into ONE persistent [nbatch, B, ...] buffer (so the captured multi-step graphs and the
+        optimizer's next-batch prefetch stay bound to it), then ``run_resident`` replays
+        steps_per_execution steps per graph launch with no per-batch host work; every step's loss /
+        correct count is added on the device (``on_out``).  A partial last batch runs as one step."""
+        st = self._step
+        key = (id(x), id(y), len(x), "any")
+        c = getattr(self, "_res_any", None)
+        if c is None or c[0] != key:
+            self._res_any = c = (key, _to_tensor(x, self.device), _to_tensor(y, self.device, label=True))
+        xs_all, ys_all = c[1], self._labels(c[2])
+        N, B = xs_all.shape[0], int(batch_size)
+        nb = N // B
+        buf = getattr(self, "_ep_buf", None)
+        if buf is None or buf[0].shape != (nb, B) + tuple(xs_all.shape[1:]) or buf[1].shape != (nb, B) + tuple(ys_all.shape[1:]):
+            buf = (torch.empty((nb, B) + tuple(xs_all.shape[1:]), device=self.device, dtype=xs_all.dtype),
+                   torch.empty((nb, B) + tuple(ys_all.shape[1:]), device=self.device, dtype=ys_all.dtype))
+            self._ep_buf = buf
+        xs, ys = buf
+        if shuffle:
+            g = torch.Generator(device=self.device)
+            g.manual_seed(int(rng.integers(1 << 62)))
+            idx = torch.randperm(N, device=self.device, generator=g)
+        else:
+            idx = torch.arange(N, device=self.device)
+        torch.index_select(xs_all, 0, idx[: nb * B], out=xs.view((nb * B,) + tuple(xs_all.shape[1:])))
+        torch.index_select(ys_all, 0, idx[: nb * B], out=ys.view((nb * B,) + tuple(ys_all.shape[1:])))
+        # the epoch starts at its first batch: the graph's static input buffers hold the batch the next
+        # replay trains on (the previous epoch's prefetch), so they are refilled and the cursor reset
+        st._rn = 0
+        if st._cursor is not None and st._sx is not None and not isinstance(st._sx, (tuple, list)):
+            st._sx.copy_(xs[0])
+            st._sy.copy_(ys[0])
+            st._cursor.zero_()
+        tot = torch.zeros(2, device=self.device)
+
+        def on_out(o):
+            cor = o.get("correct")
+            tot.add_(torch.stack((o["loss"].reshape(-1)[0].float() * B,
+                                  cor.reshape(-1)[0].float() if cor is not None else torch.zeros((), device=self.device))))
+
+        st.prepare_resident(xs, ys, n=nb)
+        st.run_resident(xs, ys, nb, on_out=on_out)
+        if N > nb * B:
+            j = idx[nb * B:]
+            r = st(xs_all.index_select(0, j), ys_all.index_select(0, j))
+            cor = r.get("correct")
+            tot.add_(torch.stack((r["loss"].reshape(-1)[0].float() * (N - nb * B),
+                                  cor.reshape(-1)[0].float() if cor is not None else torch.zeros((), device=self.device))))
+        return tot[0], tot[1], N, ys_all
+
     def _fit_epoch_fast(self, x, y, shuffle, rng):
         """One epoch on the persistent engine: the epoch's batches (shuffled on the device) resident in
         HBM, 32 steps per launch, per-step loss / correct read back once per launch on the device; a
@@ -629,10 +709,16 @@ class Sequential(tnn.Module):
         arrays = isinstance(x, (np.ndarray, torch.Tensor)) and y is not None
         fast_ok = (arrays and not per_batch and steps_per_epoch is None and len(x) >= batch_size
                    and str(x.dtype) in ("uint8", "torch.uint8") and tuple(x.shape[1:]) in ((28, 28), (28, 28, 1)))
-        if fast_ok and self._step is None:
-            self._batch_hint = int(batch_size)
+        if arrays and self._step is None:  # build / place the model now (the device decides the batch source)
+            if fast_ok:
+                self._batch_hint = int(batch_size)
             self._prepare(_to_tensor(x[:1], "cpu"))
         fast = fast_ok and self._fast is not None and int(batch_size) == self.geom_batch
+        # any other model on whole arrays: the TrainStep's resident multi-step path (same epoch semantics)
+        resident = (not fast and arrays and not per_batch and steps_per_epoch is None and len(x) >= batch_size
+                    and self.device is not None and self.device.type == "cuda" and self._step is not None
+                    and getattr(self._step, "dp", None) is None and _fits_hbm(x, y)
+                    and os.environ.get("HOPSX_KERAS_RESIDENT", "1") == "1")
         for c in cbs:
             getattr(c, "on_train_begin", lambda *a: None)({})
         dataset_iter = None
@@ -640,11 +726,16 @@ class Sequential(tnn.Module):
             t0 = time.time()
             for c in cbs:
                 getattr(c, "on_epoch_begin", lambda *a: None)(epoch, {})
-            if fast:
-                tl, tcor, tn = self._fit_epoch_fast(x, y, shuffle, rng)
+            if fast or resident:
+                if fast:
+                    tl, tcor, tn = self._fit_epoch_fast(x, y, shuffle, rng)
+                    width = 1
+                else:
+                    tl, tcor, tn, ys_all = self._fit_epoch_resident(x, y, batch_size, shuffle, rng)
+                    width = self._label_width(ys_all)
                 logs = {"loss": float(tl) / tn}
                 if "accuracy" in self._metrics or "acc" in self._metrics:
-                    logs["accuracy"] = float(tcor) / tn
+                    logs["accuracy"] = float(tcor) / (tn * width)
                 if validation_data is not None:
                     vl = self.evaluate(*validation_data, batch_size=batch_size, verbose=0, return_dict=True)
                     logs.update({"val_" + k: v for k, v in vl.items()})
@@ -657,7 +748,11 @@ class Sequential(tnn.Module):
                 if self.stop_training:
                     break
                 continue
-            if y is None and x is not None and not isinstance(x, (np.ndarray, torch.Tensor)):
+            if arrays and self.device is not None and self.device.type == "cuda" and _fits_hbm(x, y):
+                # whole arrays: uploaded once, the epoch's batches gathered on the device (no host-to-device
+                # copy per batch; the numpy permutation's seed drives the device permutation)
+                src = self._device_batches(x, y, batch_size, shuffle, rng)
+            elif y is None and x is not None and not isinstance(x, (np.ndarray, torch.Tensor)):
                 if dataset_iter is None or steps_per_epoch is None:
                     dataset_iter = iter(x)
                 src = dataset_iter

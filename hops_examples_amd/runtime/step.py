@@ -95,6 +95,7 @@ class TrainStep:
         self._gU = None
         self._outU = None
         self._gR: dict = {}  # remainder graphs: U -> (graph, outputs)
+        self._outs_of: dict = {}  # id(multi-step graph) -> every captured step's outputs
         self._pool = None
         if dp is not None:
             optimizer.grad_scale = dp.grad_scale()
@@ -288,13 +289,16 @@ class TrainStep:
         self._sync_hp()
         try:
             g = torch.cuda.CUDAGraph()
+            outs = []
             with _capture_graph(g, pool=self._pool):
                 for _ in range(U):
                     out = self._fwd_bwd(self._sx, self._sy)
+                    outs.append(out)  # every step's outputs stay valid in the graph's pool (run_resident on_out)
                     self._tail()  # the same tail as the one-step graph (incl. the PS post-step)
         finally:
             self._pf_opt.prefetch = None
         torch.cuda.synchronize()
+        self._outs_of[id(g)] = outs
         if U == self.steps_per_execution:
             self._gU, self._outU = g, out
         return g, out
@@ -311,38 +315,45 @@ class TrainStep:
             if rem > 1 and rem not in self._gR:
                 self._gR[rem] = self._capture_multi(xs, ys, rem)
 
-    def _replay_multi(self, g, U: int):
+    def _replay_multi(self, g, U: int, on_out=None):
         health.beat_range(self._n + 1, U)  # one heartbeat (and fault check) for the U replayed steps
         self._n += U
         self._sync_hp()
         g.replay()
         self._after_replay()
+        if on_out is not None:
+            for o in self._outs_of[id(g)]:
+                on_out(o)
 
-    def run_resident(self, xs, ys, n: int):
+    def run_resident(self, xs, ys, n: int, on_out=None):
         """``n`` consecutive steps on the resident epoch (see step_resident); returns the last
         step's outputs.  Single-GPU and P2P data-parallel graph steps run ``steps_per_execution`` at
-        a time (a prepared remainder graph takes the tail)."""
+        a time (a prepared remainder graph takes the tail).  ``on_out(outputs)`` is called for EVERY
+        step, in order, right after the launch that ran it (device tensors: e.g. keras.fit's epoch
+        loss / accuracy totals)."""
         r = None
         rem = n % self.steps_per_execution
         if n > self.steps_per_execution and rem in self._gR and self._multi_ok(xs, ys):
             # the short remainder graph first: its launch is cheaper, so the GPU starts sooner and the
             # full graphs are issued while it runs
             g, r = self._gR[rem]
-            self._replay_multi(g, rem)
+            self._replay_multi(g, rem, on_out)
             n -= rem
         while n > 0:
             if n in self._gR and n < self.steps_per_execution and self._multi_ok(xs, ys):
                 g, r = self._gR[n]
-                self._replay_multi(g, n)
+                self._replay_multi(g, n, on_out)
                 n = 0
                 continue
             if n < self.steps_per_execution or not self._multi_ok(xs, ys):
                 r = self.step_resident(xs, ys)
+                if on_out is not None:
+                    on_out(r)
                 n -= 1
                 continue
             if self._gU is None:
                 self._capture_multi(xs, ys)
-            self._replay_multi(self._gU, self.steps_per_execution)
+            self._replay_multi(self._gU, self.steps_per_execution, on_out)
             n -= self.steps_per_execution
             r = self._outU
         return r

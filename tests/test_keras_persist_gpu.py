@@ -81,3 +81,46 @@ def test_keras_fit_persistent_throughput():
     ips = 2 * 60000 / (time.perf_counter() - t)
     print(f"keras fit on the persistent engine: {ips:,.0f} images/s")
     assert m._fast is not None and ips > 3e5, ips
+
+
+def test_keras_fit_resident_e1_model():
+    """Any model fit on whole arrays (here the E1 Keras MNIST CNN, mnist.ipynb:154-164: k4 convs, pool 4,
+    dropout, Adam) trains on device-resident data: by default the TrainStep's multi-step graphs over a
+    resident epoch buffer (keras.py _fit_epoch_resident); HOPSX_KERAS_RESIDENT=0 gathers per batch on the
+    device; HOPSX_KERAS_DEVICE_BATCHES=0 copies every batch from the host.  All learn alike; images/s printed."""
+    from hops_examples_amd import keras
+
+    x, y = _data(8192 + 5, seed=2)  # + a partial last batch
+    modes = {"resident": {}, "device_batches": {"HOPSX_KERAS_RESIDENT": "0"},
+             "host_batches": {"HOPSX_KERAS_RESIDENT": "0", "HOPSX_KERAS_DEVICE_BATCHES": "0"}}
+    res = {}
+    for name, env in modes.items():
+        os.environ.update(env)
+        try:
+            torch.manual_seed(0)
+            m = keras.Sequential([
+                keras.layers.Conv2D(32, 4, activation="relu", input_shape=(28, 28, 1)),
+                keras.layers.Conv2D(64, 4, activation="relu"),
+                keras.layers.MaxPooling2D(4),
+                keras.layers.Dropout(0.5),
+                keras.layers.Flatten(),
+                keras.layers.Dense(128, activation="relu"),
+                keras.layers.Dropout(0.5),
+                keras.layers.Dense(10, activation="softmax"),
+            ])
+            m.compile(optimizer="adam", loss="sparse_categorical_crossentropy", metrics=["accuracy"])
+            h0 = m.fit(x, y, batch_size=32, epochs=1, verbose=0)  # warm-up epoch (build, graph capture)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            h = m.fit(x, y, batch_size=32, epochs=2, verbose=0)
+            torch.cuda.synchronize()
+            res[name] = (round(2 * len(x) / (time.perf_counter() - t)), h0.history["loss"][0],
+                         h.history["loss"][-1], h.history["accuracy"][-1])
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+    print("keras fit E1 model (images/s, first-epoch loss, last loss, last accuracy):", res)
+    for name, (_, l0, l1, acc) in res.items():
+        assert acc > 0.9 and l1 < l0, (name, res)
+    # the first epoch sees the same data in the same order in every mode: its mean loss agrees
+    assert abs(res["resident"][1] - res["host_batches"][1]) < 0.1 * res["host_batches"][1] + 0.05, res
