@@ -590,8 +590,12 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
   if (smallk_ok(g, dy, y, ws, ws_elems, counter)) {
     const long total = (long)K * (g.CO / 8);
     // ~16 work items per thread: the in-launch combine then reads only blocks x CO x (K+1)
-    // floats (one row per workgroup; ~23 rows at the MNIST batch of 32)
-    long blocks = (total + 4095) / 4096;
+    // floats (one row per workgroup; ~23 rows at the MNIST batch of 32).  At 16 taps (the E1 / HPO
+    // models' 4x4 input convs) a thread holds 8 x 17 accumulators (one wave per SIMD): 2 items per thread
+    // instead, ~6x the workgroups (E1 keras fit 131 k -> 158 k img/s: profiles/r5_e1_fit_kernels.txt)
+    static const long items_env = hopsx_env_int("HOPSX_SMALLK_ITEMS", 0);
+    const long items = items_env > 0 ? items_env : (N >= 16 ? 2 : 16);
+    long blocks = (total + 256 * items - 1) / (256 * items);
     if (blocks > 128) blocks = 128;
     if (blocks < 1) blocks = 1;
 #define HOPSX_SMALLK(KK)                                                                                      \

@@ -615,22 +615,23 @@ class Sequential(tnn.Module):
             st._sx.copy_(xs[0])
             st._sy.copy_(ys[0])
             st._cursor.zero_()
-        tot = torch.zeros(2, device=self.device)
+        tot_l = torch.zeros((), device=self.device)
+        tot_c = torch.zeros((), device=self.device, dtype=torch.int64)
 
-        def on_out(o):
-            cor = o.get("correct")
-            tot.add_(torch.stack((o["loss"].reshape(-1)[0].float() * B,
-                                  cor.reshape(-1)[0].float() if cor is not None else torch.zeros((), device=self.device))))
+        def on_out(outs):  # one launch's steps: a stack + a sum per statistic, not ops per step
+            tot_l.add_(torch.stack([o["loss"].reshape(()) for o in outs]).sum(), alpha=B)
+            if outs[0].get("correct") is not None:
+                tot_c.add_(torch.stack([o["correct"].reshape(()) for o in outs]).sum())
 
         st.prepare_resident(xs, ys, n=nb)
         st.run_resident(xs, ys, nb, on_out=on_out)
         if N > nb * B:
             j = idx[nb * B:]
             r = st(xs_all.index_select(0, j), ys_all.index_select(0, j))
-            cor = r.get("correct")
-            tot.add_(torch.stack((r["loss"].reshape(-1)[0].float() * (N - nb * B),
-                                  cor.reshape(-1)[0].float() if cor is not None else torch.zeros((), device=self.device))))
-        return tot[0], tot[1], N, ys_all
+            tot_l.add_(r["loss"].reshape(()), alpha=N - nb * B)
+            if r.get("correct") is not None:
+                tot_c.add_(r["correct"].reshape(()))
+        return tot_l, tot_c, N, ys_all
 
     def _fit_epoch_fast(self, x, y, shuffle, rng):
         """One epoch on the persistent engine: the epoch's batches (shuffled on the device) resident in

@@ -322,15 +322,14 @@ class TrainStep:
         g.replay()
         self._after_replay()
         if on_out is not None:
-            for o in self._outs_of[id(g)]:
-                on_out(o)
+            on_out(self._outs_of[id(g)])
 
     def run_resident(self, xs, ys, n: int, on_out=None):
         """``n`` consecutive steps on the resident epoch (see step_resident); returns the last
         step's outputs.  Single-GPU and P2P data-parallel graph steps run ``steps_per_execution`` at
-        a time (a prepared remainder graph takes the tail).  ``on_out(outputs)`` is called for EVERY
-        step, in order, right after the launch that ran it (device tensors: e.g. keras.fit's epoch
-        loss / accuracy totals)."""
+        a time (a prepared remainder graph takes the tail).  ``on_out(list of outputs)`` receives EVERY
+        step's outputs, once per launch (a replayed graph's U steps together), right after it (device
+        tensors: e.g. keras.fit's epoch loss / accuracy totals, a few small ops per launch)."""
         r = None
         rem = n % self.steps_per_execution
         if n > self.steps_per_execution and rem in self._gR and self._multi_ok(xs, ys):
@@ -348,7 +347,7 @@ class TrainStep:
             if n < self.steps_per_execution or not self._multi_ok(xs, ys):
                 r = self.step_resident(xs, ys)
                 if on_out is not None:
-                    on_out(r)
+                    on_out([r])
                 n -= 1
                 continue
             if self._gU is None:
