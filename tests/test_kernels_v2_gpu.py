@@ -405,7 +405,9 @@ def test_paired_conv_backward_matches_separate_launches(monkeypatch, model):
         # backward amplify): the pair must agree with the separate launches as well as a rerun does
         cos = lambda a, b: float(torch.nn.functional.cosine_similarity(a, b, dim=0))  # noqa: E731
         noise, diff = cos(grads[0], grads[2]), cos(grads[0], grads[1])
-        assert diff > 0.97 and diff > noise - 0.01, (diff, noise)
+        # (with deterministic BN sums a rerun is near bit-exact, so the relative bound is capped:
+        # the pair and the separate launches still sum in a different order)
+        assert diff > 0.97 and diff > min(noise, 0.99) - 0.02, (diff, noise)
 
 
 @pytest.mark.parametrize("model", ["mirrored", "torch"])
