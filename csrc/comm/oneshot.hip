@@ -554,6 +554,30 @@ __global__ __launch_bounds__(kThreads) void dp_rs_k(float* grad, long n, long bl
   if (threadIdx.x == 0) sy.epochs[b] = e;
 }
 
+// ---- exchange-protocol instruments (runtime/persist_sim.py and the cross-process tests) ----
+// A peer rank emulated from another process: push `n` 4-byte words into a (typically IPC-mapped,
+// uncached) exchange buffer with system-scope stores, as a producer rank's persistent kernel does.
+// The flags go in a SECOND launch on the same stream (xfill_k), so every payload word has completed
+// before any flag is visible — the producer side of the persistent step's hand-off.
+__global__ __launch_bounds__(kThreads) void xpush_k(unsigned* dst, const unsigned* __restrict__ src, long n) {
+  for (long i = blockIdx.x * (long)kThreads + threadIdx.x; i < n; i += (long)gridDim.x * kThreads)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(kThreads) void xfill_k(unsigned* dst, long n, unsigned v) {
+  for (long i = blockIdx.x * (long)kThreads + threadIdx.x; i < n; i += (long)gridDim.x * kThreads)
+    __hip_atomic_store(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Occupancy hog: `gridDim.x` workgroups that hold `lds` bytes of LDS each (one per CU at > 80 KiB) and
+// sleep for `ticks` of the 100 MHz wall clock — a concurrently resident kernel for the persistent
+// step's co-residency test.  Bounded: every wave leaves after `ticks`.
+__global__ __launch_bounds__(64) void hog_k(long long ticks, unsigned* touch) {
+  extern __shared__ unsigned hog_lds[];
+  const long long t0 = wall_clock64();
+  hog_lds[threadIdx.x] = threadIdx.x;
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  if (touch && threadIdx.x == 0 && blockIdx.x == 0) touch[0] = hog_lds[1];
+}
+
 py::bytes handle_of(u ptr) {
   hipIpcMemHandle_t h;
   HIP_OK(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr)));
@@ -612,6 +636,36 @@ PYBIND11_MODULE(_hopsx_comm, m) {
   });
   m.def("close", [](u p) { HIP_OK(hipIpcCloseMemHandle(reinterpret_cast<void*>(p))); });
   m.def("handle_size", []() { return (int)sizeof(hipIpcMemHandle_t); });
+  // synchronous device copy between raw pointers (exchange buffers <-> tensors, runtime/persist_sim.py)
+  m.def("copy", [](u dst, u src, long bytes) {
+    if (bytes <= 0) return;
+    HIP_OK(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes, hipMemcpyDefault));
+  });
+  // system-scope payload push / flag fill (4-byte words) on `stream`: the emulated peer's producer side
+  m.def("xpush", [](u dst, u src, long bytes, u stream) {
+    if (bytes <= 0 || (bytes & 3) || ((dst | src) & 3u)) throw std::runtime_error("xpush: 4-B aligned words");
+    const long n = bytes / 4;
+    const int blocks = (int)std::min<long>(256, (n + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(xpush_k, dim3(blocks), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<unsigned*>(dst), reinterpret_cast<const unsigned*>(src), n);
+    HIP_OK(hipGetLastError());
+  });
+  m.def("xfill", [](u dst, long nwords, unsigned value, u stream) {
+    if (nwords <= 0 || (dst & 3u)) throw std::runtime_error("xfill: 4-B aligned words");
+    const int blocks = (int)std::min<long>(64, (nwords + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(xfill_k, dim3(blocks), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<unsigned*>(dst), nwords, value);
+    HIP_OK(hipGetLastError());
+  });
+  m.def("hog", [](double seconds, int blocks, int lds_bytes, u touch, u stream) {
+    if (blocks < 1 || blocks > 4096 || lds_bytes < 256 || lds_bytes > 160 * 1024 || !(seconds > 0 && seconds < 10))
+      throw std::runtime_error("hog: bad shape");
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(hog_k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               lds_bytes));
+    hipLaunchKernelGGL(hog_k, dim3(blocks), dim3(64), lds_bytes, reinterpret_cast<hipStream_t>(stream),
+                       spin_ticks(seconds), reinterpret_cast<unsigned*>(touch));
+    HIP_OK(hipGetLastError());
+  });
 
   // out = sum over ranks of in (fp32, n elements, n <= cap); blocks <= MAX_BLOCKS, identical on all
   // ranks; epochs: int32[MAX_BLOCKS] device counters (zeroed once); err: int32 sticky device flag;

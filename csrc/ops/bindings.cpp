@@ -215,7 +215,7 @@ HX_PYMOD(HOPSX_MODNAME) {
     return hopsx_unpad_cin_add(P<float>(g), R, C, cp, P<float>(tgt), S(st));
   });
   m.def("mnist_persist_geom", []() {
-    std::vector<long> g(14);
+    std::vector<long> g(22);
     hopsx_mnist_persist_geom(g.data());
     return g;
   });

@@ -148,6 +148,7 @@ struct Args {
   int nsteps;
   int acquire;  // 1: agent-scope acquire after every poll (diagnostic; the sc1 form needs none)
   long long tmo;  // wall-clock ticks a poll waits before it declares the producer lost
+  long long tmo0;  // the same for step 0's purely local waits (co-residency: HOPSX_PERSIST_START_MS)
   int pollw, stagger;  // waves polling a hand-off wait and their start offsets (HOPSX_PERSIST_POLLW / _STAGGER)
   int pollw_a, pollw_b, pollw_c, pollw_d;  // per hand-off (HOPSX_PERSIST_POLLW_A.._D, default POLLW; C: 4)
   int head1w;          // 1: one wave computes the head from registers and publishes B (HOPSX_PERSIST_HEAD1W)
@@ -600,7 +601,11 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     if (s + 1 < a.nsteps) xv = xload(s + 1);  // next step's patch, consumed next iteration
     stamp(a, s, 2);
     // ---- B: dh of all 32 images ----
-    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(2, s), a.acquire, s_ok, a.tmo, a.pollw_b, a.stagger)) return;
+    // (step 0: the heads run on this GPU only, so a B that has not come within tmo0 means workgroups of
+    // this launch are not resident — fail fast with the co-residency code instead of waiting out tmo)
+    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, s ? ecode(2, s) : ecode(12, 0), a.acquire, s_ok,
+                  s ? a.tmo : a.tmo0, a.pollw_b, a.stagger))
+      return;
     if constexpr (DP) {
       drain();
       __syncthreads();
@@ -1033,7 +1038,9 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     const int par = s & 1;
     const int y = (int)a.ys[((cur0 + s) % a.nbatch) * B + i];
     // ---- A: reduce the 169 fc1 partial rows of image i (fixed order) ----
-    if (!wait_all(a.flags + FL_A, NPOS, ep, a.err, ecode(1, s), a.acquire, s_ok, a.tmo, a.pollw_a, a.stagger)) return;
+    if (!wait_all(a.flags + FL_A, NPOS, ep, a.err, s ? ecode(1, s) : ecode(12, 0), a.acquire, s_ok,
+                  s ? a.tmo : a.tmo0, a.pollw_a, a.stagger))
+      return;
     stamp(a, s, 0);
     {
       const int n4 = tid & 31, g = tid >> 5;
@@ -1164,7 +1171,9 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
     }
     stamp(a, s, 1);
     // ---- replicated fc2 / fc1-bias update from every image's payload ----
-    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, ecode(5, s), a.acquire, s_ok, a.tmo, a.pollw, a.stagger)) return;
+    if (!wait_all(a.flags + FL_B, NHEAD, ep, a.err, s ? ecode(5, s) : ecode(12, 0), a.acquire, s_ok,
+                  s ? a.tmo : a.tmo0, a.pollw, a.stagger))
+      return;
     {
       const auto R = rsrc(a.slabB + (long)par * NHEAD * PAY);
       constexpr int NK = (NHEAD * PAY / 4 + 255) / 256;
@@ -1365,8 +1374,10 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.loopback = (int)iv[15];
   a.xfence = (int)iv[17];
   a.tmo = (long long)iv[16] * 100000ll;  // ms -> 100 MHz ticks
+  a.tmo0 = a.tmo;
   // launch knobs (environment), read once and again after hopsx_mnist_persist_reload_knobs (tools/persist_ab.py)
-  static int kn_ok = 0, kn_pollw, kn_stagger, kn_a, kn_b, kn_c, kn_d, kn_head1w, kn_memset;
+  static int kn_ok = 0, kn_pollw, kn_stagger, kn_a, kn_b, kn_c, kn_d, kn_head1w, kn_memset, kn_coop;
+  static long kn_start_ms;
   if (!kn_ok || g_persist_reload) {
     auto pw = [&](const char* name, long dflt) {
       const long v = hopsx_env_int(name, dflt);
@@ -1383,6 +1394,15 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
     kn_d = pw("HOPSX_PERSIST_POLLW_D", kn_pollw);
     kn_head1w = (int)hopsx_env_int("HOPSX_PERSIST_HEAD1W", 1);  // 25.8 -> 25.5 us/step (same profile)
     kn_memset = (int)hopsx_env_int("HOPSX_PERSIST_MEMSET", 0);  // (the round-4 form, for A/B)
+    // co-residency: step 0's local hand-offs give up after HOPSX_PERSIST_START_MS (every workgroup starts
+    // within microseconds when the grid is resident; anything else means a concurrent kernel holds CUs the
+    // grid needs): measured 50 ms to the co-residency error with a kernel holding 128 CUs, instead of the
+    // 2 s / 60 s hand-off timeout.  HOPSX_PERSIST_COOP=1 launches cooperatively instead: ROCm then checks
+    // the grid against the device's capacity only (what launchable() already does), not against kernels
+    // already resident, and costs 0.6 us/step at 32 steps per launch (1.226M -> 1.200M img/s,
+    // profiles/r6_persist_dp_sim.txt), so it is off by default
+    kn_coop = (int)hopsx_env_int("HOPSX_PERSIST_COOP", 0);
+    kn_start_ms = hopsx_env_int("HOPSX_PERSIST_START_MS", 50);
     kn_ok = 1;
     g_persist_reload = 0;
   }
@@ -1393,6 +1413,7 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   a.pollw_c = kn_c;
   a.pollw_d = kn_d;
   a.head1w = kn_head1w;
+  if (kn_start_ms > 0 && kn_start_ms * 100000ll < a.tmo) a.tmo0 = kn_start_ms * 100000ll;
   a.inv_gb = 1.f / (float)(world * B);
   if (dp) {
     a.xstep = (long long*)p[18];
@@ -1416,6 +1437,17 @@ extern "C" int hopsx_mnist_persist(const uint64_t* p, int np, const long* iv, in
   if (kn_memset) {  // (the round-4 form, for A/B: zeroed flags each launch)
     const hipError_t e = hipMemsetAsync(a.flags, 0, FL_WORDS * sizeof(unsigned), st);
     if (e != hipSuccess) return (int)e;
+  }
+  if (kn_coop) {
+    // cooperative launch: refused at once (hipErrorCooperativeLaunchTooLarge) when the device cannot hold
+    // all GRID workgroups together, instead of workgroups spinning on hand-offs that cannot come
+    void* kargs[] = {(void*)&a};
+    const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(GRID), dim3(256), kargs, LDS_BYTES, st);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // clear the sticky launch error; the caller raises on the return code
+      return (int)e;
+    }
+    return (int)hipSuccess;
   }
   if (dp)
     hipLaunchKernelGGL(mnist_persist_k<true>, dim3(GRID), dim3(256), LDS_BYTES, st, a);
@@ -1453,4 +1485,14 @@ extern "C" void hopsx_mnist_persist_geom(long* g) {
   g[11] = X_BYTES;
   g[12] = XF_WORDS;
   g[13] = XMAX;
+  // exchange-buffer layout (runtime/persist_sim.py): region offset, per-slot bytes, for the pooled
+  // fragments, dh^T fragments, head gradients and conv slice sums ([2 parities][XMAX slots] each)
+  g[14] = XO_POOL;
+  g[15] = XS_POOL;
+  g[16] = XO_DHT;
+  g[17] = XS_DHT;
+  g[18] = XO_FC2;
+  g[19] = XS_FC2;
+  g[20] = XO_CONV;
+  g[21] = XS_CONV;
 }

@@ -51,7 +51,8 @@ def geometry() -> dict:
     if _GEOM is None:
         g = _ext().mnist_persist_geom()
         _GEOM = dict(zip(["batch", "npos", "nhead", "grid", "nconv", "nslice", "slice", "pay", "flag_words",
-                          "lds_bytes", "d_bytes", "x_bytes", "xflag_words", "max_ranks"], g))
+                          "lds_bytes", "d_bytes", "x_bytes", "xflag_words", "max_ranks", "xo_pool", "xs_pool",
+                          "xo_dht", "xs_dht", "xo_fc2", "xs_fc2", "xo_conv", "xs_conv"], g))
     return _GEOM
 
 
@@ -138,9 +139,12 @@ class PersistentMnistStep:
         return launchable(a.device, world)[0]
 
     def __init__(self, model, opt, steps_per_launch: int = 32, debug_stamps: bool = False, world: int | None = None,
-                 loopback: int = 0, timeout_s: float | None = None):
+                 loopback: int = 0, timeout_s: float | None = None, exchange=None):
         """``world``: replicas (default: the process group's size; 1 without one).  ``loopback``: play
-        that many ranks in this one process (tests).  ``timeout_s``: how long a hand-off waits before
+        that many ranks in this one process (tests).  ``exchange``: a simulated exchange
+        (runtime/persist_sim.py ExchangeSim) — the real data-parallel instantiation (loopback off), whose
+        peer buffers / flag pages the simulator owns, so one process can play ranks that hold DIFFERENT
+        batches.  ``timeout_s``: how long a hand-off waits before
         the launch is declared failed (default 2 s on one GPU, ``HOPSX_PERSIST_TIMEOUT_S`` or 60 s
         across ranks, whose launches can start far apart)."""
         from ..ops.functional import rng_state
@@ -175,7 +179,9 @@ class PersistentMnistStep:
         # system-scope write-through and drained before the flag, which is the release for them; the
         # fence only writes back OTHER dirty L2 lines (measured +3 us / step at 8 loopback ranks)
         self.xfence = int(os.environ.get("HOPSX_PERSIST_XFENCE", "0"))
-        if self.loopback > 1:
+        if exchange is not None:
+            self.world, self.rank = int(exchange.world), 0
+        elif self.loopback > 1:
             self.world, self.rank = self.loopback, 0
         else:
             self.world = int(world) if world is not None else hdist.world_size()
@@ -187,7 +193,12 @@ class PersistentMnistStep:
         self._xptrs: list[int] = []
         self._owned: list[int] = []
         self._opened: list[int] = []
-        if self.world > 1:
+        self.exchange = exchange
+        self.selftest_report: dict | None = None
+        if exchange is not None:
+            self.xstep = torch.zeros(1, device=self.device, dtype=torch.int64)
+            exchange.attach(self)
+        elif self.world > 1:
             self._setup_exchange()
         self.use_graph = False
         self.steps_per_execution = self.spl
@@ -286,41 +297,145 @@ class PersistentMnistStep:
         dist.all_gather_object(objs, d)
         return {"identical": all(o == objs[0] for o in objs), "digests": objs}
 
-    def selftest(self, steps: int = 3) -> bool:
-        """Collective pre-flight of the cross-rank exchange on a scratch copy of the model state: a few
-        launches on this rank's own random batch, then every rank must report no hand-off error and
-        bit-identical scratch parameters.  The real state (arena, optimizer, RNG counter, cursor)
-        is untouched.  Returns the verdict every rank agrees on."""
+    def views(self) -> dict:
+        """name -> (fp32 master, Adadelta E[g^2], E[dx^2]) views of every parameter in the arena."""
+        named = dict(self.model.named_parameters())
+        out = {}
+        for k in self.PARAMS:
+            t = named[k]
+            o, n = int(t._hx_off), t.numel()
+            out[k] = tuple(x[o:o + n].view(t.shape) for x in (self.arena.master, self.s1, self.s2))
+        return out
+
+    def _state(self):
+        a = self.arena
+        return (a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor)
+
+    def numeric_probe(self, xs=None, ys=None, reduce=None, tries: int = 6) -> dict:
+        """One data-parallel training step of the kernel on a scratch copy of the state (optimizer
+        accumulators zeroed, so E[g^2] after the step is 0.05 g^2 exactly), checked against fp64:
+        this replica's bf16-emulating fp64 gradient of its share of the global-batch loss
+        (``reference_grads``), summed over the replicas by ``reduce`` (default: an all-reduce over the
+        process group), one fp64 Adadelta step, ``compare_update``.  ``xs``/``ys``: this replica's batch
+        [1, 32, 28, 28, 1] / [1, 32] (default: a random batch, redrawn while an fc1 ReLU input sits
+        within 2e-5 of 0, where fp32-vs-fp64 accumulation can flip it).  With a simulated exchange
+        (``exchange``) the step is ExchangeSim.step over W random batches and the reference sums the W
+        replicas' gradients in-process.  The real state is restored.  Returns compare_update's report
+        plus "err" (the launch's error word)."""
         import torch.distributed as dist
 
-        a = self.arena
         B = self.geom["batch"]
-        saved = [t.clone() for t in (a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor)]
-        ok = True
+        V = self.views()
+        P0 = {k: v[0].detach().to(torch.float64).clone() for k, v in V.items()}
+        pool = self.model.pool
+        drop = float(pool.dropout) if pool.training else 0.0
+        seed, ctr = int(self.rng[0].item()) & ((1 << 64) - 1), int(self.rng[1].item())
+        scale, shift = self.model.conv1.in_affine
+        denom = self.world * B
+        rf = dict(xscale=float(scale), xshift=float(shift), emulate_bf16=True)
+
+        def draw(rank, xs=None, ys=None):
+            g = torch.Generator().manual_seed(0x5E1F + 7919 * rank)
+            for t in range(tries if xs is None else 1):
+                if xs is None or t > 0:
+                    xs = torch.randint(0, 256, (1, B, 28, 28, 1), dtype=torch.uint8, generator=g).to(self.device)
+                    ys = torch.randint(0, 10, (1, B), dtype=torch.int64, generator=g).to(self.device)
+                P = {k: v.clone().requires_grad_(True) for k, v in P0.items()}
+                mg = []
+                grads, _ = reference_grads(P, xs[0], ys[0], seed, ctr, int(pool.salt), drop, rank * B, denom,
+                                           margins=mg, **rf)
+                if mg[0]["fc1"] > 2e-5:
+                    break
+            return xs, ys, torch.cat([gr.flatten() for gr in grads])
+
+        sim = self.exchange
+        if sim is not None:
+            batches = [draw(r) for r in range(self.world)]
+            flat = sum(b[2] for b in batches)
+        else:
+            xs, ys, flat = draw(self.rank, xs, ys)
+            if reduce is not None:
+                flat = reduce(flat)
+            elif self.loopback > 1:
+                flat = flat * self.world  # every simulated peer holds this rank's batch (and masks)
+            elif self.world > 1:
+                dist.all_reduce(flat)
+        grads, o = [], 0
+        for k, v in P0.items():
+            grads.append(flat[o:o + v.numel()].view_as(v))
+            o += v.numel()
+        S1r = {k: torch.zeros_like(v) for k, v in P0.items()}
+        S2r = {k: torch.zeros_like(v) for k, v in P0.items()}
+        opt = self.opt
+        opt.sync_hp()
+        lr, _, _, rho, eps = [float(v) for v in opt._hp()][:5]
+        Pr = adadelta_ref(P0, S1r, S2r, grads, lr, rho, eps)
+        saved = [t.clone() for t in self._state()]
+        try:
+            self.s1.zero_()
+            self.s2.zero_()
+            if sim is not None:
+                sim.step([b[0] for b in batches], [b[1] for b in batches])
+            else:
+                self._launch(xs, ys, 1, 1)
+            torch.cuda.synchronize(self.device)
+            err = int(self.err[0].item())
+            V = self.views()
+            P1 = {k: v[0].detach().clone() for k, v in V.items()}
+            S1k = {k: v[1].detach().clone() for k, v in V.items()}
+        finally:
+            for t, sv in zip(self._state(), saved):
+                t.copy_(sv)
+            torch.cuda.synchronize(self.device)
+        rep = compare_update(P0, P1, S1k, Pr, S1r)
+        rep["err"] = err
+        rep["ok"] = rep["ok"] and err == 0
+        return rep
+
+    def selftest(self, steps: int = 3, numeric: bool = True) -> bool:
+        """Collective pre-flight of the cross-rank exchange on a scratch copy of the model state.
+        (1) ``numeric_probe``: one step on this rank's own random batch must match the fp64
+        reference of the GLOBAL batch — every replica's gradient, all-reduced over the process group
+        (RCCL) — per parameter tensor (update cosine >= 0.999, E[g^2] within 2 %): a dropped peer, a
+        wrong world-size scale or a mis-ordered slot fails here even when every rank is wrong the same
+        way.  (2) a few launches, then every rank must report no hand-off error and bit-identical
+        scratch parameters.  The real state (arena, optimizer, RNG counter, cursor) is untouched.
+        Returns the verdict every rank agrees on; ``selftest_report`` keeps the details."""
+        import torch.distributed as dist
+
+        B = self.geom["batch"]
+        saved = [t.clone() for t in self._state()]
+        ok, rep = True, None
         # the self-test's launches start together (right after a collective): a hand-off that has not
         # arrived within a few seconds never will, so a broken exchange costs seconds here, not the
         # 60 s a training launch waits for a late peer (HOPSX_PERSIST_SELFTEST_TIMEOUT_S)
         t_run = self.timeout_ms
         self.timeout_ms = min(t_run, int(1000 * float(os.environ.get("HOPSX_PERSIST_SELFTEST_TIMEOUT_S", "8"))))
         try:
+            if numeric:
+                rep = self.numeric_probe()
+                ok = rep["ok"]
             xs = torch.randint(0, 256, (2, B, 28, 28, 1), dtype=torch.uint8, device=self.device)
             ys = torch.randint(0, 10, (2, B), dtype=torch.int64, device=self.device)
-            for k in (steps, 1):
-                self._launch(xs, ys, 2, k)
+            if int(self.err[0].item()) == 0 and self.exchange is None:
+                for k in (steps, 1):
+                    self._launch(xs, ys, 2, k)
             torch.cuda.synchronize(self.device)
-            ok = int(self.err[0].item()) == 0
+            ok = ok and int(self.err[0].item()) == 0
             dig = self.param_digest()
-        except Exception:
+        except Exception as e:
             ok, dig = False, None
+            rep = dict(rep or {}, exception=repr(e)[:300])
         finally:
             self.timeout_ms = t_run
-            for t, s in zip((a.master, a.shadow, self.s1, self.s2, self.opt.step_count, self.rng, self.cursor), saved):
-                t.copy_(s)
+            for t, sv in zip(self._state(), saved):
+                t.copy_(sv)
             torch.cuda.synchronize(self.device)
-        if self.world > 1 and self.loopback <= 1:
+        if self.world > 1 and self.loopback <= 1 and self.exchange is None:
             objs = [None] * self.world
             dist.all_gather_object(objs, (ok, dig))
             ok = all(o[0] for o in objs) and all(o[1] == objs[0][1] for o in objs)
+        self.selftest_report = {"ok": ok, "numeric": rep}
         if ok:
             self.err.zero_()
         return ok
@@ -352,13 +467,17 @@ class PersistentMnistStep:
         pool = self.model.pool
         key = (xs.data_ptr(), ys.data_ptr(), nb, k, float(pool.dropout) if pool.training else 0.0, int(pool.salt),
                tuple(hp), self.acquire, self.xfence, self.timeout_ms, id(self.dbg), id(self.cursor), id(self.rng),
-               id(self.arena.master), id(self.s1))
+               id(self.arena.master), id(self.s1), self.world, self.rank, tuple(self._xptrs))
         ext = self._ext
         if getattr(self, "_args_key", None) != key:
             # converted once into a C++-side slot; a launch then passes the slot id and the stream only
             self._slot = ext.mnist_persist_store(getattr(self, "_slot", -1), *self._build_args(xs, ys, nb, k, hp))
             self._args_key = key
-        _C.check(ext.mnist_persist_slot(self._slot, _C.stream()), "mnist_persist")
+        rc = ext.mnist_persist_slot(self._slot, _C.stream())
+        if rc == 720:  # hipErrorCooperativeLaunchTooLarge
+            raise PersistentError("mnist_persist: cooperative launch refused — the device cannot hold all "
+                                  f"{self.geom['grid']} workgroups at once")
+        _C.check(rc, "mnist_persist")
 
     def _build_args(self, xs, ys, nb: int, k: int, hp: list):
         opt, a, m = self.opt, self.arena, self.model
@@ -423,6 +542,10 @@ class PersistentMnistStep:
             # so a later launch (after the caller resets err) cannot match a stale flag
             self.flags.zero_()
             phase, step, wg = (e >> 24) & 0x7F, (e >> 12) & 0xFFF, e & 0xFFF
+            if phase == 12:
+                raise PersistentError(f"mnist_persist: the grid's workgroups were not co-resident (workgroup {wg} "
+                                      "waited out step 0's local hand-off: another kernel holds CUs this launch "
+                                      "needs); arena state of the failed launch is partial")
             raise PersistentError(f"mnist_persist: hand-off wait timed out (phase {phase}, step {step}, "
                                   f"workgroup {wg}); arena state of the failed launch is partial")
 
@@ -485,13 +608,84 @@ class _RoundGrad(torch.autograd.Function):
         return g.to(torch.bfloat16).to(g.dtype)
 
 
+def reference_grads(P: dict, x_u8: torch.Tensor, y: torch.Tensor, seed: int, ctr: int, salt: int, drop_p: float,
+                    image_offset: int = 0, denom: int | None = None, xscale: float = 1.0 / 255.0,
+                    xshift: float = -0.5, emulate_bf16: bool = False, margins: list | None = None):
+    """fp64 gradient of ONE replica's share of the MirroredStrategy loss: ``sum_b CE(image b) / denom``
+    over this replica's images ``x_u8`` [B, 28, 28(, 1)], whose dropout masks are those of global images
+    ``image_offset .. image_offset + B - 1`` (the kernel keys a mask on the global image index
+    rank * 32 + b).  ``denom`` = the global batch (default B).  Summing every replica's result is the
+    gradient of the global-batch mean — what an all-reduce of the replicas' gradients produces
+    (mirroredstrategy_mnist_example.ipynb:128-131).  P: name -> fp64 tensor with requires_grad.
+    Returns (grads in P's order, sum of this replica's CE losses).  ``emulate_bf16`` / ``margins``: see
+    ``reference_steps``."""
+    import torch.nn.functional as F
+
+    rf = _RoundFwd.apply if emulate_bf16 else (lambda t: t)
+    rg = _RoundGrad.apply if emulate_bf16 else (lambda t: t)
+    B = y.shape[0]
+    denom = B if denom is None else int(denom)
+    x = x_u8.reshape(B, 1, 28, 28).to(torch.float64) * xscale + xshift
+    z1 = F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"])
+    h = rf(F.relu(z1))
+    z2 = F.conv2d(h, rf(P["conv2.weight"]).permute(0, 3, 1, 2), P["conv2.bias"])
+    h = rg(rf(F.relu(z2)))
+    h = F.max_pool2d(h, 2).permute(0, 2, 3, 1).reshape(B, -1)  # NHWC flatten
+    if drop_p > 0:
+        per = 169 * 64
+        po = torch.arange(B * per, dtype=torch.int64, device=x_u8.device) + int(image_offset) * per
+        keep = dropout_keep(seed, ctr, salt, po, drop_p).reshape(B, -1)
+        h = h * keep.to(h.dtype) / (1.0 - drop_p)
+    z3 = rg(F.linear(rf(h), rf(P["fc1.weight"]))) + P["fc1.bias"]
+    h = F.relu(z3)
+    if margins is not None:
+        margins.append({k: float(z.detach().abs().min()) for k, z in (("conv1", z1), ("conv2", z2), ("fc1", z3))})
+    logits = F.linear(h, P["fc2.weight"], P["fc2.bias"])
+    loss = F.cross_entropy(logits, y, reduction="sum")
+    grads = torch.autograd.grad(loss / denom, list(P.values()))
+    return grads, float(loss.detach())
+
+
+def adadelta_ref(P: dict, S1: dict, S2: dict, grads, lr: float, rho: float, eps: float) -> dict:
+    """One fp64 Adadelta step (optim_core.h upd<3>) in place on S1 / S2; returns the new parameters."""
+    out = {}
+    with torch.no_grad():
+        for (k, w), g in zip(list(P.items()), grads):
+            S1[k].mul_(rho).addcmul_(g, g, value=1 - rho)
+            d = (S2[k] + eps).sqrt() / (S1[k] + eps).sqrt() * g
+            S2[k].mul_(rho).addcmul_(d, d, value=1 - rho)
+            out[k] = w.detach() - lr * d
+    return out
+
+
+def compare_update(P0: dict, P1: dict, S1k: dict, Pr: dict, S1r: dict, cos_min: float = 0.999,
+                   srel_max: float = 2e-2) -> dict:
+    """Per parameter tensor: the cosine between the kernel's update P1 - P0 and the reference's Pr - P0,
+    and the relative L2 error of the kernel's Adadelta E[g^2] against the reference's.  E[g^2] carries
+    the gradient's MAGNITUDE (the first Adadelta steps are nearly sign(g) x const, so the update's
+    direction alone misses a gradient that is scaled wrong, e.g. by the wrong world size); the update
+    cosine carries its direction.  Returns {"ok": bool, "tensors": {name: (cos, srel)}}."""
+    rep, ok = {}, True
+    for k in P0:
+        dk = (P1[k].double() - P0[k].double()).flatten()
+        dr = (Pr[k].double() - P0[k].double()).flatten()
+        cos = float(torch.nn.functional.cosine_similarity(dk, dr, dim=0))
+        sk, sr = S1k[k].double().flatten(), S1r[k].double().flatten()
+        srel = float((sk - sr).norm() / sr.norm().clamp_min(1e-300))
+        rep[k] = (cos, srel)
+        ok = ok and cos >= cos_min and srel <= srel_max
+    return {"ok": ok, "tensors": rep}
+
+
 def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torch.Tensor, cursor: int, n: int,
                     seed: int, ctr: int, salt: int, drop_p: float, lr: float, rho: float, eps: float,
                     xscale: float = 1.0 / 255.0, xshift: float = -0.5, emulate_bf16: bool = False,
                     margins: list | None = None):
     """``n`` fp64 training steps of MirroredMnistCNN with the kernel's data order, dropout masks,
     loss (mean sparse CE) and Adadelta.  params / s1 / s2: name -> tensor (hopsx layouts: conv OHWI,
-    dense [out, in]).  Returns fp64 (params, s1, s2, losses).
+    dense [out, in]).  Returns fp64 (params, s1, s2, losses).  A data-parallel step of W replicas is
+    this with the replicas' batches concatenated along the batch axis (replica r's images are global
+    images r * 32 .. r * 32 + 31, the kernel's dropout key).
 
     ``emulate_bf16``: round exactly the tensors the persistent kernel stores as bf16 MFMA operands —
     conv1 output, conv2 weight, the relu'd conv2 output (before the max-pool, as the kernel ties it),
@@ -502,43 +696,17 @@ def reference_steps(params: dict, s1: dict, s2: dict, xs: torch.Tensor, ys: torc
     ``margins``: a list that receives, per step, the smallest |pre-activation| of each ReLU (conv1,
     conv2, fc1) — how close the step came to a tie that fp32-vs-fp64 accumulation can flip.  A flip
     at fc1 moves a whole fc1 row's gradient and, through dh, every conv gradient."""
-    import torch.nn.functional as F
-
-    rf = _RoundFwd.apply if emulate_bf16 else (lambda t: t)
-    rg = _RoundGrad.apply if emulate_bf16 else (lambda t: t)
     P = {k: v.detach().to(torch.float64).clone() for k, v in params.items()}
     S1 = {k: v.detach().to(torch.float64).clone() for k, v in s1.items()}
     S2 = {k: v.detach().to(torch.float64).clone() for k, v in s2.items()}
     nb, B = ys.shape
-    po = torch.arange(B * 169 * 64, dtype=torch.int64, device=xs.device)  # NHWC pooled element index
     losses = []
     for s in range(n):
         bt = (cursor + s) % nb
-        x = xs[bt].reshape(B, 1, 28, 28).to(torch.float64) * xscale + xshift
-        y = ys[bt]
         for v in P.values():
             v.requires_grad_(True)
-        z1 = F.conv2d(x, P["conv1.weight"].permute(0, 3, 1, 2), P["conv1.bias"])
-        h = rf(F.relu(z1))
-        z2 = F.conv2d(h, rf(P["conv2.weight"]).permute(0, 3, 1, 2), P["conv2.bias"])
-        h = rg(rf(F.relu(z2)))
-        h = F.max_pool2d(h, 2).permute(0, 2, 3, 1).reshape(B, -1)  # NHWC flatten
-        if drop_p > 0:
-            keep = dropout_keep(seed, ctr + s, salt, po, drop_p).reshape(B, -1)
-            h = h * keep.to(h.dtype) / (1.0 - drop_p)
-        z3 = rg(F.linear(rf(h), rf(P["fc1.weight"]))) + P["fc1.bias"]
-        h = F.relu(z3)
-        if margins is not None:
-            margins.append({k: float(z.detach().abs().min()) for k, z in (("conv1", z1), ("conv2", z2), ("fc1", z3))})
-        logits = F.linear(h, P["fc2.weight"], P["fc2.bias"])
-        loss = F.cross_entropy(logits, y)
-        grads = torch.autograd.grad(loss, list(P.values()))
-        losses.append(float(loss.detach()))
-        with torch.no_grad():
-            for (k, w), g in zip(list(P.items()), grads):
-                w = w.detach()
-                S1[k].mul_(rho).addcmul_(g, g, value=1 - rho)
-                d = (S2[k] + eps).sqrt() / (S1[k] + eps).sqrt() * g
-                S2[k].mul_(rho).addcmul_(d, d, value=1 - rho)
-                P[k] = w - lr * d
+        grads, lsum = reference_grads(P, xs[bt], ys[bt], seed, ctr + s, salt, drop_p, 0, B, xscale, xshift,
+                                      emulate_bf16, margins)
+        losses.append(lsum / B)
+        P = adadelta_ref(P, S1, S2, grads, lr, rho, eps)
     return {k: v.detach() for k, v in P.items()}, S1, S2, losses

@@ -25,7 +25,7 @@ R=$(pwd)
 
 fail() { tail -30 "$1"; exit 1; }
 # pytest: 1 = an assertion failed (the GPU is fine, keep measuring); anything else stops the job
-pyt() { local log=$1; shift; timeout -k 10 ${T:-300} python -u -m pytest -x -v --timeout 120 --timeout-method thread "$@" > $log 2>&1
+pyt() { local log=$1; shift; timeout -k 10 ${T:-300} python -u -m pytest ${PYX--x} -v --timeout 120 --timeout-method thread "$@" > $log 2>&1
         local rc=$?; tail -6 $log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
 bench() { local name=$1; shift; timeout -k 10 ${T:-300} python -u "$@" > $out/$name.json 2> $out/$name.err || fail $out/$name.err
           tail -1 $out/$name.json | cut -c1-400; }
@@ -110,6 +110,14 @@ taxipmc)
 tables)
   ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10 --inline
   ktable p50 r50_b64_kernels.txt benchmarks/run.py resnet50 --batch 64 --steps 20 --warmup 5 ;;
+dpsim)
+  # the persistent flagship's data-parallel exchange on distinct per-rank data (ExchangeSim, cross-process
+  # peer, co-residency), its loopback / one-GPU suites, and the cooperative-launch A/B on the bench
+  T=600 pyt $out/pytest.log tests/test_persist_dp_sim_gpu.py tests/test_persist_dp_gpu.py tests/test_persist_gpu.py -s
+  for s in "HOPSX_PERSIST_COOP=0" "HOPSX_PERSIST_COOP=1" "HOPSX_PERSIST_COOP=0" "HOPSX_PERSIST_COOP=1"; do
+    r=$(env $s timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-taxi 2>>$out/err.log) || { echo "FAIL [$s]"; fail $out/err.log; }
+    echo "[$s] $(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')" | tee -a $out/ab.txt
+  done ;;
 knobs)
   for s in "$@"; do
     r=$(env $s timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-taxi 2>>$out/err.log) || { echo "FAIL [$s]"; fail $out/err.log; }
