@@ -103,6 +103,11 @@ HX_PYMOD(HOPSX_MODNAME) {
     return hopsx_widedeep_slots(iv.data(), (int)iv.size(), P<int>(out), n);
   });
   m.def("taxi_step2_ok", [](std::vector<long> iv, long rows) { return hopsx_taxi_step2_ok(iv.data(), (int)iv.size(), rows); });
+  m.def("taxi_step2_xgeom", []() {
+    std::vector<long> g(4);
+    hopsx_taxi_step2_xgeom(g.data());
+    return g;
+  });
   m.def("taxi_step2", [](std::vector<uint64_t> p, std::vector<long> iv, std::vector<float> fv, long rows, u st) {
     return hopsx_taxi_step2(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(), rows, S(st));
   });

@@ -109,6 +109,7 @@ int hopsx_widedeep_step(const uint64_t* ptrs, int np, const long* iv, int ni, co
                         hipStream_t st);
 // ---- taxi step v2: bf16 MFMA, LDS-resident model + wide table, optimizer state in registers (taxi_step.hip) ----
 long hopsx_taxi_step2_ok(const long* iv, int ni, long rows);
+void hopsx_taxi_step2_xgeom(long* g);
 int hopsx_taxi_step2(const uint64_t* ptrs, int np, const long* iv, int ni, const float* fv, int nf, long rows,
                      hipStream_t st);
 // ---- flagship MNIST CNN: nsteps whole training steps in one persistent launch (mnist_persist.hip) ----

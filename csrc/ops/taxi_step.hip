@@ -61,6 +61,9 @@ constexpr int D0 = 3, D1 = 100, D2 = 70, D3 = 48, D4 = 34;  // dense input + hid
 
 constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 constexpr int pad32(int x) { return (x + 31) & ~31; }
+// dW tile rounds a lane owns (the deep exchange payload's slots; = NSLOT below, checked there)
+constexpr int NSLOT_X = cdiv(cdiv(D4, 16) * cdiv(D3 + 1, 16), NT / 64) + cdiv(cdiv(D3, 16) * cdiv(D2 + 1, 16), NT / 64) +
+                        cdiv(cdiv(D2, 16) * cdiv(D1 + 1, 16), NT / 64) + 1;
 
 // ---- LDS images (bf16 element offsets); strides are odd multiples of 16 elements
 constexpr int SA0 = 16, SA1 = 144, SA2 = 112, SA3 = 80, SA4 = 48, SG = 112;
@@ -83,10 +86,30 @@ constexpr int BF_BYTES = BF_END * 2;
 constexpr int F_B0 = 0, F_B1 = F_B0 + 16 * cdiv(D1, 16), F_B2 = F_B1 + 16 * cdiv(D2, 16),
               F_B3 = F_B2 + 16 * cdiv(D3, 16), F_W4 = F_B3 + 16 * cdiv(D4, 16), F_MISC = F_W4 + 48,
               F_RED = F_MISC + 16, F_DW4 = F_RED + 16, F_GV = F_DW4 + 3 * 48, F_IDT = F_GV + BP, F_LT = F_IDT + 16 * BP,
-              F_GS = F_LT + 16 * BP, F_WTAB = F_GS + 16 * BP, F_END = F_WTAB + MAXROWS;
+              F_GS = F_LT + 16 * BP, F_WTAB = F_GS + 16 * BP, F_VD = F_WTAB + MAXROWS, F_END = F_VD + 4;
 constexpr int LDS_BYTES = BF_BYTES + F_END * 4;
 constexpr int STAGE_MAX = LDS_BYTES / 4;  // floats of the deep arena span staged through LDS
 static_assert(BF_BYTES % 16 == 0 && LDS_BYTES <= 160 * 1024, "taxi2 LDS budget");
+
+// ---- data-parallel instantiation (DP = true; world 2..8 ranks, models/widedeep.py TaxiExchange) ----
+// Each rank runs this one-workgroup step on ITS OWN batch.  The weight gradients are not applied as
+// they leave the MFMAs: every owner lane PUSHES its dW accumulators (16 B a tile round) into every
+// rank's uncached exchange buffer at slot [this rank] (system-scope write-through stores, off the
+// critical path while the backward continues); the gradient waves push every wide entry's (id, summed
+// gradient).  After the backward: drain, raise this rank's flag word in every peer's flag page, poll
+// the own page.  Then each owner lane sums the W ranks' gradients of its elements in RANK ORDER and
+// applies Adagrad in registers (so every replica computes bit-identical weights), and the wide rows
+// touched by ANY rank get ONE FTRL update each with the rank-order sum of their gradients (an LDS
+// gradient/tag table in the dead activation region, one pass per rank).  One cross-rank hop a step.
+// Payloads are double-buffered by the parity of the global step epoch (a rank cannot push step s + 2
+// before every peer raised step s + 1, which they do after reading step s).
+constexpr int XMAX = 8;
+constexpr int XD_BYTES = NSLOT_X * NT * 16;           // deep dW: [slot][thread] f32x4 (owner-lane-major)
+constexpr int XL4_OFF = XD_BYTES;                      // logits-layer gradient: [64] floats (wave 7 lanes)
+constexpr int XW_OFF = XL4_OFF + 64 * 4;               // wide entries: [13 col][BP] (id | -1, gradient)
+constexpr int XPAY = XW_OFF + NWIDE * BP * 8;          // bytes per (parity, slot)
+constexpr long X_BYTES = 2L * XMAX * XPAY;
+constexpr int XF_WORDS = 64;                           // flag page: word r = rank r's step epoch
 
 struct Args {
   float* master;
@@ -111,6 +134,13 @@ struct Args {
   long woff[5], boff[5];
   int rw[5], rb[5];  // woff / boff relative to deep_lo (staging-copy offsets)
   OptHP ada, ftrl;
+  // data parallel (DP instantiation)
+  int world, rank, loopback;   // loopback: one process plays every rank (the peers' buffers are its own)
+  long long tmo;               // wall-clock ticks the exchange wait polls before it gives up
+  unsigned* err;               // sticky error word (0 = ok)
+  long long* xstep;            // global step counter: the exchange epoch base (advanced by nsteps)
+  unsigned char* xbuf[XMAX];   // exchange buffers of ranks 0..world-1 (own at [rank])
+  unsigned* xflag[XMAX];       // flag pages of ranks 0..world-1
 };
 
 typedef __attribute__((address_space(3))) bf16x4* lds4_t;
@@ -221,6 +251,34 @@ constexpr int NDW4 = cdiv(D4 + 1, 16);  // logits layer dW tiles (output column 
 constexpr int R3 = cdiv(L3::NDW, NW), R2 = cdiv(L2::NDW, NW), R1 = cdiv(L1::NDW, NW);
 static_assert(L0::NDW < NW && NW == 8, "tile map");
 constexpr int S3 = 0, S2 = S3 + R3, S1 = S2 + R2, S0 = S1 + R1, NSLOT = S0 + 1;
+static_assert(NSLOT == NSLOT_X, "exchange payload slots");
+
+// ---- cross-rank exchange primitives (DP): system-scope (sc0 sc1) buffer stores / loads on the uncached
+// exchange buffers, system-scope relaxed flag words (the persistent MNIST step's hand-off form)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+typedef unsigned __attribute__((address_space(1))) gu32_t;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xrsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void xst16(const void* base, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), xrsrc(base), off, 0, 17);
+}
+__device__ __forceinline__ void xst8(const void* base, int off, int a, float b) {
+  __builtin_amdgcn_raw_buffer_store_b64((v2i_t){a, __float_as_int(b)}, xrsrc(base), off, 0, 17);
+}
+__device__ __forceinline__ void xst4(const void* base, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), xrsrc(base), off, 0, 17);
+}
+__device__ __forceinline__ f32x4 xld16(const void* base, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc(base), off, 0, 17));
+}
+__device__ __forceinline__ v2i_t xld8(const void* base, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(xrsrc(base), off, 0, 17);
+}
+__device__ __forceinline__ float xld4(const void* base, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrsrc(base), off, 0, 17));
+}
 __device__ __forceinline__ int perm8(int wave) { return (wave + 5) & 7; }
 
 struct Own {
@@ -301,9 +359,11 @@ __device__ __forceinline__ DwOps dw_load(const bf16_raw* Aimg, const bf16_raw* G
   }
   return d;
 }
-template <class Ly, int R, bool RSQ>
+// (DP) this lane's dW accumulator of exchange slot `slot` into every rank's buffer at [parity][this rank]
+__device__ __forceinline__ void xpush_dw(int slot, int par, f32x4 acc);
+template <class Ly, int R, bool RSQ, bool DP = false>
 __device__ __forceinline__ void dw_seq(const bf16_raw* Aimg, const bf16_raw* G, int p, int lane, float (*w)[4],
-                                       float (*s)[4], const OptHP& h) {
+                                       float (*s)[4], const OptHP& h, int sbase = 0, int par = 0) {
   // padding elements (o >= OUT, i > IN) and a dummy round update registers nothing ever reads (put_w and
   // the write-back skip them), so no validity selects here
   DwOps cur = dw_load<Ly>(Aimg, G, p, lane);
@@ -316,10 +376,15 @@ __device__ __forceinline__ void dw_seq(const bf16_raw* Aimg, const bf16_raw* G, 
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < BP / 16; ++k) acc = mma16(cur.a[k], cur.g[k], acc);
+    if constexpr (DP) {
+      // the update waits for every rank's gradient (apply phase): push this one (a dummy round owns nothing)
+      if (t < Ly::NDW) xpush_dw(sbase + j, par, acc);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if constexpr (RSQ) w[j][r] = adagrad_rsq(w[j][r], acc[r] * h.gscale, s[j][r], nlr);
-      else w[j][r] = adagrad(w[j][r], acc[r] * h.gscale, s[j][r], h);
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (RSQ) w[j][r] = adagrad_rsq(w[j][r], acc[r] * h.gscale, s[j][r], nlr);
+        else w[j][r] = adagrad(w[j][r], acc[r] * h.gscale, s[j][r], h);
+      }
     }
     cur = nxt;
     fence_c();
@@ -433,6 +498,15 @@ __device__ __forceinline__ kargs_t cold_p() {
 }
 #define COLD (*cold_p())
 
+__device__ __forceinline__ void xpush_dw(int slot, int par, f32x4 acc) {
+  const auto& C = COLD;
+  const int off = (slot * NT + (int)threadIdx.x) * 16;
+  for (int r = 0; r < C.world; ++r) {
+    const int sl = C.loopback ? r : C.rank;
+    xst16(C.xbuf[r] + (long)(par * XMAX + sl) * XPAY, off, acc);
+  }
+}
+
 template <bool GET, bool PASS_S>
 __device__ __forceinline__ void own_stage(float* stage, Own& own, int wave, int lane) {
   const auto& C = COLD;
@@ -502,7 +576,226 @@ __device__ __forceinline__ void gather_in(float* dst, const float* src, int n, i
 }
 constexpr unsigned SENT = 0xFFFFFFFFu;  // staging sentinel (a NaN no owner writes): "not owned, keep"
 
+// OUT a multiple of 16: no epilogue tile reaches the ones column (the next layer's bias input), which is
+// then constant — written at the launch start (and, data parallel, again after each step's apply phase,
+// whose gradient table borrows the activation images)
+__device__ __forceinline__ void ones_columns(bf16_raw* Lb, int B, int tid) {
+  if (tid < B) {
+    if (D1 % 16 == 0) Lb[OFF_A1 + tid * SA1 + D1] = f2b(1.f);
+    if (D2 % 16 == 0) Lb[OFF_A2 + tid * SA2 + D2] = f2b(1.f);
+    if (D3 % 16 == 0) Lb[OFF_A3 + tid * SA3 + D3] = f2b(1.f);
+    if (D4 % 16 == 0) Lb[OFF_A4 + tid * SA4 + D4] = f2b(1.f);
+  }
+}
+
+// (DP) the step's exchange: drain this wave's pushes, barrier (every payload store of the workgroup has
+// completed at the system coherence point: the release for them), raise this rank's flag word in every
+// peer's page, then wave 0 polls the own page until every peer's word has reached `epoch` (wrap-safe),
+// bounded by the wall clock and the sticky error word.  Returns the verdict to the whole workgroup.
+__device__ __forceinline__ bool exchange_step(const Args& A, long long epoch64, int step, unsigned char* lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const auto& C = COLD;
+  const bool last = step + 1 == C.nsteps;
+  if (last) stamp(A, 31);
+  const unsigned ep = (unsigned)epoch64;
+  volatile int* verdict = (volatile int*)(lds + BF_BYTES + F_VD * 4);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (lane < C.world && lane != C.rank)
+      __hip_atomic_store((gu32_t*)(C.xflag[lane] + (C.loopback ? lane : C.rank)), ep, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* page = C.xflag[C.rank];
+    int good = 1;
+    const long long t0 = wall_clock64();
+    for (unsigned spins = 0;; ++spins) {
+      const bool peer = lane < C.world && lane != C.rank;
+      const int ok = !peer || (int)(__hip_atomic_load((gu32_t*)(page + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) >= 0;
+      if (__all(ok)) break;
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32_t*)C.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u) {
+        good = 0;
+        break;
+      }
+      if ((spins & 15u) == 15u && wall_clock64() - t0 > C.tmo) {
+        if (lane == 0) atomicCAS(C.err, 0u, 0x80000000u | ((unsigned)step & 0xFFFFFFu));
+        good = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) *verdict = good;
+  }
+  __syncthreads();
+  if (last) stamp(A, 25);
+  return *verdict != 0;
+}
+static_assert(MAXROWS * 4 <= (OFF_W0 - OFF_A1) * 2, "DP wide gradient table fits the activation images");
+
+// (DP) owner lanes: the rank-order sum of every rank's dW for each owned element, Adagrad in registers, the
+// new W images / biases / logits weights; then the wide rows: the rank-order sum of every rank's entry
+// gradients per distinct id (gradient + first-rank tag tables in the activation images, dead until the next
+// forward), and ONE FTRL update per id touched by any rank, by the lane holding its first occurrence.
+// (DP) is exchange slot S (a dW tile round) owned by this wave?  S -> (layer, round j): S3.. L3, S2.. L2,
+// S1.. L1, S0 L0 (p = perm8(wave); L0: waves 0..6 own one tile each)
+template <int S>
+__device__ __forceinline__ bool slot_owned(int p, int wave) {
+  if constexpr (S < S2) return p + 8 * (S - S3) < L3::NDW;
+  else if constexpr (S < S1) return p + 8 * (S - S2) < L2::NDW;
+  else if constexpr (S < S0) return p + 8 * (S - S1) < L1::NDW;
+  else return wave < L0::NDW;
+}
+// (DP) unit U = (slot U / 2, rank group U % 2 of 4 ranks): this lane's 16-B gradient of that slot from the
+// group's ranks (zeros past W or for a slot the wave does not own)
+constexpr int XG = 4, NU = 2 * NSLOT;
+static_assert(2 * XG == XMAX, "two rank groups");
+template <int U>
+__device__ __forceinline__ void load_unit(f32x4 (&v)[XG], const unsigned char* X, int W, int tid, int p, int wave) {
+  constexpr int S = U / 2, G = U % 2;
+  const bool on = slot_owned<S>(p, wave) && G * XG < W;
+#pragma unroll
+  for (int r = 0; r < XG; ++r)
+    v[r] = on && G * XG + r < W ? xld16(X + (long)(G * XG + r) * XPAY, (S * NT + tid) * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
+}
+template <int U, bool RSQ>
+__device__ __forceinline__ void sum_unit(Own& own, f32x4& g, const f32x4 (&v)[XG], int W, int p, int wave,
+                                         const OptHP& h) {
+  constexpr int S = U / 2, G = U % 2;
+  if (!(slot_owned<S>(p, wave) && G * XG < W)) return;
+  // rank order: ((v0 + v1) + v2) + ... across both groups
+#pragma unroll
+  for (int r = 0; r < XG; ++r)
+    if (G * XG + r < W) g = (G == 0 && r == 0) ? v[r] : g + v[r];
+  if (G == 1 || W <= XG) {  // the slot's last group: every rank is in g
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if constexpr (RSQ) own.w[S][e] = adagrad_rsq(own.w[S][e], g[e] * h.gscale, own.s[S][e], -h.lr);
+      else own.w[S][e] = adagrad(own.w[S][e], g[e] * h.gscale, own.s[S][e], h);
+    }
+  }
+}
+// the NU units software-pipelined: unit U + 1's loads are in flight while unit U is summed and applied
+template <int U, bool RSQ>
+__device__ __forceinline__ void apply_units(Own& own, f32x4& g, f32x4 (&cur)[XG], const unsigned char* X, int W,
+                                            int tid, int p, int wave, const OptHP& h) {
+  if constexpr (U < NU) {
+    f32x4 nxt[XG];
+    if constexpr (U + 1 < NU) load_unit<U + 1>(nxt, X, W, tid, p, wave);
+    sum_unit<U, RSQ>(own, g, cur, W, p, wave, h);
+    if constexpr (U + 1 < NU) {
+#pragma unroll
+      for (int r = 0; r < XG; ++r) cur[r] = nxt[r];
+    }
+    fence_c();
+    apply_units<U + 1, RSQ>(own, g, cur, X, W, tid, p, wave, h);
+  }
+}
+
 template <bool RSQ>
+__device__ __forceinline__ void apply_dp(Own& own, unsigned char* lds, int par, int wave, int lane, int tid) {
+  const auto& C = COLD;
+  bf16_raw* const Lb = (bf16_raw*)lds;
+  float* const LF = (float*)(lds + BF_BYTES);
+  const int W = C.world;
+  const unsigned char* X = C.xbuf[C.rank] + (long)par * XMAX * XPAY;  // own buffer, slots 0..W-1
+  // ---- wide entries of every rank (this thread: entries tid, tid + 512 of each rank): loads issued first,
+  // in flight during the deep apply
+  constexpr int NE = NWIDE * BP;
+  int eid[XMAX][2];
+  float eg[XMAX][2];
+#pragma unroll
+  for (int r = 0; r < XMAX; ++r)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + NT * k;
+      v2i_t q = (v2i_t){-1, 0};
+      if (r < W && e < NE) q = xld8(X + (long)r * XPAY, XW_OFF + e * 8);
+      eid[r][k] = q[0];
+      eg[r][k] = __int_as_float(q[1]);
+    }
+  // ---- deep: rank-order sums + Adagrad, software-pipelined over the owned slots
+  {
+    const OptHP ha = {C.ada.lr, C.ada.gscale, C.ada.wd, C.ada.a, C.ada.b, C.ada.c, C.ada.d, C.ada.e};
+    const int p = perm8(wave);
+    f32x4 cur[XG], g = {0.f, 0.f, 0.f, 0.f};
+    load_unit<0>(cur, X, W, tid, p, wave);
+    apply_units<0, RSQ>(own, g, cur, X, W, tid, p, wave, ha);
+    if (C.dbg && tid == 0) C.dbg[28] = wall_clock64();  // (HOPSX_PHASE_DBG: every step overwrites; the last stays)
+    if (wave == NW - 1 && lane <= D4) {
+      float g = 0.f;
+      for (int r = 0; r < W; ++r) g += xld4(X + (long)r * XPAY, XL4_OFF + lane * 4);
+      own.w4 = RSQ ? adagrad_rsq(own.w4, g * ha.gscale, own.s4, -ha.lr) : adagrad(own.w4, g * ha.gscale, own.s4, ha);
+    }
+  }
+  // ---- the wide rows' gradient table over the dead activation images (A1 .. GY): one pass per rank in
+  // rank order (within a rank the leader ids are distinct, so no two lanes touch a row); the first pass that
+  // touches a row finds the sentinel and marks the entry as the row's updater.  Every entry's (z, n) is
+  // fetched first (in flight during the passes; only the updater's is used)
+  constexpr unsigned GSENT = 0x7FC0DEADu;  // a NaN no gradient sum produces
+  float* gacc = (float*)(lds + OFF_A1 * 2);
+  float2 zn[XMAX][2];
+#pragma unroll
+  for (int r = 0; r < XMAX; ++r)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      zn[r][k] = C.zn[eid[r][k] >= 0 ? eid[r][k] : 0];  // (unconditional: a predicated load kept zn in scratch)
+#pragma unroll
+  for (int r = 0; r < XMAX; ++r)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (eid[r][k] >= 0) gacc[eid[r][k]] = __uint_as_float(GSENT);
+  __syncthreads();
+  unsigned mine = 0u;
+#pragma unroll
+  for (int r = 0; r < XMAX; ++r) {
+    if (r < W) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (eid[r][k] >= 0) {
+          const int id = eid[r][k];
+          const float o = gacc[id];
+          const bool first = __float_as_uint(o) == GSENT;
+          gacc[id] = first ? eg[r][k] : o + eg[r][k];
+          mine |= first ? 1u << (2 * r + k) : 0u;
+        }
+      __syncthreads();
+    }
+  }
+  // FTRL-proximal once per distinct row, by the lane holding its first occurrence; (z, n) from the private copy
+  const OptHP hf = {C.ftrl.lr, C.ftrl.gscale, C.ftrl.wd, C.ftrl.a, C.ftrl.b, C.ftrl.c, C.ftrl.d, C.ftrl.e};
+  const float ilr = __builtin_amdgcn_rcpf(hf.lr);
+#pragma unroll
+  for (int r = 0; r < XMAX; ++r)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (mine & (1u << (2 * r + k))) {
+        const int id = eid[r][k];
+        const float g = gacc[id] * hf.gscale;
+        gacc[id] = 0.f;  // (the row's only reader: its slot is padding-clean again for the forward)
+        const float wo = LF[F_WTAB + id];
+        const float n0 = zn[r][k].y;
+        const float nn = fmaf(g, g, n0);
+        const float rs = __builtin_amdgcn_sqrtf(nn);
+        const float zz = zn[r][k].x + g - (rs - __builtin_amdgcn_sqrtf(n0)) * ilr * wo;
+        const float den = (hf.c + rs) * ilr + 2.f * hf.b;
+        LF[F_WTAB + id] = (fabsf(zz) <= hf.a) ? 0.f : -(zz - copysignf(hf.a, zz)) * __builtin_amdgcn_rcpf(den);
+        C.zn[id] = make_float2(zz, nn);
+      }
+  // ---- give the activation images back as the forward expects them: every table slot was zeroed by its
+  // row's updater above (padding columns the MFMAs read must hold 0, never the sentinel NaN); the constant
+  // ones columns 1 again
+  __syncthreads();
+  ones_columns(Lb, C.B, tid);
+  // ---- the new bf16 W images, fp32 biases and logits weights for the next forward
+  const int p = perm8(wave);
+  put_seq<L3, R3>(Lb, LF, p, lane, own.w + S3);
+  put_seq<L2, R2>(Lb, LF, p, lane, own.w + S2);
+  put_seq<L1, R1>(Lb, LF, p, lane, own.w + S1);
+  if (wave < L0::NDW) put_w<L0>(Lb, LF, wave, lane, own.w[S0]);
+  if (wave == NW - 1 && lane <= D4) LF[lane < D4 ? F_W4 + lane : F_MISC] = own.w4;
+}
+
+template <bool RSQ, bool DP>
 __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   bf16_raw* const Lb = (bf16_raw*)lds;
@@ -585,13 +878,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     if (D3 + tid < 16 * L2::OT) LF[F_B2 + D3 + tid] = tid ? -1e30f : 1.f;
     if (D4 + tid < 16 * L3::OT) LF[F_B3 + D4 + tid] = tid ? -1e30f : 1.f;
   }
-  // OUT a multiple of 16: no epilogue tile reaches the ones column, which is then constant
-  if (tid < B) {
-    if (D1 % 16 == 0) Lb[OFF_A1 + tid * SA1 + D1] = f2b(1.f);
-    if (D2 % 16 == 0) Lb[OFF_A2 + tid * SA2 + D2] = f2b(1.f);
-    if (D3 % 16 == 0) Lb[OFF_A3 + tid * SA3 + D3] = f2b(1.f);
-    if (D4 % 16 == 0) Lb[OFF_A4 + tid * SA4 + D4] = f2b(1.f);
-  }
+  ones_columns(Lb, B, tid);
   if (evb && eg < D0) Lb[OFF_A0 + eb * SA0 + eg] = f2b(nd);
   {
     const int p = perm8(wave);
@@ -612,7 +899,10 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
   stamp(A, 1);
 
   float lsum = 0.f, csum = 0.f, gb = 0.f;
-  const float invB = 1.f / (float)B;
+  // data parallel: every replica's gradient carries 1 / (global batch), so the rank-order sum of the W
+  // replicas' gradients is the gradient of the global-batch mean loss (MirroredStrategy semantics)
+  const float invB = 1.f / (float)(DP ? B * A.world : B);
+  const long long xs0 = DP ? A.xstep[0] : 0;
   stamp_clk(A, 20);
   float wv[4], zl[4], nl[4];  // (tile waves) gathered wide weights; FTRL state of the rows this lane leads
   unsigned lead = 0u;
@@ -624,6 +914,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
   };
   for (int step = 0; step < A.nsteps; ++step) {
     const bool last = step + 1 == A.nsteps;
+    const int par = (int)((xs0 + step) & 1);  // (DP) exchange-buffer parity of this step
     const bf16_raw* A0 = Lb + OFF_A0 + (step & 1) * BP * SA0;
     if (last) stamp(A, 7);
     // ============================================================ FWD: tile waves, no barrier inside | leaders
@@ -725,9 +1016,9 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       dx_tile<L3>(Lb, Lb + OFF_GX, Lb + OFF_GY, b0, lane);
       if (last) stampw(A, 13, 0);
       // the previous step's (z, n) stores (same CU) completed before these loads: by now the wait is free
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lead = 0u;
-      {
+      if constexpr (!DP) {  // (data parallel: the apply phase updates every touched row after the exchange)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const auto& C = COLD;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -748,8 +1039,9 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       for (int k = 0; k < 2; ++k) {  // 2 x 320 lanes >= 13 x 48 entries
         int c, b;
         gl_entry(k, c, b);
-        if (c < NWIDE && ltab[c * BP + b] == b) {
-          float g = 0.f;
+        const bool ld = c < NWIDE && ltab[c * BP + b] == b;
+        float g = 0.f;
+        if (ld) {
 #pragma unroll
           for (int q = 0; q < BP / 4; ++q) {
             const int4 l4 = *(const int4*)(ltab + c * BP + 4 * q);
@@ -759,21 +1051,37 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
             g += l4.z == b ? g4[2] : 0.f;
             g += l4.w == b ? g4[3] : 0.f;
           }
-          LF[F_GS + c * BP + b] = g;
+          if constexpr (!DP) LF[F_GS + c * BP + b] = g;
+        }
+        if constexpr (DP) {
+          // every entry of the step (id of a leader, -1 otherwise) with its summed gradient, to every rank
+          if (c < NWIDE) {
+            const auto& C = COLD;
+            const int id = ld ? idt[c * BP + b] : -1;
+            for (int r = 0; r < C.world; ++r)
+              xst8(C.xbuf[r] + (long)(par * XMAX + (C.loopback ? r : C.rank)) * XPAY, XW_OFF + (c * BP + b) * 8, id, g);
+          }
         }
       }
     }
-    dw_seq<L3, R3, RSQ>(Lb + L3::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S3, own.s + S3, ha);
+    dw_seq<L3, R3, RSQ, DP>(Lb + L3::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S3, own.s + S3, ha, S3, par);
     if (last) stampw(A, 15, 3);
     if (wave == NW - 1) {  // the logits layer: sum the tiles' partials in order, Adagrad, new w4 / b4 now
       const int i = lane <= D4 ? lane : 0;
       const float g = (LF[F_DW4 + i] + LF[F_DW4 + 48 + i]) + LF[F_DW4 + 96 + i];
+      if constexpr (DP) {
+        const auto& C = COLD;
+        if (lane <= D4)
+          for (int r = 0; r < C.world; ++r)
+            xst4(C.xbuf[r] + (long)(par * XMAX + (C.loopback ? r : C.rank)) * XPAY, XL4_OFF + lane * 4, g);
+      } else {
       float s1 = own.s4;
       const float wn = RSQ ? adagrad_rsq(own.w4, g * ha.gscale, s1, -ha.lr) : adagrad(own.w4, g * ha.gscale, s1, ha);
       if (lane <= D4) {
         own.w4 = wn;
         own.s4 = s1;
         LF[lane < D4 ? F_W4 + lane : F_MISC] = wn;
+      }
       }
     }
     bar();
@@ -783,8 +1091,8 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     wave = fresh_s(wave0);
     b0 = 16 * wave;
     if (tw) dx_tile<L2>(Lb, Lb + OFF_GY, Lb + OFF_GX, b0, lane);
-    put_seq<L3, R3>(Lb, LF, perm8(wave), lane, own.w + S3);
-    dw_seq<L2, R2, RSQ>(Lb + L2::OFFA, Lb + OFF_GY, perm8(wave), lane, own.w + S2, own.s + S2, ha);
+    if constexpr (!DP) put_seq<L3, R3>(Lb, LF, perm8(wave), lane, own.w + S3);
+    dw_seq<L2, R2, RSQ, DP>(Lb + L2::OFFA, Lb + OFF_GY, perm8(wave), lane, own.w + S2, own.s + S2, ha, S2, par);
     bar();
     if (last) stamp(A, 4);
     // ============================================================ B1: dX1 | W2 image, dW1
@@ -793,8 +1101,8 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     b0 = 16 * wave;
     if (tw) dx_tile<L1>(Lb, Lb + OFF_GX, Lb + OFF_GY, b0, lane);
     if (last) stampw(A, 16, 0);
-    put_seq<L2, R2>(Lb, LF, perm8(wave), lane, own.w + S2);
-    dw_seq<L1, R1, RSQ>(Lb + L1::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S1, own.s + S1, ha);
+    if constexpr (!DP) put_seq<L2, R2>(Lb, LF, perm8(wave), lane, own.w + S2);
+    dw_seq<L1, R1, RSQ, DP>(Lb + L1::OFFA, Lb + OFF_GX, perm8(wave), lane, own.w + S1, own.s + S1, ha, S1, par);
     if (last) stampw(A, 17, 3);
     bar();
     if (last) stamp(A, 5);
@@ -803,10 +1111,10 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     wave = fresh_s(wave0);
     b0 = 16 * wave;
     if (wave < L0::NDW) {
-      dw_seq<L0, 1, RSQ>(A0, Lb + OFF_GY, wave, lane, own.w + S0, own.s + S0, ha);
-      put_w<L0>(Lb, LF, wave, lane, own.w[S0]);
+      dw_seq<L0, 1, RSQ, DP>(A0, Lb + OFF_GY, wave, lane, own.w + S0, own.s + S0, ha, S0, par);
+      if constexpr (!DP) put_w<L0>(Lb, LF, wave, lane, own.w[S0]);
     }
-    put_seq<L1, R1>(Lb, LF, perm8(wave), lane, own.w + S1);
+    if constexpr (!DP) put_seq<L1, R1>(Lb, LF, perm8(wave), lane, own.w + S1);
     if (tw) {
       // FTRL-proximal on the rows this lane leads: the summed gradient from the leader sums, the old
       // weight in wv; the new weight goes back to the table, (z, n) to the private copy
@@ -816,6 +1124,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       float w1[4], z1[4], n1[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
+        if constexpr (DP) break;  // (the apply phase updates the rows after the exchange)
         const float g = LF[F_GS + (eg + 4 * m) * BP + eb] * hf.gscale;
         const float nn = fmaf(g, g, nl[m]);
         const float rs = __builtin_amdgcn_sqrtf(nn);
@@ -827,7 +1136,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        if (lead & (1u << m)) LF[F_WTAB + cid[m]] = w1[m];
+        if (!DP && (lead & (1u << m))) LF[F_WTAB + cid[m]] = w1[m];
       // the next batch (loaded during B3) into registers / the other A0 image / the id table BEFORE the
       // (z, n) stores: a wait for these loads must not include those stores (conditional: the compiler
       // would wait for every outstanding access)
@@ -841,7 +1150,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
         if (eg + 4 * m < NWIDE) idt[(eg + 4 * m) * BP + eb] = cn[m];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        if (lead & (1u << m)) C.zn[cid[m]] = make_float2(z1[m], n1[m]);
+        if (!DP && (lead & (1u << m))) C.zn[cid[m]] = make_float2(z1[m], n1[m]);
 #pragma unroll
       for (int m = 0; m < 4; ++m) cid[m] = cn[m];
       yv = yn;
@@ -849,6 +1158,15 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
     }
     bar();
     if (last) stamp(A, 6);
+    if constexpr (DP) {
+      // ========================================================== exchange: every rank's gradients, then apply
+      if (!exchange_step(A, xs0 + step + 1, step, lds)) return;  // (sticky error word set; state partial)
+      lane = fresh(tid & 63);
+      wave = fresh_s(wave0);
+      apply_dp<RSQ>(own, lds, par, wave, lane, tid);
+      bar();
+      if (last) stamp(A, 30);
+    }
   }
   stamp_clk(A, 21);
 
@@ -941,6 +1259,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       if (C.step_ftrl) C.step_ftrl[0] += (float)C.nsteps;
       if (C.rng) C.rng[1] += (unsigned long long)C.rng_bumps * (unsigned long long)C.nsteps;
       if (C.cursor) C.cursor[0] = (bi0 + C.nsteps) % C.nbatch;
+      if (DP) C.xstep[0] = xs0 + C.nsteps;
     }
   }
   stamp(A, 19);
@@ -991,6 +1310,13 @@ int fill(Args& a, const long* iv, int ni, const float* fv, int nf, long rows) {
 }  // namespace taxi2
 
 // rows = wide table rows.  Returns the LDS bytes if the v2 kernel takes this configuration, else -1.
+// exchange geometry for the host (models/widedeep.py TaxiExchange): buffer bytes, flag words, max ranks
+extern "C" void hopsx_taxi_step2_xgeom(long* g) {
+  g[0] = taxi2::X_BYTES;
+  g[1] = taxi2::XF_WORDS;
+  g[2] = taxi2::XMAX;
+  g[3] = taxi2::XPAY;
+}
 extern "C" long hopsx_taxi_step2_ok(const long* iv, int ni, long rows) {
   taxi2::Args a{};
   const float f[16] = {};
@@ -1000,11 +1326,32 @@ extern "C" long hopsx_taxi_step2_ok(const long* iv, int ni, long rows) {
 
 // ptrs: master grad shadow ada_s ftrl_z ftrl_n dense cat label cursor loss correct step_ada step_ftrl rng dbg
 // (widedeep_step.hip's order; grad is unused: the gradients never leave the kernel), zn ([rows] float2
-// scratch), rsq (nonzero: the host checked wd == 0 and eps < 1e-7 sqrt(initial Adagrad accumulator))
+// scratch), rsq (nonzero: the host checked wd == 0 and eps < 1e-7 sqrt(initial Adagrad accumulator));
+// data parallel (np = 22 + 2 world): world | rank << 8 | loopback << 16, timeout_ms, err, xstep,
+// xbuf[world], xflag[world]
 extern "C" int hopsx_taxi_step2(const uint64_t* p, int np, const long* iv, int ni, const float* fv, int nf, long rows,
                                 hipStream_t st) {
   taxi2::Args a{};
-  if (np != 18 || taxi2::fill(a, iv, ni, fv, nf, rows)) return -2;
+  if (np < 18 || taxi2::fill(a, iv, ni, fv, nf, rows)) return -2;
+  bool dp = false;
+  if (np > 18) {
+    a.world = (int)(p[18] & 0xFF);
+    a.rank = (int)((p[18] >> 8) & 0xFF);
+    a.loopback = (int)((p[18] >> 16) & 0xFF);
+    if (a.world < 2 || a.world > taxi2::XMAX || a.rank >= a.world || np != 22 + 2 * a.world) return -2;
+    a.tmo = (long long)p[19] * 100000ll;  // ms -> 100 MHz ticks
+    a.err = (unsigned*)p[20];
+    a.xstep = (long long*)p[21];
+    for (int r = 0; r < a.world; ++r) {
+      a.xbuf[r] = (unsigned char*)p[22 + r];
+      a.xflag[r] = (unsigned*)p[22 + a.world + r];
+      if (!a.xbuf[r] || !a.xflag[r] || ((uint64_t)a.xbuf[r] & 15)) return -2;
+    }
+    if (!a.err || !a.xstep || a.tmo <= 0) return -2;
+    dp = true;
+  } else {
+    a.world = 1;
+  }
   a.master = (float*)p[0];
   a.shadow = (bf16_raw*)p[2];
   a.ada_s = (float*)p[3];
@@ -1026,13 +1373,18 @@ extern "C" int hopsx_taxi_step2(const uint64_t* p, int np, const long* iv, int n
   if (a.ada_rsq && a.ada.wd != 0.f) return -2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)taxi2::taxi_step_k<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              taxi2::LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)taxi2::taxi_step_k<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              taxi2::LDS_BYTES);
+    const void* fns[4] = {(const void*)taxi2::taxi_step_k<true, false>, (const void*)taxi2::taxi_step_k<false, false>,
+                          (const void*)taxi2::taxi_step_k<true, true>, (const void*)taxi2::taxi_step_k<false, true>};
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, taxi2::LDS_BYTES);
     attr = true;
   }
-  if (a.ada_rsq) hipLaunchKernelGGL(taxi2::taxi_step_k<true>, dim3(1), dim3(taxi2::NT), (size_t)taxi2::LDS_BYTES, st, a);
-  else hipLaunchKernelGGL(taxi2::taxi_step_k<false>, dim3(1), dim3(taxi2::NT), (size_t)taxi2::LDS_BYTES, st, a);
+  const size_t lds = (size_t)taxi2::LDS_BYTES;
+  if (dp) {
+    if (a.ada_rsq) hipLaunchKernelGGL((taxi2::taxi_step_k<true, true>), dim3(1), dim3(taxi2::NT), lds, st, a);
+    else hipLaunchKernelGGL((taxi2::taxi_step_k<false, true>), dim3(1), dim3(taxi2::NT), lds, st, a);
+  } else {
+    if (a.ada_rsq) hipLaunchKernelGGL((taxi2::taxi_step_k<true, false>), dim3(1), dim3(taxi2::NT), lds, st, a);
+    else hipLaunchKernelGGL((taxi2::taxi_step_k<false, false>), dim3(1), dim3(taxi2::NT), lds, st, a);
+  }
   return (int)hipGetLastError();
 }

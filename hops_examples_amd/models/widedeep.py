@@ -94,20 +94,139 @@ def make_optimizer(model: TaxiWideDeep, ftrl_lr: float = 0.2, adagrad_lr: float 
                        optim.Adagrad(model.deep, lr=adagrad_lr, initial_accumulator_value=0.1))
 
 
+class TaxiExchange:
+    """The cross-rank exchange of the data-parallel v2 taxi step (csrc/ops/taxi_step.hip, DP
+    instantiation): this rank's uncached exchange buffer and flag page, every peer's mapped through IPC
+    handles exchanged over the default process group (ranks on one node; they may share a GPU — the step
+    is one workgroup), the global step counter (exchange epoch base) and a sticky error word.
+
+    Each rank's kernel pushes its dW accumulators and wide-row gradients into every rank's buffer, raises
+    its flag word in every peer's page and sums the W ranks' gradients in rank order before the update:
+    one cross-rank hop per step and bit-identical replicas, the MirroredStrategy global-batch step of the
+    reference's TFX trainer (README.md:99-112) at 2..8 GPUs.  ``loopback=W``: ONE process plays W ranks
+    (the peers' buffers are its own), for tests."""
+
+    def __init__(self, device, world: int | None = None, loopback: int = 0, timeout_s: float | None = None):
+        import torch.distributed as dist
+
+        from ..ops import _C
+        from ..parallel import dist as hdist
+        from ..parallel import oneshot
+
+        self.device = torch.device(device)
+        xb, xf, xmax, self.pay = _C.ext().taxi_step2_xgeom()
+        self.loopback = int(loopback)
+        if self.loopback > 1:
+            self.world, self.rank = self.loopback, 0
+        else:
+            self.world = int(world) if world is not None else hdist.world_size()
+            self.rank = hdist.rank() if self.world > 1 else 0
+        if not 2 <= self.world <= xmax:
+            raise ValueError(f"the data-parallel taxi step takes 2..{xmax} ranks")
+        self.timeout_ms = int(1000 * float(timeout_s or os.environ.get("HOPSX_TAXI_DP_TIMEOUT_S", "60")))
+        C = oneshot.ext()
+        self._owned, self._opened = [], []
+        err = None
+        try:
+            buf, hb = C.alloc(int(xb), True)
+            self._owned.append(buf)
+            flg, hf = C.alloc(int(xf) * 4, True)
+            self._owned.append(flg)
+        except Exception as e:  # every rank must learn of it before the handle exchange
+            err, hb, hf = repr(e), None, None
+        self.xstep = torch.zeros(1, device=self.device, dtype=torch.int64)
+        self.err = torch.zeros(4, device=self.device, dtype=torch.int32)
+        if self.loopback > 1:
+            if err:
+                raise RuntimeError(f"taxi DP exchange setup failed: {err}")
+            self.bufs, self.flags = [buf] * self.world, [flg] * self.world
+            return
+        objs = [None] * self.world
+        dist.all_gather_object(objs, (self.rank, None if err else bytes(hb), None if err else bytes(hf), err))
+        bad = [(o[0], o[3]) for o in objs if o[3]]
+        if bad:
+            self.close()
+            raise RuntimeError(f"taxi DP exchange setup failed on ranks {bad}")
+        self.bufs, self.flags = [0] * self.world, [0] * self.world
+        try:
+            for r, b, f, _ in objs:
+                if r == self.rank:
+                    self.bufs[r], self.flags[r] = buf, flg
+                else:
+                    self.bufs[r] = C.open(b)
+                    self._opened.append(self.bufs[r])
+                    self.flags[r] = C.open(f)
+                    self._opened.append(self.flags[r])
+        except Exception as e:
+            err = repr(e)
+        oks = [None] * self.world
+        dist.all_gather_object(oks, err)
+        if any(oks):
+            self.close()
+            raise RuntimeError(f"taxi DP: mapping a peer's exchange buffer failed: {oks}")
+
+    def ptrs(self) -> list[int]:
+        """The kernel's data-parallel pointer tail (taxi_step.hip hopsx_taxi_step2)."""
+        mode = self.world | (self.rank << 8) | ((1 if self.loopback > 1 else 0) << 16)
+        return [mode, self.timeout_ms, self.err.data_ptr(), self.xstep.data_ptr()] + list(self.bufs) + list(self.flags)
+
+    def sync_replicas(self, arena) -> None:
+        """Collective: every replica starts from rank 0's parameters and optimizer state."""
+        import torch.distributed as dist
+
+        if self.loopback > 1:
+            return
+        gloo = dist.get_backend() == "gloo"  # (rehearsals: ranks sharing a GPU; gloo broadcasts host copies)
+        for t in [arena.master] + [arena.state(k) for k in ("adagrad_s0", "ftrl_s0", "ftrl_s1")]:
+            if gloo:
+                h = t.cpu()
+                dist.broadcast(h, 0)
+                t.copy_(h)
+            else:
+                dist.broadcast(t, 0)
+        if arena.shadow is not None:
+            arena.shadow.copy_(arena.master.to(arena.shadow.dtype))
+        torch.cuda.synchronize(self.device)
+        dist.barrier()
+
+    def check(self) -> None:
+        e = int(self.err[0].item()) & 0xFFFFFFFF
+        if e:
+            raise RuntimeError(f"taxi DP: a peer's gradients did not arrive within {self.timeout_ms} ms "
+                               f"(step {e & 0xFFFFFF} of its launch); the replicas' state is partial")
+
+    def close(self) -> None:
+        if not self._owned:
+            return
+        from ..parallel import oneshot
+
+        C = oneshot.ext()
+        torch.cuda.synchronize(self.device)
+        for q in self._opened:
+            C.close(q)
+        for q in self._owned:
+            C.free(q)
+        self._opened, self._owned = [], []
+
+
 class FusedWideDeepStep:
     """The whole taxi training step as ONE kernel launch (csrc/ops/widedeep_step.hip): forward,
     sigmoid cross-entropy, backward, FTRL (wide) + Adagrad (deep) updates, step counters and the
     batch cursor of an HBM-resident epoch — one workgroup holding the model and the batch in LDS.
 
     Same model, optimizers and results as ``TrainStep(model, make_optimizer(model), "bce_logits")``
-    (fp32 GEMMs instead of bf16).  Data-parallel (``dp``): the kernel stops at the gradients, which
-    are all-reduced and applied by the regular optimizer kernels.  ``ok()`` says whether the
-    model/batch fit one workgroup's LDS; otherwise use TrainStep."""
+    (fp32 GEMMs instead of bf16).  Data-parallel, two forms: ``xdp`` (a :class:`TaxiExchange`) runs the
+    v2 kernel's data-parallel instantiation — the replicas exchange gradients inside the launch and
+    update in registers, "fused-v2-dp"; ``dp`` (a DataParallel engine): the v1 kernel stops at the
+    gradients, which are all-reduced and applied by the regular optimizer kernels.  ``ok()`` says whether
+    the model/batch fit one workgroup's LDS; otherwise use TrainStep."""
 
-    def __init__(self, model: TaxiWideDeep, optimizer, dp=None):
+    def __init__(self, model: TaxiWideDeep, optimizer, dp=None, xdp: "TaxiExchange | None" = None):
         from ..runtime.arena import ParamArena  # noqa: F401 (the model must live in an arena)
 
-        self.model, self.opt, self.dp = model, optimizer, dp
+        self.model, self.opt, self.dp, self.xdp = model, optimizer, dp, xdp
+        if dp is not None and xdp is not None:
+            raise ValueError("dp (v1 + all-reduce) and xdp (in-kernel exchange) are exclusive")
         self.arena = model.wide.weight._hx_arena
         self.ftrl, self.ada = optimizer.opts
         lins = [m for m in model.deep if isinstance(m, hnn.Linear)]
@@ -149,15 +268,27 @@ class FusedWideDeepStep:
         from ..ops import _C
 
         dev = self.arena.device
+        if self.xdp is not None:  # the in-kernel exchange exists in the v2 kernel only
+            return dev.type == "cuda" and self.v2(B)
         return (dev.type == "cuda" and self.acts_ok and self.dims[-1] == 1
                 and (self.v2(B) or _C.ext().widedeep_step_lds(self._ints(B, 1)) > 0))
+
+    def check(self) -> None:
+        """Raise if the data-parallel exchange of any launch failed (sticky device error word)."""
+        if self.xdp is not None:
+            self.xdp.check()
+
+    def digest(self) -> tuple[float, int]:
+        """(sum, integer bit-sum) of the fp32 arena: equal on every replica iff the replicas agree."""
+        m = self.arena.master
+        return float(m.double().sum()), int(m.view(torch.int32).long().sum())
 
     def v2(self, B: int) -> bool:
         """The v2 kernel (csrc/ops/taxi_step.hip: bf16 MFMA, wide table + optimizer state on chip) takes
         the default taxi shape on one GPU; HOPSX_TAXI_KERNEL=v1 forces the fp32 v1 kernel."""
         from ..ops import _C
 
-        key = (B, self.dp is None, os.environ.get("HOPSX_TAXI_KERNEL", "v2"))
+        key = (B, self.dp is None, os.environ.get("HOPSX_TAXI_KERNEL", "v2"), self.xdp is not None)
         r = self._v2.get(key)
         if r is None:
             r = (self.dp is None and key[2] != "v1" and self.acts_ok and self.arena.device.type == "cuda"
@@ -167,7 +298,8 @@ class FusedWideDeepStep:
 
     @property
     def kernel(self) -> str:
-        return "v2" if self.v2(self._B or TRAIN_BATCH_SIZE) else "v1"
+        k = "v2" if self.v2(self._B or TRAIN_BATCH_SIZE) else "v1"
+        return k + "-dp" if self.xdp is not None and k == "v2" else k
 
     def _slots(self, B: int):
         """Host-built table: LDS slot of every deep arena element for batch size B (cached)."""
@@ -203,7 +335,7 @@ class FusedWideDeepStep:
         if self.v2(B):
             fl = self._floats()
             key = (dense.data_ptr(), cat.data_ptr(), label.data_ptr(), nbatch, cursor.data_ptr(), nsteps, B,
-                   tuple(fl), id(a.master), self.dbg is not None)
+                   tuple(fl), id(a.master), self.dbg is not None, id(self.xdp))
             ext = _C.ext()
             if self._v2key != key:
                 # the argument vectors change only with the data, the step count or the hyper-parameters
@@ -219,6 +351,8 @@ class FusedWideDeepStep:
                         ptr(a.state("ftrl_s0")), ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label),
                         ptr(cursor), ptr(self.loss), ptr(self.correct), ptr(self.ada.step_count),
                         ptr(self.ftrl.step_count), ptr(rng_state(a.device)), ptr(self.dbg), ptr(self._zn), rsq]
+                if self.xdp is not None:
+                    ptrs += self.xdp.ptrs()
                 self._v2slot = ext.taxi_step2_store(self._v2slot, ptrs, self._ints(B, nbatch, nsteps), fl, rows)
                 self._v2key = key
             check(ext.taxi_step2_slot(self._v2slot, stream()), "taxi_step2")
@@ -376,6 +510,94 @@ class FusedWideDeepStep:
         return r
 
 
+def reference_steps(W, b, w4, b4, wide, ada_s, ftrl_z, ftrl_n, hp_ada, hp_ftrl, dense, cat, label, steps):
+    """fp64 replay of ``steps`` v2 taxi steps that rounds to bf16 exactly where the kernel
+    (csrc/ops/taxi_step.hip) holds bf16 images: inputs, hidden activations, W images and the backward
+    gradients G.  W/b: the 4 hidden layers ([out, in] / [out]); w4, b4: logits; wide: [rows];
+    ada_s: name -> Adagrad accumulator ("W0".."W3", "b0".."b3", "w4", "b4"); ftrl_z/n: [rows];
+    hp_ada / hp_ftrl: the kernel's 8-float hyper-parameter vectors; dense/cat/label: [nb, B, ...].
+    Everything is updated in place; returns the per-step mean losses.  A data-parallel step of W
+    replicas is this with their batches concatenated along the batch axis (global-batch mean, one FTRL
+    update per touched row with the summed gradient)."""
+    def bf(x):
+        return x.to(torch.bfloat16).to(torch.float64)
+
+    lr, gscale, wd, eps = hp_ada[:4]
+    flr, fgs, _, l1, l2, beta = hp_ftrl[:6]
+
+    def adagrad(p, g, s):
+        g = g * gscale + wd * p
+        s += g * g
+        return p - lr * g / (s.sqrt() + eps)
+
+    losses = []
+    for i in range(steps):
+        j = i % dense.shape[0]
+        x, c, y = dense[j], cat[j], label[j].reshape(-1)
+        B = x.shape[0]
+        acts = [bf(x)]
+        a = acts[0]
+        for l in range(4):
+            a = bf(torch.relu(a @ bf(W[l]).T + b[l]))
+            acts.append(a)
+        z = a @ w4 + b4 + wide[c].sum(1)
+        p = torch.sigmoid(z)
+        losses.append(float(torch.nn.functional.binary_cross_entropy_with_logits(z, y)))
+        g = (p - y) / B
+        grads = {"w4": g @ a, "b4": g.sum()}  # the logits layer: fp32 g times the bf16 activations
+        G = bf(g[:, None] * w4[None, :] * (a > 0))
+        for l in (3, 2, 1, 0):
+            grads[f"W{l}"] = G.T @ acts[l]
+            grads[f"b{l}"] = G.sum(0)
+            if l > 0:
+                G = bf((G @ bf(W[l])) * (acts[l] > 0))
+        # wide: summed example gradients per touched row, FTRL
+        gw = torch.zeros_like(wide)
+        gw.index_add_(0, c.reshape(-1), g[:, None].expand(-1, c.shape[1]).reshape(-1))
+        rows = torch.unique(c.reshape(-1))
+        gr = gw[rows] * fgs
+        n_old = ftrl_n[rows]
+        nn_ = n_old + gr * gr
+        sigma = (nn_.sqrt() - n_old.sqrt()) / flr
+        ftrl_z[rows] += gr - sigma * wide[rows]
+        ftrl_n[rows] = nn_
+        zz = ftrl_z[rows]
+        wide[rows] = torch.where(zz.abs() <= l1, torch.zeros_like(zz),
+                                 -(zz - torch.sign(zz) * l1) / ((beta + nn_.sqrt()) / flr + 2 * l2))
+        for l in range(4):
+            W[l] = adagrad(W[l], grads[f"W{l}"], ada_s[f"W{l}"])
+            b[l] = adagrad(b[l], grads[f"b{l}"], ada_s[f"b{l}"])
+        w4[:] = adagrad(w4, grads["w4"], ada_s["w4"])
+        b4[:] = adagrad(b4, grads["b4"].reshape(1), ada_s["b4"])
+    return losses
+
+
+def reference_state(model, fused):
+    """The fp64 host copies ``reference_steps`` takes, from a model's arena: (W, b, w4, b4, wide, ada_s,
+    ftrl_z, ftrl_n, hp_ada, hp_ftrl)."""
+    a = model.wide.weight._hx_arena
+    lins = fused.lins
+    f64 = lambda t: t.detach().double().cpu().clone()  # noqa: E731
+    W = [f64(m.weight).reshape(m.weight.shape) for m in lins[:4]]
+    b = [f64(m.bias) for m in lins[:4]]
+    w4 = f64(lins[4].weight).reshape(-1)
+    b4 = f64(lins[4].bias).reshape(1)
+    s = a.state("adagrad_s0").double().cpu()
+    ada = {}
+    for l in range(5):
+        m = lins[l]
+        ws = s[m.weight._hx_off:m.weight._hx_off + m.weight.numel()].clone()
+        bs = s[m.bias._hx_off:m.bias._hx_off + m.bias.numel()].clone()
+        ada[f"W{l}" if l < 4 else "w4"] = ws.reshape(m.weight.shape) if l < 4 else ws
+        ada[f"b{l}" if l < 4 else "b4"] = bs
+    wo, rows = int(model.wide.weight._hx_off), model.wide.weight.shape[0]
+    wide = a.master[wo:wo + rows].double().cpu().clone()
+    z = a.state("ftrl_s0")[wo:wo + rows].double().cpu().clone()
+    n = a.state("ftrl_s1")[wo:wo + rows].double().cpu().clone()
+    fl = fused._floats()
+    return W, b, w4, b4, wide, ada, z, n, fl[:8], fl[8:]
+
+
 def synth_taxi(n: int, seed: int = 0, device="cpu"):
     """Transformed-feature synthetic taxi trips with a learnable tip rule.
     Returns dense [n, 3] f32, cat [n, 13] int64 (global one-hot ids), label [n, 1] f32."""
@@ -410,7 +632,12 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
     model = TaxiWideDeep().to(dev)
     ParamArena.from_module(model, dev)
     opt = make_optimizer(model)
-    dp = DataParallel(model) if world > 1 else None
+    xdp = None
+    if (world > 1 and dev.type == "cuda" and os.environ.get("HOPSX_TAXI_FUSED", "1") == "1"
+            and os.environ.get("HOPSX_TAXI_DP_FUSED", "1") == "1" and FusedWideDeepStep(model, opt).v2(batch)):
+        # every rank decides alike (same model, batch and environment): the in-kernel exchange (collective setup)
+        xdp = TaxiExchange(dev, world)
+    dp = DataParallel(model) if world > 1 and xdp is None else None
     nb = max(8, -(-pool_examples // batch))
     transform_s = None
     if from_transform:
@@ -426,11 +653,16 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
             torch.cuda.synchronize(dev)
         transform_s = round(_time.perf_counter() - t0, 3)
     else:
-        dense, cat, label = synth_taxi(nb * batch, seed=7, device=dev)
+        from ..parallel import dist as hdist
+
+        # every replica trains on its own examples (data parallel): the seed carries the rank
+        dense, cat, label = synth_taxi(nb * batch, seed=7 + 1009 * hdist.rank(), device=dev)
     cat = cat.view(nb, batch, -1)
     label = label.view(nb, batch, 1)
     out = {}
-    fused = FusedWideDeepStep(model, opt, dp=dp) if os.environ.get("HOPSX_TAXI_FUSED", "1") == "1" else None
+    fused = FusedWideDeepStep(model, opt, dp=dp, xdp=xdp) if os.environ.get("HOPSX_TAXI_FUSED", "1") == "1" else None
+    if xdp is not None:
+        xdp.sync_replicas(model.wide.weight._hx_arena)
     if fused is not None and fused.ok(batch):
         dense = dense.view(nb, batch, -1)
         path = f"fused-{fused.kernel}"
@@ -459,8 +691,18 @@ def bench_taxi(dev, batch: int, steps: int, warmup: int, timed, world: int = 1, 
         run.prepare()  # build the multi-step graph outside the timed region
     el = timed(run, steps, dev)
     loss = float(out["r"]["loss"].reshape(-1)[0])
+    replicas = None
+    if xdp is not None:
+        import torch.distributed as dist
+
+        fused.check()  # the exchange's sticky error word (outside the timed region)
+        digs = [None] * world
+        dist.all_gather_object(digs, fused.digest())
+        replicas = all(d == digs[0] for d in digs)
+        xdp.close()
     return {"steps_per_sec": round(steps / el, 1), "examples_per_sec": round(batch * world * steps / el, 1),
             "ms_per_step": round(el / steps * 1e3, 4), "batch_per_gpu": batch, "loss": round(loss, 4),
             "params": sum(p.numel() for p in model.parameters()), "hidden_units": hidden_units(), "step": path,
             "data": "tfx-transform" if from_transform else "synthetic-transformed",
+            **({"replicas_identical": replicas} if replicas is not None else {}),
             **({"transform_s": transform_s} if transform_s is not None else {})}

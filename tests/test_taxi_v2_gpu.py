@@ -2,7 +2,6 @@
 optimizer state in registers) against an fp64 reference that rounds to bf16 at exactly the kernel's
 points (inputs, hidden activations, W images, the backward gradients), so the check is tight; plus
 a loose check against the fp32 CPU TrainStep of the same model (the reference's own numerics)."""
-import math
 
 import pytest
 import torch
@@ -18,61 +17,7 @@ from hops_examples_amd.runtime.step import TrainStep  # noqa: E402
 dev = torch.device("cuda", 0)
 
 
-def bf(x):
-    return x.to(torch.bfloat16).to(torch.float64)
-
-
-def reference_steps(W, b, w4, b4, wide, ada_s, ftrl_z, ftrl_n, hp_ada, hp_ftrl, dense, cat, label, steps):
-    """fp64 replay of `steps` v2 steps.  W/b: the 4 hidden layers; w4, b4: logits; wide: [rows];
-    ada_s: dict name -> Adagrad accumulator; ftrl_z/n: [rows].  Returns the per-step losses."""
-    lr, gscale, wd, eps = hp_ada[:4]
-    flr, fgs, _, l1, l2, beta = hp_ftrl[:6]
-
-    def adagrad(p, g, s):
-        g = g * gscale + wd * p
-        s += g * g
-        return p - lr * g / (s.sqrt() + eps)
-
-    losses = []
-    for i in range(steps):
-        j = i % dense.shape[0]
-        x, c, y = dense[j], cat[j], label[j].reshape(-1)
-        B = x.shape[0]
-        acts = [bf(x)]
-        a = acts[0]
-        for l in range(4):
-            a = bf(torch.relu(a @ bf(W[l]).T + b[l]))
-            acts.append(a)
-        z = a @ w4 + b4 + wide[c].sum(1)
-        p = torch.sigmoid(z)
-        losses.append(float(torch.nn.functional.binary_cross_entropy_with_logits(z, y)))
-        g = (p - y) / B
-        grads = {"w4": g @ a, "b4": g.sum()}  # the logits layer: fp32 g times the bf16 activations
-        G = bf(g[:, None] * w4[None, :] * (a > 0))
-        for l in (3, 2, 1, 0):
-            grads[f"W{l}"] = G.T @ acts[l]
-            grads[f"b{l}"] = G.sum(0)
-            if l > 0:
-                G = bf((G @ bf(W[l])) * (acts[l] > 0))
-        # wide: summed example gradients per touched row, FTRL
-        gw = torch.zeros_like(wide)
-        gw.index_add_(0, c.reshape(-1), g[:, None].expand(-1, c.shape[1]).reshape(-1))
-        rows = torch.unique(c.reshape(-1))
-        gr = gw[rows] * fgs
-        n_old = ftrl_n[rows]
-        nn_ = n_old + gr * gr
-        sigma = (nn_.sqrt() - n_old.sqrt()) / flr
-        ftrl_z[rows] += gr - sigma * wide[rows]
-        ftrl_n[rows] = nn_
-        zz = ftrl_z[rows]
-        wide[rows] = torch.where(zz.abs() <= l1, torch.zeros_like(zz),
-                                 -(zz - torch.sign(zz) * l1) / ((beta + nn_.sqrt()) / flr + 2 * l2))
-        for l in range(4):
-            W[l] = adagrad(W[l], grads[f"W{l}"], ada_s[f"W{l}"])
-            b[l] = adagrad(b[l], grads[f"b{l}"], ada_s[f"b{l}"])
-        w4[:] = adagrad(w4, grads["w4"], ada_s["w4"])
-        b4[:] = adagrad(b4, grads["b4"].reshape(1), ada_s["b4"])
-    return losses
+reference_steps = WD.reference_steps
 
 
 def _setup(B, nb, seed):
@@ -103,27 +48,7 @@ def _close_update(got, ref, init, name):
 
 
 def _ref_state(g, fs):
-    a = g._hx_arena
-    lins = fs.lins
-    f64 = lambda t: t.detach().double().cpu().clone()  # noqa: E731
-    W = [f64(m.weight).reshape(m.weight.shape) for m in lins[:4]]
-    b = [f64(m.bias) for m in lins[:4]]
-    w4 = f64(lins[4].weight).reshape(-1)
-    b4 = f64(lins[4].bias).reshape(1)
-    s = a.state("adagrad_s0").double().cpu()
-    ada = {}
-    for l in range(5):
-        m = lins[l]
-        ws = s[m.weight._hx_off:m.weight._hx_off + m.weight.numel()].clone()
-        bs = s[m.bias._hx_off:m.bias._hx_off + m.bias.numel()].clone()
-        ada[f"W{l}" if l < 4 else "w4"] = ws.reshape(m.weight.shape) if l < 4 else ws
-        ada[f"b{l}" if l < 4 else "b4"] = bs
-    wo, rows = int(g.wide.weight._hx_off), g.wide.weight.shape[0]
-    wide = a.master[wo:wo + rows].double().cpu().clone()
-    z = a.state("ftrl_s0")[wo:wo + rows].double().cpu().clone()
-    n = a.state("ftrl_s1")[wo:wo + rows].double().cpu().clone()
-    fl = fs._floats()
-    return W, b, w4, b4, wide, ada, z, n, fl[:8], fl[8:]
+    return WD.reference_state(g, fs)
 
 
 @pytest.mark.parametrize("B,graph,spe", [(40, True, 1), (40, False, 1), (48, True, 1), (13, True, 1), (40, True, 8)])
@@ -220,4 +145,3 @@ def test_taxi_v2_declines_other_shapes(monkeypatch):
     assert fs.v2(40) and not fs.v2(49)
     monkeypatch.setenv("HOPSX_TAXI_KERNEL", "v1")
     assert not fs.v2(40) and fs.kernel == "v1"
-    assert math.isfinite(0.0)

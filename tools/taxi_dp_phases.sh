@@ -1,0 +1,12 @@
+set -o pipefail
+mkdir -p gpurun_out/r6j
+for w in 2 4 8; do
+  mkdir -p gpurun_out/r6j/w$w
+  timeout -k 10 200 python -c "
+import sys; sys.path.insert(0,'.')
+from hops_examples_amd.parallel import launch
+sys.exit(launch.launch($w, ['tools/taxi_dp_worker.py','--out','gpurun_out/r6j/w$w','--steps','4','--bench','4000','--phases'], rehearse=True, timeout_s=180, extra_env={'HOPSX_TAXI_DP_TIMEOUT_S':'20'}))
+" > gpurun_out/r6j/w$w/log.txt 2>&1 || exit 1
+  cat gpurun_out/r6j/w$w/bench.json; echo; cat gpurun_out/r6j/w$w/phases.txt
+done
+timeout -k 10 120 python tools/taxi_phases.py 32 > gpurun_out/r6j/single_phases.txt 2>&1 && head -12 gpurun_out/r6j/single_phases.txt
