@@ -247,6 +247,36 @@ __global__ __launch_bounds__(kThreads) void twoshot_ar_k(const float* __restrict
   if (threadIdx.x == 0) sy.epochs[b] = e;
 }
 
+// Owner pieces of the fused step: the arena is cut into pieces [c_k, c_{k+1}) — the DP buckets when the
+// per-bucket reduce-scatter overlaps the backward, else one piece [0, n) — and rank r owns slice r of
+// EVERY piece (L_k = ceil(len_k / world) rounded to 4), so every rank reduces a share of every bucket and
+// the tail after the backward is 1/N of the last bucket, not a whole slice of the arena.  Workgroup b
+// owns [c_k + s L_k + b per_k, ...) of slice s of piece k.  Cut points are multiples of 4 (the arena
+// aligns parameters to 64 elements).
+constexpr int kMaxCuts = 32;
+struct Cuts {
+  long c[kMaxCuts + 1];
+  int k;  // pieces
+};
+struct PieceSlices {
+  const Cuts& cu;
+  int world, G;
+  __device__ PieceSlices(const Cuts& c, int w, int g) : cu(c), world(w), G(g) {}
+  __device__ void sub(int piece, int slice, int b, long& lo, long& hi) const {
+    const long p0 = cu.c[piece], p1 = cu.c[piece + 1];
+    long L = (p1 - p0 + world - 1) / world;
+    L = (L + 3) & ~3L;
+    long per = (L + G - 1) / G;
+    per = (per + 3) & ~3L;
+    const long s0 = p0 + (long)slice * L;
+    lo = s0 + (long)b * per;
+    hi = lo + per;
+    if (hi > s0 + L) hi = s0 + L;
+    if (hi > p1) hi = p1;
+    if (lo > hi) lo = hi;
+  }
+};
+
 // ------------------------------------------------------------------ fused data-parallel step
 // Wire formats (what crosses xGMI per parameter and step; each GPU reads (N-1)/N of it):
 //   gradients  GB = 0: fp32 reduce-scatter (4 B)   GB = 1: bf16, accumulated in fp32 (2 B)
@@ -425,12 +455,13 @@ __device__ inline void owner_update1(const DpArgs& a, const Peers& peers, int wo
 }
 
 template <int KIND, bool GB>
-__global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int rank, int world, Peers peers, Sync sy) {
+__global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int rank, int world, Peers peers, Sync sy,
+                                                      Cuts cuts) {
   if (poisoned(sy.err)) return;
   const int b = blockIdx.x;
   const unsigned e = sy.epochs[b] + 1;
   const long base = (long)(e & 1u) * kParity * cap;
-  const Slices S(a.n, world, gridDim.x);
+  const PieceSlices S(cuts, world, gridDim.x);
   const OptHP h = load_hp(a.h, a.hp_dev);
   const float t = (a.step_dev ? a.step_dev[0] : 0.f) + 1.f;  // read by every workgroup before the last bumps it
   float bc1, bc2;
@@ -442,20 +473,21 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
   // phase 0: stage this workgroup's share of every slice (in the gradient wire format) and zero the
   // local gradient for the next step's accumulation; the next batch's prefetch overlaps the wait.
   // Zero-copy: nothing to stage (the peers read the gradient itself); zeroing moves after the reads
-  for (int sl = 0; sl < world && !zc; ++sl) {
-    S.sub(sl, b, lo, hi);
-    for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
-      if (i + 3 < hi) {
-        st4<GB>(mine, i, *reinterpret_cast<const float4*>(a.grad + i));
-        *reinterpret_cast<float4*>(a.grad + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        for (long j = i; j < hi; ++j) {
-          st1<GB>(mine, j, a.grad[j]);
-          a.grad[j] = 0.f;
+  for (int k = 0; k < cuts.k && !zc; ++k)
+    for (int sl = 0; sl < world; ++sl) {
+      S.sub(k, sl, b, lo, hi);
+      for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+        if (i + 3 < hi) {
+          st4<GB>(mine, i, *reinterpret_cast<const float4*>(a.grad + i));
+          *reinterpret_cast<float4*>(a.grad + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          for (long j = i; j < hi; ++j) {
+            st1<GB>(mine, j, a.grad[j]);
+            a.grad[j] = 0.f;
+          }
         }
       }
     }
-  }
   prefetch_copy(a.pf);
   // round 1 (every rank's gradient final) — already held per bucket when dp_rs_k pre-reduced the slice
   if (!(zc && a.pre_reduced) && !flag_round(peers, rank, world, 1, b, e, sy)) return;
@@ -463,25 +495,27 @@ __global__ __launch_bounds__(kThreads) void dp_step_k(DpArgs a, long cap, int ra
   // phase 1: reduce + update this rank's slice; publish the new weights in their wire format
   float* red = mine + cap;
   bf16_raw* red16 = reinterpret_cast<bf16_raw*>(mine + 2 * cap);
-  S.sub(rank, b, lo, hi);
-  for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
-    if (i + 3 < hi) {
-      owner_update<KIND, GB>(a, peers, world, base, red, red16, i, h, bc1, bc2);
-    } else {
-      for (long j = i; j < hi; ++j) owner_update1<KIND, GB>(a, peers, world, base, red, red16, j, h, bc1, bc2);
+  for (int k = 0; k < cuts.k; ++k) {
+    S.sub(k, rank, b, lo, hi);
+    for (long i = lo + 4L * threadIdx.x; i < hi; i += 4L * kThreads) {
+      if (i + 3 < hi) {
+        owner_update<KIND, GB>(a, peers, world, base, red, red16, i, h, bc1, bc2);
+      } else {
+        for (long j = i; j < hi; ++j) owner_update1<KIND, GB>(a, peers, world, base, red, red16, j, h, bc1, bc2);
+      }
     }
+    // zero-copy: this rank's own slice of its gradient is read by nobody else — clear it now (the same
+    // threads read it above, so no barrier is needed)
+    if (zc) zero_range(a.grad, lo, hi);
   }
-  // zero-copy: this rank's own slice of its gradient is read by nobody else — clear it now (the same
-  // threads read it above, so no barrier is needed)
-  if (zc) zero_range(a.grad, lo, hi);
   if (!flag_round(peers, rank, world, 2, b, e, sy)) return;
 
   // phase 2: every other owner's new weights -> bf16 shadow (+ fp32 master on fp32-wire chunks)
-  for (int k = 1; k < world; ++k) {
-    const int p = (rank + k) % world;
+  for (int q = 0; q < cuts.k * (world - 1); ++q) {
+    const int k = q / (world - 1), p = (rank + 1 + q % (world - 1)) % world;
     const float* src = peers.buf[p] + base + cap;
     const bf16_raw* src16 = reinterpret_cast<const bf16_raw*>(peers.buf[p] + base + 2 * cap);
-    S.sub(p, b, lo, hi);
+    S.sub(k, p, b, lo, hi);
     // zero-copy: rank p's workgroup b read our gradient over [lo, hi) in its phase 1 (or its dp_rs_k),
     // and round 2 says it is done: clear it for the next step's accumulation
     if (zc) zero_range(a.grad, lo, hi);
@@ -523,10 +557,10 @@ __global__ __launch_bounds__(kThreads) void dp_rs_k(float* grad, long n, long bl
   const int b = blockIdx.x, G = gridDim.x;
   const unsigned e = sy.epochs[b] + 1;
   if (!flag_round(peers, rank, world, 1, b, e, sy)) return;
-  long L = (n + world - 1) / world;
+  // the bucket is one owner piece of the step tail (PieceSlices): this rank's slice of it
+  long L = (bhi - blo + world - 1) / world;
   L = (L + 3) & ~3L;
-  long lo = (long)rank * L, hi = lo + L;
-  if (lo < blo) lo = blo;
+  long lo = blo + (long)rank * L, hi = lo + L;
   if (hi > bhi) hi = bhi;
   if (hi > n) hi = n;
   if (hi > lo) {
@@ -692,8 +726,19 @@ PYBIND11_MODULE(_hopsx_comm, m) {
                       u hp_dev, u step_dev, u arrive, u rng, std::vector<u> pf_src, std::vector<u> pf_dst,
                       std::vector<long> pf_bytes, u pf_cursor, int pf_nbatch, long cap, int rank, int world,
                       std::vector<u> bufs, std::vector<u> flags, u epochs, u err, int blocks, u stream,
-                      double timeout, bool grad_bf16, u wmask, std::vector<u> gpeers, bool pre_reduced) {
+                      double timeout, bool grad_bf16, u wmask, std::vector<u> gpeers, bool pre_reduced,
+                      std::vector<long> cuts) {
     const Peers pr = make_peers(rank, world, bufs, flags);
+    // owner pieces: the cut points 0 = c_0 < ... < c_K = n (empty: one piece), multiples of 4
+    Cuts cu{};
+    if (cuts.empty()) cuts = {0, n};
+    if ((int)cuts.size() < 2 || (int)cuts.size() > kMaxCuts + 1 || cuts.front() != 0 || cuts.back() != n)
+      throw std::runtime_error("cuts must run 0 .. n with at most 32 pieces");
+    for (size_t i = 0; i < cuts.size(); ++i) {
+      if ((i && cuts[i] <= cuts[i - 1]) || (cuts[i] & 3)) throw std::runtime_error("cuts: increasing multiples of 4");
+      cu.c[i] = cuts[i];
+    }
+    cu.k = (int)cuts.size() - 1;
     if (n < 0 || n > cap) throw std::runtime_error("arena exceeds the staging capacity");
     if (blocks < 1 || blocks > kMaxBlocks) throw std::runtime_error("blocks out of range");
     if (!master || !grad || !shadow) throw std::runtime_error("dp_step needs master, grad and shadow");
@@ -745,9 +790,9 @@ PYBIND11_MODULE(_hopsx_comm, m) {
 #define DP_CASE(K)                                                                                  \
   case K:                                                                                           \
     if (grad_bf16) {                                                                                \
-      hipLaunchKernelGGL((dp_step_k<K, true>), dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy); \
+      hipLaunchKernelGGL((dp_step_k<K, true>), dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy, cu); \
     } else {                                                                                        \
-      hipLaunchKernelGGL((dp_step_k<K, false>), dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy); \
+      hipLaunchKernelGGL((dp_step_k<K, false>), dim3(blocks), dim3(kThreads), 0, st, a, cap, rank, world, pr, sy, cu); \
     }                                                                                               \
     break;
     switch (kind) {

@@ -645,66 +645,89 @@ __device__ __forceinline__ bool slot_owned(int p, int wave) {
   else if constexpr (S < S0) return p + 8 * (S - S1) < L1::NDW;
   else return wave < L0::NDW;
 }
-// (DP) unit U = (slot U / 2, rank group U % 2 of 4 ranks): this lane's 16-B gradient of that slot from the
-// group's ranks (zeros past W or for a slot the wave does not own)
-constexpr int XG = 4, NU = 2 * NSLOT;
-static_assert(2 * XG == XMAX, "two rank groups");
-template <int U>
+// (DP) the deep apply streams this lane's gradients of every rank from the uncached exchange buffer, 4
+// 16-B loads a unit (latency-bound: the next unit's loads are in flight while one is summed):
+//   NR = 8 (3..8 ranks): unit U = slot U / 2 from rank group U % 2 (ranks 4g .. 4g + 3);
+//   NR = 2 (2 ranks):    unit U = slots 2U and 2U + 1 from both ranks — half the units, half the trips.
+constexpr int XG = 4;
+static_assert(2 * XG == XMAX && NSLOT % 2 == 0, "unit geometry");
+template <int NR>
+constexpr int n_units() { return NR == 2 ? NSLOT / 2 : 2 * NSLOT; }
+template <int NR, int U>
 __device__ __forceinline__ void load_unit(f32x4 (&v)[XG], const unsigned char* X, int W, int tid, int p, int wave) {
-  constexpr int S = U / 2, G = U % 2;
-  const bool on = slot_owned<S>(p, wave) && G * XG < W;
+  if constexpr (NR == 2) {
 #pragma unroll
-  for (int r = 0; r < XG; ++r)
-    v[r] = on && G * XG + r < W ? xld16(X + (long)(G * XG + r) * XPAY, (S * NT + tid) * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
-}
-template <int U, bool RSQ>
-__device__ __forceinline__ void sum_unit(Own& own, f32x4& g, const f32x4 (&v)[XG], int W, int p, int wave,
-                                         const OptHP& h) {
-  constexpr int S = U / 2, G = U % 2;
-  if (!(slot_owned<S>(p, wave) && G * XG < W)) return;
-  // rank order: ((v0 + v1) + v2) + ... across both groups
-#pragma unroll
-  for (int r = 0; r < XG; ++r)
-    if (G * XG + r < W) g = (G == 0 && r == 0) ? v[r] : g + v[r];
-  if (G == 1 || W <= XG) {  // the slot's last group: every rank is in g
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if constexpr (RSQ) own.w[S][e] = adagrad_rsq(own.w[S][e], g[e] * h.gscale, own.s[S][e], -h.lr);
-      else own.w[S][e] = adagrad(own.w[S][e], g[e] * h.gscale, own.s[S][e], h);
+    for (int q = 0; q < XG; ++q) {
+      constexpr int S0_ = 2 * U;
+      const int S = S0_ + q / 2, r = q % 2;
+      const bool on = (q / 2 ? slot_owned<2 * U + 1>(p, wave) : slot_owned<2 * U>(p, wave)) && r < W;
+      v[q] = on ? xld16(X + (long)r * XPAY, (S * NT + tid) * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
     }
+  } else {
+    constexpr int S = U / 2, G = U % 2;
+    const bool on = slot_owned<S>(p, wave) && G * XG < W;
+#pragma unroll
+    for (int r = 0; r < XG; ++r)
+      v[r] = on && G * XG + r < W ? xld16(X + (long)(G * XG + r) * XPAY, (S * NT + tid) * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
 }
-// the NU units software-pipelined: unit U + 1's loads are in flight while unit U is summed and applied
-template <int U, bool RSQ>
+template <int S, bool RSQ>
+__device__ __forceinline__ void adagrad_slot(Own& own, const f32x4& g, const OptHP& h) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if constexpr (RSQ) own.w[S][e] = adagrad_rsq(own.w[S][e], g[e] * h.gscale, own.s[S][e], -h.lr);
+    else own.w[S][e] = adagrad(own.w[S][e], g[e] * h.gscale, own.s[S][e], h);
+  }
+}
+template <int NR, int U, bool RSQ>
+__device__ __forceinline__ void sum_unit(Own& own, f32x4& g, const f32x4 (&v)[XG], int W, int p, int wave,
+                                         const OptHP& h) {
+  if constexpr (NR == 2) {  // both ranks of two slots: rank order v0 + v1
+    if (slot_owned<2 * U>(p, wave)) adagrad_slot<2 * U, RSQ>(own, v[0] + v[1], h);
+    if (slot_owned<2 * U + 1>(p, wave)) adagrad_slot<2 * U + 1, RSQ>(own, v[2] + v[3], h);
+  } else {
+    constexpr int S = U / 2, G = U % 2;
+    if (!(slot_owned<S>(p, wave) && G * XG < W)) return;
+    // rank order: ((v0 + v1) + v2) + ... across both groups
+#pragma unroll
+    for (int r = 0; r < XG; ++r)
+      if (G * XG + r < W) g = (G == 0 && r == 0) ? v[r] : g + v[r];
+    if (G == 1 || W <= XG) adagrad_slot<S, RSQ>(own, g, h);  // the slot's last group: every rank is in g
+  }
+}
+// the units software-pipelined: unit U + 1's loads are in flight while unit U is summed and applied
+template <int NR, int U, bool RSQ>
 __device__ __forceinline__ void apply_units(Own& own, f32x4& g, f32x4 (&cur)[XG], const unsigned char* X, int W,
                                             int tid, int p, int wave, const OptHP& h) {
+  constexpr int NU = n_units<NR>();
   if constexpr (U < NU) {
     f32x4 nxt[XG];
-    if constexpr (U + 1 < NU) load_unit<U + 1>(nxt, X, W, tid, p, wave);
-    sum_unit<U, RSQ>(own, g, cur, W, p, wave, h);
+    if constexpr (U + 1 < NU) load_unit<NR, U + 1>(nxt, X, W, tid, p, wave);
+    sum_unit<NR, U, RSQ>(own, g, cur, W, p, wave, h);
     if constexpr (U + 1 < NU) {
 #pragma unroll
       for (int r = 0; r < XG; ++r) cur[r] = nxt[r];
     }
     fence_c();
-    apply_units<U + 1, RSQ>(own, g, cur, X, W, tid, p, wave, h);
+    apply_units<NR, U + 1, RSQ>(own, g, cur, X, W, tid, p, wave, h);
   }
 }
 
-template <bool RSQ>
+template <bool RSQ, int NR>
 __device__ __forceinline__ void apply_dp(Own& own, unsigned char* lds, int par, int wave, int lane, int tid) {
   const auto& C = COLD;
   bf16_raw* const Lb = (bf16_raw*)lds;
   float* const LF = (float*)(lds + BF_BYTES);
   const int W = C.world;
+  constexpr int XR = NR == 2 ? 2 : XMAX;  // ranks the wide-entry registers cover
   const unsigned char* X = C.xbuf[C.rank] + (long)par * XMAX * XPAY;  // own buffer, slots 0..W-1
   // ---- wide entries of every rank (this thread: entries tid, tid + 512 of each rank): loads issued first,
   // in flight during the deep apply
   constexpr int NE = NWIDE * BP;
-  int eid[XMAX][2];
-  float eg[XMAX][2];
+  int eid[XR][2];
+  float eg[XR][2];
 #pragma unroll
-  for (int r = 0; r < XMAX; ++r)
+  for (int r = 0; r < XR; ++r)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + NT * k;
@@ -718,8 +741,8 @@ __device__ __forceinline__ void apply_dp(Own& own, unsigned char* lds, int par, 
     const OptHP ha = {C.ada.lr, C.ada.gscale, C.ada.wd, C.ada.a, C.ada.b, C.ada.c, C.ada.d, C.ada.e};
     const int p = perm8(wave);
     f32x4 cur[XG], g = {0.f, 0.f, 0.f, 0.f};
-    load_unit<0>(cur, X, W, tid, p, wave);
-    apply_units<0, RSQ>(own, g, cur, X, W, tid, p, wave, ha);
+    load_unit<NR, 0>(cur, X, W, tid, p, wave);
+    apply_units<NR, 0, RSQ>(own, g, cur, X, W, tid, p, wave, ha);
     if (C.dbg && tid == 0) C.dbg[28] = wall_clock64();  // (HOPSX_PHASE_DBG: every step overwrites; the last stays)
     if (wave == NW - 1 && lane <= D4) {
       float g = 0.f;
@@ -733,21 +756,21 @@ __device__ __forceinline__ void apply_dp(Own& own, unsigned char* lds, int par, 
   // fetched first (in flight during the passes; only the updater's is used)
   constexpr unsigned GSENT = 0x7FC0DEADu;  // a NaN no gradient sum produces
   float* gacc = (float*)(lds + OFF_A1 * 2);
-  float2 zn[XMAX][2];
+  float2 zn[XR][2];
 #pragma unroll
-  for (int r = 0; r < XMAX; ++r)
+  for (int r = 0; r < XR; ++r)
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       zn[r][k] = C.zn[eid[r][k] >= 0 ? eid[r][k] : 0];  // (unconditional: a predicated load kept zn in scratch)
 #pragma unroll
-  for (int r = 0; r < XMAX; ++r)
+  for (int r = 0; r < XR; ++r)
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (eid[r][k] >= 0) gacc[eid[r][k]] = __uint_as_float(GSENT);
   __syncthreads();
   unsigned mine = 0u;
 #pragma unroll
-  for (int r = 0; r < XMAX; ++r) {
+  for (int r = 0; r < XR; ++r) {
     if (r < W) {
 #pragma unroll
       for (int k = 0; k < 2; ++k)
@@ -765,7 +788,7 @@ __device__ __forceinline__ void apply_dp(Own& own, unsigned char* lds, int par, 
   const OptHP hf = {C.ftrl.lr, C.ftrl.gscale, C.ftrl.wd, C.ftrl.a, C.ftrl.b, C.ftrl.c, C.ftrl.d, C.ftrl.e};
   const float ilr = __builtin_amdgcn_rcpf(hf.lr);
 #pragma unroll
-  for (int r = 0; r < XMAX; ++r)
+  for (int r = 0; r < XR; ++r)
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (mine & (1u << (2 * r + k))) {
@@ -795,7 +818,7 @@ __device__ __forceinline__ void apply_dp(Own& own, unsigned char* lds, int par, 
   if (wave == NW - 1 && lane <= D4) LF[lane < D4 ? F_W4 + lane : F_MISC] = own.w4;
 }
 
-template <bool RSQ, bool DP>
+template <bool RSQ, bool DP, int NR = 8>
 __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   bf16_raw* const Lb = (bf16_raw*)lds;
@@ -1163,7 +1186,7 @@ __global__ __launch_bounds__(NT) void taxi_step_k(Args A) {
       if (!exchange_step(A, xs0 + step + 1, step, lds)) return;  // (sticky error word set; state partial)
       lane = fresh(tid & 63);
       wave = fresh_s(wave0);
-      apply_dp<RSQ>(own, lds, par, wave, lane, tid);
+      apply_dp<RSQ, NR>(own, lds, par, wave, lane, tid);
       bar();
       if (last) stamp(A, 30);
     }
@@ -1373,13 +1396,17 @@ extern "C" int hopsx_taxi_step2(const uint64_t* p, int np, const long* iv, int n
   if (a.ada_rsq && a.ada.wd != 0.f) return -2;
   static bool attr = false;
   if (!attr) {
-    const void* fns[4] = {(const void*)taxi2::taxi_step_k<true, false>, (const void*)taxi2::taxi_step_k<false, false>,
-                          (const void*)taxi2::taxi_step_k<true, true>, (const void*)taxi2::taxi_step_k<false, true>};
+    const void* fns[6] = {(const void*)taxi2::taxi_step_k<true, false>, (const void*)taxi2::taxi_step_k<false, false>,
+                          (const void*)taxi2::taxi_step_k<true, true>, (const void*)taxi2::taxi_step_k<false, true>,
+                          (const void*)taxi2::taxi_step_k<true, true, 2>, (const void*)taxi2::taxi_step_k<false, true, 2>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, taxi2::LDS_BYTES);
     attr = true;
   }
   const size_t lds = (size_t)taxi2::LDS_BYTES;
-  if (dp) {
+  if (dp && a.world == 2) {  // (the deep apply's two-rank unit shape)
+    if (a.ada_rsq) hipLaunchKernelGGL((taxi2::taxi_step_k<true, true, 2>), dim3(1), dim3(taxi2::NT), lds, st, a);
+    else hipLaunchKernelGGL((taxi2::taxi_step_k<false, true, 2>), dim3(1), dim3(taxi2::NT), lds, st, a);
+  } else if (dp) {
     if (a.ada_rsq) hipLaunchKernelGGL((taxi2::taxi_step_k<true, true>), dim3(1), dim3(taxi2::NT), lds, st, a);
     else hipLaunchKernelGGL((taxi2::taxi_step_k<false, true>), dim3(1), dim3(taxi2::NT), lds, st, a);
   } else {

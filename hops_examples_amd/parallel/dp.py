@@ -223,7 +223,7 @@ class DataParallel:
     def fused_update(self, opt) -> None:
         if self._rs_mode:
             self._finish_rs()
-            self._oneshot.dp_step(opt, self._wmask, pre_reduced=True)
+            self._oneshot.dp_step(opt, self._wmask, pre_reduced=True, cuts=self._cuts())
         else:
             self._oneshot.dp_step(opt, self._wmask)
         self._stale = self.master_sharded
@@ -234,13 +234,22 @@ class DataParallel:
                                "HOPSX_P2P_WEIGHT_WIRE=bf16); call dp.sync_master() on EVERY rank (collective) "
                                "before state_dict() / export / save, or dp.close() at the end of training")
 
-    def owner_slices(self) -> list[slice] | None:
-        """Per-rank slices whose optimizer state only the owner keeps current (fused mode), else None."""
+    def _cuts(self) -> list[int] | None:
+        """Owner-piece boundaries of the fused step: the buckets when their reduce-scatters overlap the
+        backward (rank r owns slice r of EVERY bucket, so every rank reduces a share of every bucket and
+        the post-backward tail is 1/N of the last bucket), else None (one piece: slice r of the arena)."""
+        if not getattr(self, "_rs_mode", False):
+            return None
+        return sorted({0, self.arena.numel} | {int(s) for s, _, _ in self.buckets} | {int(e) for _, e, _ in self.buckets})
+
+    def owner_slices(self) -> list[list[slice]] | None:
+        """Per rank, the slices whose optimizer state only that rank keeps current (fused mode: slice r of
+        every owner piece, parallel.oneshot.owner_pieces), else None."""
         if self._fused_opt is None:
             return None
-        n, w = self.arena.numel, self.world
-        L = ((n + w - 1) // w + 3) & ~3
-        return [slice(min(n, r * L), min(n, (r + 1) * L)) for r in range(w)]
+        from .oneshot import owner_pieces
+
+        return owner_pieces(self.arena.numel, self.world, self._cuts())
 
     @property
     def master_sharded(self) -> bool:
@@ -429,15 +438,22 @@ class DataParallel:
                 self._oneshot = None
 
 
-def _gather_slices(t: torch.Tensor, slices: list[slice], rank: int) -> None:
-    """All-gather variable-size owner slices of a flat tensor in place (any backend)."""
+def _gather_slices(t: torch.Tensor, slices: list, rank: int) -> None:
+    """All-gather each rank's owner slices (a slice or a list of slices per rank) of a flat tensor in
+    place (any backend)."""
     if not hdist.is_dist():
         return
-    sizes = [s.stop - s.start for s in slices]
+    per = [s if isinstance(s, list) else [s] for s in slices]
+    sizes = [sum(x.stop - x.start for x in ss) for ss in per]
     mx = max(sizes)
     buf = torch.zeros(mx, dtype=t.dtype, device=t.device)
-    buf[:sizes[rank]].copy_(t[slices[rank]])
-    parts = [torch.empty_like(buf) for _ in slices]
+    if sizes[rank]:
+        buf[:sizes[rank]].copy_(torch.cat([t[x] for x in per[rank]]))
+    parts = [torch.empty_like(buf) for _ in per]
     dist.all_gather(parts, buf)
-    for s, n, p in zip(slices, sizes, parts):
-        t[s].copy_(p[:n])
+    for ss, p in zip(per, parts):
+        o = 0
+        for x in ss:
+            m = x.stop - x.start
+            t[x].copy_(p[o:o + m])
+            o += m

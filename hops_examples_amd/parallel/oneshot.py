@@ -235,12 +235,15 @@ class OneShotAllReduce:
                     self.flags, self.gpeers, self.epochs.data_ptr(), self.err.data_ptr(), int(blocks),
                     stream.cuda_stream, self.timeout)
 
-    def dp_step(self, opt, wmask: torch.Tensor | None = None, pre_reduced: bool = False) -> None:
+    def dp_step(self, opt, wmask: torch.Tensor | None = None, pre_reduced: bool = False,
+                cuts: list[int] | None = None) -> None:
         """Reduce-scatter the arena gradient, run ``opt``'s update on this rank's slice, all-gather the
         new weights; one launch (see the module docstring).  ``opt`` must own the whole arena.
         ``wmask`` (arena.wire_mask()): chunks whose weights travel in bf16 (ZeRO-1).  When the arena
         gradient is this comm's zero-copy buffer the peers' gradients are read in place (no staging
-        copy); ``pre_reduced``: dp_rs already summed this rank's slice (per-bucket overlap)."""
+        copy); ``pre_reduced``: dp_rs already summed this rank's slice (per-bucket overlap).  ``cuts``: the
+        owner pieces' boundaries 0 = c_0 < ... < c_K = numel (the per-bucket reduce-scatter's buckets: rank r
+        owns slice r of every piece, see ``owner_pieces``); None: one piece."""
         from ..ops._C import OPTIM
 
         a = opt.arena
@@ -264,7 +267,7 @@ class OneShotAllReduce:
                       self.rank, self.world, self.bufs, self.flags, self.epochs.data_ptr(), self.err.data_ptr(),
                       self.blocks, torch.cuda.current_stream(self.device).cuda_stream, self.timeout,
                       self.grad_bf16, wmask.data_ptr() if (wmask is not None and self.weight_bf16) else 0,
-                      self._zc_peers(a.grad), bool(pre_reduced))
+                      self._zc_peers(a.grad), bool(pre_reduced), [int(c) for c in (cuts or [])])
 
     def _zc_peers(self, grad: torch.Tensor) -> list:
         zg = getattr(self, "zc_grad", None)
@@ -339,6 +342,21 @@ def _agree(ok: bool) -> bool:
 SELFTEST_KINDS = ("sgd", "adam", "adadelta", "rmsprop")
 
 
+def owner_pieces(n: int, world: int, cuts: list[int] | None = None) -> list[list[slice]]:
+    """Per rank, the slices of a length-``n`` arena whose update that rank owns in the fused step
+    (csrc/comm/oneshot.hip PieceSlices): the arena is cut at ``cuts`` (0 .. n; None: one piece) and rank r
+    owns slice r — ceil(len / world) rounded up to 4 — of every piece."""
+    cuts = list(cuts) if cuts else [0, n]
+    out: list[list[slice]] = [[] for _ in range(world)]
+    for p0, p1 in zip(cuts[:-1], cuts[1:]):
+        L = ((p1 - p0 + world - 1) // world + 3) & ~3
+        for r in range(world):
+            lo, hi = min(p1, p0 + r * L), min(p1, p0 + (r + 1) * L)
+            if hi > lo:
+                out[r].append(slice(lo, hi))
+    return out
+
+
 def _dp_selftest_hp(kind: str, world: int) -> list[float]:
     return {"sgd": [0.5, 1.0 / world, 0.0, 0.9, 0.0, 0.0], "adam": [1e-2, 1.0 / world, 0.0, 0.9, 0.999, 1e-8],
             "adadelta": [1.0, 1.0 / world, 0.0, 0.95, 1e-7], "rmsprop": [1e-2, 1.0 / world, 0.0, 0.9, 1e-7, 0.0, 0.0]}[kind]
@@ -358,8 +376,6 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
     n = min(comm.cap, 8192 * W + 20)
     n -= n % 4
     idx = torch.arange(n, device=dev, dtype=torch.float32)
-    L = ((n + W - 1) // W + 3) & ~3
-    own = slice(min(n, r * L), min(n, (r + 1) * L))
     st = torch.cuda.current_stream(dev).cuda_stream
     # weight wire: every other 64-element chunk in bf16 (both formats cross every slice boundary)
     chunks = -(-n // C.WIRE_CHUNK)
@@ -392,11 +408,16 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
             # rounds alternate the gradient paths: staged copy, zero-copy (peers read in place), and
             # zero-copy with two per-bucket reduce-scatters ahead of a pre-reduced tail
             zmode = it % 3 if zg is not None else 0
+            # the per-bucket rounds cut the arena into two owner pieces (every rank owns a slice of each)
+            half = (n // 2) & ~63
+            cuts = [0, half, n] if zmode == 2 else [0, n]
+            own = torch.zeros(n, dtype=torch.bool, device=dev)
+            for s in owner_pieces(n, W, cuts)[r]:
+                own[s] = True
             if zmode:
                 zg[:n].copy_(grad)
                 grad = zg[:n]
             if zmode == 2:
-                half = (n // 2) & ~63
                 for lo, hi in ((half, n), (0, half)):
                     C.dp_rs(grad.data_ptr(), n, lo, hi, comm.cap, r, W, comm.bufs, comm.flags, comm.gpeers,
                             comm.epochs.data_ptr(), comm.err.data_ptr(), min(comm.blocks, 16), st, comm.timeout)
@@ -405,7 +426,7 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
                       arrive.data_ptr(), 0, [], [], [], 0, 0, comm.cap, r, W, comm.bufs, comm.flags,
                       comm.epochs.data_ptr(), comm.err.data_ptr(), comm.blocks, st, comm.timeout,
                       comm.grad_bf16, 0 if wmask is None else wmask.data_ptr(),
-                      list(comm.gpeers) if zmode else [], zmode == 2)
+                      list(comm.gpeers) if zmode else [], zmode == 2, cuts)
             K.optim_step(k, ref_m, gsum, ref_s[0], ref_s[1], ref_s[2], ref_sh, hp, ref_step, zero_grad=True,
                          arrive=ref_arrive, hp_dev=hp_dev)
             torch.cuda.synchronize(dev)

@@ -171,7 +171,24 @@ def check_step(model, x, y, round_grads: bool = True) -> dict:
             continue
         r = ref[n]
         grads[n] = (_cos(g, r), float((g.double() - r).norm() / r.norm().clamp_min(1e-30)))
-    return {"forward": fwd, "grads": grads, "loss": float(loss)}
+    return {"forward": fwd, "grads": grads, "loss": float(loss.detach())}
+
+
+def resnet20_check(batch: int = 16, flags: str = "", seed: int = 0) -> dict:
+    """``check_step`` of a random-init CIFAR ResNet-20 (training mode) on a random uint8 batch with
+    HOPSX_DISABLE=``flags``; adds "min_grad_cos" / "min_fwd_cos" (the worst tensor / op)."""
+    from ..models.resnet import cifar_resnet
+
+    with disabled(flags):
+        torch.manual_seed(seed)
+        m = cifar_resnet(20).to("cuda").train()
+        g = torch.Generator().manual_seed(batch + seed)
+        x = torch.randint(0, 256, (batch, 32, 32, 3), dtype=torch.uint8, generator=g).to("cuda")
+        y = torch.randint(0, 10, (batch,), generator=g).to("cuda")
+        r = check_step(m, x, y)
+    r["min_grad_cos"] = min(c for c, _ in r["grads"].values())
+    r["min_fwd_cos"] = min(c for _, c, _ in r["forward"])
+    return r
 
 
 @contextlib.contextmanager

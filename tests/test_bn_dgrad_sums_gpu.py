@@ -125,6 +125,12 @@ def test_resnet20_step_with_bn_sums_in_dgrad():
     # run-to-run noise of this random-init network is itself cos ~0.99 (float-atomic orders, amplified; see
     # test_bnstats_gpu.test_resnet20_step_bnstats_matches_unfused): compare against it
     assert cos > 0.97 and cos > noise - 0.01, (cos, noise)
+    # tight, per layer: both BN-sums paths against fp64 at their own operating point (runtime/layercheck.py)
+    from hops_examples_amd.runtime import layercheck as LC
+
+    for dis in ("", "bn_dgrad_sums"):
+        r = LC.resnet20_check(32, dis)
+        assert r["min_grad_cos"] > 0.999 and r["min_fwd_cos"] > 0.9999, (dis, r["min_grad_cos"])
 
 
 # the separate dgrad launch (conv.hip hopsx_conv2d_dgrad_bn): direct MFMA, gg 1x1 / implicit GEMM, gemm_core

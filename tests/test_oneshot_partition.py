@@ -62,4 +62,50 @@ def test_dp_owner_slices_match_kernel_geometry(n, world):
         for b in range(64):
             lo, hi = rng[(b, r)]
             idx.update(range(lo, hi))
-        assert idx == set(range(sl[r].start, sl[r].stop)), r
+        assert idx == set().union(*[set(range(s.start, s.stop)) for s in sl[r]]), r
+
+
+def piece_ranges(cuts, world, G):
+    """csrc/comm/oneshot.hip PieceSlices: workgroup b's range of slice s of piece k."""
+    out = {}
+    for k, (p0, p1) in enumerate(zip(cuts[:-1], cuts[1:])):
+        L = ((p1 - p0 + world - 1) // world + 3) & ~3
+        per = ((L + G - 1) // G + 3) & ~3
+        for s in range(world):
+            for b in range(G):
+                lo = p0 + s * L + b * per
+                hi = min(lo + per, p0 + s * L + L, p1)
+                out[(k, s, b)] = (min(lo, hi), hi)
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("cuts", [[0, 1024, 4096, 4160, 100000], [0, 64, 128], [0, 25_600_000, 51_200_000, 76_800_000,
+                                                                              102_400_064]])
+def test_per_bucket_owner_pieces(world, cuts):
+    """Per-bucket ownership (DataParallel rs-mode): the kernel's piece ranges tile the arena exactly once,
+    every rank owns part of every bucket large enough to split, and ``owner_pieces`` is exactly rank r's
+    ranges — the dp_rs_k bucket slice and the step tail's pieces agree."""
+    from hops_examples_amd.parallel.oneshot import owner_pieces
+
+    n = cuts[-1]
+    G = 16
+    rng = piece_ranges(cuts, world, G)
+    own = owner_pieces(n, world, cuts)
+    cover = {}
+    for (k, s, b), (lo, hi) in rng.items():
+        assert lo % 4 == 0 or lo == hi
+        cover[(k, s)] = cover.get((k, s), 0) + (hi - lo)
+    assert sum(cover.values()) == n
+    for r in range(world):
+        total = sum(x.stop - x.start for x in own[r])
+        assert total == sum(v for (k, s), v in cover.items() if s == r)
+        for k, (p0, p1) in enumerate(zip(cuts[:-1], cuts[1:])):
+            if p1 - p0 >= 4 * world * 2:
+                assert any(p0 <= x.start < p1 for x in own[r]), (r, k)  # a share of every bucket
+        # dp_rs_k's slice of bucket k: [p0 + r L, p0 + (r + 1) L) clipped
+        for k, (p0, p1) in enumerate(zip(cuts[:-1], cuts[1:])):
+            L = ((p1 - p0 + world - 1) // world + 3) & ~3
+            lo, hi = min(p1, p0 + r * L), min(p1, p0 + (r + 1) * L)
+            if hi > lo:
+                assert slice(lo, hi) in own[r]

@@ -54,7 +54,7 @@ def test_p2p_timeout_writes_nothing_and_poisons():
         arrive = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
         C.dp_step(3, master.data_ptr(), grad.data_ptr(), s1.data_ptr(), s2.data_ptr(), 0, shadow.data_ptr(), n,
                   [1.0, 0.5, 0.0, 0.95, 1e-7], hp.data_ptr(), step.data_ptr(), arrive.data_ptr(), 0, [], [], [], 0, 0,
-                  cap, 0, 2, bufs, flags, epochs.data_ptr(), err.data_ptr(), 8, st, 0.05, False, 0, [], False)
+                  cap, 0, 2, bufs, flags, epochs.data_ptr(), err.data_ptr(), 8, st, 0.05, False, 0, [], False, [])
         torch.cuda.synchronize()
         assert torch.equal(master, m0) and torch.equal(grad, g0) and float(step.item()) == 0.0
     finally:

@@ -20,19 +20,11 @@ from hops_examples_amd.runtime import layercheck as LC  # noqa: E402
 
 dev = torch.device("cuda", 0)
 VARIANTS = {"fused": "", "bnstats-off": "bnstats", "bnsums-off": "bn_dgrad_sums",
-            "both-off": "bnstats,bn_dgrad_sums"}
+            "both-off": "bnstats,bn_dgrad_sums", "pair-off": "bwd_pair"}
 
 
 def _check(batch, variant):
-    from hops_examples_amd.models.resnet import cifar_resnet
-
-    with LC.disabled(VARIANTS[variant]):
-        torch.manual_seed(0)
-        m = cifar_resnet(20).to(dev).train()
-        g = torch.Generator().manual_seed(batch)
-        x = torch.randint(0, 256, (batch, 32, 32, 3), dtype=torch.uint8, generator=g).to(dev)
-        y = torch.randint(0, 10, (batch,), generator=g).to(dev)
-        return LC.check_step(m, x, y)
+    return LC.resnet20_check(batch, VARIANTS[variant])
 
 
 @pytest.mark.parametrize("batch", [16, 128])

@@ -116,12 +116,16 @@ def main():
     obj = [d]
     torch.distributed.broadcast_object_list(obj, 0)
     d = obj[0]
-    owners = dpA.owner_slices()
+    owners = dpA.owner_slices()  # per rank: its slice of every owner piece
     truth = {}
     for k, t in optA.arena.states.items():  # each slice as its owner holds it
         objs = [None] * world
-        torch.distributed.all_gather_object(objs, t[owners[rank]].cpu())
-        truth[k] = torch.cat(objs)
+        torch.distributed.all_gather_object(objs, [t[s].cpu() for s in owners[rank]])
+        full = torch.empty_like(t).cpu()
+        for r in range(world):
+            for s, v in zip(owners[r], objs[r]):
+                full[s] = v
+        truth[k] = full
     p = checkpoint.save(d, mA, optA, step=10)
     if rank == 0:
         sd = torch.load(p, map_location="cpu", weights_only=True)

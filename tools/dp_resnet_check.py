@@ -47,6 +47,16 @@ def main():
         assert dp.overlap and dp._oneshot is None, (dp.overlap, dp.path)
     else:
         assert dp.path.endswith("-zerocopy-overlap"), dp.path
+    rs_calls = []
+    if MODE != "pg":
+        # per-bucket ownership: every rank reduces its slice of EVERY bucket (the tail then updates pieces)
+        orig_rs = dp._oneshot.dp_rs
+
+        def logged(grad, lo, hi, blocks, stream):
+            rs_calls.append((int(lo), int(hi)))
+            return orig_rs(grad, lo, hi, blocks, stream)
+
+        dp._oneshot.dp_rs = logged
     g = torch.Generator(device="cpu").manual_seed(200 + rank)  # every rank its own batch
     x = torch.randint(0, 256, (4, 16, 32, 32, 3), dtype=torch.uint8, generator=g).to(dev)
     y = torch.randint(0, 10, (4, 16), generator=g).to(dev)
@@ -62,6 +72,20 @@ def main():
     moved = float((stem.detach() - w0).abs().max())
     res["stem_moved"] = moved
     assert moved > 0.0  # the stem gradient reached the update
+    if MODE != "pg":
+        own = dp.owner_slices()[rank]
+        per_bucket = []
+        for lo, hi, _ in dp.buckets:
+            mine = sum(max(0, min(hi, x.stop) - max(lo, x.start)) for x in own)
+            per_bucket.append(mine)
+        res[f"rank{rank}_owned_per_bucket"] = per_bucket
+        res[f"rank{rank}_dp_rs_per_step"] = len(set(rs_calls))
+        assert all(v > 0 for v in per_bucket), per_bucket  # a share of every bucket
+        assert len(set(rs_calls)) == len(dp.buckets), (rs_calls, dp.buckets)
+        objs = [None] * world
+        torch.distributed.all_gather_object(objs, res)
+        for o in objs:
+            res.update(o)
     dp.close()
     if rank == 0:
         print("DPRESNET " + json.dumps(res), flush=True)
