@@ -16,6 +16,12 @@
 #                                        env setting ("" = default), <reps> rounds -> <tag>/ab.txt (the round-4
 #                                        A/Bs in profiles/r4_*_ab.txt were run this way)
 #   tools/gpu.sh tables  <tag>           rocprofv3 kernel tables of ResNet-20 (in-process) and ResNet-50 B=64
+#   tools/gpu.sh dpsim   <tag>           persistent flagship DP exchange on distinct data (ExchangeSim, 2-process
+#                                        peer, co-residency) + cooperative-launch A/B
+#   tools/gpu.sh taxidp  <tag>           data-parallel v2 taxi step: 2/4/8 processes on one GPU, phases, tests
+#   tools/gpu.sh numerics <tag>          ResNet-20 per-layer fp64 checks (runtime/layercheck.py) + P2P DP suites
+#   tools/gpu.sh e1prof  <tag>           rocprofv3 kernel table of the E1 Keras fit (tools/e1_fit.py)
+#   tools/gpu.sh convgemm <tag>          tools/bench_conv_gemm.py --torch at batch 64 and 8
 set -o pipefail
 job=${1:?job}; tag=${2:-$1}; shift 2
 out=gpurun_out/$tag
@@ -110,6 +116,21 @@ taxipmc)
 tables)
   ktable p20 r20_kernels.txt benchmarks/run.py cifar_resnet --depth 20 --batch 128 --steps 50 --warmup 10 --inline
   ktable p50 r50_b64_kernels.txt benchmarks/run.py resnet50 --batch 64 --steps 20 --warmup 5 ;;
+taxidp)
+  # the data-parallel v2 taxi step: 2/4/8 processes sharing the GPU (phase stamps + steps/s), its tests
+  bash tools/taxi_dp_phases.sh $tag || exit 1
+  pyt $out/pytest.log tests/test_taxi_dp_gpu.py tests/test_taxi_v2_gpu.py ;;
+numerics)
+  # per-layer (teacher-forced fp64) ResNet-20 numerics + the whole-step tests built on them; P2P DP suites
+  T=900 PYX= pyt $out/layers.log tests/test_resnet_layers_gpu.py tests/test_bnstats_gpu.py tests/test_kernels_v2_gpu.py \
+    tests/test_bn_dgrad_sums_gpu.py -s
+  T=600 PYX= pyt $out/p2p.log tests/test_p2p_gpu.py -s; grep DPRESNET $out/p2p.log | cut -c1-600 ;;
+e1prof)
+  ktable pf e1_kernels.txt tools/e1_fit.py ;;
+convgemm)
+  for b in 64 8; do
+    timeout -k 10 300 python -u tools/bench_conv_gemm.py --batch $b --torch > $out/convgemm_b$b.jsonl 2> $out/convgemm_b$b.err || fail $out/convgemm_b$b.err
+  done ;;
 dpsim)
   # the persistent flagship's data-parallel exchange on distinct per-rank data (ExchangeSim, cross-process
   # peer, co-residency), its loopback / one-GPU suites, and the cooperative-launch A/B on the bench
