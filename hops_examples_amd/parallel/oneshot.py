@@ -376,6 +376,14 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
     n = min(comm.cap, 8192 * W + 20)
     n -= n % 4
     idx = torch.arange(n, device=dev, dtype=torch.float32)
+    # two owner pieces (every rank owns a slice of each: the per-bucket layout), the same in every round —
+    # on the bf16 weight wire only the owner's fp32 master and optimizer state are current, so ownership
+    # must not move between steps; the per-bucket rounds reduce-scatter exactly these two buckets
+    half = (n // 2) & ~63
+    cuts = [0, half, n]
+    own = torch.zeros(n, dtype=torch.bool, device=dev)
+    for s in owner_pieces(n, W, cuts)[r]:
+        own[s] = True
     st = torch.cuda.current_stream(dev).cuda_stream
     # weight wire: every other 64-element chunk in bf16 (both formats cross every slice boundary)
     chunks = -(-n // C.WIRE_CHUNK)
@@ -408,12 +416,6 @@ def dp_self_test(comm: "OneShotAllReduce", kinds=SELFTEST_KINDS, rounds: int = 3
             # rounds alternate the gradient paths: staged copy, zero-copy (peers read in place), and
             # zero-copy with two per-bucket reduce-scatters ahead of a pre-reduced tail
             zmode = it % 3 if zg is not None else 0
-            # the per-bucket rounds cut the arena into two owner pieces (every rank owns a slice of each)
-            half = (n // 2) & ~63
-            cuts = [0, half, n] if zmode == 2 else [0, n]
-            own = torch.zeros(n, dtype=torch.bool, device=dev)
-            for s in owner_pieces(n, W, cuts)[r]:
-                own[s] = True
             if zmode:
                 zg[:n].copy_(grad)
                 grad = zg[:n]

@@ -9,6 +9,6 @@ import sys; sys.path.insert(0,'.')
 from hops_examples_amd.parallel import launch
 sys.exit(launch.launch($w, ['tools/taxi_dp_worker.py','--out','gpurun_out/$tag/w$w','--steps','4','--bench','4000','--phases'], rehearse=True, timeout_s=180, extra_env={'HOPSX_TAXI_DP_TIMEOUT_S':'20'}))
 " > gpurun_out/$tag/w$w/log.txt 2>&1 || exit 1
-  cat gpurun_out/$tag/w$w/bench.json; echo; cat gpurun_out/r6j/w$w/phases.txt
+  cat gpurun_out/$tag/w$w/bench.json; echo; cat gpurun_out/$tag/w$w/phases.txt
 done
-timeout -k 10 120 python tools/taxi_phases.py 32 > gpurun_out/$tag/single_phases.txt 2>&1 && head -12 gpurun_out/r6j/single_phases.txt
+timeout -k 10 120 python tools/taxi_phases.py 32 > gpurun_out/$tag/single_phases.txt 2>&1 && head -12 gpurun_out/$tag/single_phases.txt
