@@ -169,7 +169,7 @@ def main():
         try:
             from hops_examples_amd.models.widedeep import bench_taxi
 
-            taxi = None if dev.type != "cuda" else bench_taxi(dev, a.taxi_batch, max(20, a.steps // 2), max(5, a.warmup // 2), timed, world,
+            taxi = None if dev.type != "cuda" else bench_taxi(dev, a.taxi_batch, max(200, a.steps // 2), max(5, a.warmup // 2), timed, world,
                               graph=not a.no_graph)
         except Exception as e:  # keep the headline metric even if the secondary one fails
             taxi = {"error": repr(e)[:300]}

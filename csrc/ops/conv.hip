@@ -263,6 +263,165 @@ __global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __res
   }
 }
 
+// Weight gradient of a ONE-channel input layer (C = 1, K = KH*KW <= 25 taps, CO in {8,16,32,64}): the E1 /
+// HPO MNIST models' 4x4 input conv (mnist.ipynb:154-164), 20,000 pixels x 32 channels x 17 outputs at
+// batch 32 — ~11 M MACs that the channel-group kernel above spent 65 us on (25-way xor-shuffle trees per
+// accumulator, a 128-row single-workgroup combine: profiles/r6_e1_fit_kernels.txt).  Here:
+//   * workgroup = a contiguous range of PPW pixels; it stages d = dY * act'(y) for them [PPW][CO] fp32
+//     and the im2col rows of the input [PPW][K] in LDS (16-B dY loads, every load in flight at once);
+//   * thread (co, tap group): accumulates its <= 7 (tap, co) outputs (the bias as tap K) over the range
+//     from LDS — no shuffles, no atomics;
+//   * partial rows -> the slab; a two-level ticket combine: the last of each group of 16 workgroups sums
+//     its group's rows in row order, the last group sums the group rows in order and adds dW / db —
+//     deterministic (fixed summation order) and ~2 L2 round trips instead of one per 16 rows.
+constexpr int C1_GROUP = 16;
+__global__ __launch_bounds__(256) void conv_wgrad_c1_k(const bf16_raw* __restrict__ dy, const void* __restrict__ x,
+                                                      float xscale, float xshift, float* __restrict__ dw,
+                                                      float* __restrict__ dbias, const bf16_raw* __restrict__ y,
+                                                      int yact, ConvGeom g, int P, int PPW, float* __restrict__ slab,
+                                                      unsigned* __restrict__ counter, int stop) {
+  extern __shared__ float c1s[];
+  const int CO = g.CO, K = g.KH * g.KW, NE = CO * (K + 1);
+  float* D = c1s;                  // [PPW][CO] masked dY
+  float* XS = c1s + PPW * CO;      // [PPW][K] input taps
+  __shared__ int last;
+  const int m0 = blockIdx.x * PPW, np = min(PPW, P - m0);
+  // ---- stage d and the taps
+  // (every load of a thread is issued before any LDS store: a load -> store loop waits out one memory
+  // round trip per iteration)
+  const int G8 = CO >> 3;
+  constexpr int QD = 8, QX = 20;  // per-thread items: PPW * CO / 8 / 256 <= 8, PPW * K / 256 <= 20
+  {
+    bf16x8 dv[QD], yv[QD];
+#pragma unroll
+    for (int q = 0; q < QD; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int pi = min(i / G8, np - 1), cg = i % G8;
+      const long o = (long)(m0 + pi) * CO + cg * 8;
+      dv[q] = *(const bf16x8*)(dy + o);
+      yv[q] = y ? *(const bf16x8*)(y + o) : dv[q];
+    }
+#pragma unroll
+    for (int q = 0; q < QD; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      if (i < np * G8) {
+        const int pi = i / G8, cg = i - pi * G8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float d = bf2f((uint16_t)dv[q][j]);
+          if (y) d *= act_grad_from_out(bf2f((uint16_t)yv[q][j]), yact);
+          D[pi * CO + cg * 8 + j] = d;
+        }
+      }
+    }
+  }
+  {
+    float xv[QX];
+#pragma unroll
+    for (int q = 0; q < QX; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      const int pi = i / K, k = i - pi * K;
+      const int m = m0 + min(pi, np - 1);
+      const int b = g.fOHW.div(m), rem = m - b * (g.OH * g.OW);
+      const int oh = g.fOW.div(rem), ow = rem - oh * g.OW;
+      const int kw = k % g.KW, kh = k / g.KW;
+      const int ih = oh * g.sh - g.ph + kh * g.dh, iw = ow * g.sw - g.pw + kw * g.dw;
+      const bool in = i < np * K && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const float v = in_at(x, xscale, xshift, in ? ((long)b * g.H + ih) * g.W + iw : 0);
+      xv[q] = in ? v : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < QX; ++q) {
+      const int i = threadIdx.x + 256 * q;
+      if (i < np * K) XS[i] = xv[q];
+    }
+  }
+  __syncthreads();
+  if (stop == 1) return;  // (HOPSX_C1_STOP: timing of the phases, tools/c1_wgrad_bench.py)
+  // ---- accumulate: thread (co, pixel lane pl) sums ALL K + 1 outputs of channel co over pixels pl, pl + PL,
+  // ... (a thread walking every pixel for a few taps was a 179-deep LDS-latency chain at one wave per SIMD)
+  constexpr int KMAX = 25;
+  const int PL = 256 / CO, co = threadIdx.x % CO, pl = threadIdx.x / CO;
+  float acc[KMAX + 1];
+#pragma unroll
+  for (int k = 0; k <= KMAX; ++k) acc[k] = 0.f;
+  for (int pi = pl; pi < np; pi += PL) {
+    const float d = D[pi * CO + co];
+    const float* xr = XS + pi * K;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < K) acc[k] = fmaf(d, xr[k], acc[k]);
+    acc[KMAX] += d;
+  }
+  __syncthreads();  // (D / XS are read; their LDS becomes the pixel-lane reduction buffer)
+  float* RD = c1s;  // [PL][CO][K + 1]
+#pragma unroll
+  for (int k = 0; k <= KMAX; ++k) {
+    if (k < K) RD[(pl * CO + co) * (K + 1) + k] = acc[k];
+  }
+  RD[(pl * CO + co) * (K + 1) + K] = acc[KMAX];
+  __syncthreads();
+  for (int e = threadIdx.x; e < NE; e += 256) {
+    float t = 0.f;
+    for (int q = 0; q < PL; ++q) t += RD[q * NE + e];  // pixel-lane order: deterministic
+    slab[(long)blockIdx.x * NE + e] = t;
+  }
+  if (stop == 2) return;
+  // ---- level 1: the last workgroup of this group of 16 sums the group's rows (row order)
+  const int ngrp = (gridDim.x + C1_GROUP - 1) / C1_GROUP, grp = blockIdx.x / C1_GROUP;
+  const int g0 = grp * C1_GROUP, g1 = min((int)gridDim.x, g0 + C1_GROUP);
+  float* slab2 = slab + (long)gridDim.x * NE;  // [ngrp][NE]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(counter + 1 + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (unsigned)(g1 - g0 - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    counter[1 + grp] = 0u;  // re-armed for the next launch
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NE; e += 256) {
+    float v[C1_GROUP];
+#pragma unroll
+    for (int q = 0; q < C1_GROUP; ++q) v[q] = g0 + q < g1 ? slab[(long)(g0 + q) * NE + e] : 0.f;
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < C1_GROUP; ++q) t += v[q];
+    slab2[(long)grp * NE + e] = t;
+  }
+  // ---- level 2: the last group sums the group rows (group order) into dW / db
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (unsigned)(ngrp - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    counter[0] = 0u;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NE; e += 256) {
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = q < ngrp ? slab2[(long)q * NE + e] : 0.f;  // (ngrp <= 14)
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += v[q];
+    const int c = e / (K + 1), k = e - c * (K + 1);
+    if (k < K) dw[(long)c * K + k] += t;
+    else if (dbias) dbias[c] += t;
+  }
+}
+
 // sums the per-workgroup partials: element e < KC is dW[co][k] (slab index r = k*CO + co),
 // e >= KC the bias of channel e - KC
 // one workgroup per output element: 256 lanes stride over the workgroup partials
@@ -587,6 +746,33 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
                                   unsigned* counter, hipStream_t st) {
   ConvGeom g = make_geom(geom);
   const int M = g.CO, N = g.KH * g.KW * g.C, K = g.B * g.OH * g.OW;
+  // one-channel input layers: the pixel-range kernel (conv_wgrad_c1_k)
+  if (g.C == 1 && N <= 25 && (g.CO == 8 || g.CO == 16 || g.CO == 32 || g.CO == 64) && (uintptr_t)dy % 16 == 0 &&
+      (uintptr_t)y % 16 == 0 && counter && ws && !hopsx_disabled("c1_wgrad")) {
+    const int NE = g.CO * (N + 1);
+    // <= 224 workgroups + their <= 14 group rows fit the caller's 256-row slab (kernels.conv2d_wgrad)
+    int nwg = (K + 63) / 64;
+    if (nwg > 224) nwg = 224;
+    if (nwg < 1) nwg = 1;
+    const int ppw = (K + nwg - 1) / nwg;
+    const int ngrp = (nwg + C1_GROUP - 1) / C1_GROUP;
+    size_t lds = (size_t)ppw * (g.CO + N) * sizeof(float);
+    const size_t lds_red = (size_t)256 * (N + 1) * sizeof(float);  // the pixel-lane reduction [PL][CO][K+1]
+    if (lds < lds_red) lds = lds_red;
+    // (the staging loops' per-thread item counts are compile-time: 8 dY vectors, 20 taps)
+    if (ws_elems >= (long)(nwg + ngrp) * NE && lds <= 64 * 1024 && (long)ppw * (g.CO / 8) <= 8 * 256 &&
+        (long)ppw * N <= 20 * 256) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)conv_wgrad_c1_k, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        attr = true;
+      }
+      static const int stop = (int)hopsx_env_int("HOPSX_C1_STOP", 0);
+      hipLaunchKernelGGL(conv_wgrad_c1_k, dim3(nwg), dim3(256), lds, st, (const bf16_raw*)dy, x, xscale, xshift, dw,
+                         dbias, (const bf16_raw*)y, yact, g, K, ppw, ws, counter, stop);
+      return (int)hipGetLastError();
+    }
+  }
   if (smallk_ok(g, dy, y, ws, ws_elems, counter)) {
     const long total = (long)K * (g.CO / 8);
     // ~16 work items per thread: the in-launch combine then reads only blocks x CO x (K+1)

@@ -440,7 +440,10 @@ extern "C" int hopsx_maxpool2d_bwd(const void* dy, const unsigned char* argmax, 
     return e ? e : hopsx_colsum_bf16(dx, colsum, B * H * W, C, st);
   }
   const size_t shm = colsum ? (size_t)C * sizeof(float) : 0;
-  if (pool_fast(C, KH, KW, sh, sw, ph, pw, dy, dx, argmax, x)) {
+  // (a thread per pooled output walks its whole window: with few outputs and big windows — the E1 model's
+  // 4x4 pool, 6,400 threads in 25 workgroups, 28 us — the per-input-pixel kernel below fills the GPU)
+  const bool few_big = (long)B * OH * OW * (C / 8) < 32768 && KH * KW >= 9 && !colsum;
+  if (!few_big && pool_fast(C, KH, KW, sh, sw, ph, pw, dy, dx, argmax, x)) {
     const long n8 = (long)B * OH * OW * (C / 8);
     int g = grid_for(n8);
     if (g > 1024) g = 1024;

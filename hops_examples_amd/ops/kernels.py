@@ -374,6 +374,16 @@ def conv2d_bwd_pair(dy, w, geom, x, dw, dbias=None, y=None, act=0, prev=None, ad
 def conv_wgrad_uses_ticket(geom, in_affine=None) -> bool:
     """True when conv2d_wgrad would take the small-K kernel, whose in-launch combine draws from the
     shared per-device ticket counter (so it must not run concurrently with another such kernel)."""
+    return _c1_wgrad(geom) or _smallk_wgrad(geom)
+
+
+def _c1_wgrad(geom) -> bool:
+    """conv.hip conv_wgrad_c1_k: a one-channel input layer (K <= 25 taps, CO in 8/16/32/64)."""
+    K = geom[7] * geom[8] * geom[3]
+    return geom[3] == 1 and K <= 25 and geom[6] in (8, 16, 32, 64) and "c1_wgrad" not in os.environ.get("HOPSX_DISABLE", "")
+
+
+def _smallk_wgrad(geom) -> bool:
     K = geom[7] * geom[8] * geom[3]
     return K in (4, 9, 16) and geom[6] % 8 == 0 and geom[6] <= 256 and \
         "smallk_wgrad" not in os.environ.get("HOPSX_DISABLE", "")
@@ -388,10 +398,9 @@ def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0, in_affine=None):
     K = geom[7] * geom[8] * geom[3]
     KC = K * geom[6]
     ws = None
-    smallk = K in (4, 9, 16) and geom[6] % 8 == 0 and geom[6] <= 256 and "smallk_wgrad" not in \
-        os.environ.get("HOPSX_DISABLE", "")
-    if smallk:  # per-workgroup partial rows (<= 128 workgroups), combined in-launch
-        ws = torch.empty(128 * geom[6] * (K + 1), device=dy.device, dtype=F32)
+    smallk = _c1_wgrad(geom) or _smallk_wgrad(geom)
+    if smallk:  # per-workgroup partial rows (<= 256: workgroups + group rows), combined in-launch
+        ws = torch.empty((256 if _c1_wgrad(geom) else 128) * geom[6] * (K + 1), device=dy.device, dtype=F32)
     elif K <= 64 and KC <= 1024:  # older direct kernel: slab workspace
         ws = torch.empty(1024 * (KC + geom[6]), device=dy.device, dtype=F32)
     sc, sh = (float(in_affine[0]), float(in_affine[1])) if in_affine else (0.0, 0.0)
