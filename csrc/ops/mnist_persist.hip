@@ -421,7 +421,22 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
     else if (j < OFF_B1) CW1[j - OFF_W1] = v;
     else CB1[j - OFF_B1] = v;
   };
-  for (int j = tid; j < NCONV; j += 256) put_conv(j, a.master[conv_idx(a, j)]);
+  {
+    // every load in flight before the LDS stores: a load -> store loop waited out one memory round trip per
+    // iteration (33 of them: the launch prologue measured 16 us, tools/persist_check.py "launch:")
+    constexpr int NJ = (NCONV + 255) / 256;
+    float cv[NJ];
+#pragma unroll
+    for (int q = 0; q < NJ; ++q) {
+      const int j = tid + 256 * q;
+      cv[q] = j < NCONV ? a.master[conv_idx(a, j)] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < NJ; ++q) {
+      const int j = tid + 256 * q;
+      if (j < NCONV) put_conv(j, cv[q]);
+    }
+  }
   const bool owner = p < NSLICE;
   if (owner && tid < SLICE) {
     const int e = p * SLICE + tid;
@@ -980,6 +995,7 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       a.shadow[ci] = f2bf(SLm[tid]);
     }
   }
+  stamp(a, a.nsteps - 1, 14);  // (debug stamps: write-back issued)
   // every workgroup has started (D of the last step needs C of every position, which needs B of
   // every head): the run-state words can advance
   if (p == 0 && tid == 0) {
@@ -1010,11 +1026,22 @@ __device__ __forceinline__ void head_wg(const Args& a, unsigned char* smem, int*
   float* LOG = (float*)(smem + H_LOG);
   float* PAYL = (float*)(smem + H_PAY);
   float* ALL = (float*)(smem + H_ALL);
-  for (int j = tid; j < NCLS * HID; j += 256) {
-    const long ai = a.off[6] + j;
-    HW[j] = a.master[ai];
-    HW1[j] = a.s1[ai];
-    HW2[j] = a.s2[ai];
+  {
+    constexpr int NJ = NCLS * HID / 256;  // (all loads in flight before the LDS stores)
+    float v0[NJ], v1[NJ], v2[NJ];
+#pragma unroll
+    for (int q = 0; q < NJ; ++q) {
+      const long ai = a.off[6] + tid + 256 * q;
+      v0[q] = a.master[ai];
+      v1[q] = a.s1[ai];
+      v2[q] = a.s2[ai];
+    }
+#pragma unroll
+    for (int q = 0; q < NJ; ++q) {
+      HW[tid + 256 * q] = v0[q];
+      HW1[tid + 256 * q] = v1[q];
+      HW2[tid + 256 * q] = v2[q];
+    }
   }
   if (tid < NCLS) {
     const long ai = a.off[7] + tid;
@@ -1315,6 +1342,7 @@ template <bool DP>
 __global__ __launch_bounds__(256, 1) void mnist_persist_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_ok[2];  // [0] a wait's verdict, [1] the multi-wave wait's done word (wait_all)
+  stamp(a, 0, 13);  // (debug stamps: workgroup entry, before the launch prologue)
   if (threadIdx.x == 0) s_ok[0] = s_ok[1] = 0;  // (read after the first barrier of either role)
   const OptHP hp = load_hp(a.hp, a.hp_dev);
   const long long cur0 = a.cursor[0];

@@ -80,6 +80,14 @@ def timing(n, reps=5, loopback=0):
     own = pos[:162]
     step_us = (pos[:, 2:, 0] - pos[:, 1:-1, 0]).median().item()
     print(f"[loopback {loopback}] host wall {min(ts):.2f} us/step (best of {reps}), in-kernel step {step_us:.2f} us")
+    # launch boundaries (stamps 13: workgroup entry in step 0, 14: write-back issued in the last step)
+    entry, first = pos[:, 0, 13], pos[:, 0, 0]
+    wb = pos[:, n - 1, 14]
+    print(f"  launch: workgroup entry spread {(entry.max() - entry.min()).item():.2f} us; prologue (entry -> step 0) "
+          f"median {(first - entry).median().item():.2f} max {(first - entry).max().item():.2f} us; step 0 "
+          f"{(pos[:, 1, 0] - pos[:, 0, 0]).median().item():.2f} us; last step end -> write-back issued "
+          f"{(wb - pos[:, n - 1, 11]).median().item():.2f} us; first entry -> last write-back "
+          f"{(wb.max() - entry.min()).item():.2f} us = {(wb.max() - entry.min()).item() / n:.2f} us/step over {n} steps")
 
     def med(t, a, b):
         return (t[:, 1:, b] - t[:, 1:, a]).median().item()
