@@ -228,11 +228,11 @@ HX_PYMOD(HOPSX_MODNAME) {
     return hopsx_widedeep_step(p.data(), (int)p.size(), iv.data(), (int)iv.size(), fv.data(), (int)fv.size(),
                                S(st));
   });
-  m.def("conv2d_fwd_pool_ok", [](std::vector<int> g, int act) { return hopsx_conv_fwd_pool_ok(g.data(), act); });
+  m.def("conv2d_fwd_pool_ok", [](std::vector<int> g, int act, int pk) { return hopsx_conv_fwd_pool_ok(g.data(), act, pk); });
   m.def("conv2d_fwd_pool", [](u x, u w, std::vector<int> g, u out, u am, u bias, int act, float p, u rng,
-                              unsigned salt, u st) {
+                              unsigned salt, int pk, u st) {
     return hopsx_conv2d_fwd_pool(P<void>(x), P<void>(w), g.data(), P<void>(out), P<void>(am), P<float>(bias), act, p,
-                                 P<unsigned long long>(rng), salt, S(st));
+                                 P<unsigned long long>(rng), salt, pk, S(st));
   });
   m.def("conv2d_fwd_pool_in_ok", [](std::vector<int> g0, std::vector<int> g, int act) {
     return hopsx_conv_fwd_pool_in_ok(g0.data(), g.data(), act);

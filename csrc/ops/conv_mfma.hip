@@ -54,6 +54,11 @@ __device__ __forceinline__ int cm_swz(int r, int c, int cpr) {
 // argmax are written.  With a ReLU the argmax of an all-zero window is stored as 0xFF, so every
 // pool backward (which routes the gradient to the tap equal to the argmax) applies ReLU' for
 // free and the full conv output is never needed again.
+// PK = 4: a 4x4/stride-4 pool.  The 16 rows of a group are ONE pooled output's 16 window taps
+// (row = tap = 4*kh + kw), so lane (fr, fq) holds window row kh = fq of channel nf*16+fr in its 4
+// registers: max over them, then over the 4 lane quads by two xor shuffles (ties to the lower tap,
+// the unfused pool's raster order).  Both pool sizes use floor windows (a remainder row / column of
+// the conv output that no window covers is never computed).
 struct PoolEpi {
   unsigned char* am;
   const unsigned long long* rng;
@@ -83,7 +88,7 @@ struct In0 {
   int H0, W0, KH0, KW0, ph0, pw0, act0;
 };
 
-template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false, int T0 = 0>
+template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false, int T0 = 0, int PK = 2>
 __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
                                                       const float* __restrict__ bias, bf16_raw* __restrict__ y,
                                                       ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{},
@@ -128,8 +133,9 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
   phase_mark(pe.dbg, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int PH = g.OH >> 1, PW = g.OW >> 1;
-  const int M = POOL ? g.B * PH * PW * 4 : g.B * g.OH * g.OW;  // A rows (pooled: 4 taps per output)
+  static_assert(PK == 2 || (PK == 4 && T0 == 0), "pool 4x4 without the fused input layer");
+  const int PH = g.OH / PK, PW = g.OW / PK;
+  const int M = POOL ? g.B * PH * PW * PK * PK : g.B * g.OH * g.OW;  // A rows (pooled: PK*PK taps per output)
   const int ngroups = (M + 15) / 16;
   bf16_raw* sc = scratch + wave * 16 * CO;
   float bv[NF];
@@ -154,11 +160,12 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
       const int pp = pok ? px : 0;
       int b, oh, ow;
       if constexpr (POOL) {
-        const int po = pp >> 2, tap = pp & 3;  // pooled output index, window tap
+        constexpr int SH = PK == 2 ? 2 : 4;  // log2 of the taps per window
+        const int po = pp >> SH, tap = pp & (PK * PK - 1);  // pooled output index, window tap
         const int pr = po / PW, pw_ = po - pr * PW;
         b = pr / PH;
-        oh = 2 * (pr - b * PH) + (tap >> 1);
-        ow = 2 * pw_ + (tap & 1);
+        oh = PK * (pr - b * PH) + tap / PK;
+        ow = PK * pw_ + tap % PK;
       } else {
         b = g.fOHW.div(pp);
         const int rem = pp - b * (g.OH * g.OW);
@@ -238,6 +245,37 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
         }
       }
       if (u == 0) phase_mark(pe.dbg, 2);
+      if constexpr (POOL && PK == 4) {
+        // lane (fr, fq): window row fq of pooled output g0+u, channel nf*16+fr; the 4 quads' maxima
+        // combined by xor shuffles, then lane (fr, fq) stores channel nf*16+fr for nf % 4 == fq (a
+        // 128-B row per 4 fragments)
+        const long po = g0 + u;
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          float best = -INFINITY;
+          int bi = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = bf2f(f2bf(apply_act(acc[nf][r] + bv[nf], act)));
+            if (v > best) { best = v; bi = fq * 4 + r; }
+          }
+#pragma unroll
+          for (int d = 16; d <= 32; d *= 2) {
+            const float ob = __shfl_xor(best, d, 64);
+            const int oi = __shfl_xor(bi, d, 64);
+            if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+          }
+          if (act == ACT_RELU && !(best > 0.f)) bi = 0xFF;
+          const int co = nf * 16 + fr;
+          if ((nf & 3) == fq) {
+            if (pe.p > 0.f)
+              best = uniform01(dkey, (uint64_t)(po * CO + co)) >= pe.p ? best * (1.f / (1.f - pe.p)) : 0.f;
+            y[po * CO + co] = f2bf(best);
+            pe.am[po * CO + co] = (unsigned char)bi;
+          }
+        }
+        continue;
+      }
       if constexpr (POOL) {
         // lane (fr, fq): channel nf*16+fr of pooled output 4*(g0+u)+fq; acc[nf][0..3] = its window
         const int po = (g0 + u) * 4 + fq;
@@ -988,11 +1026,11 @@ bool hopsx_conv_fwd_mfma_ok(const int* geom) {
          !hopsx_disabled("conv_mfma");
 }
 
-// conv (act none / relu) -> 2x2 stride-2 max-pool (+ dropout p) in one launch (POOL epilogue):
-// needs the plain MFMA forward and an even output size
-bool hopsx_conv_fwd_pool_ok(const int* geom, int act) {
-  return hopsx_conv_fwd_mfma_ok(geom) && geom[4] % 2 == 0 && geom[5] % 2 == 0 && (act == ACT_NONE || act == ACT_RELU) &&
-         !hopsx_disabled("conv_pool");
+// conv (act none / relu) -> pk x pk stride-pk max-pool (+ dropout p) in one launch (POOL epilogue):
+// needs the plain MFMA forward; pk = 2 (any output size >= 2, floor windows) or 4 (output >= 4)
+bool hopsx_conv_fwd_pool_ok(const int* geom, int act, int pk) {
+  return hopsx_conv_fwd_mfma_ok(geom) && (pk == 2 || (pk == 4 && !hopsx_disabled("conv_pool4"))) && geom[4] >= pk &&
+         geom[5] >= pk && (act == ACT_NONE || act == ACT_RELU) && !hopsx_disabled("conv_pool");
 }
 
 // stride 1 only; K = KH*KW*CO <= 512, CO % 8 == 0, C in {16, 32, 64, 128}
@@ -1440,8 +1478,8 @@ static int conv2d_bwd_pair_impl(const void* dy, const void* w, const int* geom, 
 
 extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* out, void* am,
                                      const float* bias, int act, float p, const unsigned long long* rng, unsigned salt,
-                                     hipStream_t st) {
-  if (!hopsx_conv_fwd_pool_ok(geom, act)) return -2;
+                                     int pk, hipStream_t st) {
+  if (!hopsx_conv_fwd_pool_ok(geom, act, pk)) return -2;
   ConvGeom g;
   g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
   g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
@@ -1449,7 +1487,7 @@ extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* ge
   g.init_div();
   const int K = g.KH * g.KW * g.C;
   const int KS = cm_ks((K + 31) / 32);
-  const long rows = (long)g.B * (g.OH / 2) * (g.OW / 2) * 4;
+  const long rows = (long)g.B * (g.OH / pk) * (g.OW / pk) * pk * pk;
   // one 16-row group per wave per trip when two would leave CUs idle (HOPSX_CMP_UN=1/2 forces)
   static const int un_env = getenv("HOPSX_CMP_UN") ? atoi(getenv("HOPSX_CMP_UN")) : 0;
   const long ngr = (rows + 15) / 16;
@@ -1459,7 +1497,13 @@ extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* ge
   static const int dbg = getenv("HOPSX_PHASE_DBG") ? 1 : 0;
   const PoolEpi pe{(unsigned char*)am, rng, salt, p, dbg};
 #define HOPSX_CMP(NF, KSV)                                                                                      \
-  if (un == 1)                                                                                                  \
+  if (pk == 4 && un == 1)                                                                                       \
+    hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true, 1, false, 0, 4>), dim3(grid), dim3(256), shm, st,         \
+                       (const bf16_raw*)x, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe);            \
+  else if (pk == 4)                                                                                             \
+    hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true, 2, false, 0, 4>), dim3(grid), dim3(256), shm, st,         \
+                       (const bf16_raw*)x, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe);            \
+  else if (un == 1)                                                                                             \
     hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, true, 1>), dim3(grid), dim3(256), shm, st, (const bf16_raw*)x,  \
                        (const bf16_raw*)w, bias, (bf16_raw*)out, g, act, K, pe);                                \
   else                                                                                                          \
@@ -1489,7 +1533,7 @@ extern "C" int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* ge
 // (+ dropout) in ONE launch (conv_fwd_mfma_k IN0); geom is this conv's geometry over the input
 // layer's output (stride 1, dilation 1)
 bool hopsx_conv_fwd_pool_in_ok(const int* geom0, const int* geom, int act) {
-  return hopsx_conv_fwd_pool_ok(geom, act) && geom0[3] == 1 && geom0[9] == 1 && geom0[10] == 1 && geom0[13] == 1 &&
+  return hopsx_conv_fwd_pool_ok(geom, act, 2) && geom[4] % 2 == 0 && geom[5] % 2 == 0 && geom0[3] == 1 && geom0[9] == 1 && geom0[10] == 1 && geom0[13] == 1 &&
          geom0[14] == 1 && geom0[7] == geom0[8] && (geom0[7] == 2 || geom0[7] == 3) && geom0[4] == geom[1] && geom0[5] == geom[2] &&
          geom0[6] == geom[3] && geom0[0] == geom[0] && geom[9] == 1 && geom[10] == 1 && geom[13] == 1 &&
          geom[14] == 1 && geom[6] == 64 && geom[3] % 8 == 0 && geom[3] <= 64 &&

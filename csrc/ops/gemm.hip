@@ -169,10 +169,14 @@ extern "C" int hopsx_linear_bwd_pair(const void* dy, const void* w, const void* 
   DenseLoader aA{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
   DenseLoader bA{(const bf16_raw*)w, K, is_vec_ok(w, K)};
   EpiDActBF16 eA{(bf16_raw*)dx, K, (const bf16_raw*)yprev, K, act_prev, colsum};
-  // pool = {C, PH, PW, KH, KW, act}: dx is the pool INPUT gradient (see EpiPoolScatterBF16)
+  // pool = {C, PH, PW, KH, KW, act, H, W}: dx is the pool INPUT gradient [B][H][W][C] (see
+  // EpiPoolScatterBF16; H >= PH*KH, W >= PW*KW: floor windows)
   EpiPoolScatterBF16 eP{(bf16_raw*)dx, pool_am, (const bf16_raw*)pool_x, pool ? pool[5] : 0, pool_rng, pool_salt,
                         pool_p, K, pool ? pool[0] : 1, pool ? pool[2] : 1, pool ? pool[3] : 1, pool ? pool[4] : 1,
-                        pool ? pool[1] * pool[3] : 1, pool ? pool[2] * pool[4] : 1, nullptr};
+                        pool ? pool[6] : 1, pool ? pool[7] : 1, nullptr, pool ? pool[1] : 1};
+  if (pool && (pool[6] < pool[1] * pool[3] || pool[7] < pool[2] * pool[4] || pool[6] >= (pool[1] + 1) * pool[3] ||
+               pool[7] >= (pool[2] + 1) * pool[4]))
+    return -3;
   if (pool && pool[0] * pool[1] * pool[2] != K) return -2;
   DenseLoader aB{(const bf16_raw*)dy, N, is_vec_ok(dy, N) && is_vec_ok(ay ? ay : dy, N), (const bf16_raw*)ay, aact};
   DenseLoader bB{(const bf16_raw*)x, K, is_vec_ok(x, K)};

@@ -440,7 +440,8 @@ struct has_bn2<EP, decltype((void)EP::kBn2)> { static constexpr bool value = EP:
 // the pool backward — each pooled-gradient element (row m, column n = (ph, pw, c)) is routed to
 // its argmax position of the pool input (dropout mask regenerated, ReLU' of the pool input
 // applied), the rest of the window gets zeros.  Removes the pool-backward launch and the dX
-// round trip between them.
+// round trip between them.  Floor windows: the last pooled row / column also zero-fills the
+// remainder rows / columns of the pool input that no window covers (as maxpool_bwd8_k).
 struct EpiPoolScatterBF16 {
   static constexpr bool kPre = true;  // two-phase: all gathers issued before any dX store
   bf16_raw* dx;                 // pool-input gradient [B][H][W][C]
@@ -452,6 +453,7 @@ struct EpiPoolScatterBF16 {
   float p;                      // dropout probability of the pool (0: none)
   int N, C, PW, KH, KW, H, W;
   float* colsum;                // unused (kept for the epilogue interface)
+  int PH;
   // phase 1: argmax byte | ReLU'(pooled value) << 8.  The pooled value is positive iff the window
   // max is (dropout only scales or zeroes it, and a zeroed element has no gradient anyway).
   __device__ __forceinline__ unsigned pre(int m, int n) const {
@@ -471,7 +473,10 @@ struct EpiPoolScatterBF16 {
     const int a = aux & 0xff;
     const float g = (aux >> 8) ? v : 0.f;
     bf16_raw* base = dx + (((long)m * H + ph * KH) * W + pw * KW) * C + c;
-    for (int q = 0; q < KH * KW; ++q) base[((long)(q / KW) * W + q % KW) * C] = f2bf(q == a ? g : 0.f);
+    const int eh = ph == PH - 1 ? H - ph * KH : KH, ew = pw == PW - 1 ? W - pw * KW : KW;
+    const int ah = a / KW, aw = a - ah * KW;  // a = 0xFF (ReLU' == 0 from a fused conv-pool) matches no tap
+    for (int qh = 0; qh < eh; ++qh)
+      for (int qw = 0; qw < ew; ++qw) base[((long)qh * W + qw) * C] = f2bf(qh == ah && qw == aw ? g : 0.f);
     return v;
   }
 };

@@ -118,14 +118,15 @@ int hopsx_mnist_persist(const uint64_t* ptrs, int np, const long* iv, int ni, co
 void hopsx_mnist_persist_geom(long* g);
 
 bool hopsx_conv_fwd_mfma_ok(const int* geom);
-bool hopsx_conv_fwd_pool_ok(const int* geom, int act);
+bool hopsx_conv_fwd_pool_ok(const int* geom, int act, int pk);
 bool hopsx_conv_fwd_pool_in_ok(const int* geom0, const int* geom, int act);
 int hopsx_conv2d_fwd_pool_in(const void* x0, float xscale, float xshift, const void* w0, const float* b0, int act0,
                              const int* geom0, void* y1, const void* w, const int* geom, void* out, void* am,
                              const float* bias, int act, float p, const unsigned long long* rng, unsigned salt,
                              hipStream_t st);
+// pk = 2 or 4: a pk x pk / stride-pk max-pool with floor windows
 int hopsx_conv2d_fwd_pool(const void* x, const void* w, const int* geom, void* out, void* am, const float* bias, int act,
-                          float p, const unsigned long long* rng, unsigned salt, hipStream_t st);
+                          float p, const unsigned long long* rng, unsigned salt, int pk, hipStream_t st);
 bool hopsx_conv_dgrad_mfma_ok(const int* geom);
 int hopsx_conv2d_fwd_mfma(const void* x, const void* w, const int* geom, void* out, const float* bias, int act,
                           hipStream_t st);

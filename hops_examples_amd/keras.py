@@ -451,6 +451,12 @@ class Sequential(tnn.Module):
         if isinstance(first, hnn.Conv2d) and first.in_affine is None:
             first.in_affine = (1.0 / 255.0, 0.0)
             mods[0].raw_u8 = True
+        # Conv2D -> MaxPooling2D: the pool (+ its fused dropout) runs in the conv's epilogue where the pair
+        # qualifies (functional.conv2d_maxpool; the unfused chain otherwise), the pool module passes through
+        for a, b in zip(mods, mods[1:]):
+            if isinstance(a, hnn.Conv2d) and isinstance(b, hnn.MaxPool2d) and "keras_conv_pool" not in \
+                    os.environ.get("HOPSX_DISABLE", ""):
+                a._pool_next, b._absorbed = (b,), True
         self.net = tnn.Sequential(*mods)
         self._input_shape = shape
 

@@ -75,6 +75,9 @@ class Conv2d(nn.Module):
         self.cfg = dict(stride=stride, padding=padding, dilation=dilation)
         self.activation = activation
         self.in_affine = None  # (scale, shift) when this layer receives raw uint8 pixels
+        # (pool,): the max-pool right after this conv runs in this conv's epilogue (keras.Sequential sets
+        # it; a tuple, so the pool is not registered as a child module)
+        self._pool_next = ()
         self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, (kh, kw)
         fan_in, fan_out = in_channels * kh * kw, out_channels * kh * kw
         if init == "glorot":
@@ -93,6 +96,11 @@ class Conv2d(nn.Module):
             self.register_parameter("bias", None)
 
     def forward(self, x, bnstats: bool = False, gslot=None):
+        if self._pool_next and not bnstats and gslot is None:
+            return conv_pool(self, self._pool_next[0], x)
+        return self.conv_only(x, bnstats, gslot)
+
+    def conv_only(self, x, bnstats: bool = False, gslot=None):
         w = self.weight
         if x.shape[-1] != self.in_channels:
             # an input laid out with zero channels beyond in_channels (models/resnet.py image stems: the
@@ -120,10 +128,14 @@ class MaxPool2d(nn.Module):
         super().__init__()
         self.k, self.s, self.p = kernel_size, stride, padding
         self.dropout = float(dropout)
+        self._absorbed = False  # run by the preceding conv (Conv2d._pool_next): a pass-through here
         _salt_counter[0] += 1
         self.salt = _salt_counter[0] * 7919
 
     def forward(self, x):
+        return x if self._absorbed else self.pool_only(x)
+
+    def pool_only(self, x):
         return HF.max_pool2d(x, self.k, self.s, self.p, self.dropout, self.training, self.salt)
 
 
@@ -133,8 +145,8 @@ MaxPooling2D = MaxPool2d
 def conv_pool(conv: Conv2d, pool: MaxPool2d, x):
     """``pool(conv(x))`` as ONE fused launch when the pair qualifies (functional.conv2d_maxpool);
     parameters and results are those of the two modules applied in sequence."""
-    if conv.in_affine is not None or x.dtype == torch.uint8:
-        return pool(conv(x))
+    if conv.in_affine is not None or x.dtype == torch.uint8 or x.shape[-1] != conv.in_channels:
+        return pool.pool_only(conv.conv_only(x))
     return HF.conv2d_maxpool(x, conv.weight, conv.bias, act=conv.activation, pool_kernel=pool.k,
                              pool_stride=pool.s, pool_padding=pool.p, dropout_p=pool.dropout,
                              training=pool.training, salt=pool.salt, **conv.cfg)
@@ -148,7 +160,7 @@ def input_conv_pool(conv0: Conv2d, conv: Conv2d, pool: MaxPool2d, x):
                               conv.weight, conv.bias, conv.activation, conv.cfg, pool_kernel=pool.k,
                               pool_stride=pool.s, pool_padding=pool.p, dropout_p=pool.dropout,
                               training=pool.training, salt=pool.salt)
-    return y if y is not None else conv_pool(conv, pool, conv0(x))
+    return y if y is not None else conv_pool(conv, pool, conv0.conv_only(x))
 
 
 class GlobalAvgPool2d(nn.Module):

@@ -183,7 +183,11 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0] and wflop < _PAR_MIN_FLOP and "bwd_pair" not in _disabled():
             # small layer: dgrad and wgrad (+ bias grad) as ONE launch (horizontal fusion); when the
             # input is a flattened max-pool output, the dgrad epilogue also does the pool backward
-            pool = ctx.pool if "pool_scatter" not in _disabled() else None
+            # (4x4 and bigger windows: the separate per-input-pixel pool backward, maxpool_bwdv_k, writes the
+            # pool input as 16-B vectors; the scatter's per-element window stores measured 18.6 vs 5.7 + 6.6 us
+            # on the E1 model, profiles/r6_e1_fit_kernels.txt)
+            pool = ctx.pool if "pool_scatter" not in _disabled() and (ctx.pool is None or
+                                                                      ctx.pool[3][0] * ctx.pool[3][1] <= 4) else None
             r = K.linear_bwd_pair(dy2, _arena.weight_bf16(w), x2, gw, y=ymask, act=act, dbias=gb, pool=pool,
                                   dw_store=_sole_use(w) and gw is _arena.grad_target(w))
             if r is not False:
@@ -347,18 +351,20 @@ class _Conv2dFn(torch.autograd.Function):
                 y._hx_bnstats = True
                 return y
         if pool is not None:
-            # conv + act + 2x2 max-pool (+ dropout) as one launch; only the pooled tensor and the
+            # conv + act + pk x pk max-pool (+ dropout) as one launch; only the pooled tensor and the
             # argmax exist afterwards (ReLU' is encoded in the argmax, see conv2d_fwd_pool)
-            drop_p, salt = pool
+            drop_p, salt = pool[:2]
+            pk = pool[2] if len(pool) > 2 else 2
             x = x.contiguous()
             rng = rng_state(x.device) if drop_p > 0 else None
-            y, am = K.conv2d_fwd_pool(x, _arena.weight_bf16(w), g, bias=b, act=act, drop_p=drop_p, rng=rng, salt=salt)
+            y, am = K.conv2d_fwd_pool(x, _arena.weight_bf16(w), g, bias=b, act=act, drop_p=drop_p, rng=rng, salt=salt,
+                                      pk=pk)
             ctx.save_for_backward(x, am)
             ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
             ctx.plain = False
-            ctx.pool = (drop_p, rng, salt)
+            ctx.pool = (drop_p, rng, salt, pk)
             ctx.set_materialize_grads(False)
-            y._hx_pool = (am, False, (g[0], g[4], g[5], g[6]), (2, 2), 0, rng, salt, drop_p, True)
+            y._hx_pool = (am, False, (g[0], g[4], g[5], g[6]), (pk, pk), 0, rng, salt, drop_p, True)
             return y
         if x.dtype == BF16 and _plain_gemm_conv(g, b, act, in_affine, prev):
             x = x.contiguous()
@@ -431,13 +437,14 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.pool is not None:
             x, am = ctx.saved_tensors
             y = None
-            drop_p, rng, salt = ctx.pool
+            drop_p, rng, salt = ctx.pool[:3]
+            pk = ctx.pool[3] if len(ctx.pool) > 3 else 2
             oshape = (g[0], g[4], g[5], g[6])
             ent = _PRESCATTERED.pop(dy.data_ptr(), None)
             if ent is not None and ent[0]() is not None and tuple(ent[1].shape) == oshape:
                 dy = ent[1]  # the consuming Linear's dgrad epilogue already did the pool backward
             else:
-                dy = K.maxpool2d_bwd(dy.to(BF16).contiguous(), am, oshape, (2, 2), (2, 2), (0, 0), drop_p=drop_p,
+                dy = K.maxpool2d_bwd(dy.to(BF16).contiguous(), am, oshape, (pk, pk), (pk, pk), (0, 0), drop_p=drop_p,
                                      rng=rng, salt=salt)
             premasked = True  # ReLU' rode on the argmax
         else:
@@ -602,23 +609,26 @@ def _add_addend(ctx, dx):
 def conv2d_maxpool(x, w, b=None, stride=1, padding=0, dilation=1, act=None, pool_kernel=2, pool_stride=None,
                    pool_padding=0, dropout_p: float = 0.0, training: bool = True, salt: int = 0):
     """max_pool2d(conv2d(x, ...), ...) with the pool (+ its fused dropout) folded into the conv's
-    epilogue when the pair qualifies (bf16 NHWC on the GPU, 2x2 stride-2 unpadded pool, even conv
-    output, ReLU or no activation): one launch, and neither the conv output nor a pool pass."""
+    epilogue when the pair qualifies (bf16 NHWC on the GPU, unpadded 2x2/2 or 4x4/4 pool, floor
+    windows, ReLU or no activation): one launch, and neither the conv output nor a pool pass."""
     pk = (pool_kernel, pool_kernel) if isinstance(pool_kernel, int) else tuple(pool_kernel)
     ps = pk if pool_stride is None else ((pool_stride,) * 2 if isinstance(pool_stride, int) else tuple(pool_stride))
     pp = (pool_padding,) * 2 if isinstance(pool_padding, int) else tuple(pool_padding)
     a = ACT[act] if not isinstance(act, int) else act
-    if (x.is_cuda and x.dtype == BF16 and pk == (2, 2) and ps == (2, 2) and pp == (0, 0)
-            and padding != "valid" and "conv_pool" not in _disabled() and x.data_ptr() % 16 == 0
+    if (x.is_cuda and x.dtype == BF16 and pk in ((2, 2), (4, 4)) and ps == pk and pp == (0, 0)
+            and "conv_pool" not in _disabled() and x.data_ptr() % 16 == 0
             and not (padding == "same" and (w.shape[1] % 2 == 0 or w.shape[2] % 2 == 0))):
         st = (stride, stride) if isinstance(stride, int) else tuple(stride)
         dl = (dilation, dilation) if isinstance(dilation, int) else tuple(dilation)
         if padding == "same":
             pd = (_pad_same(w.shape[1], dl[0]), _pad_same(w.shape[2], dl[1]))
+        elif padding == "valid":
+            pd = (0, 0)
         else:
             pd = (padding, padding) if isinstance(padding, int) else tuple(padding)
-        if K.conv_fwd_pool_ok(K.conv_geom(x.shape, w.shape, st, pd, dl), a):
-            return _conv_apply(x, w, b, st, pd, dl, a, None, pool=(float(dropout_p) if training else 0.0, salt))
+        if K.conv_fwd_pool_ok(K.conv_geom(x.shape, w.shape, st, pd, dl), a, pk[0]):
+            return _conv_apply(x, w, b, st, pd, dl, a, None,
+                               pool=(float(dropout_p) if training else 0.0, salt, pk[0]))
     y = conv2d(x, w, b, stride, padding, dilation, act)
     return max_pool2d(y, pool_kernel, pool_stride, pool_padding, dropout_p, training, salt)  # unfused
 
@@ -881,8 +891,9 @@ class _MaxPoolFn(torch.autograd.Function):
             ctx.save_for_backward(am)
         ctx.cfg = (x.shape, k, s, p, drop_p, rng, salt, premask)
         B, H, W, C = x.shape
-        if x.is_cuda and s == k and p == (0, 0) and H % k[0] == 0 and W % k[1] == 0 and k[0] * k[1] <= 255:
+        if x.is_cuda and s == k and p == (0, 0) and H >= k[0] and W >= k[1] and k[0] * k[1] <= 255:
             # a Linear consuming the (flattened) output can do this backward in its dgrad epilogue
+            # (floor windows: the remainder rows / columns get zeros there)
             y._hx_pool = (am, bool(premask), tuple(x.shape), k, "relu" if premask else 0,
                           rng, salt, drop_p, bool(premask))
         return y

@@ -123,7 +123,7 @@ def linear_bwd_pair(dy, w, x, dw, y=None, act=0, dbias=None, pool=None, dw_store
     if pool is not None:
         am, xin, in_shape, (kh, kw), pact, rng, salt, p = pool[:8]
         B, H, W, C = in_shape
-        pl = [C, H // kh, W // kw, kh, kw, act_id(pact) if xin else 0]
+        pl = [C, H // kh, W // kw, kh, kw, act_id(pact) if xin else 0, H, W]
         pam, px, prng, psalt, pp = ptr(am), (ptr(x) if xin else 0), ptr(rng), int(salt) & 0xFFFFFFFF, float(p)
         dx = torch.empty(B, H, W, C, device=dy.device, dtype=BF16)
     else:
@@ -201,22 +201,25 @@ def conv2d_fwd(x, w, geom, bias=None, act=0, out=None, colsum=None, in_affine=No
     return out
 
 
-def conv_fwd_pool_ok(geom, act) -> bool:
-    """conv(geom, act) -> 2x2/2 max-pool can run as one launch (conv_mfma.hip POOL epilogue)."""
-    return bool(_C.ext().conv2d_fwd_pool_ok(list(geom), act_id(act)))
+def conv_fwd_pool_ok(geom, act, pk: int = 2) -> bool:
+    """conv(geom, act) -> pk x pk / stride-pk max-pool (pk 2 or 4, floor windows) can run as one launch
+    (conv_mfma.hip POOL epilogue)."""
+    return bool(_C.ext().conv2d_fwd_pool_ok(list(geom), act_id(act), int(pk)))
 
 
-def conv2d_fwd_pool(x, w, geom, bias=None, act=0, drop_p=0.0, rng=None, salt=0):
-    """Conv + act + 2x2/stride-2 max-pool (+ dropout) in one launch: returns (pooled [B, OH/2, OW/2,
-    CO] bf16, argmax uint8).  With a ReLU an all-zero window's argmax is 0xFF (no gradient), so
-    the pool backward applies ReLU' and the conv output itself is never stored."""
+def conv2d_fwd_pool(x, w, geom, bias=None, act=0, drop_p=0.0, rng=None, salt=0, pk: int = 2):
+    """Conv + act + pk x pk / stride-pk max-pool (+ dropout) in one launch: returns (pooled [B, OH//pk,
+    OW//pk, CO] bf16, argmax uint8 = the window tap kh*pk+kw).  With a ReLU an all-zero window's argmax
+    is 0xFF (no gradient), so the pool backward applies ReLU' and the conv output itself is never
+    stored."""
     _req(x, BF16, "x")
     _req(w, BF16, "w")
     B, OH, OW, CO = geom[0], geom[4], geom[5], geom[6]
-    y = torch.empty(B, OH // 2, OW // 2, CO, device=x.device, dtype=BF16)
-    am = torch.empty(B, OH // 2, OW // 2, CO, device=x.device, dtype=torch.uint8)
+    y = torch.empty(B, OH // pk, OW // pk, CO, device=x.device, dtype=BF16)
+    am = torch.empty(B, OH // pk, OW // pk, CO, device=x.device, dtype=torch.uint8)
     check(_C.ext().conv2d_fwd_pool(ptr(x), ptr(w), list(geom), ptr(y), ptr(am), ptr(bias), act_id(act),
-                                   float(drop_p), ptr(rng), int(salt) & 0xFFFFFFFF, stream()), "conv2d_fwd_pool")
+                                   float(drop_p), ptr(rng), int(salt) & 0xFFFFFFFF, int(pk), stream()),
+          "conv2d_fwd_pool")
     return y, am
 
 

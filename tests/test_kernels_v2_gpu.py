@@ -482,10 +482,15 @@ def test_pool_backward_fused_into_linear_dgrad(monkeypatch, model):
     torch.testing.assert_close(grads[0], grads[1], atol=3e-2 * grads[1].abs().max().item(), rtol=3e-2)
 
 
-@pytest.mark.parametrize("C,CO,k,H,pad,act,p", [(32, 64, 2, 27, 0, "relu", 0.01), (32, 64, 3, 28, 1, "relu", 0.45),
-                                               (16, 32, 3, 14, 0, 0, 0.0), (64, 128, 2, 9, 0, "relu", 0.0)])
-def test_conv_fwd_pool_matches_conv_then_pool(C, CO, k, H, pad, act, p):
-    """POOL epilogue of conv_fwd_mfma_k == conv kernel followed by the max-pool(+dropout) kernel."""
+@pytest.mark.parametrize("C,CO,k,H,pad,act,p,pk", [(32, 64, 2, 27, 0, "relu", 0.01, 2), (32, 64, 3, 28, 1, "relu", 0.45, 2),
+                                                  (16, 32, 3, 14, 0, 0, 0.0, 2), (64, 128, 2, 9, 0, "relu", 0.0, 2),
+                                                  (32, 64, 2, 28, 0, "relu", 0.3, 2),  # odd conv output: floor
+                                                  (32, 64, 4, 25, 0, "relu", 0.5, 4),  # E1: 22x22 -> 5x5
+                                                  (32, 64, 4, 25, 0, "relu", 0.0, 4), (16, 32, 3, 14, 0, 0, 0.0, 4),
+                                                  (32, 128, 3, 19, 1, "relu", 0.2, 4), (64, 16, 2, 9, 0, "relu", 0.0, 4)])
+def test_conv_fwd_pool_matches_conv_then_pool(C, CO, k, H, pad, act, p, pk):
+    """POOL epilogue of conv_fwd_mfma_k (2x2 and 4x4 windows, floor remainders) == conv kernel followed
+    by the max-pool(+dropout) kernel, bitwise, argmax included (ties to the lower tap)."""
     from hops_examples_amd.ops import functional as HF
 
     torch.manual_seed(1)
@@ -494,21 +499,74 @@ def test_conv_fwd_pool_matches_conv_then_pool(C, CO, k, H, pad, act, p):
     w = (torch.randn(CO, k, k, C, device=dev) * 0.2).to(bf)
     b = torch.randn(CO, device=dev) * 0.1
     g = K.conv_geom(x.shape, w.shape, (1, 1), (pad, pad), (1, 1))
-    assert K.conv_fwd_pool_ok(g, act)
+    assert K.conv_fwd_pool_ok(g, act, pk)
     rng = HF.rng_state(dev)
-    yp, am = K.conv2d_fwd_pool(x, w, g, bias=b, act=act, drop_p=p, rng=rng, salt=4242)
+    yp, am = K.conv2d_fwd_pool(x, w, g, bias=b, act=act, drop_p=p, rng=rng, salt=4242, pk=pk)
     yc = K.conv2d_fwd(x, w, g, bias=b, act=act)
-    yr, amr = K.maxpool2d_fwd(yc, (2, 2), (2, 2), (0, 0), drop_p=p, rng=rng, salt=4242)
+    yr, amr = K.maxpool2d_fwd(yc, (pk, pk), (pk, pk), (0, 0), drop_p=p, rng=rng, salt=4242)
     torch.cuda.synchronize()
+    assert yp.shape == yr.shape == (B, g[4] // pk, g[5] // pk, CO)
     torch.testing.assert_close(yp.float(), yr.float(), rtol=0, atol=0)
     if act == "relu":
         # the argmax carries ReLU': 0xFF exactly where the window max is 0
-        wmax = yc.float().view(B, g[4] // 2, 2, g[5] // 2, 2, CO).amax((2, 4))
+        PH, PW = g[4] // pk, g[5] // pk
+        wmax = yc[:, :PH * pk, :PW * pk].float().reshape(B, PH, pk, PW, pk, CO).amax((2, 4))
         assert torch.equal(am == 255, wmax <= 0)
         live = am != 255
         assert torch.equal(am[live], amr[live])
     else:
         assert torch.equal(am, amr)
+
+
+def _e1_net(fuse: bool):
+    """The E1 MNIST CNN (mnist.ipynb:154-164: 4x4 convs, 4x4 pool + dropout, dense + dropout) as hopsx
+    modules, conv2 -> pool fused in conv2's epilogue when ``fuse`` (what keras.Sequential sets up)."""
+    from hops_examples_amd import nn as hnn
+
+    c1 = hnn.Conv2d(1, 32, 4, activation="relu")
+    c1.in_affine = (1.0 / 255.0, 0.0)
+    c2 = hnn.Conv2d(32, 64, 4, activation="relu")
+    pool = hnn.MaxPool2d(4, dropout=0.5)
+    drop = hnn.Dropout(0.5)
+    pool.salt, drop.salt = 7919, 2 * 7919
+    if fuse:
+        c2._pool_next, pool._absorbed = (pool,), True
+    return torch.nn.Sequential(c1, c2, pool, hnn.Flatten(), hnn.Linear(1600, 128, activation="relu"), drop,
+                               hnn.Linear(128, 10))
+
+
+@pytest.mark.parametrize("fused_scatter", [True, False])
+def test_e1_conv_pool4_grads_match_unfused(monkeypatch, fused_scatter):
+    """E1: conv2 + 4x4 pool (+dropout) in one launch, and the floor-window pool backward (22x22 -> 5x5:
+    the 2 remainder rows / columns get zero gradient) in the Linear's dgrad epilogue or the separate
+    pool backward, against the unfused chain: logits and every gradient."""
+    from hops_examples_amd.ops import functional as HF
+    from hops_examples_amd.runtime.arena import ParamArena
+
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setenv("HOPSX_DISABLE", "" if fused_scatter else "pool_scatter")
+        HF.seed_device_rng(9, dev)
+        torch.manual_seed(0)
+        m = _e1_net(fuse).to(dev)
+        ParamArena.from_module(m, dev)
+        calls = []
+        real = K.conv2d_fwd_pool
+        monkeypatch.setattr(K, "conv2d_fwd_pool", lambda *a, **kw: calls.append(kw.get("pk")) or real(*a, **kw))
+        x = torch.randint(0, 256, (32, 28, 28, 1), dtype=torch.uint8, device=dev)
+        t = torch.randint(0, 10, (32,), device=dev)
+        out = m(x)
+        _, _, _, root, g = HF.loss_and_grad_root(out, t, "sparse_ce")
+        root.backward(g)
+        torch.cuda.synchronize()
+        monkeypatch.setattr(K, "conv2d_fwd_pool", real)
+        assert calls == ([4] if fuse else []), calls
+        res.append((out.float().clone(), None, m._hx_arena.grad.float().clone()))
+    assert not HF._PRESCATTERED
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(res[0][2], res[1][2], atol=3e-2 * res[1][2].abs().max().item(), rtol=3e-2)
+    cos = torch.nn.functional.cosine_similarity(res[0][2].double(), res[1][2].double(), dim=0)
+    assert cos > 0.9999, float(cos)
 
 
 @pytest.mark.parametrize("model", ["mirrored", "fashion"])
