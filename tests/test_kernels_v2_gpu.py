@@ -49,8 +49,8 @@ def test_smallk_wgrad(k, C, CO, B, H, masked):
 @pytest.mark.parametrize("k,CO,B,stride,pad", [(4, 32, 32, 1, 0), (5, 16, 8, 1, 2), (3, 64, 4, 2, 1), (2, 8, 9, 1, 0)])
 def test_c1_wgrad_pixel_range_kernel(k, CO, B, stride, pad, monkeypatch):
     """conv_wgrad_c1_k (one-channel input layers: the E1 model's 4x4 conv at batch 32 first) against the fp32
-    reference, bit-identical across runs (two-level ordered combine), and equal to the channel-group kernel
-    it replaced within fp32 summation-order noise."""
+    reference, bit-identical across runs (two-level ordered combine: a one-atomic-per-workgroup combine measured
+    36.4 vs 32.0 us on the E1 fit, 224 workgroups into 544 addresses)."""
     torch.manual_seed(7)
     H = 28
     xu = torch.randint(0, 256, (B, H, H, 1), dtype=torch.uint8, device=dev)
@@ -133,19 +133,25 @@ def test_conv_mfma_fwd(k, C, CO, H, pad):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("k,C,CO,H,pad", [(2, 32, 64, 27, 0), (3, 32, 64, 14, 1), (4, 32, 64, 13, 0), (2, 16, 32, 9, 0),
-                                          (3, 16, 16, 12, 1)])
-def test_conv_mfma_dgrad_masks_colsum(k, C, CO, H, pad):
+@pytest.mark.parametrize("k,C,CO,H,pad,B,masked", [(2, 32, 64, 27, 0, 2, True), (3, 32, 64, 14, 1, 2, True),
+                                                   (4, 32, 64, 13, 0, 2, True), (2, 16, 32, 9, 0, 2, True),
+                                                   (3, 16, 16, 12, 1, 2, True),
+                                                   # K = 16 x 64 = 1024 (32 K-steps): the E1 model's conv2
+                                                   (4, 32, 64, 25, 0, 32, False), (4, 32, 64, 25, 0, 3, True),
+                                                   (4, 16, 64, 11, 1, 4, True), (5, 32, 40, 9, 2, 2, False)])
+def test_conv_mfma_dgrad_masks_colsum(k, C, CO, H, pad, B, masked):
     torch.manual_seed(3)
-    B = 2
     xprev = torch.relu(torch.randn(B, H, H, C, device=dev)).to(bf)  # previous layer's activation output
     w = (torch.randn(CO, k, k, C, device=dev) * 0.1).to(bf)
     g = K.conv_geom(xprev.shape, w.shape, (1, 1), (pad, pad), (1, 1))
     OH = g[4]
     y = torch.relu(torch.randn(B, OH, OH, CO, device=dev)).to(bf)
     dy = torch.randn(B, OH, OH, CO, device=dev).to(bf)
+    if not masked:  # pre-masked dY (the fused pool backward applied ReLU'): no y operand
+        dy = (dy.float() * (y.float() > 0)).to(bf)
     cs = torch.zeros(C, device=dev)
-    dx = K.conv2d_dgrad(dy, w, g, yprev=xprev, act_prev="relu", colsum=cs, y=y, act="relu")
+    dx = K.conv2d_dgrad(dy, w, g, yprev=xprev, act_prev="relu", colsum=cs, y=y if masked else None,
+                        act="relu" if masked else 0)
     xr = xprev.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
     out = F.conv2d(xr, w.float().permute(0, 3, 1, 2), padding=pad)
     out.backward((dy.float() * (y.float() > 0)).permute(0, 3, 1, 2))
