@@ -260,10 +260,10 @@ HX_PYMOD(HOPSX_MODNAME) {
   });
   m.def("head_ce_ok", [](int C, int KD) { return hopsx_head_ce_ok(C, KD); });
   m.def("head_ce", [](int kind, u logits, int lf32, u target, int B, int C, int KD, float gs, u h, u w, u dw, u db,
-                      u dh, u loss, u correct, u bias, u lout, u st) {
+                      u dh, u loss, u correct, u bias, u lout, float dp, u drng, unsigned dsalt, u st) {
     return hopsx_head_ce(kind, P<void>(logits), lf32, P<void>(target), B, C, KD, gs, P<void>(h), P<void>(w),
                          P<float>(dw), P<float>(db), P<void>(dh), P<float>(loss), P<int>(correct), P<float>(bias),
-                         P<void>(lout), S(st));
+                         P<void>(lout), dp, P<unsigned long long>(drng), dsalt, S(st));
   });
   m.def("mlp_head_debug", [](u p) { hopsx_mlp_head_debug(P<void>(p)); });
   // upload an instantiated hipGraph's executable to the device now (capture time) instead of at its

@@ -276,7 +276,8 @@ __device__ inline void head_ce_body(int kind, const void* __restrict__ logits, i
                                     float* __restrict__ dw, float* __restrict__ db, bf16_raw* __restrict__ dh,
                                     float* __restrict__ loss_sum, int* __restrict__ correct, int vec,
                                     const float* __restrict__ bias, void* __restrict__ lout, int bx, int by, int gx,
-                                    int gy) {
+                                    int gy, float dp = 0.f, const unsigned long long* __restrict__ drng = nullptr,
+                                    unsigned dsalt = 0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char head_smem[];
   bf16_raw* sh = (bf16_raw*)head_smem;
   bf16_raw* sw = sh + HEAD_ROWS * KD;
@@ -297,6 +298,17 @@ __device__ inline void head_ce_body(int kind, const void* __restrict__ logits, i
     if (h)
       for (int i = threadIdx.x; i < nr * KD; i += blockDim.x) sh[i] = h[(long)r0 * KD + i];
     for (int i = threadIdx.x; i < C * KD; i += blockDim.x) sw[i] = w[i];
+  }
+  // dp > 0: a Dropout between the previous layer and this head, folded in: h is the dropout's INPUT, the
+  // staged tile gets dropout_k's mask and rounding, and the input gradient below the same mask (so dh is
+  // the gradient of the dropout's input): neither dropout launch remains
+  const uint64_t dkey = dp > 0.f ? drop_key(drng, dsalt) : 0;
+  const float dscale = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
+  if (dp > 0.f && h) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nr * KD; i += blockDim.x)
+      sh[i] = f2bf(bf2f(sh[i]) * (uniform01(dkey, (uint64_t)((long)r0 * KD + i)) >= dp ? dscale : 0.f));
+    __syncthreads();
   }
   if (lout) {
     // forward mode: the head layer's own GEMM (logits = h W^T + b) runs here from the staged
@@ -433,7 +445,10 @@ __device__ inline void head_ce_body(int kind, const void* __restrict__ logits, i
       }
     }
     for (; n < C; ++n) s0 = fmaf(sdl[r * C + n], bf2f(sw[n * KD + k]), s0);
-    dh[(long)(r0 + r) * KD + k] = f2bf(s0 + s1);
+    float v = s0 + s1;
+    if (dp > 0.f)  // (the unfused chain: bf16 dX, then dropout_k on it)
+      v = bf2f(f2bf(v)) * (uniform01(dkey, (uint64_t)((long)(r0 + r) * KD + k)) >= dp ? dscale : 0.f);
+    dh[(long)(r0 + r) * KD + k] = f2bf(v);
   }
 }
 
@@ -443,9 +458,10 @@ __global__ __launch_bounds__(1024) void head_ce_k(int kind, const void* __restri
                                                  float* __restrict__ dw, float* __restrict__ db,
                                                  bf16_raw* __restrict__ dh, float* __restrict__ loss_sum,
                                                  int* __restrict__ correct, int vec, const float* __restrict__ bias,
-                                                 void* __restrict__ lout) {
+                                                 void* __restrict__ lout, float dp,
+                                                 const unsigned long long* __restrict__ drng, unsigned dsalt) {
   head_ce_body(kind, logits, lf32, target, B, C, KD, gs, h, w, dw, db, dh, loss_sum, correct, vec, bias, lout,
-               blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
+               blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, dp, drng, dsalt);
 }
 
 static size_t head_lds_bytes(int C, int KD) {
@@ -456,8 +472,10 @@ bool hopsx_head_ce_ok(int C, int KD) { return C >= 1 && C <= HEAD_CMAX && KD >= 
 
 extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
                              float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh,
-                             float* loss_sum, int* correct, const float* bias, void* logits_out, hipStream_t st) {
+                             float* loss_sum, int* correct, const float* bias, void* logits_out, float drop_p,
+                             const unsigned long long* drop_rng, unsigned drop_salt, hipStream_t st) {
   if (!hopsx_head_ce_ok(C, KD) || B < 1) return -2;
+  if (drop_p > 0.f && (!drop_rng || !h || drop_p >= 1.f)) return -3;
   const int grid = (B + HEAD_ROWS - 1) / HEAD_ROWS;
   // column blocks of >= 32 columns so a small batch still spreads over several CUs
   int gy = KD / 32;
@@ -471,7 +489,7 @@ extern "C" int hopsx_head_ce(int kind, const void* logits, int logits_f32, const
   const int vec = KD % 8 == 0 && ((uintptr_t)h % 16 == 0) && ((uintptr_t)w % 16 == 0);
   hipLaunchKernelGGL(head_ce_k, dim3(grid, gy), dim3(1024), head_lds_bytes(C, KD), st, kind, logits, logits_f32, target, B, C,
                      KD, grad_scale, (const bf16_raw*)h, (const bf16_raw*)w, dw, db, (bf16_raw*)dh, loss_sum,
-                     correct, vec, bias, logits_out);
+                     correct, vec, bias, logits_out, drop_p, drop_rng, drop_salt);
   return (int)hipGetLastError();
 }
 

@@ -53,7 +53,10 @@ int hopsx_avgpool_global_bwd(const void* dy, void* dx, int B, int HW, int C, hip
 bool hopsx_head_ce_ok(int C, int KD);
 int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* target, int B, int C, int KD,
                   float grad_scale, const void* h, const void* w, float* dw, float* db, void* dh, float* loss_sum,
-                  int* correct, const float* bias, void* logits_out, hipStream_t st);
+                  int* correct, const float* bias, void* logits_out, float drop_p,
+                  const unsigned long long* drop_rng, unsigned drop_salt, hipStream_t st);
+// (drop_p > 0: h is the input of a Dropout feeding the head, applied inside with dropout_k's mask; dh is then
+// the gradient of that input)
 // fused last hidden Dense + head (loss.hip mlp_head_k): y = act(x W1^T + b1) stored, then head_ce from
 // LDS; ws fp32 [B][N1] and arrive (kArriveWords) persistent, zero at rest.  -2: shape not supported
 int hopsx_mlp_head(const void* x, const void* w1, const float* b1, int act1, void* y, float* ws, unsigned* arrive,

@@ -453,10 +453,14 @@ class Sequential(tnn.Module):
             mods[0].raw_u8 = True
         # Conv2D -> MaxPooling2D: the pool (+ its fused dropout) runs in the conv's epilogue where the pair
         # qualifies (functional.conv2d_maxpool; the unfused chain otherwise), the pool module passes through
+        # Dropout -> Dense: the Dense applies the dropout to its input (HF.linear drop_in), which the logits
+        # layer's fused loss kernel does in-kernel (no dropout launch forward or backward)
+        dis = os.environ.get("HOPSX_DISABLE", "")
         for a, b in zip(mods, mods[1:]):
-            if isinstance(a, hnn.Conv2d) and isinstance(b, hnn.MaxPool2d) and "keras_conv_pool" not in \
-                    os.environ.get("HOPSX_DISABLE", ""):
+            if isinstance(a, hnn.Conv2d) and isinstance(b, hnn.MaxPool2d) and "keras_conv_pool" not in dis:
                 a._pool_next, b._absorbed = (b,), True
+            if isinstance(a, hnn.Dropout) and isinstance(b, hnn.Linear) and a.p > 0 and "keras_drop_in" not in dis:
+                b._drop_in, a._absorbed = (a.p, a.salt), True
         self.net = tnn.Sequential(*mods)
         self._input_shape = shape
 

@@ -55,8 +55,13 @@ class Linear(nn.Module):
         else:
             self.register_parameter("bias", None)
 
+    # (p, salt) of a Dropout right before this layer that this layer applies (keras.Sequential sets it with
+    # the Dropout module passing through): the logits layer's fused loss kernel then applies it
+    _drop_in = None
+
     def forward(self, x):
-        return HF.linear(x, self.weight, self.bias, self.activation, self.out_f32)
+        drop = self._drop_in if self.training else None
+        return HF.linear(x, self.weight, self.bias, self.activation, self.out_f32, drop_in=drop)
 
     def extra_repr(self):
         return f"{self.in_features}, {self.out_features}, act={self.activation}"
@@ -177,11 +182,12 @@ class Dropout(nn.Module):
     def __init__(self, p=0.5):
         super().__init__()
         self.p = float(p)
+        self._absorbed = False  # applied by the next Linear (its _drop_in): a pass-through here
         _salt_counter[0] += 1
         self.salt = _salt_counter[0] * 7919
 
     def forward(self, x):
-        return HF.dropout(x, self.p, self.training, self.salt)
+        return x if self._absorbed else HF.dropout(x, self.p, self.training, self.salt)
 
 
 class Flatten(nn.Module):

@@ -207,9 +207,16 @@ class _LinearFn(torch.autograd.Function):
         return dx, _ret_grad(w, gw), (_ret_grad(b, gb) if b is not None else None), None, None, None
 
 
-def linear(x, w, b=None, act=None, out_f32=False):
-    """y = act(x @ w.T + b); w is [out, in] (fp32 master; bf16 shadow used on GPU)."""
+def linear(x, w, b=None, act=None, out_f32=False, drop_in=None):
+    """y = act(x @ w.T + b); w is [out, in] (fp32 master; bf16 shadow used on GPU).  ``drop_in`` = (p, salt):
+    a training-mode Dropout applied to ``x`` first (keras.Sequential hands a Dense -> Dropout -> logits Dense
+    chain's dropout to the logits layer): when this layer's forward is deferred to the fused loss kernel,
+    the kernel applies it (loss.hip head_ce_k dp), so neither dropout launch runs."""
+    if drop_in is not None and drop_in[0] <= 0:
+        drop_in = None
     if not x.is_cuda:
+        if drop_in is not None:
+            x = F.dropout(x.float(), drop_in[0], True)
         return _cpu_act(F.linear(x.float(), w, b), act)
     a = ACT[act] if not isinstance(act, int) else act
     xc = to_compute(x)
@@ -218,12 +225,17 @@ def linear(x, w, b=None, act=None, out_f32=False):
     head = (not a and x.dim() == 2 and w.shape[0] <= 32 and xc.dtype == BF16 and torch.is_grad_enabled()
             and w.requires_grad and _arena.grad_target(w) is not None
             and (b is None or _arena.grad_target(b) is not None))
-    if head and HEAD["defer"] and "head_fwd" not in _disabled() and K.head_ce_ok(w.shape[0], x.shape[1]):
+    if head and HEAD["defer"] and "head_fwd" not in _disabled() and K.head_ce_ok(w.shape[0], x.shape[1]) and (
+            drop_in is None or "head_drop" not in _disabled()):
         # deferred logits layer (TrainStep verified that these logits are the model's output and
         # only feed the loss): no forward launch — the loss kernel computes and stores the logits
+        # (and applies the dropout on its input, drop_in)
         y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=F32 if out_f32 else BF16)
-        y._hx_dense_head = (xc, w, b, out_f32, True)
+        drop = (float(drop_in[0]), rng_state(x.device), int(drop_in[1])) if drop_in is not None else None
+        y._hx_dense_head = (xc, w, b, out_f32, True, drop)
         return y
+    if drop_in is not None:
+        xc = dropout(xc, float(drop_in[0]), True, int(drop_in[1]))
     if PREHEAD["pending"] and xc.data_ptr() in PREHEAD["pending"]:
         flush_pending()  # a deferred pre-head output read by anything but the deferred head
     pre = (HEAD["defer"] and PREHEAD["w"] is w and not head and a in (0, 1) and xc.dim() == 2 and xc.dtype == BF16
@@ -1216,6 +1228,7 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
     kernel and the head's two backward GEMMs collapse into one launch."""
     head = getattr(logits, "_hx_dense_head", None)
     k = LOSS[kind]
+    drop = head[5] if head is not None and len(head) > 5 else None
     pend = PREHEAD["pending"].pop(head[0].data_ptr(), None) if (head is not None and head[4]) else None
     flush_pending()  # deferred outputs other than the head's input
     if (head is None or not logits.is_cuda or logits.dim() != 2 or "head_ce" in _disabled()
@@ -1223,12 +1236,17 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
         if pend is not None:
             K.linear_fwd(pend[0], pend[1], pend[2], act=pend[3], out=pend[4])
         if head is not None and head[4]:  # deferred logits the fused kernel cannot take: compute them now
-            real = _LinearFn.apply(head[0], head[1], head[2], 0, head[3], None)
+            hin = dropout(head[0], drop[0], True, drop[2]) if drop is not None else head[0]
+            real = _LinearFn.apply(hin, head[1], head[2], 0, head[3], None)
             logits.copy_(real.detach())
             logits = real
         loss_, correct, count, dl = loss_and_grad(logits, target, kind)
         return loss_, correct, count, logits, dl
-    h, w, b, _, deferred = head
+    h, w, b, _, deferred = head[:5]
+    if drop is not None and pend is not None:
+        # (the fused Dense -> head kernel has no dropout between the two: the Dense runs on its own)
+        K.linear_fwd(pend[0], pend[1], pend[2], act=pend[3], out=pend[4])
+        pend = None
     B, C = logits.shape
     cnt = B * (C if k in (2, 3, 4) else 1)
     if k in (2, 3, 4) and target.dim() == 1:
@@ -1251,7 +1269,7 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
     dh = K.head_ce(k, logits if deferred else logits.detach().contiguous(), target, h.detach(),
                    _arena.weight_bf16(w), _arena.grad_target(w), _arena.grad_target(b) if b is not None else None,
                    1.0 / cnt, loss_sum, correct, bias=b.detach() if (deferred and b is not None) else None,
-                   forward=deferred)
+                   forward=deferred, drop=drop)
     hooks.grad_ready(w)
     if b is not None:
         hooks.grad_ready(b)

@@ -881,11 +881,13 @@ def head_ce_ok(C: int, KD: int) -> bool:
 
 
 def head_ce(kind: int, logits, target, h, w, dw, db, grad_scale: float, loss_sum, correct, bias=None,
-            forward: bool = False):
+            forward: bool = False, drop=None):
     """Loss + dlogits (never materialised) + dW += dl^T h + db += sum dl + returns dh = dl W, in one
     launch (loss.hip head_ce_k).  logits [B, C<=32] fp32/bf16, h [B, KD] bf16, w [C, KD] bf16.
     ``forward``: the layer's forward runs in the same launch — logits = h W^T + bias are computed
-    from the staged operands and WRITTEN into ``logits`` (which is only an output then)."""
+    from the staged operands and WRITTEN into ``logits`` (which is only an output then).
+    ``drop`` = (p, rng, salt): ``h`` is the input of a Dropout feeding the head; the head applies it
+    (dropout_k's mask and rounding) and dh is the gradient of that input."""
     B, C = logits.shape
     KD = h.shape[1]
     _req(h, BF16, "h")
@@ -894,6 +896,7 @@ def head_ce(kind: int, logits, target, h, w, dw, db, grad_scale: float, loss_sum
     dh = torch.empty(B, KD, device=h.device, dtype=BF16)
     check(_C.ext().head_ce(kind, ptr(logits), int(logits.dtype == F32), ptr(target), B, C, KD, float(grad_scale),
                            ptr(h), ptr(w), ptr(dw), ptr(db), ptr(dh), ptr(loss_sum), ptr(correct), ptr(bias),
-                           ptr(logits) if forward else 0, stream()),
+                           ptr(logits) if forward else 0, float(drop[0]) if drop else 0.0,
+                           ptr(drop[1]) if drop else 0, (int(drop[2]) & 0xFFFFFFFF) if drop else 0, stream()),
           "head_ce")
     return dh

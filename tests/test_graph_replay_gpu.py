@@ -11,6 +11,7 @@ if not torch.cuda.is_available():  # pragma: no cover
 
 from hops_examples_amd.models.mnist import MirroredMnistCNN  # noqa: E402
 from hops_examples_amd.ops import functional as HF  # noqa: E402
+from hops_examples_amd.ops import kernels as K  # noqa: E402
 from hops_examples_amd.runtime.arena import ParamArena  # noqa: E402
 
 
@@ -169,3 +170,59 @@ def test_steps_per_execution_matches_single_step_replays():
     assert d <= max(3 * noise + 0.05, 0.12), (d, noise)
     cos = float(torch.nn.functional.cosine_similarity(runs[0][1], runs[1][1], dim=0))
     assert cos >= 0.99, cos
+
+
+def _e1_modules(fold: bool):
+    """The E1 MNIST CNN (mnist.ipynb:154-164) as keras.Sequential wires it: conv2 -> 4x4 pool (+dropout)
+    in one launch, and with ``fold`` the Dense -> Dropout -> logits chain's dropout handed to the logits
+    layer (Linear._drop_in), which the deferred head's loss kernel applies."""
+    from hops_examples_amd import nn as hnn
+
+    c1 = hnn.Conv2d(1, 32, 4, activation="relu")
+    c1.in_affine = (1.0 / 255.0, 0.0)
+    c2 = hnn.Conv2d(32, 64, 4, activation="relu")
+    pool = hnn.MaxPool2d(4, dropout=0.5)
+    c2._pool_next, pool._absorbed = (pool,), True
+    d1, drop, d2 = hnn.Linear(1600, 128, activation="relu"), hnn.Dropout(0.5), hnn.Linear(128, 10)
+    pool.salt, drop.salt = 7919, 3 * 7919
+    if fold:
+        d2._drop_in, drop._absorbed = (drop.p, drop.salt), True
+    return torch.nn.Sequential(c1, c2, pool, hnn.Flatten(), d1, drop, d2)
+
+
+def test_dropout_folded_into_deferred_head_matches_unfolded(monkeypatch):
+    """E1: the Dropout between the last hidden Dense and the logits layer applied inside the fused loss
+    kernel (head_ce_k dp: mask on the staged input, the same mask on the input gradient) trains like the
+    separate dropout launches — losses and weights after 8 TrainStep steps (eager warm-up + graph replays),
+    with no dropout launch left."""
+    from hops_examples_amd import optim
+    from hops_examples_amd.runtime.step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    B = 32
+    xs = torch.randint(0, 256, (8, B, 28, 28, 1), dtype=torch.uint8, device=dev)
+    ys = torch.randint(0, 10, (8, B), device=dev)
+    runs = []
+    for fold in (True, False):
+        HF.seed_device_rng(5, dev)
+        torch.manual_seed(0)
+        m = _e1_modules(fold).to(dev)
+        ParamArena.from_module(m, dev)
+        calls = {"drop": 0, "head": []}
+        real_d, real_h = K.dropout, K.head_ce
+        monkeypatch.setattr(K, "dropout", lambda *a, **kw: calls.__setitem__("drop", calls["drop"] + 1) or real_d(*a, **kw))
+        monkeypatch.setattr(K, "head_ce", lambda *a, **kw: calls["head"].append(kw.get("drop")) or real_h(*a, **kw))
+        st = TrainStep(m, optim.Adam(m, lr=1e-3), "sparse_ce")
+        ls = [float(st(xs[i], ys[i])["loss"].reshape(-1)[0]) for i in range(8)]
+        monkeypatch.setattr(K, "dropout", real_d)
+        monkeypatch.setattr(K, "head_ce", real_h)
+        assert st._head_defer
+        if fold:
+            assert calls["drop"] == 0, calls
+            assert calls["head"] and all(d is not None and d[0] == 0.5 for d in calls["head"]), calls["head"]
+        else:
+            assert calls["drop"] > 0 and all(d is None for d in calls["head"])
+        runs.append((ls, m._hx_arena.master.float().clone()))
+    assert abs(runs[0][0][0] - runs[1][0][0]) <= 1e-3 * abs(runs[1][0][0]) + 1e-4
+    torch.testing.assert_close(torch.tensor(runs[0][0]), torch.tensor(runs[1][0]), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(runs[0][1], runs[1][1], rtol=1e-2, atol=5e-3)
