@@ -459,8 +459,9 @@ class Sequential(tnn.Module):
         for a, b in zip(mods, mods[1:]):
             if isinstance(a, hnn.Conv2d) and isinstance(b, hnn.MaxPool2d) and "keras_conv_pool" not in dis:
                 a._pool_next, b._absorbed = (b,), True
-            if isinstance(a, hnn.Dropout) and isinstance(b, hnn.Linear) and a.p > 0 and "keras_drop_in" not in dis:
-                b._drop_in, a._absorbed = (a.p, a.salt), True
+            lin = b[0] if isinstance(b, tnn.Sequential) and len(b) and isinstance(b[0], hnn.Linear) else b
+            if isinstance(a, hnn.Dropout) and isinstance(lin, hnn.Linear) and a.p > 0 and "keras_drop_in" not in dis:
+                lin._drop_in, a._absorbed = (a.p, a.salt), True  # (Dense(softmax) is Sequential(Linear, softmax))
         self.net = tnn.Sequential(*mods)
         self._input_shape = shape
 

@@ -218,8 +218,11 @@ def test_dropout_folded_into_deferred_head_matches_unfolded(monkeypatch):
         monkeypatch.setattr(K, "head_ce", real_h)
         assert st._head_defer
         if fold:
-            assert calls["drop"] == 0, calls
-            assert calls["head"] and all(d is not None and d[0] == 0.5 for d in calls["head"]), calls["head"]
+            # (the first, probing step runs the head undeferred: its dropout is the separate kernel, fwd + bwd)
+            undeferred = sum(d is None for d in calls["head"])
+            assert calls["drop"] == 2 * undeferred and undeferred <= 1, calls
+            assert calls["head"] and all(d[0] == 0.5 for d in calls["head"] if d is not None), calls["head"]
+            assert calls["head"][-1] is not None
         else:
             assert calls["drop"] > 0 and all(d is None for d in calls["head"])
         runs.append((ls, m._hx_arena.master.float().clone()))
