@@ -275,6 +275,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_smallk_k(const bf16_raw* __res
 //     its group's rows in row order, the last group sums the group rows in order and adds dW / db —
 //     deterministic (fixed summation order) and ~2 L2 round trips instead of one per 16 rows.
 constexpr int C1_GROUP = 16;
+// the combine's partial rows cross workgroups (and XCDs, each with its own L2) inside one launch: written
+// write-through (sc1) and read with sc1 loads, after a vmcnt drain and a relaxed ticket, so neither an
+// agent-scope release (an L2 write-back) nor an acquire (an L2 invalidate) is needed per level
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t c1_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void c1_st(__amdgpu_buffer_rsrc_t r, long e, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(e * 4), 0, 16);
+}
+__device__ __forceinline__ float c1_ld(__amdgpu_buffer_rsrc_t r, long e) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(e * 4), 0, 16));
+}
+
 __global__ __launch_bounds__(256) void conv_wgrad_c1_k(const bf16_raw* __restrict__ dy, const void* __restrict__ x,
                                                       float xscale, float xshift, float* __restrict__ dw,
                                                       float* __restrict__ dbias, const bf16_raw* __restrict__ y,
@@ -361,58 +374,52 @@ __global__ __launch_bounds__(256) void conv_wgrad_c1_k(const bf16_raw* __restric
   }
   RD[(pl * CO + co) * (K + 1) + K] = acc[KMAX];
   __syncthreads();
+  // rows padded to whole 128-B lines: a line is only ever written by one workgroup, so no reader's L2 can
+  // hold a copy of it filled before that write
+  const int NEP = (NE + 31) & ~31;
+  const auto SR = c1_rsrc(slab);
   for (int e = threadIdx.x; e < NE; e += 256) {
     float t = 0.f;
     for (int q = 0; q < PL; ++q) t += RD[q * NE + e];  // pixel-lane order: deterministic
-    slab[(long)blockIdx.x * NE + e] = t;
+    c1_st(SR, (long)blockIdx.x * NEP + e, t);
   }
   if (stop == 2) return;
   // ---- level 1: the last workgroup of this group of 16 sums the group's rows (row order)
   const int ngrp = (gridDim.x + C1_GROUP - 1) / C1_GROUP, grp = blockIdx.x / C1_GROUP;
   const int g0 = grp * C1_GROUP, g1 = min((int)gridDim.x, g0 + C1_GROUP);
-  float* slab2 = slab + (long)gridDim.x * NE;  // [ngrp][NE]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const long s2 = (long)gridDim.x * NEP;  // slab2 = slab + s2: [ngrp][NEP]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's rows written through
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(counter + 1 + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == (unsigned)(g1 - g0 - 1);
   }
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    counter[1 + grp] = 0u;  // re-armed for the next launch
-  }
-  __syncthreads();
+  if (threadIdx.x == 0) counter[1 + grp] = 0u;  // re-armed for the next launch
   for (int e = threadIdx.x; e < NE; e += 256) {
     float v[C1_GROUP];
 #pragma unroll
-    for (int q = 0; q < C1_GROUP; ++q) v[q] = g0 + q < g1 ? slab[(long)(g0 + q) * NE + e] : 0.f;
+    for (int q = 0; q < C1_GROUP; ++q) v[q] = g0 + q < g1 ? c1_ld(SR, (long)(g0 + q) * NEP + e) : 0.f;
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < C1_GROUP; ++q) t += v[q];
-    slab2[(long)grp * NE + e] = t;
+    c1_st(SR, s2 + (long)grp * NEP + e, t);
   }
   // ---- level 2: the last group sums the group rows (group order) into dW / db
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == (unsigned)(ngrp - 1);
   }
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    counter[0] = 0u;
-  }
-  __syncthreads();
+  if (threadIdx.x == 0) counter[0] = 0u;
   for (int e = threadIdx.x; e < NE; e += 256) {
     float v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = q < ngrp ? slab2[(long)q * NE + e] : 0.f;  // (ngrp <= 14)
+    for (int q = 0; q < 16; ++q) v[q] = q < ngrp ? c1_ld(SR, s2 + (long)q * NEP + e) : 0.f;  // (ngrp <= 14)
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) t += v[q];
@@ -749,7 +756,7 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
   // one-channel input layers: the pixel-range kernel (conv_wgrad_c1_k)
   if (g.C == 1 && N <= 25 && (g.CO == 8 || g.CO == 16 || g.CO == 32 || g.CO == 64) && (uintptr_t)dy % 16 == 0 &&
       (uintptr_t)y % 16 == 0 && counter && ws && !hopsx_disabled("c1_wgrad")) {
-    const int NE = g.CO * (N + 1);
+    const int NE = g.CO * (N + 1), NEP = (NE + 31) & ~31;  // rows padded to 128-B lines
     // <= 224 workgroups + their <= 14 group rows fit the caller's 256-row slab (kernels.conv2d_wgrad)
     int nwg = (K + 63) / 64;
     if (nwg > 224) nwg = 224;
@@ -760,7 +767,7 @@ extern "C" int hopsx_conv2d_wgrad(const void* dy, const void* x, const int* geom
     const size_t lds_red = (size_t)256 * (N + 1) * sizeof(float);  // the pixel-lane reduction [PL][CO][K+1]
     if (lds < lds_red) lds = lds_red;
     // (the staging loops' per-thread item counts are compile-time: 8 dY vectors, 20 taps)
-    if (ws_elems >= (long)(nwg + ngrp) * NE && lds <= 64 * 1024 && (long)ppw * (g.CO / 8) <= 8 * 256 &&
+    if (ws_elems >= (long)(nwg + ngrp) * NEP && lds <= 64 * 1024 && (long)ppw * (g.CO / 8) <= 8 * 256 &&
         (long)ppw * N <= 20 * 256) {
       static bool attr = false;
       if (!attr) {

@@ -403,7 +403,9 @@ def conv2d_wgrad(dy, x, geom, dw, dbias=None, y=None, act=0, in_affine=None):
     ws = None
     smallk = _c1_wgrad(geom) or _smallk_wgrad(geom)
     if smallk:  # per-workgroup partial rows (<= 256: workgroups + group rows), combined in-launch
-        ws = torch.empty((256 if _c1_wgrad(geom) else 128) * geom[6] * (K + 1), device=dy.device, dtype=F32)
+        # (c1: rows padded to 128-B lines)
+        row = (geom[6] * (K + 1) + 31) // 32 * 32 if _c1_wgrad(geom) else geom[6] * (K + 1)
+        ws = torch.empty((256 if _c1_wgrad(geom) else 128) * row, device=dy.device, dtype=F32)
     elif K <= 64 and KC <= 1024:  # older direct kernel: slab workspace
         ws = torch.empty(1024 * (KC + geom[6]), device=dy.device, dtype=F32)
     sc, sh = (float(in_affine[0]), float(in_affine[1])) if in_affine else (0.0, 0.0)

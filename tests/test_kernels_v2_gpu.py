@@ -49,31 +49,32 @@ def test_smallk_wgrad(k, C, CO, B, H, masked):
 @pytest.mark.parametrize("k,CO,B,stride,pad", [(4, 32, 32, 1, 0), (5, 16, 8, 1, 2), (3, 64, 4, 2, 1), (2, 8, 9, 1, 0)])
 def test_c1_wgrad_pixel_range_kernel(k, CO, B, stride, pad, monkeypatch):
     """conv_wgrad_c1_k (one-channel input layers: the E1 model's 4x4 conv at batch 32 first) against the fp32
-    reference, bit-identical across runs (two-level ordered combine: a one-atomic-per-workgroup combine measured
-    36.4 vs 32.0 us on the E1 fit, 224 workgroups into 544 addresses)."""
+    reference for three different inputs in a row (the in-launch combine hands rows between workgroups and
+    XCDs through write-through stores: stale rows would show as a wrong sum), and bit-identical when an input
+    is repeated (two-level ordered combine; a one-atomic-per-workgroup combine measured 36.4 vs 32.0 us)."""
     torch.manual_seed(7)
     H = 28
-    xu = torch.randint(0, 256, (B, H, H, 1), dtype=torch.uint8, device=dev)
     sc, sh = 1 / 255.0, -0.5
-    g = K.conv_geom(xu.shape, (CO, k, k, 1), (stride, stride), (pad, pad), (1, 1))
+    g = K.conv_geom((B, H, H, 1), (CO, k, k, 1), (stride, stride), (pad, pad), (1, 1))
     OH, OW = g[4], g[5]
-    dy = torch.randn(B, OH, OW, CO, device=dev).to(bf)
-    y = torch.relu(torch.randn(B, OH, OW, CO, device=dev)).to(bf)
+    ins = [(torch.randint(0, 256, (B, H, H, 1), dtype=torch.uint8, device=dev),
+            torch.randn(B, OH, OW, CO, device=dev).to(bf), torch.relu(torch.randn(B, OH, OW, CO, device=dev)).to(bf))
+           for _ in range(3)]
     outs = []
-    for rep in range(2):
+    for xu, dy, y in ins + ins[:1]:
         dw = torch.zeros(CO, k * k, device=dev)
         db = torch.zeros(CO, device=dev)
         K.conv2d_wgrad(dy, xu, g, dw, dbias=db, y=y, act="relu", in_affine=(sc, sh))
         outs.append((dw, db))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    d = dy.float() * (y.float() > 0).float()
-    wr = torch.zeros(CO, 1, k, k, device=dev, requires_grad=True)
-    xf = (xu.float() * sc + sh).permute(0, 3, 1, 2)
-    F.conv2d(xf, wr, stride=stride, padding=pad).backward(d.permute(0, 3, 1, 2))
-    rw = wr.grad.permute(0, 2, 3, 1).reshape(CO, -1)
-    dw, db = outs[0]
-    torch.testing.assert_close(dw, rw, atol=1e-3 * rw.abs().max().item(), rtol=1e-3)
-    torch.testing.assert_close(db, d.sum((0, 1, 2)), atol=1e-3 * d.sum((0, 1, 2)).abs().max().item(), rtol=1e-3)
+    assert torch.equal(outs[0][0], outs[3][0]) and torch.equal(outs[0][1], outs[3][1])
+    for (xu, dy, y), (dw, db) in zip(ins, outs):
+        d = dy.float() * (y.float() > 0).float()
+        wr = torch.zeros(CO, 1, k, k, device=dev, requires_grad=True)
+        xf = (xu.float() * sc + sh).permute(0, 3, 1, 2)
+        F.conv2d(xf, wr, stride=stride, padding=pad).backward(d.permute(0, 3, 1, 2))
+        rw = wr.grad.permute(0, 2, 3, 1).reshape(CO, -1)
+        torch.testing.assert_close(dw, rw, atol=1e-3 * rw.abs().max().item(), rtol=1e-3)
+        torch.testing.assert_close(db, d.sum((0, 1, 2)), atol=1e-3 * d.sum((0, 1, 2)).abs().max().item(), rtol=1e-3)
 
 
 @pytest.mark.parametrize("k", [2, 3, 4])
