@@ -26,11 +26,15 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true")
+    ap.add_argument("--only", default="", help="H,C,CO,k,s of the one layer to run (profiling)")
     a = ap.parse_args()
+    only = tuple(int(v) for v in a.only.split(",")) if a.only else None
     dev = torch.device("cuda", 0)
     bf = torch.bfloat16
     tot = {}
     for (H, C, CO, k, s, n) in LAYERS:
+        if only and (H, C, CO, k, s) != only:
+            continue
         B = a.batch
         x = torch.randn(B, H, H, C, device=dev).to(bf)
         w = (torch.randn(CO, k, k, C, device=dev) * 0.05).to(bf)
