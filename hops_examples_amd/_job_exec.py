@@ -34,6 +34,16 @@ def main() -> int:
         def on_term(signum, frame):
             killed.append(True)
             proc.terminate()
+            # a program that does not exit on SIGTERM within the grace period is killed
+            import threading
+
+            def _force():
+                if proc.poll() is None:
+                    proc.kill()
+
+            t = threading.Timer(float(os.environ.get("HOPSX_JOB_KILL_GRACE", "10")), _force)
+            t.daemon = True
+            t.start()
 
         signal.signal(signal.SIGTERM, on_term)
         t0 = time.time()
