@@ -249,7 +249,7 @@ class FusedWideDeepStep:
         self._B = None
         self._v2: dict = {}
         self._zn = None
-        self._v2key, self._v2slot = None, -1  # cached v2 launch arguments (C++ slot, _launch)
+        self._v2slots = {}  # cached v2 launch arguments: key -> C++ slot (_v2_slot)
         dev = self.arena.device
         self.loss = torch.zeros(1, device=dev)
         self.correct = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -324,6 +324,41 @@ class FusedWideDeepStep:
         self.ftrl.lr = self.ftrl.param_groups[0]["lr"]
         return pad8(self.ada._hp()) + pad8(self.ftrl._hp())
 
+    def _v2_slot(self, dense, cat, label, nbatch: int, cursor, nsteps: int) -> int:
+        """The C++-side argument slot of this v2 launch shape, built once per key (the data, the step count,
+        the hyper-parameters): a run's few launch shapes (warm-up, steps_per_execution, the remainder) each
+        get their own, so no argument vector is rebuilt inside a timed loop."""
+        from ..ops import _C
+        from ..ops.functional import rng_state
+
+        a = self.arena
+        B = dense.shape[-2]
+        fl = self._floats()
+        key = (dense.data_ptr(), cat.data_ptr(), label.data_ptr(), nbatch, cursor.data_ptr(), nsteps, B,
+               tuple(fl), id(a.master), self.dbg is not None, id(self.xdp))
+        slots = self.__dict__.setdefault("_v2slots", {})
+        sid = slots.get(key)
+        if sid is not None:
+            return sid
+        ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
+        rows = int(self.model.wide.weight.shape[0])
+        if self._zn is None:
+            self._zn = torch.empty(rows, 2, device=a.device)  # the kernel's (z, n) scratch
+        # Adagrad as w -= lr g rsq(s) (one transcendental): exact to fp32 when wd == 0 and eps is
+        # below the resolution of sqrt(s), whose floor is the initial accumulator
+        floor = float(getattr(self.ada, "initial_accumulator_value", 0.0))
+        rsq = int(self.ada.weight_decay == 0 and floor > 0 and self.ada.hp["eps"] < 1e-7 * math.sqrt(floor))
+        ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")),
+                ptr(a.state("ftrl_s0")), ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label),
+                ptr(cursor), ptr(self.loss), ptr(self.correct), ptr(self.ada.step_count),
+                ptr(self.ftrl.step_count), ptr(rng_state(a.device)), ptr(self.dbg), ptr(self._zn), rsq]
+        if self.xdp is not None:
+            ptrs += self.xdp.ptrs()
+        free = slots.pop(next(iter(slots))) if len(slots) >= 8 else -1  # reuse the oldest slot id
+        sid = _C.ext().taxi_step2_store(free, ptrs, self._ints(B, nbatch, nsteps), fl, rows)
+        slots[key] = sid
+        return sid
+
     def _launch(self, dense, cat, label, nbatch: int, cursor, nsteps: int = 1):
         from ..ops import _C
         from ..ops.functional import rng_state
@@ -333,29 +368,8 @@ class FusedWideDeepStep:
         B = dense.shape[-2]
         self._B = B
         if self.v2(B):
-            fl = self._floats()
-            key = (dense.data_ptr(), cat.data_ptr(), label.data_ptr(), nbatch, cursor.data_ptr(), nsteps, B,
-                   tuple(fl), id(a.master), self.dbg is not None, id(self.xdp))
-            ext = _C.ext()
-            if self._v2key != key:
-                # the argument vectors change only with the data, the step count or the hyper-parameters
-                ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
-                rows = int(self.model.wide.weight.shape[0])
-                if self._zn is None:
-                    self._zn = torch.empty(rows, 2, device=a.device)  # the kernel's (z, n) scratch
-                # Adagrad as w -= lr g rsq(s) (one transcendental): exact to fp32 when wd == 0 and eps is
-                # below the resolution of sqrt(s), whose floor is the initial accumulator
-                floor = float(getattr(self.ada, "initial_accumulator_value", 0.0))
-                rsq = int(self.ada.weight_decay == 0 and floor > 0 and self.ada.hp["eps"] < 1e-7 * math.sqrt(floor))
-                ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")),
-                        ptr(a.state("ftrl_s0")), ptr(a.state("ftrl_s1")), ptr(dense), ptr(cat), ptr(label),
-                        ptr(cursor), ptr(self.loss), ptr(self.correct), ptr(self.ada.step_count),
-                        ptr(self.ftrl.step_count), ptr(rng_state(a.device)), ptr(self.dbg), ptr(self._zn), rsq]
-                if self.xdp is not None:
-                    ptrs += self.xdp.ptrs()
-                self._v2slot = ext.taxi_step2_store(self._v2slot, ptrs, self._ints(B, nbatch, nsteps), fl, rows)
-                self._v2key = key
-            check(ext.taxi_step2_slot(self._v2slot, stream()), "taxi_step2")
+            check(_C.ext().taxi_step2_slot(self._v2_slot(dense, cat, label, nbatch, cursor, nsteps), stream()),
+                  "taxi_step2")
             return
         ptr = lambda t: 0 if t is None else int(t.data_ptr())  # noqa: E731
         ptrs = [ptr(a.master), ptr(a.grad), ptr(a.shadow), ptr(a.state("adagrad_s0")), ptr(a.state("ftrl_s0")),
@@ -451,6 +465,11 @@ class FusedWideDeepStep:
         loop; with ``n`` also the graph of the remainder n % U (Keras steps_per_execution tail)."""
         dense, cat = xs
         U = self.steps_per_execution
+        if n and self._direct(dense) and self.v2(dense.shape[-2]):
+            # direct launches (run_resident): their argument slots for the launch shapes of n steps
+            for k in {min(int(n), U), int(n) % U} - {0}:
+                self._v2_slot(dense, cat, ys, dense.shape[0], self.cursor, k)
+            return
         if U <= 1 or not self._graphable() or self._graph is None:
             return
         key = (dense.data_ptr(), cat.data_ptr(), ys.data_ptr(), tuple(self._floats()), U)

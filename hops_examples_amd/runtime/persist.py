@@ -462,22 +462,31 @@ class PersistentMnistStep:
         opt = self.opt
         opt.sync_hp()
         hp = [float(v) for v in opt._hp()]  # lr gscale wd rho eps
-        # the argument vectors are rebuilt only when something in them changes: at bench.py's 20 steps per
-        # launch the host-side preparation is in the timed window while the GPU idles
-        pool = self.model.pool
-        key = (xs.data_ptr(), ys.data_ptr(), nb, k, float(pool.dropout) if pool.training else 0.0, int(pool.salt),
-               tuple(hp), self.acquire, self.xfence, self.timeout_ms, id(self.dbg), id(self.cursor), id(self.rng),
-               id(self.arena.master), id(self.s1), self.world, self.rank, tuple(self._xptrs))
-        ext = self._ext
-        if getattr(self, "_args_key", None) != key:
-            # converted once into a C++-side slot; a launch then passes the slot id and the stream only
-            self._slot = ext.mnist_persist_store(getattr(self, "_slot", -1), *self._build_args(xs, ys, nb, k, hp))
-            self._args_key = key
-        rc = ext.mnist_persist_slot(self._slot, _C.stream())
+        # the argument vectors are built once per launch shape (_arg_slot): at bench.py's 20 steps per launch
+        # the host-side preparation would be in the timed window while the GPU idles
+        key = self._launch_key(xs, ys, nb, k, hp)
+        rc = self._ext.mnist_persist_slot(self._arg_slot(key, xs, ys, nb, k, hp), _C.stream())
         if rc == 720:  # hipErrorCooperativeLaunchTooLarge
             raise PersistentError("mnist_persist: cooperative launch refused — the device cannot hold all "
                                   f"{self.geom['grid']} workgroups at once")
         _C.check(rc, "mnist_persist")
+
+    def _launch_key(self, xs, ys, nb: int, k: int, hp: list):
+        pool = self.model.pool
+        return (xs.data_ptr(), ys.data_ptr(), nb, k, float(pool.dropout) if pool.training else 0.0, int(pool.salt),
+                tuple(hp), self.acquire, self.xfence, self.timeout_ms, id(self.dbg), id(self.cursor), id(self.rng),
+                id(self.arena.master), id(self.s1), self.world, self.rank, tuple(self._xptrs))
+
+    def _arg_slot(self, key, xs, ys, nb: int, k: int, hp: list) -> int:
+        """The C++-side argument slot of this launch shape: built once per key (a few launch shapes per run:
+        warm-up steps, steps_per_launch, the remainder), a launch then passes the slot id and the stream."""
+        slots = self.__dict__.setdefault("_slots", {})
+        sid = slots.get(key)
+        if sid is None:
+            free = slots.pop(next(iter(slots))) if len(slots) >= 8 else -1  # reuse the oldest slot id
+            sid = self._ext.mnist_persist_store(free, *self._build_args(xs, ys, nb, k, hp))
+            slots[key] = sid
+        return sid
 
     def _build_args(self, xs, ys, nb: int, k: int, hp: list):
         opt, a, m = self.opt, self.arena, self.model
@@ -527,8 +536,16 @@ class PersistentMnistStep:
     def eager(self, x, y):
         return self(x, y)
 
-    def prepare_resident(self, xs, ys, n=None) -> None:  # TrainStep API parity: nothing to capture
-        self._check_data(xs, ys)
+    def prepare_resident(self, xs, ys, n=None) -> None:
+        """TrainStep API parity (there is no graph to capture): validates the epoch and builds the launch
+        arguments of the launch shapes ``run_resident(xs, ys, n)`` will use (``steps_per_launch`` and the
+        remainder), so none of that host work falls inside a timed run."""
+        nb = self._check_data(xs, ys)
+        if n:
+            self.opt.sync_hp()
+            hp = [float(v) for v in self.opt._hp()]
+            for k in {min(int(n), self.spl), int(n) % self.spl} - {0}:
+                self._arg_slot(self._launch_key(xs, ys, nb, k, hp), xs, ys, nb, k, hp)
 
     def losses(self, k: int) -> torch.Tensor:
         """[k, 2] (mean loss, correct) of the last launch's first k steps."""

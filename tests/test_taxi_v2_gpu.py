@@ -121,7 +121,8 @@ def test_taxi_v2_multi_step_launch_matches_single_launches():
             fs.step_resident(xs, ys)  # one step (captures the one-step graph), then ONE 15-step launch
             fs.prepare_resident(xs, ys, n - 1)
             fs.run_resident(xs, ys, n - 1)
-            assert fs._graphU is not None
+            # direct launches: prepare_resident built the launch-argument slot; graph replays: the U-step graph
+            assert len(fs._v2slots) >= 2 if fs._direct(xs[0]) else fs._graphU is not None
         else:
             for _ in range(n):
                 fs.step_resident(xs, ys)
