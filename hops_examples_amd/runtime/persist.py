@@ -463,9 +463,18 @@ class PersistentMnistStep:
         opt.sync_hp()
         hp = [float(v) for v in opt._hp()]  # lr gscale wd rho eps
         # the argument vectors are built once per launch shape (_arg_slot): at bench.py's 20 steps per launch
-        # the host-side preparation would be in the timed window while the GPU idles
-        key = self._launch_key(xs, ys, nb, k, hp)
-        rc = self._ext.mnist_persist_slot(self._arg_slot(key, xs, ys, nb, k, hp), _C.stream())
+        # the host-side preparation would be in the timed window while the GPU idles.  The launch before
+        # this one with the same epoch tensors, step count, hyper-parameters and dropout state reuses its
+        # slot without rebuilding the key (the host issue cost is in the timed window too)
+        pool = self.model.pool
+        fast = (xs, ys, xs.data_ptr(), k, hp, pool.training, pool.dropout)
+        last = getattr(self, "_last_launch", None)
+        if last is not None and last[0] is xs and last[1] is ys and last[2:-1] == fast[2:]:
+            sid = last[-1]
+        else:
+            sid = self._arg_slot(self._launch_key(xs, ys, nb, k, hp), xs, ys, nb, k, hp)
+            self._last_launch = fast + (sid,)
+        rc = self._ext.mnist_persist_slot(sid, _C.stream())
         if rc == 720:  # hipErrorCooperativeLaunchTooLarge
             raise PersistentError("mnist_persist: cooperative launch refused — the device cannot hold all "
                                   f"{self.geom['grid']} workgroups at once")
@@ -483,7 +492,10 @@ class PersistentMnistStep:
         slots = self.__dict__.setdefault("_slots", {})
         sid = slots.get(key)
         if sid is None:
-            free = slots.pop(next(iter(slots))) if len(slots) >= 8 else -1  # reuse the oldest slot id
+            free = -1
+            if len(slots) >= 8:  # reuse the oldest slot id (and forget the launch fast path, which may hold it)
+                free = slots.pop(next(iter(slots)))
+                self._last_launch = None
             sid = self._ext.mnist_persist_store(free, *self._build_args(xs, ys, nb, k, hp))
             slots[key] = sid
         return sid
