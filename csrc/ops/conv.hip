@@ -510,7 +510,9 @@ static bool gg_1x1(const ConvGeom& g) {
 // at B=256 there (profiles/r3s7_conv_gemm_vs_torch.txt); gg keeps every wider shape
 static bool gg_narrow(const ConvGeom& g, int N) {
   static const int min_n = (int)hopsx_env_int("HOPSX_GG_MIN_N", 65);
-  return !(g.KH == 1 && g.KW == 1) && N < min_n;
+  // (64 output columns: the 256x64 tile, gg_plan cfg 3)
+  static const bool n64 = !hopsx_disabled("gg_n64");
+  return !(g.KH == 1 && g.KW == 1) && N < min_n && !(N == 64 && n64);
 }
 
 template <class EP>

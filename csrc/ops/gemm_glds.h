@@ -342,18 +342,22 @@ struct EpiDgradScatterBF16 {
 // ---------------------------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool BKC = true>
 struct GgCfg {
   static constexpr int BK = 64;
+  // B rows held in LDS: a 64-column RC (n-contiguous) operand still loads a whole 128-column sub-image (its
+  // upper half is masked to the zero page, n >= N), so the RC DMA roles and swizzle stay those of 128
+  static constexpr int BL = (BKC || BN >= 128) ? BN : 128;
   // 8 waves with 64-row wave tiles: 256x128 -> 4 x 2 waves of 64x64, 128x256 -> 2 x 4 of 64x64,
   // 128x128 -> 2 x 4 of 64x32
   static constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
   static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
-  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BL * BK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int LDS = S * STAGE;
-  static_assert(BM % 128 == 0 && BN % 128 == 0, "tiles are multiples of 128");
+  // (BN = 64: the narrow-N tile, 256x64 -> 4 x 2 waves of 64x32)
+  static_assert(BM % 128 == 0 && (BN % 128 == 0 || BN == 64), "tiles are multiples of 128 (or 64 columns)");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -481,9 +485,9 @@ struct GgReader {
 template <int BM, int BN, int S, bool A_KC, bool B_KC, class AS, class BS, class EP>
 __global__ __launch_bounds__(512) void gg_kernel(const AS as, const BS bs, const EP ep, int M, int N, int K, int kps,
                                                  int tiles_n, int tiles, int diag) {
-  using C = GgCfg<BM, BN, S>;
-  constexpr int BK = C::BK, FM = C::FM, FN = C::FN;
-  constexpr int G = gg_dma_per_wave<A_KC>(BM) + gg_dma_per_wave<B_KC>(BN);
+  using C = GgCfg<BM, BN, S, B_KC>;
+  constexpr int BK = C::BK, FM = C::FM, FN = C::FN, BL = C::BL;
+  constexpr int G = gg_dma_per_wave<A_KC>(BM) + gg_dma_per_wave<B_KC>(BL);
   __shared__ __attribute__((aligned(1024))) unsigned char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
@@ -497,9 +501,9 @@ __global__ __launch_bounds__(512) void gg_kernel(const AS as, const BS bs, const
   const int nt = (kend - kbeg + BK - 1) / BK;
 
   constexpr int GA = GgLanes<A_KC, BM>::N;
-  GgSlot sa[GA], sb[GgLanes<B_KC, BN>::N];
+  GgSlot sa[GA], sb[GgLanes<B_KC, BL>::N];
   gg_slots<A_KC, BM>(as, sa, m0, kbeg, kend, wave, lane);
-  gg_slots<B_KC, BN>(bs, sb, n0, kbeg, kend, wave, lane);
+  gg_slots<B_KC, BL>(bs, sb, n0, kbeg, kend, wave, lane);
   // DMA q (0 .. G-1) of the stage of k-step ks into ring slot ks % S.  Stages past the last k-step
   // are issued too: every lane is then masked to the zero page (dk >= rem), so they only write
   // zeros into a slot nobody reads, and the loop needs no branch and a constant vmcnt.
@@ -740,12 +744,12 @@ __global__ __launch_bounds__(512) void gg_kernel(const AS as, const BS bs, const
 // is too small to fill the chip with these tiles — the caller keeps gemm_core.h's engine.
 // ---------------------------------------------------------------------------------------------
 struct GgPlan {
-  int cfg;  // 0: 256x128, 1: 128x256, 2: 128x128
+  int cfg;  // 0: 256x128, 1: 128x256, 2: 128x128, 3: 256x64 (N <= 64, both operands k-contiguous)
   int split, kps, tiles_n, tiles;
 };
 
 inline bool gg_plan(long M, long N, long K, bool allow_split, GgPlan& p, long min_wg_override = -1,
-                    int num_cu = 256) {
+                    int num_cu = 256, bool narrow_ok = false) {
   static const long force = hopsx_env_int("HOPSX_GG_CFG", -1);
   // 64: the stage-4 ResNet-50 shapes (7x7, 100 tiles of 128x128) run 1.5-2.2x faster on gg than on
   // gemm_core.h even at 0.4 workgroups per CU (profiles/r4_gg_min_wg_ab.txt); 32 (round 5): the B=8
@@ -758,6 +762,10 @@ inline bool gg_plan(long M, long N, long K, bool allow_split, GgPlan& p, long mi
   const long t0 = ntiles(256, 128), t1 = ntiles(128, 256), t2 = ntiles(128, 128);
   if (force >= 0 && force <= 2) {
     p.cfg = (int)force;
+  } else if (narrow_ok && N <= 64 && (allow_split || ntiles(256, 64) >= num_cu)) {
+    // a 64-column output (the stage-1 3x3 convs of ResNet-50, their weight gradients' 64 output channels):
+    // a 128-wide tile would waste half its MFMAs
+    p.cfg = 3;
   } else if (allow_split) {
     // split-K GEMMs get their parallelism from K: the biggest tile the output shape allows
     p.cfg = (M >= 256 && M >= N) ? 0 : (N >= 256 ? 1 : 2);
@@ -767,7 +775,7 @@ inline bool gg_plan(long M, long N, long K, bool allow_split, GgPlan& p, long mi
     else if (N >= 256 && t1 >= num_cu) p.cfg = 1;
     else p.cfg = 2;
   }
-  const int bm = p.cfg == 0 ? 256 : 128, bn = p.cfg == 1 ? 256 : 128;
+  const int bm = p.cfg == 0 || p.cfg == 3 ? 256 : 128, bn = p.cfg == 1 ? 256 : (p.cfg == 3 ? 64 : 128);
   p.tiles_n = (int)((N + bn - 1) / bn);
   p.tiles = (int)((M + bm - 1) / bm) * p.tiles_n;
   long s = 1;
@@ -796,7 +804,8 @@ inline bool launch_gg(const AS& as, const BS& bs, const EP& ep, int M, int N, in
   // deterministic mode keeps gemm_core.h's engine (one K slice per tile, turn-ordered column sums)
   if (M <= 0 || N <= 0 || K <= 0 || hopsx_disabled("gg") || hopsx_deterministic()) return false;
   GgPlan p;
-  if (!gg_plan(M, N, K, allow_split, p, min_wg_override)) return false;
+  static const bool narrow = !hopsx_disabled("gg_n64");
+  if (!gg_plan(M, N, K, allow_split, p, min_wg_override, 256, narrow)) return false;
   static const int diag = (int)hopsx_env_int("HOPSX_GG_DIAG", 0);
   const dim3 grid((unsigned)(p.tiles * p.split));
   switch (p.cfg) {
@@ -806,6 +815,10 @@ inline bool launch_gg(const AS& as, const BS& bs, const EP& ep, int M, int N, in
       break;
     case 1:
       hipLaunchKernelGGL((gg_kernel<128, 256, 3, A_KC, B_KC, AS, BS, EP>), grid, dim3(512), 0, st, as, bs, ep, M, N, K,
+                         p.kps, p.tiles_n, p.tiles, diag);
+      break;
+    case 3:
+      hipLaunchKernelGGL((gg_kernel<256, 64, 3, A_KC, B_KC, AS, BS, EP>), grid, dim3(512), 0, st, as, bs, ep, M, N, K,
                          p.kps, p.tiles_n, p.tiles, diag);
       break;
     default:

@@ -30,6 +30,8 @@ CASES = [  # B, H, C, CO, k, stride, pad
     (3, 17, 72, 136, 3, 1, 1),     # ragged: N = 648, CO = 136, 867 pixels
     (2, 9, 512, 64, 1, 1, 0),      # 162 pixels -> fails the >= 8 k-steps rule: not eligible
     (16, 7, 512, 2048, 1, 1, 0),   # stage-4 expand, many tiles
+    (8, 56, 64, 64, 3, 1, 1),      # stage-1 3x3: 576 x 64 output, the 256x64 tile (RC B, 64 live columns)
+    (8, 56, 64, 64, 1, 1, 0),      # 64 x 64 output
 ]
 
 
@@ -71,6 +73,10 @@ FWD_CASES = [  # B, H, C, CO, k, stride  (big enough that the gg engine takes th
     (32, 28, 128, 128, 3, 1),
     (32, 56, 64, 128, 3, 2),
     (16, 28, 256, 512, 1, 2),
+    # 64 output (or, for dgrad, input) channels: the 256x64 tile (gg_plan cfg 3)
+    (16, 56, 64, 64, 3, 1),
+    (8, 56, 256, 64, 1, 1),
+    (8, 56, 64, 128, 3, 2),   # dgrad N = 64 over the stride-2 parity classes
 ]
 
 
@@ -110,3 +116,23 @@ def test_conv_dgrad_addend_epilogue(B, H, C, CO, k, stride):
     fused = K.conv2d_dgrad(dy, w, g, addend=add).float()
     ref = plain + add.float()
     torch.testing.assert_close(fused, ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
+
+
+def test_gg_n64_fwd_bnstats_and_path(monkeypatch):
+    """The 256x64 gg tile with the BN-statistics epilogue (the stage-1 3x3 conv feeding a BatchNorm), and
+    that the planner takes it (HOPSX_DISABLE=gg_n64 gives the same result on the other engine)."""
+    torch.manual_seed(3)
+    B, H, C, CO = 16, 56, 64, 64
+    x = torch.randn(B, H, H, C, device=dev).to(bf)
+    w = (torch.randn(CO, 3, 3, C, device=dev) * 0.05).to(bf)
+    g = K.conv_geom(x.shape, w.shape, (1, 1), (1, 1), (1, 1))
+    y = K.conv2d_fwd_bnstats(x, w, g)
+    torch.cuda.synchronize()
+    K.bn_acc(dev, CO).zero_()  # (the statistics are not consumed here: re-zero the shared accumulator)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    if y is not None:
+        torch.testing.assert_close(y.float(), ref, atol=2e-2 * ref.abs().max().item(), rtol=2e-2)
+    y1 = K.conv2d_fwd(x, w, g)
+    monkeypatch.setenv("HOPSX_DISABLE", "gg_n64")
+    y2 = K.conv2d_fwd(x, w, g)
+    torch.testing.assert_close(y1.float(), y2.float(), atol=1e-2 * ref.abs().max().item(), rtol=1e-2)
