@@ -893,7 +893,8 @@ __device__ __forceinline__ void position_wg(const Args& a, unsigned char* smem, 
       const auto XP = rsrc(a.xbuf[a.rank] + XO_POOL + (long)par * XMAX * XS_POOL + (long)p * 4096);
       const auto XD = rsrc(a.xbuf[a.rank] + XO_DHT + (long)par * XMAX * XS_DHT);
       // rank r's fragments: own from LDS, a peer's from this rank's exchange buffer; loaded two ranks
-      // ahead of the MFMAs that consume them (three register sets, indices fixed by the unrolled loop)
+      // ahead of the MFMAs that consume them (three register sets, indices fixed by the unrolled loop;
+      // four — three peers' loads in flight — measured no faster at 8 loopback ranks: 34.2 vs 33.6 us/step)
       constexpr int PF = 3;
       bf16x8 af[PF][2], bfr[PF][4];
       auto fetch = [&](int r, int b) {
