@@ -146,8 +146,36 @@ def main():
         run(i)
     step.prepare_resident(xs, ys, n=a.steps)  # capture the steps_per_execution (+ remainder) graphs untimed
     el = timed(run, a.steps, dev)
-    if hasattr(step, "check"):
-        step.check()  # the persistent engine's sticky hand-off error word (outside the timed region)
+    if isinstance(step, PersistentMnistStep):
+        # the persistent engine's sticky hand-off error word (outside the timed region), agreed on by every
+        # rank: a run whose in-launch exchange failed is not a measurement — the ranks fall back together to
+        # the multi-kernel DP engine and time that instead (the JSON says so in persistent_note)
+        if os.environ.get("HOPSX_BENCH_FAKE_PERSIST_ERR"):  # (exercises this fallback: tests/test_bench_gpu.py)
+            step.err.fill_(int(os.environ["HOPSX_BENCH_FAKE_PERSIST_ERR"]))
+        err = int(step.err[0].item()) & 0xFFFFFFFF
+        errs = [err]
+        if world > 1:
+            import torch.distributed as dist
+
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
+        if any(errs):
+            try:
+                step.check()
+            except Exception as e:  # (the rank's own error text, for the note)
+                persist_note = f"persistent run failed ({str(e)[:160]}); timed on TrainStep instead"
+            else:
+                persist_note = f"a peer's persistent run failed (error words {errs}); timed on TrainStep instead"
+            if world > 1:
+                step.close()
+            os.environ["HOPSX_PERSIST"] = "0"
+            step = make_step(model, opt, "sparse_ce", dp="auto", batch=B, graph=not a.no_graph and dev.type == "cuda",
+                             steps_per_execution=32)
+            dp = getattr(step, "dp", None)
+            for i in range(max(a.warmup, step.warmup + 2)):
+                run(i)
+            step.prepare_resident(xs, ys, n=a.steps)
+            el = timed(run, a.steps, dev)
     loss = float(out["r"]["loss"].item())
     ms = el / a.steps * 1e3
     ips = B * world * a.steps / el
