@@ -272,10 +272,12 @@ HX_PYMOD(HOPSX_MODNAME) {
     return (int)hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), S(st));
   });
   m.def("mlp_head", [](u x, u w1, u b1, int act1, u y, u ws, u arrive, int B, int K, int N1, int kind, u target,
-                       int C, float gs, u w2, u b2, u dw2, u db2, u dh, u loss, u correct, u lout, int lf32, u st) {
+                       int C, float gs, u w2, u b2, u dw2, u db2, u dh, u loss, u correct, u lout, int lf32, float dp,
+                       u drng, unsigned dsalt, u st) {
     return hopsx_mlp_head(P<void>(x), P<void>(w1), P<float>(b1), act1, P<void>(y), P<float>(ws), P<unsigned>(arrive),
                           B, K, N1, kind, P<void>(target), C, gs, P<void>(w2), P<float>(b2), P<float>(dw2),
-                          P<float>(db2), P<void>(dh), P<float>(loss), P<int>(correct), P<void>(lout), lf32, S(st));
+                          P<float>(db2), P<void>(dh), P<float>(loss), P<int>(correct), P<void>(lout), lf32, dp,
+                          P<unsigned long long>(drng), dsalt, S(st));
   });
   m.def("zero", [](u p, long bytes, u st) { return hopsx_zero(P<void>(p), bytes, S(st)); });
   m.def("nonfinite", [](u x, long n, int is_bf16, u out, u st) {

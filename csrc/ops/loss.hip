@@ -530,6 +530,11 @@ struct MlpHeadArgs {
   int vec2;
   unsigned long long* dbg;
   int rot;  // rotate each workgroup's workspace atomics (HOPSX_MLP_ROT, default on)
+  // dp > 0: a Dropout between the Dense and the head (as head_ce_k's): y stays the Dense output (dense1's
+  // backward reads its act' from it), the head reads dropout(y), and dh is the gradient of y
+  float dp;
+  const unsigned long long* drng;
+  unsigned dsalt;
 };
 
 
@@ -663,6 +668,12 @@ __device__ inline void mlp_prefetch(const MlpHeadArgs& a, int t, int nt) {
   }
 }
 
+// the input gradient of the dropout's input at element o (the unfused chain: bf16 dX, then dropout_k on it)
+__device__ __forceinline__ float mlp_drop_grad(const MlpHeadArgs& a, float v, long o) {
+  if (!(a.dp > 0.f)) return v;
+  return bf2f(f2bf(v)) * (uniform01(drop_key(a.drng, a.dsalt), (uint64_t)o) >= a.dp ? 1.f / (1.f - a.dp) : 0.f);
+}
+
 __device__ inline void mlp_tail(const MlpHeadArgs& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char head_smem[];
   const MlpLds L(a.C, a.N1);
@@ -703,6 +714,13 @@ __device__ inline void mlp_tail(const MlpHeadArgs& a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[j] = (short)f2bf(apply_act(f[j] + sb1[c8 + j], a.act1));
       *(bf16x8*)(a.y + (long)r * N1 + c8) = q;
+      if (a.dp > 0.f) {  // (dropout_k's mask and rounding)
+        const uint64_t key = drop_key(a.drng, a.dsalt);
+        const float sc = 1.f / (1.f - a.dp);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          q[j] = (short)f2bf(bf2f((uint16_t)q[j]) * (uniform01(key, (uint64_t)((long)r * N1 + c8 + j)) >= a.dp ? sc : 0.f));
+      }
       *(bf16x8*)(sh + r * RS + c8) = q;
     }
   }
@@ -847,7 +865,7 @@ __device__ inline void mlp_tail(const MlpHeadArgs& a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = rf * 16 + 4 * fq + r;
-        if (b < B) a.dh[(long)b * N1 + f * 16 + fr] = f2bf(acc[r]);
+        if (b < B) a.dh[(long)b * N1 + f * 16 + fr] = f2bf(mlp_drop_grad(a, acc[r], (long)b * N1 + f * 16 + fr));
       }
     }
     return;
@@ -888,7 +906,7 @@ __device__ inline void mlp_tail(const MlpHeadArgs& a) {
     }
     bf16x8 q;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = (short)f2bf(acc[j]);
+    for (int j = 0; j < 8; ++j) q[j] = (short)f2bf(mlp_drop_grad(a, acc[j], (long)r * N1 + k + j));
     *(bf16x8*)(a.dh + (long)r * N1 + k) = q;
   }
 }
@@ -990,7 +1008,8 @@ __global__ __launch_bounds__(1024) void mlp_head_k(MlpHeadArgs a) {
 extern "C" int hopsx_mlp_head(const void* x, const void* w1, const float* b1, int act1, void* y, float* ws,
                               unsigned* arrive, int B, int K, int N1, int kind, const void* target, int C,
                               float grad_scale, const void* w2, const float* b2, float* dw2, float* db2, void* dh,
-                              float* loss_sum, int* correct, void* logits_out, int logits_f32, hipStream_t st) {
+                              float* loss_sum, int* correct, void* logits_out, int logits_f32, float drop_p,
+                              const unsigned long long* drop_rng, unsigned drop_salt, hipStream_t st) {
   if (hopsx_disabled("mlp_head") || B < 1 || B > HEAD_ROWS || N1 < 16 || N1 % 16 || N1 > 256 || K < 8 || K % 8 ||
       !hopsx_head_ce_ok(C, N1) || !ws || !arrive || !logits_out ||
       ((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)y | (uintptr_t)dh | (uintptr_t)ws) % 16)
@@ -1006,7 +1025,8 @@ extern "C" int hopsx_mlp_head(const void* x, const void* w1, const float* b1, in
   static const int rot_on = (int)hopsx_env_int("HOPSX_MLP_ROT", 1);
   MlpHeadArgs a{(const bf16_raw*)x, (const bf16_raw*)w1, b1, act1, (bf16_raw*)y, ws, arrive, B, K, N1, kind, target, C,
                 grad_scale, (const bf16_raw*)w2, b2, dw2, db2, (bf16_raw*)dh, loss_sum, correct, logits_out,
-                logits_f32, vec2, g_mlp_dbg, rot_on};
+                logits_f32, vec2, g_mlp_dbg, rot_on, drop_p, drop_rng, drop_salt};
+  if (drop_p > 0.f && (!drop_rng || drop_p >= 1.f)) return -3;
   const size_t lds = mlp_lds_bytes(C, N1);
   const int rf = B > 16 ? 2 : 1, cf = (N1 / 16 + 3) / 4;
 #define MLP_CASE(R, F)                                                                     \

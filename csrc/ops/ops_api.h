@@ -62,7 +62,8 @@ int hopsx_head_ce(int kind, const void* logits, int logits_f32, const void* targ
 int hopsx_mlp_head(const void* x, const void* w1, const float* b1, int act1, void* y, float* ws, unsigned* arrive,
                    int B, int K, int N1, int kind, const void* target, int C, float grad_scale, const void* w2,
                    const float* b2, float* dw2, float* db2, void* dh, float* loss_sum, int* correct,
-                   void* logits_out, int logits_f32, hipStream_t st);
+                   void* logits_out, int logits_f32, float drop_p, const unsigned long long* drop_rng,
+                   unsigned drop_salt, hipStream_t st);
 int hopsx_loss_fwd_bwd(int kind, const void* logits, int logits_f32, const void* target, int B, int C,
                        float grad_scale, float* loss_sum, int* correct, void* dlogits, int dlogits_f32,
                        hipStream_t st);

@@ -1243,10 +1243,6 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
         loss_, correct, count, dl = loss_and_grad(logits, target, kind)
         return loss_, correct, count, logits, dl
     h, w, b, _, deferred = head[:5]
-    if drop is not None and pend is not None:
-        # (the fused Dense -> head kernel has no dropout between the two: the Dense runs on its own)
-        K.linear_fwd(pend[0], pend[1], pend[2], act=pend[3], out=pend[4])
-        pend = None
     B, C = logits.shape
     cnt = B * (C if k in (2, 3, 4) else 1)
     if k in (2, 3, 4) and target.dim() == 1:
@@ -1259,7 +1255,7 @@ def loss_and_grad_root(logits, target, kind: str = "sparse_ce"):
         x2, wb, b1, act1, y = pend
         dh = K.mlp_head(x2, wb, b1.detach() if b1 is not None else None, act1, y, k, logits, target,
                         _arena.weight_bf16(w), b.detach() if b is not None else None, _arena.grad_target(w),
-                        _arena.grad_target(b) if b is not None else None, 1.0 / cnt, loss_sum, correct)
+                        _arena.grad_target(b) if b is not None else None, 1.0 / cnt, loss_sum, correct, drop=drop)
         if dh is not False:
             hooks.grad_ready(w)
             if b is not None:

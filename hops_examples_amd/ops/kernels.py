@@ -856,10 +856,12 @@ def _mlp_ws(device, n: int):
     return cur
 
 
-def mlp_head(x, w1, b1, act1, y, kind: int, logits, target, w2, b2, dw2, db2, grad_scale: float, loss_sum, correct):
+def mlp_head(x, w1, b1, act1, y, kind: int, logits, target, w2, b2, dw2, db2, grad_scale: float, loss_sum, correct,
+             drop=None):
     """Last hidden Dense layer + classifier head in ONE launch (loss.hip mlp_head_k): fills ``y`` =
     act(x W1^T + b1) (bf16 [B, N1]) and ``logits``, and does what head_ce does (loss, dW2/db2
-    accumulation); returns dh [B, N1] bf16, or False when the shape is not supported."""
+    accumulation); returns dh [B, N1] bf16, or False when the shape is not supported.  ``drop`` =
+    (p, rng, salt): a Dropout between the two (applied to the head's input, dh is then the gradient of y)."""
     B, K = x.shape
     N1 = w1.shape[0]
     C = w2.shape[0]
@@ -871,7 +873,9 @@ def mlp_head(x, w1, b1, act1, y, kind: int, logits, target, w2, b2, dw2, db2, gr
     dh = torch.empty(B, N1, device=x.device, dtype=BF16)
     rc = _C.ext().mlp_head(ptr(x), ptr(w1), ptr(b1), act_id(act1), ptr(y), ptr(ws), ptr(arrive), B, K, N1, int(kind),
                            ptr(target), C, float(grad_scale), ptr(w2), ptr(b2), ptr(dw2), ptr(db2), ptr(dh),
-                           ptr(loss_sum), ptr(correct), ptr(logits), int(logits.dtype == F32), stream())
+                           ptr(loss_sum), ptr(correct), ptr(logits), int(logits.dtype == F32),
+                           float(drop[0]) if drop else 0.0, ptr(drop[1]) if drop else 0,
+                           (int(drop[2]) & 0xFFFFFFFF) if drop else 0, stream())
     if rc == -2:
         return False
     check(rc, "mlp_head")

@@ -192,7 +192,7 @@ def _e1_modules(fold: bool):
 
 def test_dropout_folded_into_deferred_head_matches_unfolded(monkeypatch):
     """E1: the Dropout between the last hidden Dense and the logits layer applied inside the fused loss
-    kernel (head_ce_k dp: mask on the staged input, the same mask on the input gradient) trains like the
+    kernel (head_ce_k / mlp_head_k dp: mask on the staged input, the same mask on the input gradient) trains like the
     separate dropout launches — losses and weights after 8 TrainStep steps (eager warm-up + graph replays),
     with no dropout launch left."""
     from hops_examples_amd import optim
@@ -209,13 +209,16 @@ def test_dropout_folded_into_deferred_head_matches_unfolded(monkeypatch):
         m = _e1_modules(fold).to(dev)
         ParamArena.from_module(m, dev)
         calls = {"drop": 0, "head": []}
-        real_d, real_h = K.dropout, K.head_ce
+        real_d, real_h, real_m = K.dropout, K.head_ce, K.mlp_head
         monkeypatch.setattr(K, "dropout", lambda *a, **kw: calls.__setitem__("drop", calls["drop"] + 1) or real_d(*a, **kw))
+        # the deferred head runs as head_ce_k, or — with the Dense before it deferred too — as mlp_head_k
         monkeypatch.setattr(K, "head_ce", lambda *a, **kw: calls["head"].append(kw.get("drop")) or real_h(*a, **kw))
+        monkeypatch.setattr(K, "mlp_head", lambda *a, **kw: calls["head"].append(kw.get("drop")) or real_m(*a, **kw))
         st = TrainStep(m, optim.Adam(m, lr=1e-3), "sparse_ce")
         ls = [float(st(xs[i], ys[i])["loss"].reshape(-1)[0]) for i in range(8)]
         monkeypatch.setattr(K, "dropout", real_d)
         monkeypatch.setattr(K, "head_ce", real_h)
+        monkeypatch.setattr(K, "mlp_head", real_m)
         assert st._head_defer
         if fold:
             # (the first, probing step runs the head undeferred: its dropout is the separate kernel, fwd + bwd)
