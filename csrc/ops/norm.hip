@@ -426,12 +426,16 @@ __global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restric
   }
   for (long i = i0; i < nch; i += 2 * stride) {
     const long ib = i + stride < nch ? i + stride : i;
-    if (i != i0) {
-      px[0] = *(const bf16x8*)(x + i * 8);
-      px[1] = *(const bf16x8*)(x + ib * 8);
+    // the next trip's operands are requested before this trip's math and stores (twice the bytes in
+    // flight: the big ResNet-50 tensors take ~12 trips per thread, each of which waited out a round trip)
+    const long in0 = i + 2 * stride, in1 = in0 + stride < nch ? in0 + stride : in0;
+    bf16x8 nx[2], nr[2];
+    if (in0 < nch) {
+      nx[0] = *(const bf16x8*)(x + in0 * 8);
+      nx[1] = *(const bf16x8*)(x + in1 * 8);
       if (res) {
-        pr[0] = *(const bf16x8*)(res + i * 8);
-        pr[1] = *(const bf16x8*)(res + ib * 8);
+        nr[0] = *(const bf16x8*)(res + in0 * 8);
+        nr[1] = *(const bf16x8*)(res + in1 * 8);
       }
     }
     float v[2][8];
@@ -446,6 +450,12 @@ __global__ __launch_bounds__(256) void bn_apply_fin8_k(const bf16_raw* __restric
     }
     st8f(y + i * 8, v[0]);
     if (i + stride < nch) st8f(y + ib * 8, v[1]);
+    px[0] = nx[0];
+    px[1] = nx[1];
+    if (res) {
+      pr[0] = nr[0];
+      pr[1] = nr[1];
+    }
   }
   __syncthreads();
   if (last)
@@ -567,14 +577,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
   }
   for (long i = i0; i < nch; i += 2 * stride) {
     const long ib = i + stride < nch ? i + stride : i;
-    if (i != i0) {
-      pd[0] = *(const bf16x8*)(dy + i * 8);
-      pd[1] = *(const bf16x8*)(dy + ib * 8);
-      px[0] = *(const bf16x8*)(x + i * 8);
-      px[1] = *(const bf16x8*)(x + ib * 8);
+    // next trip's operands in flight behind this trip's (see bn_apply_fin8_k)
+    const long in0 = i + 2 * stride, in1 = in0 + stride < nch ? in0 + stride : in0;
+    bf16x8 nd[2], nx[2], ny[2];
+    if (in0 < nch) {
+      nd[0] = *(const bf16x8*)(dy + in0 * 8);
+      nd[1] = *(const bf16x8*)(dy + in1 * 8);
+      nx[0] = *(const bf16x8*)(x + in0 * 8);
+      nx[1] = *(const bf16x8*)(x + in1 * 8);
       if (act != ACT_NONE && !zmask) {
-        py[0] = *(const bf16x8*)(y + i * 8);
-        py[1] = *(const bf16x8*)(y + ib * 8);
+        ny[0] = *(const bf16x8*)(y + in0 * 8);
+        ny[1] = *(const bf16x8*)(y + in1 * 8);
       }
     }
 #pragma unroll
@@ -595,6 +608,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fin8_k(const bf16_raw* __res
         d[j] = k1[j] * (d[j] - md[j] - xh * k2[j]);
       }
       st8f(dx + o, d);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      pd[u] = nd[u];
+      px[u] = nx[u];
+      py[u] = ny[u];
     }
   }
   __syncthreads();
