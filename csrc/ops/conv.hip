@@ -515,6 +515,17 @@ static bool gg_narrow(const ConvGeom& g, int N) {
   return !(g.KH == 1 && g.KW == 1) && N < min_n && !(N == 64 && n64);
 }
 
+// A spatial (KH*KW > 1) conv with 64 output channels, K >= 256 and >= 8 rounds of the gg engine's 256x64 tiles
+// (the ResNet-50 7x7 stem at batch >= 16: 802,816 output pixels at batch 64): the tiled engine rather than
+// the direct MFMA kernel, whose per-wave 16-pixel groups re-gather every A row from L2 (211 us per stem
+// forward at batch 64, profiles/r6_resnet50_b64_kernels.txt)
+static bool gg_big_spatial(const int* geom) {
+  const long M = (long)geom[0] * geom[4] * geom[5];
+  const int K = geom[7] * geom[8] * geom[3];
+  return geom[7] * geom[8] > 1 && geom[6] == 64 && K >= 256 && M >= 8L * 256 * 256 && geom[3] % 8 == 0 &&
+         !hopsx_disabled("gg_stem") && !hopsx_disabled("gg_n64") && !hopsx_deterministic();
+}
+
 template <class EP>
 static bool gg_conv_fwd(const void* x, const void* w, const ConvGeom& g, const EP& e, hipStream_t st) {
   const int M = g.B * g.OH * g.OW, N = g.CO, K = g.KH * g.KW * g.C;
@@ -627,7 +638,7 @@ extern "C" int hopsx_conv2d_fwd(const void* x, const void* w, const int* geom, i
                        xshift, (const bf16_raw*)w, bias, (bf16_raw*)out, g, act);
     return (int)hipGetLastError();
   }
-  if (epi == EPI_STORE_BF16 && !colsum && hopsx_conv_fwd_mfma_ok(geom) && ((uintptr_t)x % 16 == 0) &&
+  if (epi == EPI_STORE_BF16 && !colsum && hopsx_conv_fwd_mfma_ok(geom) && !gg_big_spatial(geom) && ((uintptr_t)x % 16 == 0) &&
       ((uintptr_t)w % 16 == 0) && ((uintptr_t)out % 16 == 0))
     return hopsx_conv2d_fwd_mfma(x, w, geom, out, bias, act, st);
   Im2colLoader al{(const bf16_raw*)x, g, (g.C % 8 == 0) && ((uintptr_t)x % 16 == 0)};
@@ -656,7 +667,8 @@ extern "C" int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int*
                                         hipStream_t st) {
   if (!bnacc || hopsx_disabled("bnstats") || !hopsx_bn_prestats_ok(geom[6])) return -2;
   if (((uintptr_t)x | (uintptr_t)w | (uintptr_t)out) % 16 != 0) return -2;
-  if (hopsx_conv_fwd_mfma_ok(geom)) return hopsx_conv2d_fwd_mfma_ex(x, w, geom, out, nullptr, 0, bnacc, st);
+  if (hopsx_conv_fwd_mfma_ok(geom) && !gg_big_spatial(geom))
+    return hopsx_conv2d_fwd_mfma_ex(x, w, geom, out, nullptr, 0, bnacc, st);
   ConvGeom g = make_geom(geom);
   if (g.C % 8 != 0) return -2;
   const int M = g.B * g.OH * g.OW, N = g.CO, K = g.KH * g.KW * g.C;
