@@ -78,6 +78,7 @@ FWD_CASES = [  # B, H, C, CO, k, stride  (big enough that the gg engine takes th
     (8, 56, 256, 64, 1, 1),
     (8, 56, 64, 128, 3, 2),   # dgrad N = 64 over the stride-2 parity classes
     (48, 224, 8, 64, 7, 2),   # the ResNet-50 stem (channels padded to 8): gg instead of the direct kernel
+    (64, 56, 64, 256, 1, 1),  # stage-1 expand at batch 64: its dgrad (N = 64, K = 256) on gg, not the direct kernel
 ]
 
 
