@@ -414,6 +414,12 @@ HX_PYMOD(HOPSX_MODNAME) {
   m.def("conv2d_fwd_bnstats", [](u x, u w, std::vector<int> g, u out, u acc, u st) {
     return hopsx_conv2d_fwd_bnstats(P<void>(x), P<void>(w), g.data(), P<void>(out), P<float>(acc), S(st));
   });
+  m.def("conv2d_fwd_bnstats_inbn", [](u z, u a, u w, std::vector<int> g, u out, u acc, u inacc, u gm, u bt, u mean,
+                                      u rstd, u rm, u rv, float mom, float eps, int act, u st) {
+    return hopsx_conv2d_fwd_bnstats_inbn(P<void>(z), P<void>(a), P<void>(w), g.data(), P<void>(out), P<float>(acc),
+                                         P<float>(inacc), P<float>(gm), P<float>(bt), P<float>(mean), P<float>(rstd),
+                                         P<float>(rm), P<float>(rv), mom, eps, act, S(st));
+  });
   m.def("bn_fwd_infer", [](u x, u y, u g, u b, u rm, u rv, float eps, int M, int C, u res, int act, u st) {
     return hopsx_bn_fwd_infer(P<void>(x), P<void>(y), P<float>(g), P<float>(b), P<float>(rm), P<float>(rv), eps, M, C,
                               P<void>(res), act, S(st));

@@ -687,6 +687,17 @@ extern "C" int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int*
   return (int)hipGetLastError();
 }
 
+extern "C" int hopsx_conv2d_fwd_bnstats_inbn(const void* z, void* a, const void* w, const int* geom, void* out,
+                                             float* bnacc, float* inacc, const float* gamma, const float* beta,
+                                             float* mean_out, float* rstd_out, float* rmean, float* rvar,
+                                             float momentum, float eps, int act, hipStream_t st) {
+  if (!bnacc || hopsx_disabled("bnstats") || !hopsx_bn_prestats_ok(geom[6]) || !hopsx_bn_prestats_ok(geom[3]) ||
+      gg_big_spatial(geom))
+    return -2;
+  return hopsx_conv2d_fwd_mfma_inbn(z, a, w, geom, out, bnacc, inacc, gamma, beta, mean_out, rstd_out, rmean, rvar,
+                                    momentum, eps, act, st);
+}
+
 // dX = conv_transpose(dY, W).  If `yprev` is given, the result is multiplied by
 // act'(yprev) — the backward of the activation that produced this conv's input
 // — and `colsum` receives that layer's bias gradient.

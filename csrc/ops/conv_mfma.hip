@@ -88,11 +88,37 @@ struct In0 {
   int H0, W0, KH0, KW0, ph0, pw0, act0;
 };
 
-template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false, int T0 = 0, int PK = 2>
+// IBN: this conv's input is act(bn(z)) of a training BatchNorm (stride 1 only) whose statistics the conv
+// that produced z accumulated (acc: the zero-at-rest replica rows [HOPSX_BN_NREP][2C] + arrival words), and
+// that BN's apply launch (norm.hip bn_apply_fin8_k) is folded in here: every workgroup folds the replicas
+// into per-channel scale / shift in LDS with bn_apply_fin8_k's arithmetic, the operand gather reads z and
+// applies act(z * scale + shift) in registers (bf16-rounded, as the apply stores it), and each BN output
+// element is stored once for the backward (the In0 designated-lane rule: the lane whose tap is the first
+// covering it).  Workgroup 0 publishes mean / rstd and the running statistics; the last workgroup to have
+// read the replicas re-zeroes them.  x is z; the BN output goes to `a`.
+typedef float cm_f32x2 __attribute__((ext_vector_type(2)));
+typedef short cm_i16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 cm_bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t cm_u32x4 __attribute__((ext_vector_type(4)));
+
+struct InBn {
+  float* acc;
+  const float* gamma;
+  const float* beta;
+  float *mean_out, *rstd_out, *rmean, *rvar;
+  float momentum, eps;
+  bf16_raw* a;  // the BN output [B][H][W][C]
+  int M;        // BN rows (B*H*W)
+  int act;
+};
+
+template <int NF, int KS, bool POOL = false, int UN = CM_UN, bool BNS = false, int T0 = 0, int PK = 2,
+          bool IBN = false>
 __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restrict__ x, const bf16_raw* __restrict__ w,
                                                       const float* __restrict__ bias, bf16_raw* __restrict__ y,
                                                       ConvGeom g, int act, int K, PoolEpi pe = PoolEpi{},
-                                                      float* __restrict__ bnacc = nullptr, In0 i0 = In0{}) {
+                                                      float* __restrict__ bnacc = nullptr, In0 i0 = In0{},
+                                                      InBn ib = InBn{}) {
   constexpr int CO = NF * 16;
   extern __shared__ __attribute__((aligned(16))) bf16_raw cm_smem[];
   constexpr int cpr = KS * 4;  // 16-B chunks per weight row (K padded to 32*KS)
@@ -107,6 +133,33 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
     for (int i = threadIdx.x; i < (taps + 1) * g.C; i += 256) {
       const int t = i / g.C, c = i - t * g.C;
       sw0[i] = t < taps ? bf2f(i0.w0[c * taps + t]) : (i0.b0 ? i0.b0[c] : 0.f);
+    }
+  }
+  __shared__ int ib_last;
+  if constexpr (IBN) {
+    // IBN: scale [C] and shift [C] in sw0's place, as bn_apply_fin8_k folds them
+    for (int c = threadIdx.x; c < g.C; c += 256) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int r = 0; r < HOPSX_BN_NREP; ++r) {
+        s += ib.acc[(long)r * 2 * g.C + c];
+        q += ib.acc[(long)r * 2 * g.C + g.C + c];
+      }
+      const float mu = s / ib.M;
+      const float var = fmaxf(q / ib.M - mu * mu, 0.f);
+      const float rs = rsqrtf(var + ib.eps);
+      const float scl = rs * (ib.gamma ? ib.gamma[c] : 1.f);
+      sw0[c] = scl;
+      sw0[g.C + c] = fmaf(-mu, scl, ib.beta ? ib.beta[c] : 0.f);
+      if (blockIdx.x == 0) {
+        ib.mean_out[c] = mu;
+        ib.rstd_out[c] = rs;
+        if (ib.rmean) {
+          const float unb = ib.M > 1 ? var * ib.M / (ib.M - 1) : var;
+          ib.rmean[c] = (1.f - ib.momentum) * ib.rmean[c] + ib.momentum * mu;
+          ib.rvar[c] = (1.f - ib.momentum) * ib.rvar[c] + ib.momentum * unb;
+        }
+      }
     }
   }
   {
@@ -130,10 +183,18 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
     }
   }
   __syncthreads();
+  // IBN: every replica value this workgroup needs has been consumed (re-zeroed at the end by the last
+  // arriver).  common.h grid_arrive_last's sharded protocol split in two: the shard ticket is taken here and
+  // first used at the end, so its round trip hides behind the trip's loads (one word for every workgroup
+  // serialised ~1024 arrivals, ~12 us, in front of the loads of a one-trip grid)
+  unsigned ib_ticket = 0;
+  unsigned* const ib_arr = (unsigned*)(ib.acc + (long)HOPSX_BN_NREP * 2 * g.C);
+  if (IBN && threadIdx.x == 0) ib_ticket = atomicAdd(ib_arr + 32u * ((blockIdx.x & 7u) + 1u), 1u);
   phase_mark(pe.dbg, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   static_assert(PK == 2 || (PK == 4 && T0 == 0), "pool 4x4 without the fused input layer");
+  static_assert(!IBN || (T0 == 0 && !POOL), "input BN without the fused input layer / pool");
   const int PH = g.OH / PK, PW = g.OW / PK;
   const int M = POOL ? g.B * PH * PW * PK * PK : g.B * g.OH * g.OW;  // A rows (pooled: PK*PK taps per output)
   const int ngroups = (M + 15) / 16;
@@ -142,13 +203,24 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) bv[nf] = bias ? bias[nf * 16 + fr] : 0.f;
   const uint64_t dkey = POOL && pe.p > 0.f ? drop_key(pe.rng, pe.salt) : 0;
+  // IBN: this lane's 8 input channels are the same at every tap (32 % C == 0: ci = 8*fq mod C), so their
+  // scale / shift pairs live in registers
+  cm_f32x2 isc[4], ish[4];
+  if constexpr (IBN) {
+    const int ci0 = (8 * fq) & (g.C - 1);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      isc[p] = (cm_f32x2){sw0[ci0 + 2 * p], sw0[ci0 + 2 * p + 1]};
+      ish[p] = (cm_f32x2){sw0[g.C + ci0 + 2 * p], sw0[g.C + ci0 + 2 * p + 1]};
+    }
+  }
   float st1[NF], st2[NF];  // BNS: this lane's channel partials (channel nf*16 + fr)
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) { st1[nf] = 0.f; st2[nf] = 0.f; }
   for (int g0 = (blockIdx.x * CM_WAVES + wave) * UN; g0 < ngroups; g0 += gridDim.x * CM_WAVES * UN) {
     bf16x8 a[UN][KS];
     // T0: the input layer's pixels / lane bookkeeping of this trip (sized 1 when unused)
-    constexpr int TU = T0 > 0 ? UN : 1, TK = T0 > 0 ? KS : 1, TT = T0 > 0 ? T0 * T0 : 1;
+    constexpr int TU = T0 > 0 || IBN ? UN : 1, TK = T0 > 0 || IBN ? KS : 1, TT = T0 > 0 ? T0 * T0 : 1;
     unsigned i0px[TU][TK][TT];
     int i0ci[TU][TK];
     long i0off[TU][TK];
@@ -198,10 +270,41 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
               const unsigned raw = ((const uint8_t*)i0.x0)[pi];  // one unconditional byte load per tap
               i0px[u][kk][a0 * T0 + c0] = in ? raw : 0xFFFFFFFFu;
             }
+        } else if constexpr (IBN) {
+          a[u][kk] = *(const bf16x8*)(x + off);  // z: the BN applied after the loop
+          i0ok[u][kk] = ok;
+          i0off[u][kk] = off;
+          i0wr[u][kk] = ok && (kh == 0 || oh == g.OH - 1) && (kw == 0 || ow == g.OW - 1);
         } else {
           a[u][kk] = zero_unless(*(const bf16x8*)(x + off), ok);
         }
       }
+    }
+    if constexpr (IBN) {
+      // act(z * scale + shift) rounded to bf16: bn_apply_fin8_k's fp32 fma per element, two at a time
+      // (v_pk_fma_f32), the round-to-nearest-even by the conversion instruction (common.h f2bf's bits for
+      // every finite value) and the ReLU on the bf16 bits (max_i16 with 0: a negative bf16 is a negative
+      // int16) — the gather visits every element once per tap, so this runs KH*KW times per element;
+      // padding taps stay zero
+      const bool relu = ib.act == ACT_RELU;
+#pragma unroll
+      for (int u = 0; u < UN; ++u)
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const cm_u32x4 r = __builtin_bit_cast(cm_u32x4, a[u][kk]);
+          cm_u32x4 o;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            cm_f32x2 v = {__uint_as_float(r[p] << 16), __uint_as_float(r[p] & 0xffff0000u)};
+            v = __builtin_elementwise_fma(v, isc[p], ish[p]);
+            cm_i16x2 b = __builtin_bit_cast(cm_i16x2, __builtin_convertvector(v, cm_bf16x2));
+            if (relu) b = __builtin_elementwise_max(b, (cm_i16x2){0, 0});
+            o[p] = __builtin_bit_cast(uint32_t, b);
+          }
+          const bf16x8 t = __builtin_bit_cast(bf16x8, o);
+          a[u][kk] = zero_unless(t, i0ok[u][kk]);
+          if (i0wr[u][kk]) *(bf16x8*)(ib.a + i0off[u][kk]) = t;
+        }
     }
     if constexpr (T0 > 0) {
       // input layer: act0(b0 + sum_taps px * w0) in conv_direct_fwd_k's fp32 order, bf16-rounded;
@@ -368,6 +471,23 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_k(const bf16_raw* __restric
       atomicAdd(dst + e, t);
     }
     if (det) det_turn_end(DET_BN_FWD, blockIdx.x, gridDim.x);
+  }
+  if constexpr (IBN) {
+    if (threadIdx.x == 0) {
+      const unsigned G = gridDim.x, shard = blockIdx.x & 7u;
+      int last = 0;
+      if (ib_ticket == (G - shard + 7u) / 8u - 1u) {  // this shard's last member: arrive on the top word
+        atomicExch(ib_arr + 32u * (shard + 1u), 0u);
+        if (atomicAdd(ib_arr, 1u) == (G < 8u ? G : 8u) - 1u) {
+          atomicExch(ib_arr, 0u);
+          last = 1;
+        }
+      }
+      ib_last = last;
+    }
+    __syncthreads();
+    if (ib_last)
+      for (int i = threadIdx.x; i < HOPSX_BN_NREP * 2 * g.C; i += 256) ib.acc[i] = 0.f;
   }
   if (pe.dbg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1085,6 +1205,57 @@ extern "C" int hopsx_conv2d_fwd_mfma_ex(const void* x, const void* w, const int*
   }
 #undef HOPSX_CMF_NF
 #undef HOPSX_CMF
+  return (int)hipGetLastError();
+}
+
+// conv_fwd_mfma_k IBN: z -> a = act(bn(z)) (stored for the backward) -> conv -> out, with out's BN statistics
+// into bnacc; the input BN's statistics come from inacc (re-zeroed here; != bnacc).  -2: not this path
+// (stride / dilation != 1, the shape has no MFMA forward, act other than none / relu).
+extern "C" int hopsx_conv2d_fwd_mfma_inbn(const void* z, void* a, const void* w, const int* geom, void* out,
+                                          float* bnacc, float* inacc, const float* gamma, const float* beta,
+                                          float* mean_out, float* rstd_out, float* rmean, float* rvar, float momentum,
+                                          float eps, int act, hipStream_t st) {
+  if (!hopsx_conv_fwd_mfma_ok(geom) || hopsx_disabled("bn_fold") || !bnacc || !inacc || bnacc == inacc || !a ||
+      !mean_out || !rstd_out || (act != ACT_NONE && act != ACT_RELU))
+    return -2;
+  ConvGeom g;
+  g.B = geom[0]; g.H = geom[1]; g.W = geom[2]; g.C = geom[3]; g.OH = geom[4]; g.OW = geom[5]; g.CO = geom[6];
+  g.KH = geom[7]; g.KW = geom[8]; g.sh = geom[9]; g.sw = geom[10]; g.ph = geom[11]; g.pw = geom[12];
+  g.dh = geom[13]; g.dw = geom[14];
+  g.init_div();
+  if (g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1 || g.OH < 1 || g.OW < 1) return -2;
+  if (32 % g.C != 0) return -2;  // C in {8, 16, 32}: a lane's channels are the same at every tap (InBn)
+  if (((uintptr_t)z | (uintptr_t)a | (uintptr_t)w | (uintptr_t)out) % 16 != 0) return -2;
+  const long nx = (long)g.B * g.H * g.W * g.C;
+  if (nx >= (1L << 31) || (long)g.B * g.H * g.W >= (1L << 31)) return -2;
+  const int K = g.KH * g.KW * g.C;
+  const int KS = cm_ks5((K + 31) / 32);
+  const long M = (long)g.B * g.OH * g.OW;
+  const int grid = cm_grid((M + 15) / 16);
+  const size_t shm = (size_t)(g.CO * cm_rs(KS * 4) * 8 + CM_WAVES * 16 * g.CO) * sizeof(bf16_raw) + 2 * g.C * sizeof(float);
+  const InBn ib{inacc, gamma, beta, mean_out, rstd_out, rmean, rvar, momentum, eps, (bf16_raw*)a,
+                (int)(g.B * g.H * g.W), act};
+#define HOPSX_CMI(NF, KSV)                                                                                       \
+  hipLaunchKernelGGL((conv_fwd_mfma_k<NF, KSV, false, CM_UN, true, 0, 2, true>), dim3(grid), dim3(256), shm, st, \
+                     (const bf16_raw*)z, (const bf16_raw*)w, nullptr, (bf16_raw*)out, g, 0, K, PoolEpi{}, bnacc,   \
+                     In0{}, ib)
+#define HOPSX_CMI_NF(NF)          \
+  switch (KS) {                   \
+    case 2: HOPSX_CMI(NF, 2); break;  \
+    case 4: HOPSX_CMI(NF, 4); break;  \
+    case 5: HOPSX_CMI(NF, 5); break;  \
+    case 8: HOPSX_CMI(NF, 8); break;  \
+    case 9: HOPSX_CMI(NF, 9); break;  \
+    default: HOPSX_CMI(NF, 16); break; \
+  }
+  switch (g.CO / 16) {
+    case 1: HOPSX_CMI_NF(1); break;
+    case 2: HOPSX_CMI_NF(2); break;
+    case 4: HOPSX_CMI_NF(4); break;
+    default: return -2;
+  }
+#undef HOPSX_CMI_NF
+#undef HOPSX_CMI
   return (int)hipGetLastError();
 }
 

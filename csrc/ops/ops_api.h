@@ -140,6 +140,16 @@ int hopsx_conv2d_fwd_mfma_ex(const void* x, const void* w, const int* geom, void
 // of its output into bnacc [HOPSX_BN_NREP][2 CO] (zero at rest; hopsx_bn_fwd_apply_fin consumes and
 // re-zeroes it).  -2: not supported for this shape (nothing launched; use the plain BN path).
 int hopsx_conv2d_fwd_bnstats(const void* x, const void* w, const int* geom, void* out, float* bnacc, hipStream_t st);
+// the same, with the input a = act(bn(z)) of a training BatchNorm (statistics in inacc, from z's producing
+// conv) applied inside the operand gather instead of by hopsx_bn_fwd_apply_fin: writes a (for the
+// backward), mean / rstd / the running statistics, re-zeroes inacc.  -2: not supported (nothing launched).
+int hopsx_conv2d_fwd_bnstats_inbn(const void* z, void* a, const void* w, const int* geom, void* out, float* bnacc,
+                                  float* inacc, const float* gamma, const float* beta, float* mean_out,
+                                  float* rstd_out, float* rmean, float* rvar, float momentum, float eps, int act,
+                                  hipStream_t st);
+int hopsx_conv2d_fwd_mfma_inbn(const void* z, void* a, const void* w, const int* geom, void* out, float* bnacc,
+                               float* inacc, const float* gamma, const float* beta, float* mean_out, float* rstd_out,
+                               float* rmean, float* rvar, float momentum, float eps, int act, hipStream_t st);
 int hopsx_bn_fwd_apply_fin(const void* x, void* y, const float* gamma, const float* beta, float* mean_out,
                            float* rstd_out, float* running_mean, float* running_var, float momentum, float eps, int M,
                            int C, const void* residual, int act, float* acc, hipStream_t st);

@@ -30,14 +30,16 @@ class ConvBN(nn.Module):
         self.conv = hnn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False, init="he")
         self.bn = hnn.BatchNorm2d(cout, activation=act)
 
-    def forward(self, x, residual=None, gslot=None, res_gslot=None, sole=False):
+    def forward(self, x, residual=None, gslot=None, res_gslot=None, sole=False, fold_next=False):
         # training: the conv epilogue accumulates the BN statistics (functional.conv2d bnstats), so
         # the BN is one apply launch instead of a statistics pass + an apply.  gslot / res_gslot:
         # see BasicBlock.forward.  sole: this conv is the only autograd consumer of x (when x is a BN
-        # output, the conv's dgrad epilogue then reduces that BN's backward column sums)
+        # output, the conv's dgrad epilogue then reduces that BN's backward column sums).  fold_next: the
+        # output goes only to the next ConvBN, whose conv applies this BN in its operand gather
         if sole:
             HF.bn_sole_consumer(x)
-        return self.bn(self.conv(x, bnstats=self.bn.training, gslot=gslot), residual, gslot=res_gslot)
+        return self.bn(self.conv(x, bnstats=self.bn.training, gslot=gslot), residual, gslot=res_gslot,
+                       fold_next=fold_next)
 
 
 def _fuse_proj(block, x) -> bool:
@@ -47,6 +49,10 @@ def _fuse_proj(block, x) -> bool:
 
 class BasicBlock(nn.Module):
     expansion = 1
+    # a's BN apply is folded into b's conv (functional.batch_norm fold_next) from this width up: measured on
+    # ResNet-20 B=128 (profiles/r6_bn_fold_resnet20.txt), conv + apply 14.8 -> 12.6 us at 32 channels but
+    # 14.9 -> 16.8 us at 16 (4x the pixels: the gather applies the BN once per tap, 9x per element)
+    fold_min_width = 32
 
     def __init__(self, cin, cout, stride=1):
         super().__init__()
@@ -55,21 +61,26 @@ class BasicBlock(nn.Module):
         self.short = ConvBN(cin, cout, 1, stride, act=None) if (stride != 1 or cin != cout) else None
 
     def forward(self, x):
+        # a's BN output feeds only b's conv: where that conv has the direct MFMA forward (K = 9 * cout <= 512:
+        # the 16 / 32-channel CIFAR stages) and cout >= fold_min_width, a's BN apply runs inside it
+        # (functional.batch_norm fold_next)
+        cout = self.b.conv.weight.shape[0]
+        fn = self.training and x.is_cuda and 9 * cout <= 512 and cout >= self.fold_min_width
         if self.short is None and self.training and x.is_cuda and torch.is_grad_enabled() and \
                 "res_addend" not in os.environ.get("HOPSX_DISABLE", ""):
             # identity shortcut: the residual's gradient (from b's BN backward, which always runs
             # first) is handed to a's conv backward, whose dgrad epilogue adds it — no autograd add
             # (a's conv is then x's only autograd consumer, and b's conv always is a's output's)
             slot = {}
-            return self.b(self.a(x, gslot=slot, sole=True), residual=x, res_gslot=slot, sole=True)
+            return self.b(self.a(x, gslot=slot, sole=True, fold_next=fn), residual=x, res_gslot=slot, sole=True)
         if self.short is not None and _fuse_proj(self, x):
             # projection shortcut: conv a's dX goes to the short conv's dgrad epilogue (backpropagated
             # after a's: created first), not to an autograd add (ops.functional.GiveGrad)
             slot = {}
             s = self.short(x, gslot=slot)
-            return self.b(self.a(x, gslot=HF.GiveGrad(slot)), residual=s, sole=True)
+            return self.b(self.a(x, gslot=HF.GiveGrad(slot), fold_next=fn), residual=s, sole=True)
         s = x if self.short is None else self.short(x)
-        return self.b(self.a(x), residual=s, sole=True)
+        return self.b(self.a(x, fold_next=fn), residual=s, sole=True)
 
 
 class Bottleneck(nn.Module):

@@ -220,9 +220,9 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(num_features))
         self.momentum, self.eps, self.activation = momentum, eps, activation
 
-    def forward(self, x, residual=None, gslot=None):
+    def forward(self, x, residual=None, gslot=None, fold_next=False):
         return HF.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                             self.momentum, self.eps, residual, self.activation, gslot=gslot)
+                             self.momentum, self.eps, residual, self.activation, gslot=gslot, fold_next=fold_next)
 
 
 class EmbeddingBag(nn.Module):

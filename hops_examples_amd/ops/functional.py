@@ -350,10 +350,26 @@ class _Conv2dFn(torch.autograd.Function):
         # shortcut, _BNFn) hands over its gradient of x; this dgrad adds it (in the epilogue where
         # the kernel has one) instead of autograd launching an add
         ctx.gslot = gslot
+        fold = _take_bn_fold(x)  # x: a batch_norm(fold_next=True) output whose apply has not run yet
         if bnstats and x.dtype == BF16 and b is None and not act and in_affine is None and _bnstats_conv(g):
             # the output feeds a training BatchNorm: the conv epilogue accumulates its statistics
             # (no statistics pass over y); the BN then runs bn_fwd_apply_fin
             x = x.contiguous()
+            y = None
+            if fold is not None:
+                # ... and x's own BN apply runs inside this conv's operand gather (x written here too); the
+                # output's statistics then go to the alternate accumulator (x's are being read)
+                y = K.conv2d_fwd_bnstats_inbn(fold[0], x, _arena.weight_bf16(w), g, fold[1])
+                if y is None:
+                    _bn_fold_apply(x, fold)
+                fold = None
+            if y is not None:
+                ctx.save_for_backward(x, y)
+                ctx.w, ctx.b, ctx.g, ctx.act, ctx.in_affine, ctx.prev = w, b, g, act, in_affine, prev
+                ctx.plain = False
+                ctx.set_materialize_grads(False)
+                y._hx_bnstats = 2
+                return y
             y = K.conv2d_fwd_bnstats(x, _arena.weight_bf16(w), g)
             if y is not None:
                 ctx.save_for_backward(x, y)
@@ -362,6 +378,8 @@ class _Conv2dFn(torch.autograd.Function):
                 ctx.set_materialize_grads(False)
                 y._hx_bnstats = True
                 return y
+        if fold is not None:
+            _bn_fold_apply(x, fold)
         if pool is not None:
             # conv + act + pk x pk max-pool (+ dropout) as one launch; only the pooled tensor and the
             # argmax exist afterwards (ReLU' is encoded in the argmax, see conv2d_fwd_pool)
@@ -1023,14 +1041,22 @@ def dropout(x, p: float, training: bool = True, salt: int = 0):
 # ================================================================== batchnorm
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act, prestats=False, gslot=None):
+    def forward(ctx, x, gamma, beta, rm, rv, momentum, eps, residual, act, prestats=False, gslot=None, fold=False):
         C = x.shape[-1]
         x2 = x.contiguous().view(-1, C)
         mean = torch.empty(C, device=x.device)
         rstd = torch.empty(C, device=x.device)
         r2 = residual.contiguous().view(-1, C) if residual is not None else None
-        if prestats:  # statistics accumulated by the producing conv's epilogue
-            y = K.bn_fwd_apply_fin(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
+        deferred = None
+        if fold and prestats is True and residual is None and x2.dtype == BF16 and "bn_fold" not in _disabled():
+            # the apply is folded into the consuming conv's operand gather (conv2d_fwd_bnstats_inbn), which
+            # also writes y, mean / rstd and the running statistics; _Conv2dFn launches the apply instead
+            # when its shape has no such path (_bn_fold_apply)
+            y = torch.empty_like(x2)
+            deferred = (x2, (gamma, beta, mean, rstd, rm, rv, momentum, eps, act))
+        elif prestats:  # statistics accumulated by the producing conv's epilogue (2: the alternate buffer)
+            y = K.bn_fwd_apply_fin(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act,
+                                   alt=prestats == 2)
         else:
             y = K.bn_fwd_train(x2, gamma, beta, mean, rstd, rm, rv, momentum, eps, residual=r2, act=act)
         ctx.save_for_backward(x2, y, mean, rstd)
@@ -1041,6 +1067,8 @@ class _BNFn(torch.autograd.Function):
             # for a consumer conv's dgrad epilogue (bn_sole_consumer): the BN input, its batch statistics and
             # this BN's private sums accumulator
             out._hx_bnsrc = (x2, mean, rstd, act, K.bn_sums_acc(gamma, x.device, C))
+        if deferred is not None:
+            out._hx_bn_fold = deferred
         return out
 
     @staticmethod
@@ -1062,7 +1090,7 @@ class _BNFn(torch.autograd.Function):
                 ctx.gslot["g"] = dres.view(shape)
                 dres = None
             return (dx.view(shape), _ret_grad(gamma, gg), _ret_grad(beta, gb), None, None, None, None,
-                    dres.view(shape) if dres is not None else None, None, None, None)
+                    dres.view(shape) if dres is not None else None, None, None, None, None)
         dy2 = dy.to(BF16).contiguous().view(-1, C)
         dres = torch.empty_like(dy2) if has_res else None
         # no residual + ReLU: the backward recomputes the act' mask from x (no read of y; K.bn_bwd zbeta)
@@ -1072,14 +1100,29 @@ class _BNFn(torch.autograd.Function):
             ctx.gslot["g"] = dres.view(shape)
             dres = None
         return (dx.view(shape), _ret_grad(gamma, gg), _ret_grad(beta, gb), None, None, None, None,
-                dres.view(shape) if dres is not None else None, None, None, None)
+                dres.view(shape) if dres is not None else None, None, None, None, None)
+
+
+def _bn_fold_apply(a, fold) -> None:
+    """Launch the deferred apply of a fold_next batch_norm output ``a`` whose consumer could not fold it."""
+    z2, (gamma, beta, mean, rstd, rm, rv, momentum, eps, act) = fold
+    K.bn_fwd_apply_fin(z2, gamma, beta, mean, rstd, rm, rv, momentum, eps, act=act, out=a.view(z2.shape))
+
+
+def _take_bn_fold(x):
+    fold = getattr(x, "_hx_bn_fold", None)
+    if fold is not None:
+        x._hx_bn_fold = None
+    return fold
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentum=0.1, eps=1e-5, residual=None,
-               act=None, gslot=None):
+               act=None, gslot=None, fold_next=False):
     """NHWC batch norm with fused residual add + activation: act(bn(x) + residual).  ``gslot``: hand
     the residual's gradient to the conv that also consumes the residual (see _Conv2dFn) instead of
-    returning it to autograd."""
+    returning it to autograd.  ``fold_next``: the output goes straight to a ``conv2d(bnstats=True)`` (its
+    only consumer, next on the stream): with statistics from the producing conv and no residual, the
+    apply is deferred into that conv's operand gather (conv_mfma.hip InBn) — one launch fewer."""
     a = ACT[act] if not isinstance(act, int) else act
     C = x.shape[-1]
     if not x.is_cuda:
@@ -1094,12 +1137,13 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training=True, momentu
         if not training:
             # the conv epilogue already accumulated this tensor's statistics: re-zero the shared
             # accumulator rows before raising, or every later training BN of this width folds them in
-            K.bn_acc(x.device, C).zero_()
+            K.bn_acc(x.device, C, alt=pre == 2).zero_()
             raise RuntimeError("conv2d(bnstats=True) output fed to an eval-mode batch_norm")
     x = to_compute(x)
     residual = to_compute(residual) if residual is not None else None
     if training:
-        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a, pre, gslot)
+        return _BNFn.apply(x, gamma, beta, running_mean, running_var, momentum, eps, residual, a, pre, gslot,
+                           bool(fold_next))
     y = K.bn_fwd_infer(x.contiguous().view(-1, C), gamma, beta, running_mean, running_var, eps,
                        residual=None if residual is None else residual.contiguous().view(-1, C), act=a)
     return y.view(x.shape)

@@ -610,12 +610,14 @@ _BN_ACC: dict = {}
 BN_NREP = 8  # replica rows of the BN column-reduction accumulators (norm.hip BN_NREP)
 
 
-def bn_acc(device, C) -> torch.Tensor:
+def bn_acc(device, C, alt: bool = False) -> torch.Tensor:
     """Zero-at-rest [BN_NREP, 2C] fp32 accumulator (+ arrival counter) for the vectorized BN
     reductions: the reduction's last workgroup finalizes and re-zeroes it, so one buffer per
     (device, C) serves every BN layer of that width in stream order, with no memset or finalize
-    launches.  Created outside graph capture (warm-up)."""
-    key = (str(device), int(C))
+    launches.  Created outside graph capture (warm-up).  ``alt``: the second buffer of the width, for a
+    conv that reads one BN's statistics (its folded input BN, conv2d_fwd_bnstats_inbn) while producing
+    the next one's."""
+    key = (str(device), int(C)) + ((1,) if alt else ())
     t = _BN_ACC.get(key)
     if t is None:
         if torch.cuda.is_current_stream_capturing():
@@ -671,6 +673,28 @@ def conv2d_fwd_bnstats(x, w, geom, out=None):
     return out
 
 
+def conv2d_fwd_bnstats_inbn(z, a, w, geom, fold, out=None):
+    """conv2d_fwd_bnstats whose input a = act(bn(z)) is a training BatchNorm's output that no apply launch
+    produced (functional.batch_norm fold_next): the conv applies the BN inside its operand gather and
+    writes ``a`` itself (conv_mfma.hip InBn).  ``fold`` = (gamma, beta, mean, rstd, rmean, rvar, momentum,
+    eps, act) of that BN; its statistics are in bn_acc(C), this conv's output statistics go to
+    bn_acc(CO, alt=True).  None — nothing launched — when the shape has no such path."""
+    _req(z, BF16, "z")
+    _req(w, BF16, "w")
+    gamma, beta, mean, rstd, rm, rv, momentum, eps, act = fold
+    B, OH, OW, CO, C = geom[0], geom[4], geom[5], geom[6], geom[3]
+    if out is None:
+        out = torch.empty(B, OH, OW, CO, device=z.device, dtype=BF16)
+    rc = _C.ext().conv2d_fwd_bnstats_inbn(ptr(z), ptr(a), ptr(w), list(geom), ptr(out),
+                                          ptr(bn_acc(z.device, CO, alt=True)), ptr(bn_acc(z.device, C)), ptr(gamma),
+                                          ptr(beta), ptr(mean), ptr(rstd), ptr(rm), ptr(rv), float(momentum),
+                                          float(eps), act_id(act), stream())
+    if rc == -2:
+        return None
+    check(rc, "conv2d_fwd_bnstats_inbn")
+    return out
+
+
 def bn_coop_timeouts(device, C) -> int:
     """Nonzero if a one-launch BN backward barrier of width C ever timed out (never expected)."""
     return int(_C.ext().bn_coop_timeouts(ptr(bn_acc(device, C)), int(C)))
@@ -680,16 +704,17 @@ def bn_prestats_ok(C) -> bool:
     return bool(_C.ext().bn_prestats_ok(int(C)))
 
 
-def bn_fwd_apply_fin(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, residual=None, act=0, out=None):
+def bn_fwd_apply_fin(x2d, gamma, beta, mean, rstd, rmean, rvar, momentum, eps, residual=None, act=0, out=None,
+                     alt=False):
     """Training BN forward whose statistics the producing conv already accumulated
-    (conv2d_fwd_bnstats): one launch that finalizes them, applies act(bn(x) + residual) and
-    re-zeroes the accumulator."""
+    (conv2d_fwd_bnstats; into bn_acc(C, alt) for conv2d_fwd_bnstats_inbn): one launch that finalizes them,
+    applies act(bn(x) + residual) and re-zeroes the accumulator."""
     M, C = x2d.shape
     if out is None:
         out = torch.empty_like(x2d)
     check(_C.ext().bn_fwd_apply_fin(ptr(x2d), ptr(out), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), ptr(rmean),
                                     ptr(rvar), float(momentum), float(eps), M, C, ptr(residual), act_id(act),
-                                    ptr(bn_acc(x2d.device, C)), stream()),
+                                    ptr(bn_acc(x2d.device, C, alt=alt)), stream()),
           "bn_fwd_apply_fin")
     return out
 
