@@ -112,7 +112,7 @@ def _blocks_step(disable, cin, cout, stride, hw, calls):
         torch.cuda.synchronize()
         calls.append(n[0])
         stats = torch.cat([b.float().reshape(-1) for b in m.buffers()])
-        return y.float(), [t.float().reshape(-1) for t in gs], stats
+        return y.detach().float(), [t.float().reshape(-1) for t in gs], stats
     finally:
         K.conv2d_fwd_bnstats_inbn = real
         os.environ["HOPSX_DISABLE"] = old

@@ -99,7 +99,8 @@ pmc)
   timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES WRITE_SIZE -d "$R/$out/c" -o run --output-format csv -- $P > "$R/$out/c.log" 2>&1 ;;
 debug)
   export HOPSX_DEBUG=1; T=600 pyt $out/pytest_debug.log tests/test_debug_checks_gpu.py tests/test_kernels_gpu.py tests/test_kernels_v2_gpu.py \
-    tests/test_dgrad_par_gpu.py tests/test_wgrad_glds_gpu.py tests/test_bnstats_gpu.py tests/test_models_gpu.py ;;
+    tests/test_dgrad_par_gpu.py tests/test_wgrad_glds_gpu.py tests/test_bnstats_gpu.py tests/test_bn_fold_gpu.py \
+    tests/test_models_gpu.py ;;
 ab)
   reps=$1; args=$2; shift 2
   for rep in $(seq $reps); do for s in "" "$@"; do
